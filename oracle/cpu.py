@@ -1,0 +1,222 @@
+"""TEST INFRASTRUCTURE ONLY -- ctypes bindings for the CPU checkers.
+
+* ``Oracle``  -> ``oracle/librsoracle.so``: our plain-C restatement of
+  lib/fec.cpp + lib/rs.cpp (see rs_oracle.c for per-function citations).
+* ``Reference`` -> ``oracle/_ref/libref_rs.so``: the unmodified reference
+  lib/{fec,rs}.cpp compiled from /root/reference by oracle/Makefile, plus our
+  batch driver (ref_driver.cpp).  Present only where it was built.
+
+Also the synthetic-input definitions shared by tests, golden generation and the
+bench's CPU leg (SplitMix64 byte streams, erasure draws, the C3 ragged mix), in
+numpy.  Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may
+import this module; the product package never does.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ORACLE_SO = os.path.join(HERE, "librsoracle.so")
+REF_SO = os.path.join(HERE, "_ref", "libref_rs.so")
+
+GAMMA = np.uint64(0x9E3779B97F4A7C15)
+M1 = np.uint64(0xBF58476D1CE4E5B9)
+M2 = np.uint64(0x94D049BB133111EB)
+
+DATA_SEED = 0x5EEDC0DE
+ERASE_SEED = 0xE7A5E5EED
+RAGGED_SEED = 0x7A66ED
+
+
+def _mix(z: np.ndarray) -> np.ndarray:
+    z = (z ^ (z >> np.uint64(30))) * M1
+    z = (z ^ (z >> np.uint64(27))) * M2
+    return z ^ (z >> np.uint64(31))
+
+
+def splitmix_words(seed: int, groups: np.ndarray, nwords: int) -> np.ndarray:
+    """[len(groups), nwords] uint64: word w of group g's stream =
+    mix((seed ^ g) + (w+1)*GAMMA)."""
+    with np.errstate(over="ignore"):
+        s0 = np.uint64(seed) ^ groups.astype(np.uint64)
+        w = (np.arange(1, nwords + 1, dtype=np.uint64) * GAMMA)
+        return _mix(s0[:, None] + w[None, :])
+
+
+def group_data(seed: int, g0: int, ng: int, k: int, length: int) -> np.ndarray:
+    """Data shards of groups g0..g0+ng-1 as [ng, k, length] uint8.  Byte q of a
+    group's k*length data bytes (shard-major) is byte q%8 of stream word q//8."""
+    nbytes = k * length
+    nwords = (nbytes + 7) // 8
+    words = splitmix_words(seed, np.arange(g0, g0 + ng, dtype=np.uint64), nwords)
+    b = words.view(np.uint8).reshape(ng, nwords * 8)[:, :nbytes]
+    return b.reshape(ng, k, length)
+
+
+def erasures(seed: int, g0: int, ng: int, n: int, e: int, limit: int | None = None) -> np.ndarray:
+    """[ng, e] erased shard indices per group: partial Fisher-Yates over
+    range(limit or n) driven by words mix((seed^g)+(i+1)*GAMMA)."""
+    lim = n if limit is None else limit
+    r = splitmix_words(seed, np.arange(g0, g0 + ng, dtype=np.uint64), e)
+    perm = np.tile(np.arange(lim, dtype=np.int64), (ng, 1))
+    rows = np.arange(ng)
+    for i in range(e):
+        pick = i + (r[:, i] % np.uint64(lim - i)).astype(np.int64)
+        a = perm[rows, i].copy()
+        perm[rows, i] = perm[rows, pick]
+        perm[rows, pick] = a
+    return perm[:, :e]
+
+
+def present_from_erasures(er: np.ndarray, n: int) -> np.ndarray:
+    p = np.ones((er.shape[0], n), dtype=np.uint8)
+    p[np.arange(er.shape[0])[:, None], er] = 0
+    return p
+
+
+def ragged_draw(seed: int, g0: int, ng: int, table_y: np.ndarray,
+                kmax: int = 20, lmin: int = 64, lmax: int = 1250):
+    """C3 ragged mix: k ~ U{1..kmax}, m = rs_from_str table[k], len ~ U[lmin..lmax]."""
+    r = splitmix_words(seed, np.arange(g0, g0 + ng, dtype=np.uint64), 2)
+    k = 1 + (r[:, 0] % np.uint64(kmax)).astype(np.int64)
+    ln = lmin + (r[:, 1] % np.uint64(lmax - lmin + 1)).astype(np.int64)
+    m = table_y[k - 1].astype(np.int64)
+    return k, m, ln
+
+
+def _p(a: np.ndarray):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+class _Lib:
+    def __init__(self, path: str):
+        if not os.path.exists(path):
+            raise FileNotFoundError(f"{path} missing: run `make -C oracle`")
+        self.lib = C.CDLL(path)
+
+
+class Oracle(_Lib):
+    """Our C restatement (librsoracle.so)."""
+
+    def __init__(self, path: str = ORACLE_SO):
+        super().__init__(path)
+        L = self.lib
+        L.orc_enc_matrix.argtypes = [C.c_int, C.c_int, C.c_void_p]
+        L.orc_encode.argtypes = [C.c_int, C.c_int, C.c_void_p, C.c_int]
+        L.orc_decode.argtypes = [C.c_int, C.c_int, C.c_void_p, C.c_int]
+        L.orc_encode_batch.argtypes = [C.c_int, C.c_int, C.c_void_p, C.c_int64, C.c_int64,
+                                       C.c_int, C.c_int64]
+        L.orc_decode_batch.argtypes = [C.c_int, C.c_int, C.c_void_p, C.c_int64, C.c_int64,
+                                       C.c_int, C.c_int64, C.c_void_p, C.c_void_p]
+        L.orc_rs_from_str.argtypes = [C.c_char_p, C.c_void_p, C.c_void_p]
+        L.orc_gf_tables.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+        L.orc_gf_mul.argtypes = [C.c_uint8, C.c_uint8]
+        L.orc_gf_mul.restype = C.c_uint8
+
+    def gf_tables(self):
+        e = np.zeros(510, np.uint8); lg = np.zeros(256, np.int32); inv = np.zeros(256, np.uint8)
+        self.lib.orc_gf_tables(_p(e), _p(lg), _p(inv))
+        return e, lg, inv
+
+    def mul_table(self) -> np.ndarray:
+        e, lg, _ = self.gf_tables()
+        a = np.arange(256)
+        t = e[(lg[:, None] + lg[None, :]) % 510]
+        t[0, :] = 0
+        t[:, 0] = 0
+        return t.astype(np.uint8)
+
+    def enc_matrix(self, k: int, n: int) -> np.ndarray:
+        out = np.zeros((n, k), np.uint8)
+        if self.lib.orc_enc_matrix(k, n, _p(out)) != 0:
+            raise ValueError(f"invalid (k,n)=({k},{n})")
+        return out
+
+    def encode_batch(self, k, n, buf: np.ndarray, group_stride, shard_stride, length, ngroups):
+        assert buf.flags.c_contiguous and buf.dtype == np.uint8
+        assert (ngroups - 1) * group_stride + n * shard_stride <= buf.size or ngroups == 0
+        rc = self.lib.orc_encode_batch(k, n, _p(buf), group_stride, shard_stride, length, ngroups)
+        if rc:
+            raise ValueError("orc_encode_batch failed")
+
+    def decode_batch(self, k, n, buf, group_stride, shard_stride, length, ngroups, present):
+        present = np.ascontiguousarray(present, dtype=np.uint8)
+        assert present.shape == (ngroups, n)
+        status = np.zeros(ngroups, np.int32)
+        self.lib.orc_decode_batch(k, n, _p(buf), group_stride, shard_stride, length, ngroups,
+                                  _p(present), _p(status))
+        return status
+
+    def rs_from_str(self, s: str):
+        xs = np.zeros(256, np.uint8); ys = np.zeros(256, np.uint8)
+        cnt = self.lib.orc_rs_from_str(s.encode(), _p(xs), _p(ys))
+        if cnt < 0:
+            return None
+        return [(int(xs[i]), int(ys[i])) for i in range(cnt)]
+
+    def decode_ptrs(self, k, n, shards: list, length):
+        """Per-group rs_decode2 semantics on Python buffers: shards[i] is a
+        bytearray or None.  Returns (rc, out) where out[i] is the index of the
+        input buffer data[i] points to afterwards (or -1)."""
+        bufs = [bytearray(s) if s is not None else None for s in shards]
+        keep = [(C.c_uint8 * max(length, 1)).from_buffer(b) if b is not None else None for b in bufs]
+        arr = (C.c_void_p * n)(*[C.addressof(x) if x is not None else None for x in keep])
+        addr = {C.addressof(x): i for i, x in enumerate(keep) if x is not None}
+        rc = self.lib.orc_decode(k, n, arr, length)
+        out = [addr.get(arr[i], -1) if arr[i] else -1 for i in range(n)]
+        return rc, out, [bytes(b) if b is not None else None for b in bufs]
+
+
+class Reference(_Lib):
+    """The real reference codec (oracle/_ref/libref_rs.so), if it was built."""
+
+    def __init__(self, path: str = REF_SO):
+        super().__init__(path)
+        L = self.lib
+        L.ref_prewarm.argtypes = [C.c_int, C.c_int]
+        L.ref_encode_batch.argtypes = [C.c_int, C.c_int, C.c_void_p, C.c_int64, C.c_int64,
+                                       C.c_int, C.c_int64, C.c_int]
+        L.ref_decode_batch.argtypes = [C.c_int, C.c_int, C.c_void_p, C.c_int64, C.c_int64,
+                                       C.c_int, C.c_int64, C.c_void_p, C.c_void_p, C.c_int, C.c_int]
+        L.ref_decode_ptrs.argtypes = [C.c_int, C.c_int, C.c_void_p, C.c_int64, C.c_int,
+                                      C.c_void_p, C.c_void_p]
+
+    @staticmethod
+    def available(path: str = REF_SO) -> bool:
+        return os.path.exists(path)
+
+    def encode_batch(self, k, n, buf, group_stride, shard_stride, length, ngroups, nthreads=1):
+        assert buf.flags.c_contiguous and buf.dtype == np.uint8
+        rc = self.lib.ref_encode_batch(k, n, _p(buf), group_stride, shard_stride, length,
+                                       ngroups, nthreads)
+        if rc:
+            raise ValueError("ref_encode_batch failed")
+
+    def decode_batch(self, k, n, buf, group_stride, shard_stride, length, ngroups, present,
+                     write_back=True, nthreads=1):
+        present = np.ascontiguousarray(present, dtype=np.uint8)
+        status = np.zeros(ngroups, np.int32)
+        self.lib.ref_decode_batch(k, n, _p(buf), group_stride, shard_stride, length, ngroups,
+                                  _p(present), _p(status), int(write_back), nthreads)
+        return status
+
+    def decode_ptrs(self, k, n, buf, shard_stride, length, in_slot):
+        ins = np.ascontiguousarray(in_slot, dtype=np.int32)
+        out = np.zeros(n, np.int32)
+        rc = self.lib.ref_decode_ptrs(k, n, _p(buf), shard_stride, length, _p(ins), _p(out))
+        return rc, out
+
+    def enc_matrix(self, k: int, n: int) -> np.ndarray:
+        """Recover fec_new's matrix through rs_encode2 alone: encoding unit
+        vector e_j (1-byte shards) yields column j of the parity rows."""
+        out = np.zeros((n, k), np.uint8)
+        out[:k, :k] = np.eye(k, dtype=np.uint8)
+        buf = np.zeros(n * k, np.uint8)  # group j = unit vector e_j
+        for j in range(k):
+            buf[j * n + j] = 1
+        self.encode_batch(k, n, buf, n, 1, 1, k)
+        out[k:, :] = buf.reshape(k, n)[:, k:].T
+        return out
