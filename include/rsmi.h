@@ -1,0 +1,147 @@
+/*
+ * rsmi.h -- C ABI of the MI355X-native Reed-Solomon engine (librsmi.so).
+ *
+ * The code is bit-exact with UDPspeeder's lib/rs.cpp + lib/fec.cpp (Rizzo's
+ * systematic Vandermonde code over GF(2^8), polynomial 0x11D).  Two surfaces:
+ *
+ *  1. The drop-in per-group surface with the reference's own C++ names and
+ *     mangling (rs_encode2/rs_decode2/...): declared in rs_compat.h.
+ *  2. This extern "C" batched surface: many independent FEC groups per call,
+ *     device-resident buffers, plain pointers and sizes, hipStream_t passed
+ *     as void*.  It replaces the per-group calls fec_manager makes at
+ *     fec_manager.cpp:364 (encode), :632 and :710 (decode); see INTEGRATION.md.
+ *
+ * Shard layout (uniform batches): group g, shard j (0 <= j < n) lives at
+ *     base + g*group_stride + j*shard_stride
+ * Data shards are j < k, parity shards k <= j < n (same order as the char*
+ * data[] array of rs_encode2, lib/rs.h:41).  Each shard holds len payload
+ * bytes.  shard_stride must be a multiple of 16 and >= len; group_stride a
+ * multiple of 16.  The kernels may read and overwrite the slot padding bytes
+ * [len, round_up(len,16)) of a shard slot, never anything beyond it.
+ *
+ * Every call is asynchronous on `stream` (NULL = the default stream) of the
+ * current HIP device, and graph-capturable once the (k,n) code is resident
+ * (rsmi_prepare_code) and the workspace is large enough (rsmi_reserve).
+ * Return values: RSMI_OK or a negative RSMI_ERR_*; rsmi_last_error() gives
+ * text.  No call ever exit()s or falls back to the CPU: a missing or failing
+ * GPU is reported as RSMI_ERR_HIP.
+ */
+#ifndef RSMI_H_
+#define RSMI_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RSMI_OK 0
+#define RSMI_ERR_INVALID (-2) /* bad k/n/len/stride/alignment argument        */
+#define RSMI_ERR_HIP (-3)     /* HIP runtime error (no device, launch failure) */
+#define RSMI_ERR_NOMEM (-4)   /* device or pinned allocation failed            */
+
+/* Per-group decode status written by rsmi_decode_dev (same codes as
+ * rs_decode2, lib/rs.cpp:31-32 and lib/fec.cpp:851-856). */
+#define RSMI_DEC_OK 0
+#define RSMI_DEC_TOO_FEW (-1) /* fewer than k shards present        */
+#define RSMI_DEC_SINGULAR 1   /* decode matrix singular (never for valid codes) */
+
+/* Library version, e.g. 0x000100 = 0.1.0. */
+int rsmi_version(void);
+
+/* Initialise tables on the current device (idempotent, thread-safe). */
+int rsmi_init(void);
+
+/* Text of the last error on this thread ("" if none). */
+const char *rsmi_last_error(void);
+
+/* Host copy of fec_new(k,n)'s n x k systematic encoding matrix (row-major),
+ * lib/fec.cpp:665-720.  Valid: 1 <= k <= n <= 256. */
+int rsmi_get_matrix(int k, int n, uint8_t *out_nk);
+
+/* Host-side decode coefficients for one group: the rows fec_decode derives
+ * (lib/fec.cpp:795-825, 861-868) under rs_decode's survivor selection
+ * (lib/rs.cpp:24-39).  present[n] (nonzero = received).  Writes sel[k] (the
+ * k survivor slots used, ascending), miss[e] (missing data rows, ascending)
+ * and coef[e*k] (d[miss[r]] = sum_c coef[r*k+c] * shard[sel[c]]); buffers
+ * for miss/coef must hold k and k*k bytes.  Returns e >= 0, -1 if fewer than
+ * k shards are present, RSMI_ERR_INVALID for bad arguments. */
+int rsmi_decode_matrix(int k, int n, const uint8_t *present, uint8_t *sel,
+                       uint8_t *miss, uint8_t *coef);
+
+/* Make the (k,n) code resident on the current device (get_code's role,
+ * lib/rs.cpp:42-55).  Called implicitly by the entry points below; call it
+ * up front to keep later calls free of host<->device traffic. */
+int rsmi_prepare_code(int k, int n);
+
+/* Make (k,n) resident and pre-size the decode workspace that calls on
+ * `stream` use, for up to `ngroups` groups (needed before graph capture). */
+int rsmi_reserve(int k, int n, int64_t ngroups, void *stream);
+
+/* ---- uniform batches (all groups share k, n, len) ------------------------ */
+
+/* rs_encode2(k, n, data, len) for every group: writes parity shards k..n-1. */
+int rsmi_encode_dev(int k, int n, uint8_t *base, int64_t group_stride,
+                    int64_t shard_stride, int len, int64_t ngroups, void *stream);
+
+/* rs_decode2(k, n, data, len) for every group.  present[g*n + j] != 0 marks
+ * shard j of group g as received (device array, ngroups*n bytes).  Missing
+ * data shards j < k are reconstructed IN THEIR OWN SLOT from the first k
+ * present shards in ascending index order (the selection of lib/rs.cpp:24-39);
+ * erased slots are never read.  Parity slots are left untouched.
+ * status (device int32[ngroups], may be NULL) receives RSMI_DEC_*. */
+int rsmi_decode_dev(int k, int n, uint8_t *base, int64_t group_stride,
+                    int64_t shard_stride, int len, int64_t ngroups,
+                    const uint8_t *present, int32_t *status, void *stream);
+
+/* ---- ragged batches (mode 0 mix: each group its own k, n, len) ---------- */
+
+typedef struct rsmi_group {
+    uint64_t offset;       /* byte offset of shard 0 from base (multiple of 16) */
+    uint32_t shard_stride; /* multiple of 16, >= len                            */
+    uint32_t len;          /* payload bytes per shard                           */
+    uint16_t k;            /* data shards                                       */
+    uint16_t n;            /* total shards                                      */
+    uint32_t reserved;     /* must be 0                                         */
+} rsmi_group;              /* 24 bytes */
+
+/* Encode ngroups groups described by groups[] (HOST array).  The codes for
+ * every (k,n) in the batch are made resident and the descriptors are staged
+ * to the device on `stream`. */
+int rsmi_encode_ragged(const rsmi_group *groups, int64_t ngroups, uint8_t *base,
+                       void *stream);
+
+/* Same, with a DEVICE descriptor array (graph-capturable).  Every (k,n) used
+ * must already be resident (rsmi_prepare_code); groups whose code is not
+ * resident, or whose descriptor is invalid, are left untouched. */
+int rsmi_encode_ragged_dev(const rsmi_group *dev_groups, int64_t ngroups,
+                           uint8_t *base, void *stream);
+
+/* ---- host-memory convenience (pinned staging + H2D/D2H on an internal
+ * stream; synchronous).  Same layout contract, host pointers. --------------- */
+int rsmi_encode_host(int k, int n, uint8_t *base, int64_t group_stride,
+                     int64_t shard_stride, int len, int64_t ngroups);
+int rsmi_decode_host(int k, int n, uint8_t *base, int64_t group_stride,
+                     int64_t shard_stride, int len, int64_t ngroups,
+                     const uint8_t *present, int32_t *status);
+
+/* ---- synthetic inputs (bench / tests) ----------------------------------- */
+
+/* Fill data shards (j < k) of every group with the SplitMix64 stream:
+ * byte q of group g's k*len data bytes (shard-major) is byte q%8 of
+ * mix((seed ^ g) + (q/8 + 1) * 0x9E3779B97F4A7C15).  Groups g0..g0+ngroups-1
+ * are written at base + (g-g0)*group_stride. */
+int rsmi_fill_data(int k, int len, uint8_t *base, int64_t group_stride,
+                   int64_t shard_stride, int64_t g0, int64_t ngroups,
+                   uint64_t seed, void *stream);
+
+/* Same stream definition for a ragged batch: data rows of group i (device
+ * descriptor array) get the stream of group id g0 + i. */
+int rsmi_fill_ragged(const rsmi_group *dev_groups, int64_t ngroups, uint8_t *base,
+                     int64_t g0, uint64_t seed, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RSMI_H_ */

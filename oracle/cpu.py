@@ -161,13 +161,14 @@ class Oracle(_Lib):
         """Per-group rs_decode2 semantics on Python buffers: shards[i] is a
         bytearray or None.  Returns (rc, out) where out[i] is the index of the
         input buffer data[i] points to afterwards (or -1)."""
-        bufs = [bytearray(s) if s is not None else None for s in shards]
+        bufs = [bytearray(s) + bytearray(max(0, 1 - len(s))) if s is not None else None
+                for s in shards]
         keep = [(C.c_uint8 * max(length, 1)).from_buffer(b) if b is not None else None for b in bufs]
         arr = (C.c_void_p * n)(*[C.addressof(x) if x is not None else None for x in keep])
         addr = {C.addressof(x): i for i, x in enumerate(keep) if x is not None}
         rc = self.lib.orc_decode(k, n, arr, length)
         out = [addr.get(arr[i], -1) if arr[i] else -1 for i in range(n)]
-        return rc, out, [bytes(b) if b is not None else None for b in bufs]
+        return rc, out, [bytes(b[:length]) if b is not None else None for b in bufs]
 
 
 class Reference(_Lib):

@@ -1,0 +1,113 @@
+"""CPU: librsmi.so loads, exports every symbol include/*.h declares, and its
+host-only functions (matrix build, decode coefficients, -f table) match the
+reference fixtures.  No GPU compute here."""
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+import udpspeeder_amd as u
+from udpspeeder_amd._lib import LIB_PATH, MANGLED
+from oracle.gen_golden import MATRIX_SET, C3_STR
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared(header):
+    txt = open(os.path.join(ROOT, "include", header)).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    txt = re.sub(r"//.*", "", txt)
+    txt = re.sub(r"^\s*#.*$", "", txt, flags=re.M)
+    names = re.findall(r"\b([A-Za-z_][A-Za-z0-9_]*)\s*\([^;{]*\)\s*;", txt)
+    return [n for n in names if n not in ("if", "sizeof")]
+
+
+def _exports():
+    out = subprocess.run(["nm", "-D", "--defined-only", LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    return {line.split()[-1] for line in out.splitlines() if " T " in line}
+
+
+def test_lib_loads_and_version():
+    assert os.path.exists(LIB_PATH)
+    assert u.version() == 0x000100
+
+
+def test_exports_rsmi_h():
+    ex = _exports()
+    decl = _declared("rsmi.h")
+    assert "rsmi_encode_dev" in decl and "rsmi_decode_dev" in decl
+    missing = [d for d in decl if d not in ex]
+    assert not missing, missing
+
+
+def test_exports_rs_compat_h_mangled():
+    ex = _exports()
+    decl = _declared("rs_compat.h")
+    assert set(decl) == set(MANGLED), (set(decl) ^ set(MANGLED))
+    for name in decl:
+        assert MANGLED[name] in ex, name
+    # exactly the reference's mangling (lib/rs.h, lib/fec.h signatures)
+    assert MANGLED["rs_encode2"] == "_Z10rs_encode2iiPPci"
+    assert MANGLED["rs_decode2"] == "_Z10rs_decode2iiPPci"
+
+
+def test_no_internal_exports():
+    ex = _exports()
+    assert not [s for s in ex if s.startswith("_ZN4rsmi")]
+
+
+@pytest.mark.parametrize("kn", MATRIX_SET)
+def test_matrix_vs_reference(golden, kn):
+    k, n = kn
+    m = u.enc_matrix(k, n)
+    assert (m[:k] == np.eye(k, dtype=np.uint8)).all()
+    assert (m[k:] == golden.mats[f"{k}_{n}"]).all()
+
+
+def test_invalid_matrix():
+    for k, n in [(0, 1), (3, 2), (257, 257)]:
+        with pytest.raises(u.RsmiError):
+            u.enc_matrix(k, n)
+
+
+def test_decode_matrix_reconstructs(oracle):
+    """Host decode coefficients (the plan math the GPU kernel restates) applied
+    with the oracle's mul table reproduce the oracle's decode, random patterns."""
+    t = oracle.mul_table()
+    rng = np.random.default_rng(7)
+    for (k, n) in [(20, 30), (3, 6), (1, 4), (10, 16), (7, 13), (64, 128)]:
+        for _ in range(5):
+            ln = 9
+            buf = np.zeros((1, n, 16), np.uint8)
+            buf[0, :, :ln] = rng.integers(0, 256, (n, ln), dtype=np.uint8)  # non-codeword
+            present = np.ones(n, np.uint8)
+            ner = rng.integers(0, n - k + 1)
+            present[rng.choice(n, ner, replace=False)] = 0
+            e, sel, miss, coef = u.decode_matrix(k, n, present)
+            ref = buf.copy()
+            st = oracle.decode_batch(k, n, ref.reshape(-1), n * 16, 16, ln, 1, present[None])
+            assert st[0] == 0
+            assert e == int((present[:k] == 0).sum())
+            for r, j in enumerate(miss):
+                acc = np.zeros(ln, np.uint8)
+                for c, s in enumerate(sel):
+                    acc ^= t[coef[r, c], buf[0, s, :ln]]
+                assert (acc == ref[0, j, :ln]).all()
+
+
+def test_decode_matrix_too_few():
+    e, *_ = u.decode_matrix(3, 6, [0, 0, 0, 0, 1, 1])
+    assert e == -1
+
+
+def test_fec_param_table(oracle, golden):
+    assert u.rs_from_str(C3_STR) == [tuple(x) for x in golden.mats["c3_table"].tolist()]
+    for s in ["20:10", "1:3,2:4,10:6,20:10", "5:5,10:3,40:30", "1:0", "3:1,100:100",
+              "10:20,20:30,30:40,200:55"]:
+        assert u.rs_from_str(s) == oracle.rs_from_str(s), s
+    for bad in ["", "0:1", "3:2,2:4", "200:100", "a:b", "1:-1", "10"]:
+        assert u.rs_from_str(bad) is None
+    assert u.rs_to_str(u.rs_from_str("2:1,4:2")) == "1:1,2:1,3:2,4:2"

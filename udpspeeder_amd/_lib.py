@@ -1,0 +1,109 @@
+"""Locate and bind librsmi.so (built in-tree by ``make -C udpspeeder_amd/csrc``).
+
+The product path has no fallback: if the shared library is missing this
+module raises at import of any compute entry point, and every GPU entry point
+reports HIP errors (no device, launch failure) as exceptions.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("RSMI_LIB", os.path.join(_HERE, "librsmi.so"))
+
+RSMI_OK = 0
+RSMI_ERR_INVALID = -2
+RSMI_ERR_HIP = -3
+RSMI_ERR_NOMEM = -4
+RSMI_DEC_OK = 0
+RSMI_DEC_TOO_FEW = -1
+RSMI_DEC_SINGULAR = 1
+
+# Mangled C++ names of the drop-in surface (include/rs_compat.h); these are the
+# exact symbols the reference's objects link against (lib/rs.h, lib/fec.h).
+MANGLED = {
+    "rs_encode2": "_Z10rs_encode2iiPPci",
+    "rs_decode2": "_Z10rs_decode2iiPPci",
+    "rs_encode": "_Z9rs_encodePvPPci",
+    "rs_decode": "_Z9rs_decodePvPPci",
+    "get_code": "_Z8get_codeii",
+    "fec_new": "_Z7fec_newii",
+    "fec_free": "_Z8fec_freePv",
+    "fec_encode": "_Z10fec_encodePvPS_S_ii",
+    "fec_decode": "_Z10fec_decodePvPS_Pii",
+    "get_k": "_Z5get_kPv",
+    "get_n": "_Z5get_nPv",
+}
+
+
+class RsmiError(RuntimeError):
+    pass
+
+
+class rsmi_group(C.Structure):
+    _fields_ = [("offset", C.c_uint64), ("shard_stride", C.c_uint32), ("len", C.c_uint32),
+                ("k", C.c_uint16), ("n", C.c_uint16), ("reserved", C.c_uint32)]
+
+
+_lock = threading.Lock()
+_lib = None
+
+
+def _bind(lib: C.CDLL) -> C.CDLL:
+    vp, i64, i32 = C.c_void_p, C.c_int64, C.c_int
+    sig = {
+        "rsmi_version": ([], i32),
+        "rsmi_init": ([], i32),
+        "rsmi_last_error": ([], C.c_char_p),
+        "rsmi_get_matrix": ([i32, i32, vp], i32),
+        "rsmi_decode_matrix": ([i32, i32, vp, vp, vp, vp], i32),
+        "rsmi_prepare_code": ([i32, i32], i32),
+        "rsmi_reserve": ([i32, i32, i64, vp], i32),
+        "rsmi_encode_dev": ([i32, i32, vp, i64, i64, i32, i64, vp], i32),
+        "rsmi_decode_dev": ([i32, i32, vp, i64, i64, i32, i64, vp, vp, vp], i32),
+        "rsmi_encode_ragged": ([vp, i64, vp, vp], i32),
+        "rsmi_encode_ragged_dev": ([vp, i64, vp, vp], i32),
+        "rsmi_encode_host": ([i32, i32, vp, i64, i64, i32, i64], i32),
+        "rsmi_decode_host": ([i32, i32, vp, i64, i64, i32, i64, vp, vp], i32),
+        "rsmi_fill_data": ([i32, i32, vp, i64, i64, i64, i64, C.c_uint64, vp], i32),
+        "rsmi_fill_ragged": ([vp, i64, vp, i64, C.c_uint64, vp], i32),
+    }
+    for name, (args, res) in sig.items():
+        f = getattr(lib, name)
+        f.argtypes = args
+        f.restype = res
+    m = {k: getattr(lib, v) for k, v in MANGLED.items()}
+    m["rs_encode2"].argtypes = [i32, i32, vp, i32]; m["rs_encode2"].restype = None
+    m["rs_decode2"].argtypes = [i32, i32, vp, i32]; m["rs_decode2"].restype = i32
+    m["rs_encode"].argtypes = [vp, vp, i32]; m["rs_encode"].restype = None
+    m["rs_decode"].argtypes = [vp, vp, i32]; m["rs_decode"].restype = i32
+    m["get_code"].argtypes = [i32, i32]; m["get_code"].restype = vp
+    m["fec_new"].argtypes = [i32, i32]; m["fec_new"].restype = vp
+    m["fec_free"].argtypes = [vp]; m["fec_free"].restype = None
+    m["fec_encode"].argtypes = [vp, vp, vp, i32, i32]; m["fec_encode"].restype = None
+    m["fec_decode"].argtypes = [vp, vp, vp, i32]; m["fec_decode"].restype = i32
+    m["get_k"].argtypes = [vp]; m["get_k"].restype = i32
+    m["get_n"].argtypes = [vp]; m["get_n"].restype = i32
+    lib.compat = m
+    return lib
+
+
+def lib() -> C.CDLL:
+    """The loaded librsmi.so (raises RsmiError if it was not built)."""
+    global _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise RsmiError(
+                    f"{LIB_PATH} not found: build it with `make -C udpspeeder_amd/csrc` "
+                    "(or __graft_entry__.build()); there is no CPU fallback")
+            _lib = _bind(C.CDLL(LIB_PATH))
+        return _lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != RSMI_OK:
+        msg = lib().rsmi_last_error().decode(errors="replace")
+        raise RsmiError(f"{what} failed ({rc}): {msg}")

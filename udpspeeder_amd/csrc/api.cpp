@@ -1,0 +1,541 @@
+// api.cpp -- host runtime of librsmi.so: per-device state (GF tables, resident
+// codes, decode workspaces), argument validation, the extern "C" batched API
+// of include/rsmi.h, and the synchronous host-memory variants used by the
+// drop-in shim (compat.cpp).
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "gf256.hpp"
+#include "rsmi_internal.hpp"
+
+namespace rsmi {
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string &msg) {
+    g_err = msg;
+    return code;
+}
+
+int hip_fail(hipError_t e, const char *what) {
+    return fail(RSMI_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+#define RSMI_HIP(call, what)                          \
+    do {                                              \
+        hipError_t e_ = (call);                       \
+        if (e_ != hipSuccess) return hip_fail(e_, what); \
+    } while (0)
+
+struct Code {
+    int k = 0, n = 0;
+    std::vector<uint8_t> host;    // n x k
+    uint8_t *dev_rows = nullptr;  // (n-k) x k parity rows on the device
+};
+
+struct Workspace {
+    uint8_t *ptr = nullptr;
+    size_t bytes = 0;
+};
+
+struct Device {
+    int id = -1;
+    std::mutex mu;
+    uint32_t *ptab = nullptr;     // 256 x kPtabDwords
+    uint8_t *gftab = nullptr;     // exp[512] | log[256]
+    uint64_t *code_dir = nullptr; // 257*257 device pointers to parity rows
+    std::map<int, Code> codes;    // key k*257+n
+    std::map<hipStream_t, Workspace> ws;
+    // host-path resources (guarded by hmu, held for a whole host call)
+    std::mutex hmu;
+    hipStream_t hstream = nullptr;
+    uint8_t *pinned = nullptr;
+    size_t pinned_bytes = 0;
+    uint8_t *hdev = nullptr;
+    size_t hdev_bytes = 0;
+    int32_t *hstatus_dev = nullptr;
+    size_t hstatus_cap = 0;
+};
+
+std::mutex g_devs_mu;
+std::map<int, std::unique_ptr<Device>> g_devs;
+
+int init_device(Device &D) {
+    // caller holds D.mu
+    if (D.ptab) return RSMI_OK;
+    std::vector<uint32_t> pt(256 * kPtabDwords, 0);
+    for (int c = 0; c < 256; ++c) perm_tables((uint8_t)c, &pt[(size_t)c * kPtabDwords]);
+    const GF &F = gf();
+    std::vector<uint8_t> gt(768);
+    std::memcpy(gt.data(), F.exp, 512);
+    for (int i = 0; i < 256; ++i) gt[512 + i] = (uint8_t)F.log[i];
+    RSMI_HIP(hipMalloc(&D.ptab, pt.size() * 4), "hipMalloc(ptab)");
+    RSMI_HIP(hipMalloc(&D.gftab, gt.size()), "hipMalloc(gftab)");
+    RSMI_HIP(hipMalloc(&D.code_dir, sizeof(uint64_t) * 257 * 257), "hipMalloc(code_dir)");
+    RSMI_HIP(hipMemcpy(D.ptab, pt.data(), pt.size() * 4, hipMemcpyHostToDevice), "upload ptab");
+    RSMI_HIP(hipMemcpy(D.gftab, gt.data(), gt.size(), hipMemcpyHostToDevice), "upload gftab");
+    RSMI_HIP(hipMemset(D.code_dir, 0, sizeof(uint64_t) * 257 * 257), "clear code_dir");
+    return RSMI_OK;
+}
+
+// Returns the state of the current device, initialised; nullptr on error.
+Device *current(int *rc) {
+    int id = -1;
+    hipError_t e = hipGetDevice(&id);
+    if (e != hipSuccess) {
+        *rc = hip_fail(e, "hipGetDevice (no usable GPU?)");
+        return nullptr;
+    }
+    Device *D;
+    {
+        std::lock_guard<std::mutex> lk(g_devs_mu);
+        auto &slot = g_devs[id];
+        if (!slot) {
+            slot.reset(new Device());
+            slot->id = id;
+        }
+        D = slot.get();
+    }
+    std::lock_guard<std::mutex> lk(D->mu);
+    *rc = init_device(*D);
+    return *rc == RSMI_OK ? D : nullptr;
+}
+
+// caller holds D.mu
+int ensure_code(Device &D, int k, int n, const Code **out) {
+    if (k < 1 || n < k || k > 256 || n > 256)
+        return fail(RSMI_ERR_INVALID, "invalid (k,n): need 1 <= k <= n <= 256");
+    const int key = k * 257 + n;
+    auto it = D.codes.find(key);
+    if (it == D.codes.end()) {
+        Code c;
+        c.k = k;
+        c.n = n;
+        if (!build_enc_matrix(k, n, c.host)) return fail(RSMI_ERR_INVALID, "matrix build failed");
+        const size_t rows = (size_t)(n - k) * k;
+        if (rows) {
+            RSMI_HIP(hipMalloc(&c.dev_rows, rows), "hipMalloc(code)");
+            RSMI_HIP(hipMemcpy(c.dev_rows, c.host.data() + (size_t)k * k, rows,
+                               hipMemcpyHostToDevice), "upload code");
+            const uint64_t p = (uint64_t)(uintptr_t)c.dev_rows;
+            RSMI_HIP(hipMemcpy(D.code_dir + key, &p, sizeof(p), hipMemcpyHostToDevice),
+                     "code_dir entry");
+        }
+        it = D.codes.emplace(key, std::move(c)).first;
+    }
+    *out = &it->second;
+    return RSMI_OK;
+}
+
+// caller holds D.mu
+int ensure_ws(Device &D, hipStream_t s, size_t bytes, uint8_t **out) {
+    Workspace &w = D.ws[s];
+    if (w.bytes < bytes) {
+        if (w.ptr) {
+            // the old buffer may still be in use by work queued on s
+            RSMI_HIP(hipStreamSynchronize(s), "hipStreamSynchronize(ws grow)");
+            RSMI_HIP(hipFree(w.ptr), "hipFree(ws)");
+            w.ptr = nullptr;
+            w.bytes = 0;
+        }
+        RSMI_HIP(hipMalloc(&w.ptr, bytes), "hipMalloc(decode workspace)");
+        w.bytes = bytes;
+    }
+    *out = w.ptr;
+    return RSMI_OK;
+}
+
+int check_uniform(int k, int n, const void *base, int64_t gs, int64_t ss, int len,
+                  int64_t ngroups) {
+    if (k < 1 || n < k || k > 256 || n > 256)
+        return fail(RSMI_ERR_INVALID, "invalid (k,n): need 1 <= k <= n <= 256");
+    if (len < 0 || ngroups < 0) return fail(RSMI_ERR_INVALID, "negative len/ngroups");
+    if (ngroups > 0 && len > 0 && !base) return fail(RSMI_ERR_INVALID, "null base");
+    if (ss % 16 || gs % 16 || ((uintptr_t)base) % 16)
+        return fail(RSMI_ERR_INVALID, "base, shard_stride and group_stride must be 16-aligned");
+    if (ss < len) return fail(RSMI_ERR_INVALID, "shard_stride < len");
+    return RSMI_OK;
+}
+
+int tile_words(int len) {
+    int w = (len + 255) / 256;
+    return w < 1 ? 1 : (w > 5 ? 5 : w);
+}
+
+UniformArgs make_args(int k, int n, uint8_t *base, int64_t gs, int64_t ss, int len,
+                      int64_t ngroups, int *W) {
+    *W = tile_words(len);
+    UniformArgs a;
+    a.base = base;
+    a.group_stride = gs;
+    a.shard_stride = ss;
+    a.len = len;
+    a.k = k;
+    a.n = n;
+    a.tiles = (len + 256 * *W - 1) / (256 * *W);
+    if (a.tiles < 1) a.tiles = 1;
+    a.ngroups = ngroups;
+    return a;
+}
+
+size_t plan_bytes(int k, int n, int64_t ngroups) {
+    const int m = n - k;
+    const PlanLayout L(k, k < m ? k : m);
+    return (size_t)L.stride * (size_t)(ngroups > 0 ? ngroups : 1);
+}
+
+}  // namespace
+
+// ---- internal entry points shared with compat.cpp -------------------------
+int encode_dev(int k, int n, uint8_t *base, int64_t gs, int64_t ss, int len, int64_t ngroups,
+               hipStream_t s) {
+    int rc = check_uniform(k, n, base, gs, ss, len, ngroups);
+    if (rc) return rc;
+    Device *D = current(&rc);
+    if (!D) return rc;
+    const Code *C;
+    {
+        std::lock_guard<std::mutex> lk(D->mu);
+        rc = ensure_code(*D, k, n, &C);
+        if (rc) return rc;
+    }
+    if (n == k || len == 0 || ngroups == 0) return RSMI_OK;
+    int W;
+    UniformArgs a = make_args(k, n, base, gs, ss, len, ngroups, &W);
+    hipError_t e = hipErrorNotSupported;
+    if (has_bitslice(k, n)) e = launch_encode_bitslice(a, s);
+    if (e == hipErrorNotSupported) e = launch_encode_generic(a, W, C->dev_rows, D->ptab, s);
+    if (e != hipSuccess) return hip_fail(e, "encode launch");
+    return RSMI_OK;
+}
+
+int decode_dev(int k, int n, uint8_t *base, int64_t gs, int64_t ss, int len, int64_t ngroups,
+               const uint8_t *present, int32_t *status, hipStream_t s) {
+    int rc = check_uniform(k, n, base, gs, ss, len, ngroups);
+    if (rc) return rc;
+    if (ngroups > 0 && !present) return fail(RSMI_ERR_INVALID, "null present");
+    Device *D = current(&rc);
+    if (!D) return rc;
+    const Code *C;
+    uint8_t *plans;
+    {
+        std::lock_guard<std::mutex> lk(D->mu);
+        rc = ensure_code(*D, k, n, &C);
+        if (rc) return rc;
+        rc = ensure_ws(*D, s, plan_bytes(k, n, ngroups), &plans);
+        if (rc) return rc;
+    }
+    if (ngroups == 0) return RSMI_OK;
+    int W;
+    UniformArgs a = make_args(k, n, base, gs, ss, len, ngroups, &W);
+    hipError_t e = launch_decode_plan(a, present, C->dev_rows, plans, status, D->gftab, s);
+    if (e != hipSuccess) return hip_fail(e, "decode plan launch");
+    if (n > k && len > 0) {
+        e = launch_decode_apply(a, W, plans, D->ptab, s);
+        if (e != hipSuccess) return hip_fail(e, "decode apply launch");
+    }
+    return RSMI_OK;
+}
+
+int prepare_code(int k, int n) {
+    int rc;
+    Device *D = current(&rc);
+    if (!D) return rc;
+    std::lock_guard<std::mutex> lk(D->mu);
+    const Code *C;
+    return ensure_code(*D, k, n, &C);
+}
+
+int reserve(int k, int n, int64_t ngroups, hipStream_t s) {
+    if (k < 1 || n < k || k > 256 || n > 256 || ngroups < 0)
+        return fail(RSMI_ERR_INVALID, "invalid reserve arguments");
+    int rc;
+    Device *D = current(&rc);
+    if (!D) return rc;
+    std::lock_guard<std::mutex> lk(D->mu);
+    const Code *C;
+    rc = ensure_code(*D, k, n, &C);
+    if (rc) return rc;
+    uint8_t *ws;
+    return ensure_ws(*D, s, plan_bytes(k, n, ngroups), &ws);
+}
+
+int encode_ragged_dev(const rsmi_group *dg, int64_t ngroups, uint8_t *base, hipStream_t s) {
+    if (ngroups < 0) return fail(RSMI_ERR_INVALID, "negative ngroups");
+    if (ngroups == 0) return RSMI_OK;
+    if (!dg || !base) return fail(RSMI_ERR_INVALID, "null descriptors/base");
+    int rc;
+    Device *D = current(&rc);
+    if (!D) return rc;
+    hipError_t e = launch_encode_ragged(dg, ngroups, base, D->code_dir, D->ptab, s);
+    if (e != hipSuccess) return hip_fail(e, "ragged encode launch");
+    return RSMI_OK;
+}
+
+int encode_ragged(const rsmi_group *g, int64_t ngroups, uint8_t *base, hipStream_t s) {
+    if (ngroups < 0) return fail(RSMI_ERR_INVALID, "negative ngroups");
+    if (ngroups == 0) return RSMI_OK;
+    if (!g || !base) return fail(RSMI_ERR_INVALID, "null descriptors/base");
+    if (((uintptr_t)base) % 16) return fail(RSMI_ERR_INVALID, "base must be 16-aligned");
+    int rc;
+    Device *D = current(&rc);
+    if (!D) return rc;
+    uint8_t *ws;
+    {
+        std::lock_guard<std::mutex> lk(D->mu);
+        bool seen[257 * 257 / 8 + 1] = {};
+        for (int64_t i = 0; i < ngroups; ++i) {
+            const rsmi_group &d = g[i];
+            if (d.k < 1 || d.n < d.k || d.n > 256 || d.reserved != 0 || d.offset % 16 ||
+                d.shard_stride % 16 || d.shard_stride < d.len)
+                return fail(RSMI_ERR_INVALID, "bad rsmi_group at index " + std::to_string(i));
+            const int key = d.k * 257 + d.n;
+            if (!(seen[key >> 3] & (1 << (key & 7)))) {
+                seen[key >> 3] |= (uint8_t)(1 << (key & 7));
+                const Code *C;
+                rc = ensure_code(*D, d.k, d.n, &C);
+                if (rc) return rc;
+            }
+        }
+        rc = ensure_ws(*D, s, sizeof(rsmi_group) * (size_t)ngroups, &ws);
+        if (rc) return rc;
+    }
+    // pageable -> device copy: returns once the source has been consumed
+    RSMI_HIP(hipMemcpyAsync(ws, g, sizeof(rsmi_group) * (size_t)ngroups, hipMemcpyHostToDevice,
+                            s), "stage ragged descriptors");
+    return encode_ragged_dev(reinterpret_cast<const rsmi_group *>(ws), ngroups, base, s);
+}
+
+// ---- synchronous host-memory path (pinned staging, internal stream) --------
+namespace {
+int host_buffers(Device &D, size_t bytes, int64_t ngroups) {
+    // caller holds D.hmu
+    if (!D.hstream) RSMI_HIP(hipStreamCreateWithFlags(&D.hstream, hipStreamNonBlocking),
+                             "hipStreamCreate");
+    if (D.pinned_bytes < bytes) {
+        if (D.pinned) (void)hipHostFree(D.pinned);
+        D.pinned = nullptr;
+        D.pinned_bytes = 0;
+        RSMI_HIP(hipHostMalloc(&D.pinned, bytes, hipHostMallocDefault), "hipHostMalloc");
+        D.pinned_bytes = bytes;
+    }
+    if (D.hdev_bytes < bytes) {
+        if (D.hdev) (void)hipFree(D.hdev);
+        D.hdev = nullptr;
+        D.hdev_bytes = 0;
+        RSMI_HIP(hipMalloc(&D.hdev, bytes), "hipMalloc(host path)");
+        D.hdev_bytes = bytes;
+    }
+    if ((int64_t)D.hstatus_cap < ngroups) {
+        if (D.hstatus_dev) (void)hipFree(D.hstatus_dev);
+        D.hstatus_dev = nullptr;
+        RSMI_HIP(hipMalloc(&D.hstatus_dev, sizeof(int32_t) * (size_t)ngroups), "hipMalloc(st)");
+        D.hstatus_cap = (size_t)ngroups;
+    }
+    return RSMI_OK;
+}
+}  // namespace
+
+// Gather host shards into a packed device layout [g][n][ss] (ss =
+// round_up(len,16)), run the device op on the internal stream, scatter back.
+// ptrs[g*n + j] is shard j of group g (may be null for an erased shard when
+// decoding).  Encode writes parity rows j >= k; decode writes recovered data
+// rows j < k whose pointer was null into out[g*k + j] (non-null required).
+int host_op_ptrs(bool decode, int k, int n, uint8_t *const *ptrs, uint8_t *const *out, int len,
+                 int64_t ngroups, const uint8_t *present, int32_t *status) {
+    if (k < 1 || n < k || k > 256 || n > 256)
+        return fail(RSMI_ERR_INVALID, "invalid (k,n): need 1 <= k <= n <= 256");
+    if (len < 0 || ngroups < 0) return fail(RSMI_ERR_INVALID, "negative len/ngroups");
+    if (ngroups == 0) return RSMI_OK;
+    int rc;
+    Device *D = current(&rc);
+    if (!D) return rc;
+    std::lock_guard<std::mutex> hl(D->hmu);
+    const int64_t ss = len > 0 ? (len + 15) / 16 * 16 : 16;
+    const int64_t dgs = ss * n;
+    const size_t data_bytes = (size_t)(dgs * ngroups);
+    const size_t pres_bytes = decode ? (size_t)(n * ngroups + 15) / 16 * 16 : 0;
+    rc = host_buffers(*D, data_bytes + pres_bytes, ngroups);
+    if (rc) return rc;
+    uint8_t *P = D->pinned;
+    for (int64_t g = 0; g < ngroups; ++g)
+        for (int j = 0; j < n; ++j) {
+            const bool have = decode ? present[g * n + j] != 0 : (j < k);
+            if (have && len) std::memcpy(P + g * dgs + j * ss, ptrs[g * n + j], len);
+        }
+    if (decode) std::memcpy(P + data_bytes, present, (size_t)n * ngroups);
+    hipStream_t s = D->hstream;
+    RSMI_HIP(hipMemcpyAsync(D->hdev, P, data_bytes + pres_bytes, hipMemcpyHostToDevice, s),
+             "H2D");
+    if (decode)
+        rc = decode_dev(k, n, D->hdev, dgs, ss, len, ngroups, D->hdev + data_bytes,
+                        D->hstatus_dev, s);
+    else
+        rc = encode_dev(k, n, D->hdev, dgs, ss, len, ngroups, s);
+    if (rc) {
+        (void)hipStreamSynchronize(s);
+        return rc;
+    }
+    RSMI_HIP(hipMemcpyAsync(P, D->hdev, data_bytes, hipMemcpyDeviceToHost, s), "D2H");
+    std::vector<int32_t> st;
+    if (decode) {
+        st.resize((size_t)ngroups);
+        RSMI_HIP(hipMemcpyAsync(st.data(), D->hstatus_dev, sizeof(int32_t) * ngroups,
+                                hipMemcpyDeviceToHost, s), "D2H status");
+    }
+    RSMI_HIP(hipStreamSynchronize(s), "hipStreamSynchronize(host path)");
+    for (int64_t g = 0; g < ngroups; ++g) {
+        if (decode) {
+            if (status) status[g] = st[(size_t)g];
+            if (st[(size_t)g] != RSMI_DEC_OK) continue;
+            for (int j = 0; j < k; ++j)
+                if (!present[g * n + j] && len)
+                    std::memcpy(out[g * k + j], P + g * dgs + j * ss, len);
+        } else {
+            for (int j = k; j < n; ++j)
+                if (len) std::memcpy(ptrs[g * n + j], P + g * dgs + j * ss, len);
+        }
+    }
+    return RSMI_OK;
+}
+
+int host_op(bool decode, int k, int n, uint8_t *base, int64_t gs, int64_t ss, int len,
+            int64_t ngroups, const uint8_t *present, int32_t *status) {
+    if (k < 1 || n < k || k > 256 || n > 256)
+        return fail(RSMI_ERR_INVALID, "invalid (k,n): need 1 <= k <= n <= 256");
+    if (ngroups < 0) return fail(RSMI_ERR_INVALID, "negative ngroups");
+    std::vector<uint8_t *> p((size_t)(ngroups * n)), o(decode ? (size_t)(ngroups * k) : 0);
+    for (int64_t g = 0; g < ngroups; ++g) {
+        for (int j = 0; j < n; ++j) p[(size_t)(g * n + j)] = base + g * gs + j * ss;
+        if (decode)
+            for (int j = 0; j < k; ++j) o[(size_t)(g * k + j)] = base + g * gs + j * ss;
+    }
+    return host_op_ptrs(decode, k, n, p.data(), o.data(), len, ngroups, present, status);
+}
+
+const char *last_error() { return g_err.c_str(); }
+void set_error(const std::string &m) { g_err = m; }
+
+}  // namespace rsmi
+
+// ===== extern "C" surface (include/rsmi.h) ===================================
+extern "C" {
+
+int rsmi_version(void) { return 0x000100; }
+
+int rsmi_init(void) {
+    int rc;
+    return rsmi::current(&rc) ? RSMI_OK : rc;
+}
+
+const char *rsmi_last_error(void) { return rsmi::last_error(); }
+
+int rsmi_get_matrix(int k, int n, uint8_t *out) {
+    std::vector<uint8_t> m;
+    if (!out || !rsmi::build_enc_matrix(k, n, m)) {
+        rsmi::set_error("invalid (k,n) or null out");
+        return RSMI_ERR_INVALID;
+    }
+    std::memcpy(out, m.data(), m.size());
+    return RSMI_OK;
+}
+
+int rsmi_decode_matrix(int k, int n, const uint8_t *present, uint8_t *sel, uint8_t *miss,
+                       uint8_t *coef) {
+    if (k < 1 || n < k || k > 256 || n > 256 || !present || !sel || !miss || !coef) {
+        rsmi::set_error("invalid decode_matrix arguments");
+        return RSMI_ERR_INVALID;
+    }
+    std::vector<uint8_t> m;
+    if (!rsmi::build_enc_matrix(k, n, m)) {
+        rsmi::set_error("matrix build failed");
+        return RSMI_ERR_INVALID;
+    }
+    const int e = rsmi::decode_coeffs(k, n, m.data(), present, sel, miss, coef);
+    if (e == -2) {
+        rsmi::set_error("singular decode matrix");
+        return RSMI_ERR_INVALID;
+    }
+    return e;
+}
+
+int rsmi_prepare_code(int k, int n) { return rsmi::prepare_code(k, n); }
+
+int rsmi_reserve(int k, int n, int64_t ngroups, void *stream) {
+    return rsmi::reserve(k, n, ngroups, (hipStream_t)stream);
+}
+
+int rsmi_encode_dev(int k, int n, uint8_t *base, int64_t gs, int64_t ss, int len,
+                    int64_t ngroups, void *stream) {
+    return rsmi::encode_dev(k, n, base, gs, ss, len, ngroups, (hipStream_t)stream);
+}
+
+int rsmi_decode_dev(int k, int n, uint8_t *base, int64_t gs, int64_t ss, int len,
+                    int64_t ngroups, const uint8_t *present, int32_t *status, void *stream) {
+    return rsmi::decode_dev(k, n, base, gs, ss, len, ngroups, present, status,
+                            (hipStream_t)stream);
+}
+
+int rsmi_encode_ragged(const rsmi_group *groups, int64_t ngroups, uint8_t *base, void *stream) {
+    return rsmi::encode_ragged(groups, ngroups, base, (hipStream_t)stream);
+}
+
+int rsmi_encode_ragged_dev(const rsmi_group *groups, int64_t ngroups, uint8_t *base,
+                           void *stream) {
+    return rsmi::encode_ragged_dev(groups, ngroups, base, (hipStream_t)stream);
+}
+
+int rsmi_encode_host(int k, int n, uint8_t *base, int64_t gs, int64_t ss, int len,
+                     int64_t ngroups) {
+    return rsmi::host_op(false, k, n, base, gs, ss, len, ngroups, nullptr, nullptr);
+}
+
+int rsmi_decode_host(int k, int n, uint8_t *base, int64_t gs, int64_t ss, int len,
+                     int64_t ngroups, const uint8_t *present, int32_t *status) {
+    if (ngroups > 0 && !present) {
+        rsmi::set_error("null present");
+        return RSMI_ERR_INVALID;
+    }
+    return rsmi::host_op(true, k, n, base, gs, ss, len, ngroups, present, status);
+}
+
+int rsmi_fill_data(int k, int len, uint8_t *base, int64_t gs, int64_t ss, int64_t g0,
+                   int64_t ngroups, uint64_t seed, void *stream) {
+    if (k < 1 || len < 0 || ngroups < 0 || ss % 4 || gs % 4 || ss < len || ((uintptr_t)base) % 4) {
+        rsmi::set_error("invalid fill arguments");
+        return RSMI_ERR_INVALID;
+    }
+    if (ngroups == 0 || len == 0) return RSMI_OK;
+    hipError_t e = rsmi::launch_fill_data(k, len, base, gs, ss, g0, ngroups, seed,
+                                          (hipStream_t)stream);
+    if (e != hipSuccess) {
+        rsmi::set_error(std::string("fill launch: ") + hipGetErrorString(e));
+        return RSMI_ERR_HIP;
+    }
+    return RSMI_OK;
+}
+
+int rsmi_fill_ragged(const rsmi_group *groups, int64_t ngroups, uint8_t *base, int64_t g0,
+                     uint64_t seed, void *stream) {
+    if (ngroups < 0 || (ngroups > 0 && (!groups || !base))) {
+        rsmi::set_error("invalid fill_ragged arguments");
+        return RSMI_ERR_INVALID;
+    }
+    if (ngroups == 0) return RSMI_OK;
+    hipError_t e = rsmi::launch_fill_ragged(groups, ngroups, base, g0, seed, (hipStream_t)stream);
+    if (e != hipSuccess) {
+        rsmi::set_error(std::string("fill_ragged launch: ") + hipGetErrorString(e));
+        return RSMI_ERR_HIP;
+    }
+    return RSMI_OK;
+}
+
+}  // extern "C"

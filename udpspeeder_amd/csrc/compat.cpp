@@ -1,0 +1,193 @@
+// compat.cpp -- the link-compatible drop-in for lib/rs.h + lib/fec.h
+// (declarations and per-symbol citations in include/rs_compat.h).
+//
+// These functions keep the reference's C++ linkage, parameter types, return
+// codes and in-place pointer semantics; the GF byte arithmetic of every call
+// runs on the GPU through the host-memory path of the batched engine
+// (pinned staging -> HIP kernels -> copy back).  Per-call cost is therefore
+// PCIe-latency-bound; fec_manager-scale throughput comes from the batched
+// rsmi_* API.  There is no CPU fallback.
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/rs_compat.h"
+#include "../../include/rsmi.h"
+
+namespace rsmi {
+int host_op_ptrs(bool decode, int k, int n, uint8_t *const *ptrs, uint8_t *const *out, int len,
+                 int64_t ngroups, const uint8_t *present, int32_t *status);
+}
+
+namespace {
+
+constexpr uint64_t kMagic = 0xFECC0DEC5EEDull;  // role of FEC_MAGIC (fec.cpp:640)
+
+struct CodeHandle {
+    uint64_t magic;
+    int k, n;
+};
+
+bool valid(const CodeHandle *c) { return c && c->magic == (kMagic ^ (uint64_t)(c->k * 257 + c->n)); }
+
+void report(const char *what) {
+    std::fprintf(stderr, "rsmi: %s failed: %s\n", what, rsmi_last_error());
+}
+
+// fec_decode's shuffle (fec.cpp:755-788): move each received data packet
+// (index < k) into its own slot, swapping pointers and indices; 1 on conflict.
+int shuffle_slots(void **pkt, int *index, int k) {
+    for (int i = 0; i < k;) {
+        if (index[i] >= k || index[i] == i) {
+            ++i;
+            continue;
+        }
+        const int c = index[i];
+        if (index[c] == c) return 1;
+        std::swap(index[i], index[c]);
+        std::swap(pkt[i], pkt[c]);
+    }
+    return 0;
+}
+
+// Decode k packets pkt[0..k-1] carrying shard indices index[0..k-1] (the
+// fec_decode contract).  Rebuilt data rows are written over the parity
+// buffers sitting in slots row < k after the shuffle (fec.cpp:872-877).
+int decode_packets(const CodeHandle *c, void **pkt, int *index, int sz) {
+    const int k = c->k, n = c->n;
+    for (int i = 0; i < k; ++i)
+        if (index[i] < 0 || index[i] >= n) {
+            std::fprintf(stderr, "decode: invalid index %d (max %d)\n", index[i], n - 1);
+            return 1;
+        }
+    if (shuffle_slots(pkt, index, k)) return 1;
+    std::vector<uint8_t> present((size_t)n, 0);
+    std::vector<uint8_t *> shards((size_t)n, nullptr);
+    for (int i = 0; i < k; ++i) {
+        if (present[(size_t)index[i]]) return 1;  // duplicate index: singular (fec.cpp:497)
+        present[(size_t)index[i]] = 1;
+        shards[(size_t)index[i]] = static_cast<uint8_t *>(pkt[i]);
+    }
+    // recovered data row j lands in pkt[j] (a parity buffer after the shuffle)
+    std::vector<uint8_t *> out((size_t)k, nullptr);
+    bool any = false;
+    for (int j = 0; j < k; ++j)
+        if (!present[(size_t)j]) {
+            out[(size_t)j] = static_cast<uint8_t *>(pkt[j]);
+            any = true;
+        }
+    if (!any || sz <= 0) return 0;
+    int32_t st = 0;
+    // Rows are computed into staging before any buffer is overwritten, so
+    // writing over the parity buffers afterwards matches fec.cpp:861-877.
+    if (rsmi::host_op_ptrs(true, k, n, shards.data(), out.data(), sz, 1, present.data(), &st)) {
+        report("fec_decode");
+        return 1;
+    }
+    return st == 0 ? 0 : 1;
+}
+
+std::mutex g_table_mu;
+CodeHandle *g_table[257][257];  // role of rs.cpp's lazy table (rs.cpp:42-55), locked here
+
+}  // namespace
+
+// ---- lib/fec.h --------------------------------------------------------------
+void *fec_new(int k, int n) {
+    if (k > 256 || n > 256 || k > n || k < 1) {
+        std::fprintf(stderr, "Invalid parameters k %d n %d GF_SIZE %d\n", k, n, 255);
+        return nullptr;
+    }
+    if (rsmi_prepare_code(k, n) != RSMI_OK) report("fec_new");  // GPU state is optional here
+    CodeHandle *c = new CodeHandle;
+    c->k = k;
+    c->n = n;
+    c->magic = kMagic ^ (uint64_t)(k * 257 + n);
+    return c;
+}
+
+void fec_free(void *p) {
+    CodeHandle *c = static_cast<CodeHandle *>(p);
+    if (!valid(c)) {
+        std::fprintf(stderr, "bad parameters to fec_free\n");
+        return;
+    }
+    c->magic = 0;
+    delete c;
+}
+
+int get_k(void *code) { return static_cast<CodeHandle *>(code)->k; }
+int get_n(void *code) { return static_cast<CodeHandle *>(code)->n; }
+
+void fec_encode(void *code, void *src[], void *dst, int index, int sz) {
+    const CodeHandle *c = static_cast<CodeHandle *>(code);
+    const int k = c->k, n = c->n;
+    if (index < k) {
+        std::memcpy(dst, src[index], sz > 0 ? (size_t)sz : 0);
+        return;
+    }
+    if (index >= n) {
+        std::fprintf(stderr, "Invalid index %d (max %d)\n", index, n - 1);
+        return;
+    }
+    if (sz <= 0) return;
+    // compute every parity row into scratch, keep row `index`
+    std::vector<uint8_t> scratch((size_t)(n - k) * sz);
+    std::vector<uint8_t *> ptrs((size_t)n);
+    for (int j = 0; j < k; ++j) ptrs[(size_t)j] = static_cast<uint8_t *>(src[j]);
+    for (int j = k; j < n; ++j) ptrs[(size_t)j] = scratch.data() + (size_t)(j - k) * sz;
+    if (rsmi::host_op_ptrs(false, k, n, ptrs.data(), nullptr, sz, 1, nullptr, nullptr)) {
+        report("fec_encode");
+        return;
+    }
+    std::memcpy(dst, ptrs[(size_t)index], (size_t)sz);
+}
+
+int fec_decode(void *code, void *pkt[], int index[], int sz) {
+    return decode_packets(static_cast<CodeHandle *>(code), pkt, index, sz);
+}
+
+// ---- lib/rs.h -----------------------------------------------------------------
+void rs_encode(void *code, char *data[], int size) {
+    const CodeHandle *c = static_cast<CodeHandle *>(code);
+    const int k = c->k, n = c->n;
+    if (n == k || size <= 0) return;
+    if (rsmi::host_op_ptrs(false, k, n, reinterpret_cast<uint8_t *const *>(data), nullptr, size,
+                           1, nullptr, nullptr))
+        report("rs_encode");
+}
+
+int rs_decode(void *code, char *data[], int size) {
+    const CodeHandle *c = static_cast<CodeHandle *>(code);
+    const int k = c->k, n = c->n;
+    // rs.cpp:24-39: pack the non-null pointers to the front, remember indices
+    std::vector<int> index((size_t)n);
+    int count = 0;
+    for (int i = 0; i < n; ++i)
+        if (data[i]) index[(size_t)count++] = i;
+    if (count < k) return -1;
+    for (int i = 0; i < n; ++i) data[i] = i < count ? data[index[(size_t)i]] : nullptr;
+    return decode_packets(c, reinterpret_cast<void **>(data), index.data(), size);
+}
+
+void *get_code(int k, int n) {
+    if (k < 0 || n < 0 || k > 256 || n > 256) return nullptr;
+    std::lock_guard<std::mutex> lk(g_table_mu);
+    if (!g_table[k][n]) g_table[k][n] = static_cast<CodeHandle *>(fec_new(k, n));
+    return g_table[k][n];
+}
+
+void rs_encode2(int k, int n, char *data[], int size) {
+    void *code = get_code(k, n);
+    if (!code) return;  // the reference would dereference NULL here
+    rs_encode(code, data, size);
+}
+
+int rs_decode2(int k, int n, char *data[], int size) {
+    void *code = get_code(k, n);
+    if (!code) return 1;
+    return rs_decode(code, data, size);
+}

@@ -1,0 +1,59 @@
+// rsmi_internal.hpp -- shared declarations between the host runtime (api.cpp)
+// and the HIP kernels (kernels.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "../../include/rsmi.h"
+
+namespace rsmi {
+
+// Decode plan record (one per group, written by k_decode_plan, read by the
+// decode apply kernel).  Layout for a batch with parameters (k, emax):
+//   +0  int32 status (RSMI_DEC_*)       +4 uint8 e (missing data rows)
+//   +8  uint8 sel[k]   survivors used (ascending slot indices)
+//   +8+k uint8 miss[emax]  missing data rows
+//   +coef_off uint8 coef[emax][k]  (coef_off 16-aligned)
+struct PlanLayout {
+    int k, emax, coef_off, stride;
+    __host__ __device__ PlanLayout(int k_, int emax_) : k(k_), emax(emax_) {
+        coef_off = (8 + k + emax + 15) & ~15;
+        stride = (coef_off + emax * k + 15) & ~15;
+    }
+};
+
+// Launch descriptors (plain structs passed by value to kernels).
+struct UniformArgs {
+    uint8_t *base;
+    int64_t group_stride, shard_stride;
+    int len, k, n, tiles;   // tiles per group (of 256*W bytes)
+    int64_t ngroups;
+};
+
+// Host-side launchers implemented in kernels.hip; return hipError_t.
+hipError_t launch_encode_generic(const UniformArgs &a, int W, const uint8_t *parity_rows,
+                                 const uint32_t *ptab, hipStream_t s);
+hipError_t launch_decode_plan(const UniformArgs &a, const uint8_t *present,
+                              const uint8_t *parity_rows, uint8_t *plans, int32_t *status,
+                              const uint8_t *gftab, hipStream_t s);
+hipError_t launch_decode_apply(const UniformArgs &a, int W, const uint8_t *plans,
+                               const uint32_t *ptab, hipStream_t s);
+hipError_t launch_encode_ragged(const rsmi_group *groups, int64_t ngroups, uint8_t *base,
+                                const uint64_t *code_dir, const uint32_t *ptab, hipStream_t s);
+hipError_t launch_fill_data(int k, int len, uint8_t *base, int64_t group_stride,
+                            int64_t shard_stride, int64_t g0, int64_t ngroups, uint64_t seed,
+                            hipStream_t s);
+
+hipError_t launch_fill_ragged(const rsmi_group *groups, int64_t ngroups, uint8_t *base,
+                              int64_t g0, uint64_t seed, hipStream_t s);
+
+// Bit-sliced encode kernels specialised at build time for hot (k,n) codes
+// (gen_bitslice.py -> gen/bitslice_codes.inc).  Returns hipErrorNotSupported
+// when (k,n) has no specialised kernel.
+hipError_t launch_encode_bitslice(const UniformArgs &a, hipStream_t s);
+bool has_bitslice(int k, int n);
+
+constexpr int kPtabDwords = 8;  // per coefficient: T0lo T0hi T1lo T1hi | T2 pad pad pad
+
+}  // namespace rsmi

@@ -1,0 +1,302 @@
+"""Python surface of the MI355X Reed-Solomon engine.
+
+Two layers, mirroring the reference:
+
+* Per-group, host-buffer functions with the reference's names and semantics
+  (``rs_encode2`` / ``rs_decode2`` of lib/rs.h:41,43, ``fec_new`` ... of
+  lib/fec.h).  They call the reference-mangled symbols exported by
+  librsmi.so (the same ones fec_manager.cpp links against), so these wrappers
+  exercise exactly the drop-in C++ ABI.  A "char *data[]" is a Python list of
+  writable buffers (bytearray / numpy uint8), ``None`` for a null pointer;
+  ``rs_decode2`` permutes that list in place exactly as the C call permutes
+  the pointer array (lib/rs.h:25-38).
+
+* Batched, device-resident functions (``encode``, ``decode``,
+  ``encode_ragged``) over torch CUDA tensors, launched on the current torch
+  stream.  These are the production path: one launch covers many FEC groups.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Iterable, List, Optional, Sequence
+
+import numpy as np
+
+from ._lib import RSMI_OK, RsmiError, check, lib, rsmi_group
+
+
+# --------------------------------------------------------------------------
+# helpers
+def _addr(buf) -> int:
+    if isinstance(buf, np.ndarray):
+        if buf.dtype != np.uint8 or not buf.flags.c_contiguous or not buf.flags.writeable:
+            raise TypeError("numpy shard buffers must be writable contiguous uint8")
+        return buf.ctypes.data
+    if isinstance(buf, bytearray):
+        return C.addressof((C.c_char * max(len(buf), 1)).from_buffer(buf)) if len(buf) else 0
+    raise TypeError(f"shard buffer must be bytearray or numpy uint8, got {type(buf).__name__}")
+
+
+def _ptr_array(data: Sequence) -> C.Array:
+    arr = (C.c_void_p * len(data))()
+    for i, b in enumerate(data):
+        arr[i] = _addr(b) if b is not None else None
+    return arr
+
+
+def _check_sizes(data, n, size):
+    if len(data) < n:
+        raise ValueError(f"data has {len(data)} entries, need n={n}")
+    for b in data[:n]:
+        if b is not None and len(b) < size:
+            raise ValueError("a shard buffer is shorter than size")
+
+
+# --------------------------------------------------------------------------
+# reference-interface mirror (lib/rs.h, lib/fec.h)
+def rs_encode2(k: int, n: int, data: List, size: int) -> None:
+    """lib/rs.h:41.  data[0..k-1] hold the data shards, data[k..n-1] are
+    caller-allocated parity buffers that get overwritten."""
+    _check_sizes(data, n, size)
+    if any(b is None for b in data[:n]):
+        raise ValueError("rs_encode2 needs all n buffers")
+    lib().compat["rs_encode2"](k, n, _ptr_array(data[:n]), size)
+
+
+def rs_decode2(k: int, n: int, data: List, size: int) -> int:
+    """lib/rs.h:43.  data[i] is None for a missing shard.  Returns 0, -1 (fewer
+    than k present) or 1; on return data[0..k-1] are the recovered data shards
+    (some are former parity buffers, now overwritten), the list permuted in
+    place like the C pointer array."""
+    _check_sizes(data, n, size)
+    arr = _ptr_array(data[:n])
+    by_addr = {}
+    for b in data[:n]:
+        if b is not None:
+            by_addr[_addr(b)] = b
+    rc = lib().compat["rs_decode2"](k, n, arr, size)
+    for i in range(n):
+        data[i] = by_addr[arr[i]] if arr[i] else None
+    return rc
+
+
+def fec_new(k: int, n: int) -> Optional[int]:
+    """lib/fec.h:47; returns an opaque code handle (None for invalid k/n)."""
+    return lib().compat["fec_new"](k, n)
+
+
+def fec_free(code: int) -> None:
+    lib().compat["fec_free"](code)
+
+
+def get_k(code: int) -> int:
+    return lib().compat["get_k"](code)
+
+
+def get_n(code: int) -> int:
+    return lib().compat["get_n"](code)
+
+
+def get_code(k: int, n: int) -> Optional[int]:
+    return lib().compat["get_code"](k, n)
+
+
+def rs_encode(code: int, data: List, size: int) -> None:
+    n = get_n(code)
+    _check_sizes(data, n, size)
+    lib().compat["rs_encode"](code, _ptr_array(data[:n]), size)
+
+
+def rs_decode(code: int, data: List, size: int) -> int:
+    n = get_n(code)
+    _check_sizes(data, n, size)
+    arr = _ptr_array(data[:n])
+    by_addr = {_addr(b): b for b in data[:n] if b is not None}
+    rc = lib().compat["rs_decode"](code, arr, size)
+    for i in range(n):
+        data[i] = by_addr[arr[i]] if arr[i] else None
+    return rc
+
+
+def fec_encode(code: int, src: List, dst, index: int, sz: int) -> None:
+    """lib/fec.h:50: dst = shard `index` of the code word of src[0..k-1]."""
+    k = get_k(code)
+    lib().compat["fec_encode"](code, _ptr_array(src[:k]), _addr(dst), index, sz)
+
+
+def fec_decode(code: int, pkt: List, index: List[int], sz: int) -> int:
+    """lib/fec.h:51: pkt[0..k-1] with shard indices index[0..k-1]; both lists
+    are permuted in place like the C arrays."""
+    k = get_k(code)
+    arr = _ptr_array(pkt[:k])
+    idx = (C.c_int * k)(*index[:k])
+    by_addr = {_addr(b): b for b in pkt[:k] if b is not None}
+    rc = lib().compat["fec_decode"](code, arr, idx, sz)
+    for i in range(k):
+        pkt[i] = by_addr.get(arr[i]) if arr[i] else None
+        index[i] = idx[i]
+    return rc
+
+
+# --------------------------------------------------------------------------
+# host utilities
+def enc_matrix(k: int, n: int) -> np.ndarray:
+    """fec_new(k,n)'s n x k systematic matrix (lib/fec.cpp:665-720)."""
+    out = np.zeros((n, k), np.uint8)
+    check(lib().rsmi_get_matrix(k, n, out.ctypes.data), "rsmi_get_matrix")
+    return out
+
+
+def decode_matrix(k: int, n: int, present: Sequence[int]):
+    """(e, sel[k], miss[e], coef[e, k]) for one group; e = -1 if too few."""
+    p = np.ascontiguousarray(np.asarray(present, dtype=np.uint8))
+    if p.shape != (n,):
+        raise ValueError("present must have n entries")
+    sel = np.zeros(k, np.uint8); miss = np.zeros(k, np.uint8); coef = np.zeros(k * k, np.uint8)
+    e = lib().rsmi_decode_matrix(k, n, p.ctypes.data, sel.ctypes.data, miss.ctypes.data,
+                                 coef.ctypes.data)
+    if e < -1:
+        check(e, "rsmi_decode_matrix")
+    if e < 0:
+        return -1, sel, miss[:0], coef[:0].reshape(0, k)
+    return e, sel, miss[:e], coef[:e * k].reshape(e, k)
+
+
+def version() -> int:
+    return lib().rsmi_version()
+
+
+# --------------------------------------------------------------------------
+# batched device API (torch CUDA tensors)
+def _stream_handle(stream) -> Optional[int]:
+    import torch
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return s.cuda_stream
+
+
+def _check_dev(t, name, dtype=None):
+    import torch
+    if not isinstance(t, torch.Tensor) or not t.is_cuda:
+        raise TypeError(f"{name} must be a CUDA tensor")
+    if dtype is not None and t.dtype != dtype:
+        raise TypeError(f"{name} must be {dtype}")
+
+
+def _shard_geometry(shards, n):
+    import torch
+    _check_dev(shards, "shards", torch.uint8)
+    if shards.dim() != 3 or shards.shape[1] < n:
+        raise ValueError("shards must be [groups, >=n, stride]")
+    if shards.stride(2) != 1:
+        raise ValueError("shards rows must be contiguous")
+    return shards.shape[0], shards.stride(0), shards.stride(1), shards.shape[2]
+
+
+def encode(shards, k: int, n: int, length: Optional[int] = None, stream=None) -> None:
+    """rs_encode2 on every group of ``shards`` ([G, n, S] uint8 CUDA, S % 16 == 0):
+    parity rows k..n-1 are overwritten from data rows 0..k-1."""
+    G, gs, ss, S = _shard_geometry(shards, n)
+    L = S if length is None else int(length)
+    check(lib().rsmi_encode_dev(k, n, shards.data_ptr(), gs, ss, L, G, _stream_handle(stream)),
+          "rsmi_encode_dev")
+
+
+def decode(shards, present, k: int, n: int, length: Optional[int] = None, status=None,
+           stream=None):
+    """rs_decode2 on every group: ``present`` [G, n] uint8 CUDA (nonzero =
+    received).  Missing data rows are rebuilt in their own slot.  Returns the
+    int32 [G] status tensor (0 ok, -1 too few shards, 1 singular)."""
+    import torch
+    G, gs, ss, S = _shard_geometry(shards, n)
+    _check_dev(present, "present", torch.uint8)
+    if tuple(present.shape) != (G, n) or not present.is_contiguous():
+        raise ValueError("present must be a contiguous [G, n] uint8 tensor")
+    if status is None:
+        status = torch.empty(G, dtype=torch.int32, device=shards.device)
+    L = S if length is None else int(length)
+    check(lib().rsmi_decode_dev(k, n, shards.data_ptr(), gs, ss, L, G, present.data_ptr(),
+                                status.data_ptr(), _stream_handle(stream)), "rsmi_decode_dev")
+    return status
+
+
+def make_groups(ks: Iterable[int], ns: Iterable[int], lens: Iterable[int],
+                align: int = 16):
+    """Pack a ragged batch: returns (descriptor array, total bytes).  Each
+    group's shards are contiguous with stride round_up(len, align)."""
+    ks = np.asarray(list(ks), np.int64); ns = np.asarray(list(ns), np.int64)
+    ls = np.asarray(list(lens), np.int64)
+    ss = np.maximum((ls + align - 1) // align * align, align)
+    sizes = ss * ns
+    offs = np.concatenate([[0], np.cumsum(sizes)[:-1]]) if len(sizes) else np.zeros(0, np.int64)
+    arr = (rsmi_group * len(ks))()
+    for i in range(len(ks)):
+        arr[i] = rsmi_group(int(offs[i]), int(ss[i]), int(ls[i]), int(ks[i]), int(ns[i]), 0)
+    return arr, int(sizes.sum()) if len(sizes) else 0
+
+
+def encode_ragged(base, groups, stream=None) -> None:
+    """Encode a ragged batch in one launch.  ``base`` is a 1-D uint8 CUDA tensor,
+    ``groups`` a ctypes rsmi_group array from make_groups (host)."""
+    import torch
+    _check_dev(base, "base", torch.uint8)
+    check(lib().rsmi_encode_ragged(C.cast(groups, C.c_void_p), len(groups), base.data_ptr(),
+                                   _stream_handle(stream)), "rsmi_encode_ragged")
+
+
+def encode_ragged_dev(base, dev_groups, ngroups: int, stream=None) -> None:
+    """Graph-capturable ragged encode with a device descriptor tensor (uint8,
+    24 bytes per group); codes must be resident (prepare_code)."""
+    check(lib().rsmi_encode_ragged_dev(dev_groups.data_ptr(), ngroups, base.data_ptr(),
+                                       _stream_handle(stream)), "rsmi_encode_ragged_dev")
+
+
+def prepare_code(k: int, n: int) -> None:
+    check(lib().rsmi_prepare_code(k, n), "rsmi_prepare_code")
+
+
+def reserve(k: int, n: int, ngroups: int, stream=None) -> None:
+    check(lib().rsmi_reserve(k, n, ngroups, _stream_handle(stream)), "rsmi_reserve")
+
+
+def fill_data(shards, k: int, length: int, seed: int, g0: int = 0, stream=None) -> None:
+    """Synthetic SplitMix64 data into rows 0..k-1 of [G, n, S] ``shards``."""
+    G, gs, ss, S = _shard_geometry(shards, k)
+    check(lib().rsmi_fill_data(k, length, shards.data_ptr(), gs, ss, g0, G,
+                               C.c_uint64(seed & (2**64 - 1)), _stream_handle(stream)),
+          "rsmi_fill_data")
+
+
+def fill_data_flat(base, k: int, length: int, offset: int, group_stride: int, shard_stride: int,
+                   g0: int, ngroups: int, seed: int, stream=None) -> None:
+    check(lib().rsmi_fill_data(k, length, base.data_ptr() + offset, group_stride, shard_stride,
+                               g0, ngroups, C.c_uint64(seed & (2**64 - 1)),
+                               _stream_handle(stream)), "rsmi_fill_data")
+
+
+def groups_to_device(groups, device="cuda"):
+    """Copy a ctypes rsmi_group array to a device uint8 tensor (24 B/group)."""
+    import torch
+    raw = np.frombuffer(bytes(groups), np.uint8).copy()
+    return torch.from_numpy(raw).to(device)
+
+
+def fill_ragged(base, dev_groups, ngroups: int, seed: int, g0: int = 0, stream=None) -> None:
+    check(lib().rsmi_fill_ragged(dev_groups.data_ptr(), ngroups, base.data_ptr(), g0,
+                                 C.c_uint64(seed & (2**64 - 1)), _stream_handle(stream)),
+          "rsmi_fill_ragged")
+
+
+# host-memory batched helpers (pinned staging inside the library)
+def encode_host(buf: np.ndarray, k: int, n: int, length: int, group_stride: int,
+                shard_stride: int, ngroups: int) -> None:
+    check(lib().rsmi_encode_host(k, n, buf.ctypes.data, group_stride, shard_stride, length,
+                                 ngroups), "rsmi_encode_host")
+
+
+def decode_host(buf: np.ndarray, present: np.ndarray, k: int, n: int, length: int,
+                group_stride: int, shard_stride: int, ngroups: int) -> np.ndarray:
+    pres = np.ascontiguousarray(present, dtype=np.uint8)
+    st = np.zeros(ngroups, np.int32)
+    check(lib().rsmi_decode_host(k, n, buf.ctypes.data, group_stride, shard_stride, length,
+                                 ngroups, pres.ctypes.data, st.ctypes.data), "rsmi_decode_host")
+    return st

@@ -1,0 +1,58 @@
+"""Synthetic workload definitions for the bench and tests.
+
+All draws are counter-based SplitMix64: word w of stream (seed, g) is
+``mix((seed ^ g) + (w + 1) * 0x9E3779B97F4A7C15)``.
+
+* data bytes (C1-C4): generated on the GPU by ``rs.fill_data``;
+* erasure patterns (C2): e distinct indices per group from a partial
+  Fisher-Yates over range(limit) driven by the group's stream;
+* ragged mix (C3): k ~ U{1..kmax}, m from the ``-f`` table, len ~ U[lmin, lmax].
+"""
+from __future__ import annotations
+
+import numpy as np
+
+GAMMA = np.uint64(0x9E3779B97F4A7C15)
+DATA_SEED = 0x5EEDC0DE
+ERASE_SEED = 0xE7A5E5EED
+RAGGED_SEED = 0x7A66ED
+C3_FEC = "1:3,2:4,10:6,20:10"
+
+
+def _mix(z):
+    z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+    z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return z ^ (z >> np.uint64(31))
+
+
+def stream_words(seed: int, g0: int, ng: int, nwords: int) -> np.ndarray:
+    with np.errstate(over="ignore"):
+        s0 = np.uint64(seed) ^ np.arange(g0, g0 + ng, dtype=np.uint64)
+        w = np.arange(1, nwords + 1, dtype=np.uint64) * GAMMA
+        return _mix(s0[:, None] + w[None, :])
+
+
+def erasure_present(seed: int, g0: int, ng: int, n: int, e: int, limit: int = 0) -> np.ndarray:
+    """[ng, n] uint8 present flags with e erasures per group."""
+    lim = limit or n
+    r = stream_words(seed, g0, ng, e)
+    perm = np.tile(np.arange(lim, dtype=np.int64), (ng, 1))
+    rows = np.arange(ng)
+    for i in range(e):
+        pick = i + (r[:, i] % np.uint64(lim - i)).astype(np.int64)
+        a = perm[rows, i].copy()
+        perm[rows, i] = perm[rows, pick]
+        perm[rows, pick] = a
+    pres = np.ones((ng, n), np.uint8)
+    pres[rows[:, None], perm[:, :e]] = 0
+    return pres
+
+
+def ragged_mix(seed: int, g0: int, ng: int, table_y, kmax: int = 20, lmin: int = 64,
+               lmax: int = 1250):
+    """(k, m, len) int64 arrays for the C3 ragged batch."""
+    ty = np.asarray(table_y, np.int64)
+    r = stream_words(seed, g0, ng, 2)
+    k = 1 + (r[:, 0] % np.uint64(kmax)).astype(np.int64)
+    ln = lmin + (r[:, 1] % np.uint64(lmax - lmin + 1)).astype(np.int64)
+    return k, ty[k - 1], ln
