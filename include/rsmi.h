@@ -55,6 +55,12 @@ int rsmi_init(void);
 /* Text of the last error on this thread ("" if none). */
 const char *rsmi_last_error(void);
 
+/* Engine options (process-wide).  RSMI_OPT_BITSLICE: 1 (default) uses the
+ * build-time specialised bit-sliced encoders where available, 0 forces the
+ * generic table kernel (for A/B tests).  Returns the previous value. */
+#define RSMI_OPT_BITSLICE 1
+int rsmi_set_option(int option, int value);
+
 /* Host copy of fec_new(k,n)'s n x k systematic encoding matrix (row-major),
  * lib/fec.cpp:665-720.  Valid: 1 <= k <= n <= 256. */
 int rsmi_get_matrix(int k, int n, uint8_t *out_nk);

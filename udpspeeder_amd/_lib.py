@@ -17,6 +17,7 @@ RSMI_OK = 0
 RSMI_ERR_INVALID = -2
 RSMI_ERR_HIP = -3
 RSMI_ERR_NOMEM = -4
+RSMI_OPT_BITSLICE = 1
 RSMI_DEC_OK = 0
 RSMI_DEC_TOO_FEW = -1
 RSMI_DEC_SINGULAR = 1
@@ -55,6 +56,7 @@ def _bind(lib: C.CDLL) -> C.CDLL:
     vp, i64, i32 = C.c_void_p, C.c_int64, C.c_int
     sig = {
         "rsmi_version": ([], i32),
+        "rsmi_set_option": ([i32, i32], i32),
         "rsmi_init": ([], i32),
         "rsmi_last_error": ([], C.c_char_p),
         "rsmi_get_matrix": ([i32, i32, vp], i32),

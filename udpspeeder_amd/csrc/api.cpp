@@ -4,6 +4,7 @@
 // drop-in shim (compat.cpp).
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdio>
 #include <cstring>
 #include <map>
@@ -19,6 +20,7 @@ namespace rsmi {
 namespace {
 
 thread_local std::string g_err;
+std::atomic<int> g_opt_bitslice{1};
 
 int fail(int code, const std::string &msg) {
     g_err = msg;
@@ -211,7 +213,7 @@ int encode_dev(int k, int n, uint8_t *base, int64_t gs, int64_t ss, int len, int
     int W;
     UniformArgs a = make_args(k, n, base, gs, ss, len, ngroups, &W);
     hipError_t e = hipErrorNotSupported;
-    if (has_bitslice(k, n)) e = launch_encode_bitslice(a, s);
+    if (g_opt_bitslice.load() && has_bitslice(k, n)) e = launch_encode_bitslice(a, s);
     if (e == hipErrorNotSupported) e = launch_encode_generic(a, W, C->dev_rows, D->ptab, s);
     if (e != hipSuccess) return hip_fail(e, "encode launch");
     return RSMI_OK;
@@ -291,7 +293,7 @@ int encode_ragged(const rsmi_group *g, int64_t ngroups, uint8_t *base, hipStream
     uint8_t *ws;
     {
         std::lock_guard<std::mutex> lk(D->mu);
-        bool seen[257 * 257 / 8 + 1] = {};
+        uint8_t seen[257 * 257 / 8 + 1] = {};
         for (int64_t i = 0; i < ngroups; ++i) {
             const rsmi_group &d = g[i];
             if (d.k < 1 || d.n < d.k || d.n > 256 || d.reserved != 0 || d.offset % 16 ||
@@ -422,6 +424,7 @@ int host_op(bool decode, int k, int n, uint8_t *base, int64_t gs, int64_t ss, in
 }
 
 const char *last_error() { return g_err.c_str(); }
+std::atomic<int> &opt_bitslice() { return g_opt_bitslice; }
 void set_error(const std::string &m) { g_err = m; }
 
 }  // namespace rsmi
@@ -430,6 +433,12 @@ void set_error(const std::string &m) { g_err = m; }
 extern "C" {
 
 int rsmi_version(void) { return 0x000100; }
+
+int rsmi_set_option(int option, int value) {
+    if (option == RSMI_OPT_BITSLICE) return rsmi::g_opt_bitslice.exchange(value ? 1 : 0);
+    rsmi::set_error("unknown option");
+    return RSMI_ERR_INVALID;
+}
 
 int rsmi_init(void) {
     int rc;

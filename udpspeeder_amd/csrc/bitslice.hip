@@ -1,6 +1,118 @@
-// bitslice.hip -- placeholder until the generated bit-sliced kernels land.
+// bitslice.hip -- bit-sliced RS encode kernels, specialised at build time for
+// the hot (k,n) codes (gen_bitslice.py -> gen/bitslice_codes.inc).
+//
+// Layout: a "column" is one 16-byte piece of a shard row, P = ceil(len/16)
+// columns per group; the batch is a flat space of G*P columns.  Wave w owns
+// columns [128w, 128w+128): lane l loads piece c0 = 128w+l and c1 = c0+64 of
+// every data shard (two fully coalesced 1 KiB dwordx4 wave-loads per shard),
+// i.e. 32 bytes -> 8 dwords -> 8 bit-planes.  Lanes of one wave may belong
+// to different groups: the network is the same for every group of the code.
+// The XOR network replaces k*m GF multiply-accumulates per byte with ~3 XOR
+// ops per input byte (v_bitop3_b32), bit-exact by construction.
 #include "rsmi_internal.hpp"
+
+#include "bitslice_core.hpp"
+
+// Accumulator updates are opaque single instructions: as plain XORs LLVM
+// reassociates every accumulator chain into one tree at the end of the kernel,
+// keeping all intermediate combinations live (hundreds of spilled VGPRs).
+// The "+v" tie keeps each accumulator in one register for the whole kernel.
+#define BS_ACC3(acc, a, b) asm("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(acc) : "v"(a), "v"(b))
+#define BS_ACC2(acc, a) asm("v_xor_b32 %0, %0, %1" : "+v"(acc) : "v"(a))
+// keep the generated shard blocks in order so the raw-load ring bounds the
+// registers in flight (the scheduler would otherwise hoist every load)
+#define BS_SCHED_BARRIER() __builtin_amdgcn_sched_barrier(0)
+#include "gen/bitslice_codes.inc"
+
 namespace rsmi {
-bool has_bitslice(int, int) { return false; }
-hipError_t launch_encode_bitslice(const UniformArgs &, hipStream_t) { return hipErrorNotSupported; }
+namespace {
+
+// Buffer-descriptor IO: one wave-uniform descriptor per wave covering the
+// (at most a few) groups its 128 columns touch; per lane only two 32-bit
+// voffsets, the shard offset j*shard_stride goes in the scalar soffset.
+// Lanes past the last column get an out-of-range voffset: their loads
+// return 0 and their stores are dropped by the hardware range check.
+struct DevIO {
+    __amdgpu_buffer_rsrc_t rsrc;
+    uint32_t v0, v1;
+    uint32_t ss;
+    __device__ __forceinline__ void load(int j, uint32_t (&p)[8]) const {
+        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+        const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rsrc, v0, j * ss, 0);
+        const u32x4 y = __builtin_amdgcn_raw_buffer_load_b128(rsrc, v1, j * ss, 0);
+        p[0] = x.x; p[1] = x.y; p[2] = x.z; p[3] = x.w;
+        p[4] = y.x; p[5] = y.y; p[6] = y.z; p[7] = y.w;
+    }
+    __device__ __forceinline__ void store(int j, const uint32_t (&q)[8]) const {
+        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+        const u32x4 x = {q[0], q[1], q[2], q[3]};
+        const u32x4 y = {q[4], q[5], q[6], q[7]};
+        __builtin_amdgcn_raw_buffer_store_b128(x, rsrc, v0, j * ss, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(y, rsrc, v1, j * ss, 0);
+    }
+};
+
+__device__ __forceinline__ DevIO make_io(const UniformArgs &a, uint32_t cols, uint32_t P) {
+    const uint32_t wave = blockIdx.x * 4u + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t cfirst = wave * 128u;
+    const uint32_t clast = (cfirst + 127u < cols) ? cfirst + 127u : cols - 1u;
+    const uint32_t gfirst = cfirst / P, glast = clast / P;
+    const uint32_t gs = (uint32_t)a.group_stride;
+    const uint8_t *base = a.base + (int64_t)gfirst * a.group_stride;
+    const uint32_t bytes = (glast - gfirst + 1u) * gs;
+    DevIO io;
+    io.rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(base), 0, (int)bytes,
+                                                0x00020000);
+    const uint32_t c0 = cfirst + lane, c1 = c0 + 64u;
+    const uint32_t g0 = c0 / P, g1 = c1 / P;
+    io.v0 = c0 < cols ? (g0 - gfirst) * gs + (c0 - g0 * P) * 16u : 0x80000000u;
+    io.v1 = c1 < cols ? (g1 - gfirst) * gs + (c1 - g1 * P) * 16u : 0x80000000u;
+    io.ss = (uint32_t)a.shard_stride;
+    return io;
+}
+
+#define BS_KERNEL(K, N)                                                                   \
+    __global__ __launch_bounds__(256, 3) void k_bs_##K##_##N(UniformArgs a, uint32_t cols,     \
+                                                          uint32_t P) {                    \
+        DevIO io = make_io(a, cols, P);                                                   \
+        bs_code_##K##_##N(io);                                                            \
+    }
+BS_FOR_EACH_CODE(BS_KERNEL)
+#undef BS_KERNEL
+
+}  // namespace
+
+bool has_bitslice(int k, int n) {
+    switch (k * 257 + n) {
+#define BS_CASE(K, N) case K * 257 + N: return true;
+        BS_FOR_EACH_CODE(BS_CASE)
+#undef BS_CASE
+        default: return false;
+    }
+}
+
+hipError_t launch_encode_bitslice(const UniformArgs &a, hipStream_t s) {
+    const int64_t P = (a.len + 15) / 16;
+    const int64_t cols = a.ngroups * P;
+    if (P == 0 || cols == 0) return hipSuccess;
+    // descriptor geometry: a wave spans <= 128/P + 2 groups, all 32-bit offsets
+    const int64_t span = (128 / P + 2) * a.group_stride;
+    if (cols >= (int64_t(1) << 31) || a.shard_stride < P * 16 || span >= (int64_t(1) << 31) ||
+        a.group_stride < a.n * a.shard_stride)
+        return hipErrorNotSupported;
+    const int64_t waves = (cols + 127) / 128;
+    const int64_t blocks = (waves + 3) / 4;
+    if (blocks > 0x7fffffff) return hipErrorNotSupported;
+    switch (a.k * 257 + a.n) {
+#define BS_LAUNCH(K, N)                                                                 \
+    case K * 257 + N:                                                                   \
+        k_bs_##K##_##N<<<(unsigned)blocks, 256, 0, s>>>(a, (uint32_t)cols, (uint32_t)P); \
+        return hipGetLastError();
+        BS_FOR_EACH_CODE(BS_LAUNCH)
+#undef BS_LAUNCH
+        default: return hipErrorNotSupported;
+    }
+}
+
 }  // namespace rsmi

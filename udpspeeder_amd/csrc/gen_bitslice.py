@@ -1,0 +1,223 @@
+#!/usr/bin/env python3
+"""Build-time generator of the bit-sliced RS encoders (gen/bitslice_codes.inc).
+
+For a fixed code (k, n) the encoder is a fixed GF(2)-linear map from the 8k
+input bit-planes to the 8m output bit-planes: multiplication by a constant c
+is the 8x8 bit matrix M_c[u][t] = bit u of (c * 2^t) (GF(2^8) multiplication
+is linear over GF(2)).  The matrix of the code is fec_new's systematic
+Vandermonde matrix (lib/fec.cpp:665-720), computed here from scratch.
+
+Each lane holds 32 bytes of every shard as 8 dwords; an in-register 8x8 bit
+transpose (per byte lane) turns them into 8 bit-planes, so one 32-bit XOR
+adds 32 byte positions at once.  The XOR network is emitted with the "four
+Russians" split: per input shard, the XOR combinations of planes {0..3} and
+{4..7} that the outputs need are formed once, then every output plane takes
+at most one combination from each half -- one 3-input XOR (v_bitop3_b32) per
+(output plane, input shard).
+
+The emitted function is __host__ __device__ and templated on an IO policy,
+so the same generated network is unit-tested on the CPU (tests/) and runs in
+the HIP kernels (bitslice.hip).
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+
+# ---------------------------------------------------------------- GF(2^8), 0x11D
+EXP = [0] * 512
+LOG = [0] * 256
+_v = 1
+for _i in range(255):
+    EXP[_i] = _v
+    LOG[_v] = _i
+    _v <<= 1
+    if _v & 0x100:
+        _v ^= 0x11D
+for _i in range(255, 512):
+    EXP[_i] = EXP[_i - 255]
+
+
+def gmul(a: int, b: int) -> int:
+    if a == 0 or b == 0:
+        return 0
+    return EXP[LOG[a] + LOG[b]]
+
+
+def ginv(a: int) -> int:
+    return EXP[(255 - LOG[a]) % 255]
+
+
+def invert(mat):
+    k = len(mat)
+    a = [row[:] + [1 if i == j else 0 for j in range(k)] for i, row in enumerate(mat)]
+    for c in range(k):
+        p = next(r for r in range(c, k) if a[r][c])
+        a[c], a[p] = a[p], a[c]
+        s = ginv(a[c][c])
+        a[c] = [gmul(s, x) for x in a[c]]
+        for r in range(k):
+            if r != c and a[r][c]:
+                f = a[r][c]
+                a[r] = [x ^ gmul(f, y) for x, y in zip(a[r], a[c])]
+    return [row[k:] for row in a]
+
+
+def enc_matrix(k: int, n: int):
+    """Parity rows (n-k) x k of fec_new(k, n)."""
+    v = [[0] * k for _ in range(n)]
+    v[0][0] = 1
+    for r in range(1, n):
+        for c in range(k):
+            v[r][c] = EXP[((r - 1) * c) % 255]
+    inv = invert([row[:] for row in v[:k]])
+    out = []
+    for r in range(k, n):
+        out.append([0] * k)
+        for c in range(k):
+            acc = 0
+            for i in range(k):
+                acc ^= gmul(v[r][i], inv[i][c])
+            out[-1][c] = acc
+    return out
+
+
+def bitmat(c: int):
+    """M[u][t] = bit u of c * 2^t."""
+    cols = [gmul(c, 1 << t) for t in range(8)]
+    return [[(cols[t] >> u) & 1 for t in range(8)] for u in range(8)]
+
+
+# ---------------------------------------------------------------- emitter
+RING = 4  # raw-load ring depth: shard j+RING is requested while shard j is computed
+
+
+def emit_code(k: int, n: int) -> str:
+    m = n - k
+    P = enc_matrix(k, n)
+    L = []
+    w = L.append
+    w(f"// RS(k={k}, n={n}): {8 * m} output planes <- {8 * k} input planes")
+    w(f"template <class IO>")
+    w(f"__host__ __device__ __forceinline__ void bs_code_{k}_{n}(IO &io) {{")
+    for i in range(m):
+        w("    uint32_t " + ", ".join(f"o{i}_{u} = 0" for u in range(8)) + ";")
+    nxor = 0
+    R = min(RING, k)
+    w("    uint32_t " + ", ".join(f"rb{r}[8]" for r in range(R)) + ";")
+    for r in range(R):
+        w(f"    io.load({r}, rb{r});")
+    for j in range(k):
+        w(f"    {{  // input shard {j}")
+        w(f"        uint32_t (&p)[8] = rb{j % R};")
+        w(f"        bs_transpose8(p);")
+        need_lo, need_hi = {}, {}
+        terms = {}
+        for i in range(m):
+            M = bitmat(P[i][j])
+            for u in range(8):
+                lo = sum(M[u][t] << t for t in range(4))
+                hi = sum(M[u][t + 4] << t for t in range(4))
+                terms[(i, u)] = (lo, hi)
+                if lo:
+                    need_lo[lo] = 1
+                if hi:
+                    need_hi[hi] = 1
+        # combination names: single planes are p[t]; multi-plane masks get a temp
+        def build(needed, base, tag):
+            nonlocal nxor
+            names = {}
+            for t in range(4):
+                names[1 << t] = f"p[{base + t}]"
+            todo = sorted(needed, key=lambda x: bin(x).count("1"))
+            for mask in todo:
+                if mask in names:
+                    continue
+                # split off the highest plane; build the rest recursively
+                def get(mm):
+                    nonlocal nxor
+                    if mm in names:
+                        return names[mm]
+                    hb = mm.bit_length() - 1
+                    rest = mm & ~(1 << hb)
+                    a = get(rest)
+                    nm = f"{tag}{mm}"
+                    w(f"        const uint32_t {nm} = {a} ^ p[{base + hb}];")
+                    nxor += 1
+                    names[mm] = nm
+                    return nm
+                get(mask)
+            return names
+        lo_names = build(need_lo, 0, "l")
+        hi_names = build(need_hi, 4, "h")
+        for i in range(m):
+            for u in range(8):
+                lo, hi = terms[(i, u)]
+                a = lo_names[lo] if lo else None
+                b = hi_names[hi] if hi else None
+                acc = f"o{i}_{u}"
+                if a and b:
+                    w(f"        BS_ACC3({acc}, {a}, {b});")
+                    nxor += 1
+                elif a or b:
+                    w(f"        BS_ACC2({acc}, {a or b});")
+                    nxor += 1
+        if j + R < k:
+            w(f"        io.load({j + R}, rb{j % R});")
+        w(f"    }}")
+        w(f"    BS_SCHED_BARRIER();")
+    for i in range(m):
+        w(f"    {{")
+        w(f"        uint32_t q[8] = {{" + ", ".join(f"o{i}_{u}" for u in range(8)) + "};")
+        w(f"        bs_transpose8(q);")
+        w(f"        io.store({k + i}, q);")
+        w(f"    }}")
+    w(f"}}  // {nxor} XOR ops")
+    return "\n".join(L), nxor
+
+
+def default_codes():
+    codes = set()
+    for x in range(1, 21):
+        codes.add((x, x + 10))           # UDPspeeder default -f 20:10 (misc.cpp:57)
+    c3 = [(1, 3), (2, 4), (3, 5), (4, 5), (5, 5), (6, 5), (7, 6), (8, 6), (9, 6), (10, 6),
+          (11, 7), (12, 7), (13, 8), (14, 8), (15, 8), (16, 9), (17, 9), (18, 10), (19, 10),
+          (20, 10)]                      # rs_from_str("1:3,2:4,10:6,20:10")
+    for x, y in c3:
+        codes.add((x, x + y))
+    return sorted(codes)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--out", default=os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                                  "gen", "bitslice_codes.inc"))
+    ap.add_argument("--codes", default="", help="k:n,k:n,... (default: built-in hot set)")
+    args = ap.parse_args()
+    codes = default_codes() if not args.codes else \
+        [tuple(int(v) for v in c.split(":")) for c in args.codes.split(",")]
+    os.makedirs(os.path.dirname(args.out), exist_ok=True)
+    parts = ["// GENERATED by gen_bitslice.py -- do not edit.",
+             "// Bit-sliced XOR networks for the hot (k,n) codes of fec_new's matrix.",
+             f"#define BS_NUM_CODES {len(codes)}"]
+    stats = []
+    for (k, n) in codes:
+        src, nx = emit_code(k, n)
+        parts.append(src)
+        stats.append((k, n, nx))
+    parts.append("#define BS_FOR_EACH_CODE(X) \\")
+    parts.append(" \\\n".join(f"    X({k}, {n})" for (k, n) in codes))
+    parts.append("")
+    txt = "\n".join(parts) + "\n"
+    if os.path.exists(args.out) and open(args.out).read() == txt:
+        return
+    with open(args.out, "w") as f:
+        f.write(txt)
+    for k, n, nx in stats:
+        print(f"  bs_code_{k}_{n}: {nx} xor ops ({nx / (32 * k):.2f} per input byte)",
+              file=sys.stderr)
+
+
+if __name__ == "__main__":
+    main()

@@ -162,6 +162,13 @@ def decode_matrix(k: int, n: int, present: Sequence[int]):
     return e, sel, miss[:e], coef[:e * k].reshape(e, k)
 
 
+def set_bitslice(enabled: bool) -> bool:
+    """Use (default) or bypass the specialised bit-sliced encoders; returns
+    the previous setting.  For A/B tests of the generic kernel."""
+    from ._lib import RSMI_OPT_BITSLICE
+    return bool(lib().rsmi_set_option(RSMI_OPT_BITSLICE, int(bool(enabled))))
+
+
 def version() -> int:
     return lib().rsmi_version()
 
