@@ -13,12 +13,17 @@
 
 #include "bitslice_core.hpp"
 
-// Accumulator updates are opaque single instructions: as plain XORs LLVM
-// reassociates every accumulator chain into one tree at the end of the kernel,
-// keeping all intermediate combinations live (hundreds of spilled VGPRs).
-// The "+v" tie keeps each accumulator in one register for the whole kernel.
-#define BS_ACC3(acc, a, b) asm("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(acc) : "v"(a), "v"(b))
-#define BS_ACC2(acc, a) asm("v_xor_b32 %0, %0, %1" : "+v"(acc) : "v"(a))
+// Accumulator updates go through the v_bitop3 builtin.  Plain `acc ^= a ^ b`
+// chains get reassociated by LLVM into one tree per accumulator at the end of
+// the kernel (every intermediate combination stays live: hundreds of spilled
+// VGPRs); the builtin keeps each update in its shard block.  (Inline-asm
+// accumulators were tried and produced intermittently wrong parity under
+// load -- the compiler's hazard/wait bookkeeping does not see inside asm.)
+#ifndef BS_OCC
+#define BS_OCC 3
+#endif
+#define BS_ACC3(acc, a, b) ((acc) = __builtin_amdgcn_bitop3_b32((acc), (a), (b), 0x96))
+#define BS_ACC2(acc, a) ((acc) ^= (a))
 // keep the generated shard blocks in order so the raw-load ring bounds the
 // registers in flight (the scheduler would otherwise hoist every load)
 #define BS_SCHED_BARRIER() __builtin_amdgcn_sched_barrier(0)
@@ -72,9 +77,13 @@ __device__ __forceinline__ DevIO make_io(const UniformArgs &a, uint32_t cols, ui
     return io;
 }
 
+// Waves whose first column is past the end exit before touching memory
+// (a grid is rounded up to whole 4-wave blocks).
 #define BS_KERNEL(K, N)                                                                   \
-    __global__ __launch_bounds__(256, 3) void k_bs_##K##_##N(UniformArgs a, uint32_t cols,     \
+    __global__ __launch_bounds__(256, BS_OCC) void k_bs_##K##_##N(UniformArgs a, uint32_t cols,     \
                                                           uint32_t P) {                    \
+        const uint32_t wave = blockIdx.x * 4u + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); \
+        if (wave * 128u >= cols) return;                                                  \
         DevIO io = make_io(a, cols, P);                                                   \
         bs_code_##K##_##N(io);                                                            \
     }
