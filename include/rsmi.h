@@ -59,6 +59,10 @@ const char *rsmi_last_error(void);
  * build-time specialised bit-sliced encoders where available, 0 forces the
  * generic table kernel (for A/B tests).  Returns the previous value. */
 #define RSMI_OPT_BITSLICE 1
+/* RSMI_OPT_FUSED_DECODE: 1 (default) builds decode matrices and rebuilds the
+ * rows in one fused kernel where the code fits it, 0 forces the two-kernel
+ * path (plan kernel + apply kernel). */
+#define RSMI_OPT_FUSED_DECODE 2
 int rsmi_set_option(int option, int value);
 
 /* Host copy of fec_new(k,n)'s n x k systematic encoding matrix (row-major),

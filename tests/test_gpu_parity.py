@@ -206,6 +206,36 @@ def test_decode_vs_oracle_random(gpu, oracle, k, n, ln, ner):
     assert (out[:, k:] == buf[:, k:]).all()
 
 
+@pytest.mark.parametrize("fused", [True, False])
+@pytest.mark.parametrize("k,n,ln", [(20, 30, 1250), (20, 30, 3000), (7, 13, 100), (1, 2, 1280),
+                                    (10, 20, 1281), (40, 50, 64)])
+def test_decode_paths_agree(gpu, oracle, fused, k, n, ln):
+    """Fused (one wave per group) and two-kernel decode both match the oracle,
+    including lengths that need several 1280-B tiles and ragged tails."""
+    import udpspeeder_amd as u
+    G = 257
+    S = stride_for(ln)
+    rng = np.random.default_rng(k * n + ln)
+    buf = rng.integers(0, 256, (G, n, S), dtype=np.uint8)
+    present = np.ones((G, n), np.uint8)
+    for g in range(G):
+        present[g, rng.choice(n, rng.integers(0, n - k + 2), replace=False)] = 0
+    ref = buf.copy()
+    st_ref = oracle.decode_batch(k, n, ref.reshape(-1), n * S, S, ln, G, present)
+    t = upload(buf, gpu)
+    prev = u.rs.set_fused_decode(fused)
+    try:
+        st = u.decode(t, upload(present, gpu), k, n, ln).cpu().numpy()
+    finally:
+        u.rs.set_fused_decode(prev)
+    assert (st == st_ref).all()
+    out = t.cpu().numpy()
+    assert (out[:, :k, :ln] == ref[:, :k, :ln]).all()
+    assert (out[:, k:] == buf[:, k:]).all()
+    pad = (ln + 15) // 16 * 16
+    assert (out[:, :, pad:] == buf[:, :, pad:]).all()
+
+
 def test_decode_c2_full_noncodeword_sha(gpu, golden):
     """C2 at full size with random (non-codeword) parity: the recovered data
     rows hash to the reference's digest -- pins the survivor-selection rule

@@ -21,6 +21,7 @@ namespace {
 
 thread_local std::string g_err;
 std::atomic<int> g_opt_bitslice{1};
+std::atomic<int> g_opt_fused{1};
 
 int fail(int code, const std::string &msg) {
     g_err = msg;
@@ -227,17 +228,25 @@ int decode_dev(int k, int n, uint8_t *base, int64_t gs, int64_t ss, int len, int
     Device *D = current(&rc);
     if (!D) return rc;
     const Code *C;
-    uint8_t *plans;
+    uint8_t *plans = nullptr;
+    const bool fused = g_opt_fused.load() && n > k && decode_fused_ok(k, n, gs, ss, len);
     {
         std::lock_guard<std::mutex> lk(D->mu);
         rc = ensure_code(*D, k, n, &C);
         if (rc) return rc;
-        rc = ensure_ws(*D, s, plan_bytes(k, n, ngroups), &plans);
-        if (rc) return rc;
+        if (!fused) {
+            rc = ensure_ws(*D, s, plan_bytes(k, n, ngroups), &plans);
+            if (rc) return rc;
+        }
     }
     if (ngroups == 0) return RSMI_OK;
     int W;
     UniformArgs a = make_args(k, n, base, gs, ss, len, ngroups, &W);
+    if (fused) {
+        hipError_t e = launch_decode_fused(a, present, C->dev_rows, status, D->ptab, D->gftab, s);
+        if (e != hipSuccess) return hip_fail(e, "fused decode launch");
+        return RSMI_OK;
+    }
     hipError_t e = launch_decode_plan(a, present, C->dev_rows, plans, status, D->gftab, s);
     if (e != hipSuccess) return hip_fail(e, "decode plan launch");
     if (n > k && len > 0) {
@@ -436,6 +445,7 @@ int rsmi_version(void) { return 0x000100; }
 
 int rsmi_set_option(int option, int value) {
     if (option == RSMI_OPT_BITSLICE) return rsmi::g_opt_bitslice.exchange(value ? 1 : 0);
+    if (option == RSMI_OPT_FUSED_DECODE) return rsmi::g_opt_fused.exchange(value ? 1 : 0);
     rsmi::set_error("unknown option");
     return RSMI_ERR_INVALID;
 }

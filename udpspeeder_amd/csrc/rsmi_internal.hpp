@@ -48,6 +48,12 @@ hipError_t launch_fill_data(int k, int len, uint8_t *base, int64_t group_stride,
 hipError_t launch_fill_ragged(const rsmi_group *groups, int64_t ngroups, uint8_t *base,
                               int64_t g0, uint64_t seed, hipStream_t s);
 
+// Fused decode (plan + reconstruction in one wave per group, decode.hip).
+bool decode_fused_ok(int k, int n, int64_t group_stride, int64_t shard_stride, int len);
+hipError_t launch_decode_fused(const UniformArgs &a, const uint8_t *present,
+                               const uint8_t *parity_rows, int32_t *status,
+                               const uint32_t *ptab, const uint8_t *gftab, hipStream_t s);
+
 // Bit-sliced encode kernels specialised at build time for hot (k,n) codes
 // (gen_bitslice.py -> gen/bitslice_codes.inc).  Returns hipErrorNotSupported
 // when (k,n) has no specialised kernel.

@@ -169,6 +169,13 @@ def set_bitslice(enabled: bool) -> bool:
     return bool(lib().rsmi_set_option(RSMI_OPT_BITSLICE, int(bool(enabled))))
 
 
+def set_fused_decode(enabled: bool) -> bool:
+    """Use (default) or bypass the fused decode kernel; returns the previous
+    setting.  For A/B tests of the two-kernel (plan + apply) decode path."""
+    from ._lib import RSMI_OPT_FUSED_DECODE
+    return bool(lib().rsmi_set_option(RSMI_OPT_FUSED_DECODE, int(bool(enabled))))
+
+
 def version() -> int:
     return lib().rsmi_version()
 
