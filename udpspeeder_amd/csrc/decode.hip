@@ -29,7 +29,11 @@ namespace {
 constexpr int kWaves = 4;      // waves per block (one group each)
 constexpr int kRing = 4;       // survivors in flight per wave
 constexpr int kRows = 10;      // max e handled by the fused kernel (emax <= kRows)
+constexpr int kPass = 5;       // rows accumulated per pass over the survivors
 constexpr int kTile = 1280;    // bytes per lane-tile pass (64 x 16 + 64 x 4)
+#ifndef DEC_OCC
+#define DEC_OCC 4              // waves per SIMD the register budget is cut for
+#endif
 
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
     return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
@@ -57,7 +61,7 @@ __host__ __device__ inline int wave_lds_bytes(int k) {
     return 512 + aug + k * kRows * 32;
 }
 
-__global__ __launch_bounds__(256) void k_decode_fused(UniformArgs a, const uint8_t *present,
+__global__ __launch_bounds__(256, DEC_OCC) void k_decode_fused(UniformArgs a, const uint8_t *present,
                                                       const uint8_t *prows, int32_t *status_out,
                                                       const uint32_t *ptab, const uint8_t *gftab) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -82,13 +86,21 @@ __global__ __launch_bounds__(256) void k_decode_fused(UniformArgs a, const uint8
 
     const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
     const int64_t nwaves = (int64_t)gridDim.x * kWaves;
-    for (int64_t g = (int64_t)blockIdx.x * kWaves + wid; g < a.ngroups; g += nwaves) {
+    const int64_t g0 = (int64_t)blockIdx.x * kWaves + wid;
+    // present flags of the first 64 shards, prefetched one group ahead
+    uint32_t pf = (g0 < a.ngroups && lane < n) ? present[g0 * n + lane] : 0u;
+    uint32_t pf_next = 0;
+    for (int64_t g = g0; g < a.ngroups; g += nwaves, pf = pf_next) {
+        {
+            const int64_t gn = g + nwaves;
+            pf_next = (gn < a.ngroups && lane < n) ? present[gn * n + lane] : 0u;
+        }
         // ---- 1. survivor selection (rs.cpp:24-39) ------------------------------
         const uint8_t *pr = present + g * n;
         int cnt = 0, e = 0;
         for (int b = 0; b < n && cnt < k; b += 64) {
             const int idx = b + lane;
-            const bool f = idx < n && pr[idx] != 0;
+            const bool f = idx < n && (b == 0 ? pf : pr[idx]) != 0;
             const uint64_t mk = __ballot(f);
             const int rank = cnt + __popcll(mk & lt);
             if (f && rank < k) L.sel[rank] = (uint8_t)idx;
@@ -100,7 +112,7 @@ __global__ __launch_bounds__(256) void k_decode_fused(UniformArgs a, const uint8
         } else {
             for (int b = 0; b < k; b += 64) {
                 const int idx = b + lane;
-                const bool ms = idx < k && pr[idx] == 0;
+                const bool ms = idx < k && (b == 0 ? pf : pr[idx]) == 0;
                 const uint64_t mk = __ballot(ms);
                 if (ms) L.miss[e + __popcll(mk & lt)] = (uint8_t)idx;
                 e += __popcll(mk);
@@ -125,6 +137,24 @@ __global__ __launch_bounds__(256) void k_decode_fused(UniformArgs a, const uint8
         const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
             reinterpret_cast<uint8_t *>(gbu), 0, (int)(a.n * a.shard_stride), 0x00020000);
         const uint32_t ss = (uint32_t)a.shard_stride;
+        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+        u32x4 rq[kRing];
+        uint32_t rd[kRing];
+        uint32_t v16, v4;
+        auto start_tile = [&](int toff) {
+            const int tlen = a.len - toff;
+            v16 = (16 * lane < tlen) ? (uint32_t)(toff + 16 * lane) : 0x80000000u;
+            v4 = (1024 + 4 * lane < tlen) ? (uint32_t)(toff + 1024 + 4 * lane) : 0x80000000u;
+#pragma unroll
+            for (int q = 0; q < kRing; ++q) {
+                if (q < k) {
+                    const uint32_t so = __builtin_amdgcn_readfirstlane(L.sel[q]) * ss;
+                    rq[q] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, v16, so, 0);
+                    rd[q] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, v4, so, 0);
+                }
+            }
+        };
+        start_tile(0);  // the first survivors fly while the matrix is inverted
 
         // ---- 3. Gauss-Jordan: aug = [A | M], e x (e+k) -------------------------
         const int W = e + k;
@@ -178,72 +208,60 @@ __global__ __launch_bounds__(256) void k_decode_fused(UniformArgs a, const uint8
         }
         wave_sync();
 
-        // ---- 4. stream the survivors --------------------------------------------
+        // ---- 4. stream the survivors: passes over (tile, block of kPass rows) --
         for (int toff = 0; toff < a.len; toff += kTile) {
-            const int tlen = a.len - toff;
-            const uint32_t v16 = (16 * lane < tlen) ? (uint32_t)(toff + 16 * lane) : 0x80000000u;
-            const uint32_t v4 =
-                (1024 + 4 * lane < tlen) ? (uint32_t)(toff + 1024 + 4 * lane) : 0x80000000u;
-            typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-            u32x4 rq[kRing];
-            uint32_t rd[kRing];
+            for (int rb = 0; rb < e; rb += kPass) {
+                if (toff || rb) start_tile(toff);  // pass 0's loads are already in flight
+                uint32_t acc[kPass][5];
 #pragma unroll
-            for (int q = 0; q < kRing; ++q) {
-                if (q < k) {
-                    const uint32_t so = __builtin_amdgcn_readfirstlane(L.sel[q]) * ss;
-                    rq[q] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, v16, so, 0);
-                    rd[q] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, v4, so, 0);
-                }
-            }
-            uint32_t acc[kRows][5];
+                for (int r = 0; r < kPass; ++r)
 #pragma unroll
-            for (int r = 0; r < kRows; ++r)
+                    for (int w = 0; w < 5; ++w) acc[r][w] = 0;
+                for (int jb = 0; jb < k; jb += kRing) {
 #pragma unroll
-                for (int w = 0; w < 5; ++w) acc[r][w] = 0;
-            for (int jb = 0; jb < k; jb += kRing) {
+                    for (int q = 0; q < kRing; ++q) {
+                        const int j = jb + q;
+                        if (j < k) {
+                            const uint32_t x[5] = {rq[q].x, rq[q].y, rq[q].z, rq[q].w, rd[q]};
+                            uint32_t q0[5], q1[5], q2[5];
 #pragma unroll
-                for (int q = 0; q < kRing; ++q) {
-                    const int j = jb + q;
-                    if (j < k) {
-                        const uint32_t x[5] = {rq[q].x, rq[q].y, rq[q].z, rq[q].w, rd[q]};
-                        uint32_t q0[5], q1[5], q2[5];
+                            for (int w = 0; w < 5; ++w) {
+                                q0[w] = x[w] & 0x07070707u;
+                                q1[w] = (x[w] >> 3) & 0x07070707u;
+                                q2[w] = (x[w] >> 6) & 0x03030303u;
+                            }
+                            if (j + kRing < k) {
+                                const uint32_t so =
+                                    __builtin_amdgcn_readfirstlane(L.sel[j + kRing]) * ss;
+                                rq[q] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, v16, so, 0);
+                                rd[q] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, v4, so, 0);
+                            }
+                            const uint32_t *tj = L.tab + (j * kRows + rb) * 8;
 #pragma unroll
-                        for (int w = 0; w < 5; ++w) {
-                            q0[w] = x[w] & 0x07070707u;
-                            q1[w] = (x[w] >> 3) & 0x07070707u;
-                            q2[w] = (x[w] >> 6) & 0x03030303u;
-                        }
-                        if (j + kRing < k) {
-                            const uint32_t so =
-                                __builtin_amdgcn_readfirstlane(L.sel[j + kRing]) * ss;
-                            rq[q] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, v16, so, 0);
-                            rd[q] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, v4, so, 0);
-                        }
-                        const uint32_t *tj = L.tab + j * kRows * 8;
+                            for (int r = 0; r < kPass; ++r) {
+                                if (rb + r < e) {
+                                    const uint4 t = reinterpret_cast<const uint4 *>(tj + r * 8)[0];
+                                    const uint32_t t2 = tj[r * 8 + 4];
 #pragma unroll
-                        for (int r = 0; r < kRows; ++r) {
-                            if (r < e) {
-                                const uint4 t = reinterpret_cast<const uint4 *>(tj + r * 8)[0];
-                                const uint32_t t2 = tj[r * 8 + 4];
-#pragma unroll
-                                for (int w = 0; w < 5; ++w) {
-                                    const uint32_t p0 = __builtin_amdgcn_perm(t.y, t.x, q0[w]);
-                                    const uint32_t p1 = __builtin_amdgcn_perm(t.w, t.z, q1[w]);
-                                    const uint32_t p2 = __builtin_amdgcn_perm(t2, t2, q2[w]);
-                                    acc[r][w] = acc[r][w] ^ xor3(p0, p1, p2);
+                                    for (int w = 0; w < 5; ++w) {
+                                        const uint32_t p0 = __builtin_amdgcn_perm(t.y, t.x, q0[w]);
+                                        const uint32_t p1 = __builtin_amdgcn_perm(t.w, t.z, q1[w]);
+                                        const uint32_t p2 = __builtin_amdgcn_perm(t2, t2, q2[w]);
+                                        acc[r][w] = acc[r][w] ^ xor3(p0, p1, p2);
+                                    }
                                 }
                             }
                         }
                     }
                 }
-            }
 #pragma unroll
-            for (int r = 0; r < kRows; ++r) {
-                if (r < e) {
-                    const uint32_t so = __builtin_amdgcn_readfirstlane(L.miss[r]) * ss;
-                    const u32x4 v = {acc[r][0], acc[r][1], acc[r][2], acc[r][3]};
-                    __builtin_amdgcn_raw_buffer_store_b128(v, rsrc, v16, so, 0);
-                    __builtin_amdgcn_raw_buffer_store_b32(acc[r][4], rsrc, v4, so, 0);
+                for (int r = 0; r < kPass; ++r) {
+                    if (rb + r < e) {
+                        const uint32_t so = __builtin_amdgcn_readfirstlane(L.miss[rb + r]) * ss;
+                        const u32x4 v = {acc[r][0], acc[r][1], acc[r][2], acc[r][3]};
+                        __builtin_amdgcn_raw_buffer_store_b128(v, rsrc, v16, so, 0);
+                        __builtin_amdgcn_raw_buffer_store_b32(acc[r][4], rsrc, v4, so, 0);
+                    }
                 }
             }
         }
