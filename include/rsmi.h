@@ -135,6 +135,17 @@ int rsmi_decode_host(int k, int n, uint8_t *base, int64_t group_stride,
                      int64_t shard_stride, int len, int64_t ngroups,
                      const uint8_t *present, int32_t *status);
 
+/* Pipelined end-to-end encode from host memory (the UDP-socket side of the
+ * path): data shards of group g at host_data + g*data_gs + j*shard_stride
+ * (j < k), parity written to host_parity + g*parity_gs + (j-k)*shard_stride.
+ * Chunks of `chunk_groups` groups flow H2D -> encode -> D2H on three HIP
+ * streams so the two copy directions and the kernels overlap.  Host buffers
+ * should be pinned (hipHostMalloc / torch pin_memory) for the copies to run
+ * asynchronously.  Synchronous: returns when all parity is in host memory. */
+int rsmi_encode_pinned(int k, int n, const uint8_t *host_data, int64_t data_gs,
+                       uint8_t *host_parity, int64_t parity_gs, int64_t shard_stride,
+                       int len, int64_t ngroups, int64_t chunk_groups);
+
 /* ---- synthetic inputs (bench / tests) ----------------------------------- */
 
 /* Fill data shards (j < k) of every group with the SplitMix64 stream:

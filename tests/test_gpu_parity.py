@@ -393,6 +393,21 @@ def test_compat_lower_api(gpu, oracle):
     assert u.get_code(20, 30) == u.get_code(20, 30)
 
 
+def test_encode_pinned_pipeline(gpu, oracle):
+    import torch
+    import udpspeeder_amd as u
+    k, n, ln, G, S = 20, 30, 1250, 10000, 1280
+    data = torch.from_numpy(group_data(DATA_SEED, 0, G, k, ln)).contiguous()
+    d = torch.zeros((G, k, S), dtype=torch.uint8).pin_memory()
+    d[:, :, :ln] = data
+    par = torch.zeros((G, n - k, S), dtype=torch.uint8).pin_memory()
+    u.rs.encode_pinned(d, par, k, n, ln, chunk_groups=1536)
+    ref = np.zeros((G, n, S), np.uint8)
+    ref[:, :k] = d.numpy()
+    oracle.encode_batch(k, n, ref.reshape(-1), n * S, S, ln, G)
+    assert (par.numpy()[:, :, :ln] == ref[:, k:, :ln]).all()
+
+
 def test_host_batched_api(gpu, oracle):
     import udpspeeder_amd as u
     k, n, ln, G = 20, 30, 1250, 64

@@ -72,6 +72,7 @@ def _bind(lib: C.CDLL) -> C.CDLL:
         "rsmi_decode_host": ([i32, i32, vp, i64, i64, i32, i64, vp, vp], i32),
         "rsmi_fill_data": ([i32, i32, vp, i64, i64, i64, i64, C.c_uint64, vp], i32),
         "rsmi_fill_ragged": ([vp, i64, vp, i64, C.c_uint64, vp], i32),
+        "rsmi_encode_pinned": ([i32, i32, vp, i64, vp, i64, i64, i32, i64, i64], i32),
     }
     for name, (args, res) in sig.items():
         f = getattr(lib, name)

@@ -4,6 +4,7 @@
 // drop-in shim (compat.cpp).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <atomic>
 #include <cstdio>
 #include <cstring>
@@ -432,6 +433,60 @@ int host_op(bool decode, int k, int n, uint8_t *base, int64_t gs, int64_t ss, in
     return host_op_ptrs(decode, k, n, p.data(), o.data(), len, ngroups, present, status);
 }
 
+// ---- pipelined host <-> device encode (rsmi_encode_pinned) ----------------
+struct Pipeline {
+    static constexpr int kDepth = 3;
+    hipStream_t st[kDepth] = {};
+    uint8_t *dev[kDepth] = {};
+    size_t bytes = 0;
+};
+
+int encode_pinned(int k, int n, const uint8_t *hd, int64_t dgs, uint8_t *hp, int64_t pgs,
+                  int64_t ss, int len, int64_t ngroups, int64_t chunk) {
+    int rc = check_uniform(k, n, nullptr, 16, ss, len, 0);
+    if (rc) return rc;
+    if (ngroups < 0 || chunk < 1 || (ngroups && (!hd || (!hp && n > k))) || dgs < k * ss ||
+        (n > k && pgs < (n - k) * ss))
+        return fail(RSMI_ERR_INVALID, "invalid encode_pinned arguments");
+    if (ngroups == 0 || n == k || len == 0) return RSMI_OK;
+    Device *D = current(&rc);
+    if (!D) return rc;
+    static std::mutex pmu;  // one pipeline per process at a time
+    static Pipeline P;
+    std::lock_guard<std::mutex> lk(pmu);
+    const int64_t dgs_dev = (int64_t)n * ss;
+    const size_t need = (size_t)(dgs_dev * chunk);
+    if (P.bytes < need) {
+        for (int i = 0; i < Pipeline::kDepth; ++i) {
+            if (P.dev[i]) (void)hipFree(P.dev[i]);
+            P.dev[i] = nullptr;
+        }
+        P.bytes = 0;
+        for (int i = 0; i < Pipeline::kDepth; ++i)
+            RSMI_HIP(hipMalloc(&P.dev[i], need), "hipMalloc(pipeline)");
+        P.bytes = need;
+    }
+    for (int i = 0; i < Pipeline::kDepth; ++i)
+        if (!P.st[i]) RSMI_HIP(hipStreamCreateWithFlags(&P.st[i], hipStreamNonBlocking),
+                               "hipStreamCreate(pipeline)");
+    const int m = n - k;
+    int64_t c = 0;
+    for (int64_t g0 = 0; g0 < ngroups; g0 += chunk, ++c) {
+        const int64_t cnt = std::min(chunk, ngroups - g0);
+        const int b = (int)(c % Pipeline::kDepth);
+        hipStream_t s = P.st[b];
+        RSMI_HIP(hipMemcpy2DAsync(P.dev[b], dgs_dev, hd + g0 * dgs, dgs, (size_t)k * ss, cnt,
+                                  hipMemcpyHostToDevice, s), "H2D data");
+        rc = encode_dev(k, n, P.dev[b], dgs_dev, ss, len, cnt, s);
+        if (rc) return rc;
+        RSMI_HIP(hipMemcpy2DAsync(hp + g0 * pgs, pgs, P.dev[b] + (size_t)k * ss, dgs_dev,
+                                  (size_t)m * ss, cnt, hipMemcpyDeviceToHost, s), "D2H parity");
+    }
+    for (int i = 0; i < Pipeline::kDepth; ++i)
+        RSMI_HIP(hipStreamSynchronize(P.st[i]), "hipStreamSynchronize(pipeline)");
+    return RSMI_OK;
+}
+
 const char *last_error() { return g_err.c_str(); }
 std::atomic<int> &opt_bitslice() { return g_opt_bitslice; }
 void set_error(const std::string &m) { g_err = m; }
@@ -524,6 +579,11 @@ int rsmi_decode_host(int k, int n, uint8_t *base, int64_t gs, int64_t ss, int le
         return RSMI_ERR_INVALID;
     }
     return rsmi::host_op(true, k, n, base, gs, ss, len, ngroups, present, status);
+}
+
+int rsmi_encode_pinned(int k, int n, const uint8_t *hd, int64_t dgs, uint8_t *hp, int64_t pgs,
+                       int64_t ss, int len, int64_t ngroups, int64_t chunk) {
+    return rsmi::encode_pinned(k, n, hd, dgs, hp, pgs, ss, len, ngroups, chunk);
 }
 
 int rsmi_fill_data(int k, int len, uint8_t *base, int64_t gs, int64_t ss, int64_t g0,

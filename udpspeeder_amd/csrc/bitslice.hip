@@ -27,7 +27,11 @@
 // keep the generated shard blocks in order so the raw-load ring bounds the
 // registers in flight (the scheduler would otherwise hoist every load)
 #define BS_SCHED_BARRIER() __builtin_amdgcn_sched_barrier(0)
+#ifdef BS_INC
+#include BS_INC
+#else
 #include "gen/bitslice_codes.inc"
+#endif
 
 namespace rsmi {
 namespace {

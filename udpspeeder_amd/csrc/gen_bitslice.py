@@ -90,7 +90,7 @@ def bitmat(c: int):
 
 
 # ---------------------------------------------------------------- emitter
-RING = 4  # raw-load ring depth: shard j+RING is requested while shard j is computed
+RING = int(os.environ.get("BS_RING", "4"))  # raw-load ring: shard j+RING is requested while shard j is computed
 
 
 def emit_code(k: int, n: int) -> str:

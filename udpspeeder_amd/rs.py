@@ -287,6 +287,22 @@ def fill_data_flat(base, k: int, length: int, offset: int, group_stride: int, sh
                                _stream_handle(stream)), "rsmi_fill_data")
 
 
+def encode_pinned(data, parity, k: int, n: int, length: int, chunk_groups: int = 4096) -> None:
+    """End-to-end encode from host memory: ``data`` [G, k, S] and ``parity``
+    [G, n-k, S] uint8 CPU tensors/arrays (pin them for overlap); chunks are
+    pipelined H2D -> encode -> D2H inside the library."""
+    def geo(x):
+        if hasattr(x, "data_ptr"):
+            return x.data_ptr(), x.stride(0), x.stride(1), x.shape
+        return x.ctypes.data, x.strides[0], x.strides[1], x.shape
+    dp, dgs, dss, dsh = geo(data)
+    pp, pgs, pss, psh = geo(parity)
+    if dss != pss or dsh[0] != psh[0] or dsh[1] != k or psh[1] != n - k:
+        raise ValueError("data [G,k,S] and parity [G,n-k,S] must share G and S")
+    check(lib().rsmi_encode_pinned(k, n, dp, dgs, pp, pgs, dss, length, dsh[0], chunk_groups),
+          "rsmi_encode_pinned")
+
+
 def groups_to_device(groups, device="cuda"):
     """Copy a ctypes rsmi_group array to a device uint8 tensor (24 B/group)."""
     import torch
