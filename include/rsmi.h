@@ -115,9 +115,8 @@ typedef struct rsmi_group {
     uint32_t reserved;     /* must be 0                                         */
 } rsmi_group;              /* 24 bytes */
 
-/* Encode ngroups groups described by groups[] (HOST array).  The codes for
- * every (k,n) in the batch are made resident and the descriptors are staged
- * to the device on `stream`. */
+/* Encode ngroups groups described by groups[] (HOST array): builds a ragged
+ * plan (below), launches it on `stream` and returns once it has completed. */
 int rsmi_encode_ragged(const rsmi_group *groups, int64_t ngroups, uint8_t *base,
                        void *stream);
 
@@ -126,6 +125,19 @@ int rsmi_encode_ragged(const rsmi_group *groups, int64_t ngroups, uint8_t *base,
  * resident, or whose descriptor is invalid, are left untouched. */
 int rsmi_encode_ragged_dev(const rsmi_group *dev_groups, int64_t ngroups,
                            uint8_t *base, void *stream);
+
+/* Ragged plans (like FFT plans): built once on the host from the group
+ * descriptors, kept on the device, reused by every launch over the same
+ * layout (graph-capturable).  When every (k,n) in the batch has a
+ * specialised bit-sliced network the plan buckets groups by code and one
+ * launch covers all buckets; otherwise the generic kernel runs.  Destroy a
+ * plan only after the launches that use it have completed. */
+typedef struct rsmi_ragged_plan rsmi_ragged_plan;
+int rsmi_ragged_plan_create(const rsmi_group *groups, int64_t ngroups,
+                            rsmi_ragged_plan **plan);
+int rsmi_encode_ragged_plan(const rsmi_ragged_plan *plan, uint8_t *base, void *stream);
+int rsmi_ragged_plan_uses_bitslice(const rsmi_ragged_plan *plan);
+void rsmi_ragged_plan_destroy(rsmi_ragged_plan *plan);
 
 /* ---- host-memory convenience (pinned staging + H2D/D2H on an internal
  * stream; synchronous).  Same layout contract, host pointers. --------------- */

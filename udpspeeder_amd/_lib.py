@@ -72,6 +72,10 @@ def _bind(lib: C.CDLL) -> C.CDLL:
         "rsmi_decode_host": ([i32, i32, vp, i64, i64, i32, i64, vp, vp], i32),
         "rsmi_fill_data": ([i32, i32, vp, i64, i64, i64, i64, C.c_uint64, vp], i32),
         "rsmi_fill_ragged": ([vp, i64, vp, i64, C.c_uint64, vp], i32),
+        "rsmi_ragged_plan_create": ([vp, i64, vp], i32),
+        "rsmi_encode_ragged_plan": ([vp, vp, vp], i32),
+        "rsmi_ragged_plan_uses_bitslice": ([vp], i32),
+        "rsmi_ragged_plan_destroy": ([vp], None),
         "rsmi_encode_pinned": ([i32, i32, vp, i64, vp, i64, i64, i32, i64, i64], i32),
     }
     for name, (args, res) in sig.items():

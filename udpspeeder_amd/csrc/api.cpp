@@ -292,38 +292,14 @@ int encode_ragged_dev(const rsmi_group *dg, int64_t ngroups, uint8_t *base, hipS
     return RSMI_OK;
 }
 
-int encode_ragged(const rsmi_group *g, int64_t ngroups, uint8_t *base, hipStream_t s) {
-    if (ngroups < 0) return fail(RSMI_ERR_INVALID, "negative ngroups");
-    if (ngroups == 0) return RSMI_OK;
-    if (!g || !base) return fail(RSMI_ERR_INVALID, "null descriptors/base");
-    if (((uintptr_t)base) % 16) return fail(RSMI_ERR_INVALID, "base must be 16-aligned");
-    int rc;
-    Device *D = current(&rc);
-    if (!D) return rc;
-    uint8_t *ws;
-    {
-        std::lock_guard<std::mutex> lk(D->mu);
-        uint8_t seen[257 * 257 / 8 + 1] = {};
-        for (int64_t i = 0; i < ngroups; ++i) {
-            const rsmi_group &d = g[i];
-            if (d.k < 1 || d.n < d.k || d.n > 256 || d.reserved != 0 || d.offset % 16 ||
-                d.shard_stride % 16 || d.shard_stride < d.len)
-                return fail(RSMI_ERR_INVALID, "bad rsmi_group at index " + std::to_string(i));
-            const int key = d.k * 257 + d.n;
-            if (!(seen[key >> 3] & (1 << (key & 7)))) {
-                seen[key >> 3] |= (uint8_t)(1 << (key & 7));
-                const Code *C;
-                rc = ensure_code(*D, d.k, d.n, &C);
-                if (rc) return rc;
-            }
-        }
-        rc = ensure_ws(*D, s, sizeof(rsmi_group) * (size_t)ngroups, &ws);
-        if (rc) return rc;
-    }
-    // pageable -> device copy: returns once the source has been consumed
-    RSMI_HIP(hipMemcpyAsync(ws, g, sizeof(rsmi_group) * (size_t)ngroups, hipMemcpyHostToDevice,
-                            s), "stage ragged descriptors");
-    return encode_ragged_dev(reinterpret_cast<const rsmi_group *>(ws), ngroups, base, s);
+uint64_t *device_code_dir(int *rc) {
+    Device *D = current(rc);
+    return D ? D->code_dir : nullptr;
+}
+
+const uint32_t *device_ptab(int *rc) {
+    Device *D = current(rc);
+    return D ? D->ptab : nullptr;
 }
 
 // ---- synchronous host-memory path (pinned staging, internal stream) --------
@@ -559,7 +535,19 @@ int rsmi_decode_dev(int k, int n, uint8_t *base, int64_t gs, int64_t ss, int len
 }
 
 int rsmi_encode_ragged(const rsmi_group *groups, int64_t ngroups, uint8_t *base, void *stream) {
-    return rsmi::encode_ragged(groups, ngroups, base, (hipStream_t)stream);
+    if (ngroups == 0) return RSMI_OK;
+    rsmi_ragged_plan *plan = nullptr;
+    int rc = rsmi_ragged_plan_create(groups, ngroups, &plan);
+    if (rc) return rc;
+    rc = rsmi_encode_ragged_plan(plan, base, stream);
+    const hipError_t e = hipStreamSynchronize((hipStream_t)stream);
+    rsmi_ragged_plan_destroy(plan);
+    if (rc) return rc;
+    if (e != hipSuccess) {
+        rsmi::set_error(std::string("ragged encode: ") + hipGetErrorString(e));
+        return RSMI_ERR_HIP;
+    }
+    return RSMI_OK;
 }
 
 int rsmi_encode_ragged_dev(const rsmi_group *groups, int64_t ngroups, uint8_t *base,

@@ -94,7 +94,90 @@ __device__ __forceinline__ DevIO make_io(const UniformArgs &a, uint32_t cols, ui
 BS_FOR_EACH_CODE(BS_KERNEL)
 #undef BS_KERNEL
 
+// ---- ragged batches: one launch over (k,n) buckets -------------------------
+// The host plan (ragged.cpp) sorts groups into buckets by code and lays each
+// bucket's 16-B columns out consecutively, padded to whole waves.  colmap[c]
+// = (group << 12) | piece for a real column, ~0u for padding; every wave's
+// 128 columns belong to one bucket (waves[w] = {code index, first column}).
+// Lanes resolve their own group's offset and shard stride, so one wave can
+// mix groups of different lengths; the shard stride varies per lane and goes
+// into the per-lane voffset instead of soffset.
+struct RagIO {
+    __amdgpu_buffer_rsrc_t rsrc;
+    uint32_t o0, o1, ss0, ss1;
+    __device__ __forceinline__ void load(int j, uint32_t (&p)[8]) const {
+        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+        const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rsrc, o0 + j * ss0, 0, 0);
+        const u32x4 y = __builtin_amdgcn_raw_buffer_load_b128(rsrc, o1 + j * ss1, 0, 0);
+        p[0] = x.x; p[1] = x.y; p[2] = x.z; p[3] = x.w;
+        p[4] = y.x; p[5] = y.y; p[6] = y.z; p[7] = y.w;
+    }
+    __device__ __forceinline__ void store(int j, const uint32_t (&q)[8]) const {
+        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+        const u32x4 x = {q[0], q[1], q[2], q[3]};
+        const u32x4 y = {q[4], q[5], q[6], q[7]};
+        __builtin_amdgcn_raw_buffer_store_b128(x, rsrc, o0 + j * ss0, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(y, rsrc, o1 + j * ss1, 0, 0);
+    }
+};
+
+__device__ __forceinline__ void rag_lane(const rsmi_group *groups, uint32_t m, uint32_t &off,
+                                         uint32_t &ss) {
+    if (m == 0xFFFFFFFFu) {
+        off = 0x80000000u;  // out of range: loads read 0, stores dropped
+        ss = 0;
+        return;
+    }
+    const rsmi_group d = groups[m >> 12];
+    off = (uint32_t)d.offset + (m & 4095u) * 16u;
+    ss = d.shard_stride;
+}
+
+__global__ __launch_bounds__(256, BS_OCC) void k_bs_ragged(const rsmi_group *groups,
+                                                           const uint32_t *colmap,
+                                                           const uint2 *waves, uint32_t nwaves,
+                                                           uint8_t *base, uint32_t bytes) {
+    const uint32_t w = blockIdx.x * 4u + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (w >= nwaves) return;
+    const uint2 wr = waves[w];  // {code index, first column}
+    const uint32_t code = __builtin_amdgcn_readfirstlane(wr.x);
+    const uint32_t c0 = __builtin_amdgcn_readfirstlane(wr.y) + (threadIdx.x & 63u);
+    RagIO io;
+    io.rsrc = __builtin_amdgcn_make_buffer_rsrc(base, 0, (int)bytes, 0x00020000);
+    rag_lane(groups, colmap[c0], io.o0, io.ss0);
+    rag_lane(groups, colmap[c0 + 64], io.o1, io.ss1);
+    int idx = 0;
+#define BS_RAG_CASE(K, N)              \
+    if (code == (uint32_t)idx) {       \
+        bs_code_##K##_##N(io);         \
+        return;                        \
+    }                                  \
+    ++idx;
+    BS_FOR_EACH_CODE(BS_RAG_CASE)
+#undef BS_RAG_CASE
+}
+
 }  // namespace
+
+int bitslice_code_index(int k, int n) {
+    int idx = 0;
+#define BS_IDX(K, N)                    \
+    if (k == K && n == N) return idx;   \
+    ++idx;
+    BS_FOR_EACH_CODE(BS_IDX)
+#undef BS_IDX
+    return -1;
+}
+
+hipError_t launch_encode_bitslice_ragged(const rsmi_group *groups, const uint32_t *colmap,
+                                         const uint32_t *waves, uint32_t nwaves, uint8_t *base,
+                                         uint32_t bytes, hipStream_t s) {
+    if (nwaves == 0) return hipSuccess;
+    const uint32_t blocks = (nwaves + 3) / 4;
+    k_bs_ragged<<<blocks, 256, 0, s>>>(groups, colmap, reinterpret_cast<const uint2 *>(waves),
+                                       nwaves, base, bytes);
+    return hipGetLastError();
+}
 
 bool has_bitslice(int k, int n) {
     switch (k * 257 + n) {

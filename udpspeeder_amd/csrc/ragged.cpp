@@ -1,0 +1,174 @@
+// ragged.cpp -- ragged-batch plans (mode-0 mix: every group its own k, n, len).
+//
+// A plan is built once on the host from the rsmi_group descriptors and kept on
+// the device, like an FFT plan: launches over the same batch layout reuse it
+// (and are graph-capturable).  When every group's (k,n) has a specialised
+// bit-sliced network the plan buckets groups by code and maps every 16-byte
+// column to (group, piece) so one launch of k_bs_ragged covers all buckets;
+// otherwise it falls back to the generic one-wave-per-group kernel.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "rsmi_internal.hpp"
+
+namespace rsmi {
+int prepare_code(int k, int n);
+void set_error(const std::string &m);
+uint64_t *device_code_dir(int *rc);
+const uint32_t *device_ptab(int *rc);
+}  // namespace rsmi
+
+struct rsmi_ragged_plan {
+    int device = -1;
+    int64_t ngroups = 0;
+    bool bitslice = false;
+    uint32_t bytes = 0;       // extent of the batch from base (bitslice path)
+    uint32_t nwaves = 0;
+    uint8_t *mem = nullptr;   // one device allocation: groups | colmap | waves
+    rsmi_group *d_groups = nullptr;
+    uint32_t *d_colmap = nullptr;
+    uint32_t *d_waves = nullptr;
+};
+
+namespace {
+
+int fail(int code, const std::string &m) {
+    rsmi::set_error(m);
+    return code;
+}
+
+}  // namespace
+
+extern "C" int rsmi_ragged_plan_create(const rsmi_group *g, int64_t ngroups,
+                                       rsmi_ragged_plan **out) {
+    if (!out || ngroups < 0 || (ngroups > 0 && !g))
+        return fail(RSMI_ERR_INVALID, "invalid ragged plan arguments");
+    *out = nullptr;
+    uint64_t extent = 0;
+    bool bs = ngroups < (int64_t(1) << 20);
+    std::vector<int> code_of((size_t)ngroups, -1);
+    std::vector<uint8_t> seen(257 * 257, 0);
+    for (int64_t i = 0; i < ngroups; ++i) {
+        const rsmi_group &d = g[i];
+        if (d.k < 1 || d.n < d.k || d.n > 256 || d.reserved != 0 || d.offset % 16 ||
+            d.shard_stride % 16 || d.shard_stride < d.len)
+            return fail(RSMI_ERR_INVALID, "bad rsmi_group at index " + std::to_string(i));
+        const int key = d.k * 257 + d.n;
+        if (!seen[key]) {
+            seen[key] = 1;
+            int rc = rsmi::prepare_code(d.k, d.n);
+            if (rc) return rc;
+        }
+        if (d.n == d.k || d.len == 0) continue;  // nothing to compute
+        const uint64_t end = d.offset + (uint64_t)(d.n - 1) * d.shard_stride +
+                             ((d.len + 15u) & ~15u);
+        extent = std::max(extent, end);
+        const int ci = rsmi::bitslice_code_index(d.k, d.n);
+        if (ci < 0 || d.len > 65536) bs = false;
+        code_of[(size_t)i] = ci;
+    }
+    if (extent >= 0x80000000ull) bs = false;
+
+    rsmi_ragged_plan *P = new rsmi_ragged_plan();
+    if (hipGetDevice(&P->device) != hipSuccess) {
+        delete P;
+        return fail(RSMI_ERR_HIP, "hipGetDevice (no usable GPU?)");
+    }
+    P->ngroups = ngroups;
+    P->bitslice = bs;
+    P->bytes = (uint32_t)std::min<uint64_t>(extent, 0x7FFFFFFFull);
+    std::vector<uint32_t> colmap, waves;
+    if (bs) {
+        // bucket -> column count (each bucket padded to whole 128-column waves)
+        int nb = 0;
+        for (int v : code_of) nb = std::max(nb, v + 1);
+        std::vector<uint64_t> cols((size_t)nb, 0), base((size_t)nb, 0), fill((size_t)nb, 0);
+        for (int64_t i = 0; i < ngroups; ++i)
+            if (code_of[(size_t)i] >= 0) cols[(size_t)code_of[(size_t)i]] += (g[i].len + 15) / 16;
+        uint64_t total = 0;
+        for (int b = 0; b < nb; ++b) {
+            base[(size_t)b] = total;
+            total += (cols[(size_t)b] + 127) / 128 * 128;
+        }
+        if (total >= 0xFFFFFF80ull) {
+            delete P;
+            return fail(RSMI_ERR_INVALID, "ragged batch too large for one plan");
+        }
+        colmap.assign((size_t)total + 64, 0xFFFFFFFFu);  // +64: lane c0+64 of the last wave
+        for (int64_t i = 0; i < ngroups; ++i) {
+            const int b = code_of[(size_t)i];
+            if (b < 0) continue;
+            const uint32_t pcs = (g[i].len + 15) / 16;
+            uint64_t c = base[(size_t)b] + fill[(size_t)b];
+            for (uint32_t p = 0; p < pcs; ++p) colmap[(size_t)(c + p)] = ((uint32_t)i << 12) | p;
+            fill[(size_t)b] += pcs;
+        }
+        for (int b = 0; b < nb; ++b)
+            for (uint64_t w = 0; w < (cols[(size_t)b] + 127) / 128; ++w) {
+                waves.push_back((uint32_t)b);
+                waves.push_back((uint32_t)(base[(size_t)b] + 128 * w));
+            }
+        P->nwaves = (uint32_t)(waves.size() / 2);
+    }
+    const size_t gbytes = sizeof(rsmi_group) * (size_t)ngroups;
+    const size_t cbytes = sizeof(uint32_t) * colmap.size();
+    const size_t wbytes = sizeof(uint32_t) * waves.size();
+    const size_t goff = 0, coff = (gbytes + 255) & ~size_t(255),
+                 woff = (coff + cbytes + 255) & ~size_t(255);
+    const size_t all = woff + wbytes + 16;
+    if (hipMalloc(&P->mem, all) != hipSuccess) {
+        delete P;
+        return fail(RSMI_ERR_NOMEM, "hipMalloc(ragged plan)");
+    }
+    P->d_groups = reinterpret_cast<rsmi_group *>(P->mem + goff);
+    P->d_colmap = reinterpret_cast<uint32_t *>(P->mem + coff);
+    P->d_waves = reinterpret_cast<uint32_t *>(P->mem + woff);
+    hipError_t e = hipSuccess;
+    if (gbytes) e = hipMemcpy(P->d_groups, g, gbytes, hipMemcpyHostToDevice);
+    if (e == hipSuccess && cbytes) e = hipMemcpy(P->d_colmap, colmap.data(), cbytes,
+                                                 hipMemcpyHostToDevice);
+    if (e == hipSuccess && wbytes) e = hipMemcpy(P->d_waves, waves.data(), wbytes,
+                                                 hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        (void)hipFree(P->mem);
+        delete P;
+        return fail(RSMI_ERR_HIP, std::string("ragged plan upload: ") + hipGetErrorString(e));
+    }
+    *out = P;
+    return RSMI_OK;
+}
+
+extern "C" int rsmi_encode_ragged_plan(const rsmi_ragged_plan *P, uint8_t *base, void *stream) {
+    if (!P) return fail(RSMI_ERR_INVALID, "null plan");
+    if (P->ngroups == 0) return RSMI_OK;
+    if (!base || ((uintptr_t)base) % 16) return fail(RSMI_ERR_INVALID, "base must be 16-aligned");
+    hipStream_t s = (hipStream_t)stream;
+    hipError_t e;
+    if (P->bitslice) {
+        e = rsmi::launch_encode_bitslice_ragged(P->d_groups, P->d_colmap, P->d_waves, P->nwaves,
+                                                base, P->bytes, s);
+    } else {
+        int rc;
+        const uint64_t *dir = rsmi::device_code_dir(&rc);
+        if (!dir) return rc;
+        const uint32_t *ptab = rsmi::device_ptab(&rc);
+        if (!ptab) return rc;
+        e = rsmi::launch_encode_ragged(P->d_groups, P->ngroups, base, dir, ptab, s);
+    }
+    if (e != hipSuccess) return fail(RSMI_ERR_HIP, std::string("ragged launch: ") + hipGetErrorString(e));
+    return RSMI_OK;
+}
+
+extern "C" int rsmi_ragged_plan_uses_bitslice(const rsmi_ragged_plan *P) {
+    return P && P->bitslice ? 1 : 0;
+}
+
+extern "C" void rsmi_ragged_plan_destroy(rsmi_ragged_plan *P) {
+    if (!P) return;
+    if (P->mem) (void)hipFree(P->mem);
+    delete P;
+}

@@ -59,6 +59,12 @@ hipError_t launch_decode_fused(const UniformArgs &a, const uint8_t *present,
 // when (k,n) has no specialised kernel.
 hipError_t launch_encode_bitslice(const UniformArgs &a, hipStream_t s);
 bool has_bitslice(int k, int n);
+int bitslice_code_index(int k, int n);  // position in the generated code list, -1 if none
+// Ragged bucketed launch over a host-built plan (ragged.cpp): colmap entries
+// (group << 12) | piece, waves = {code index, first column} pairs.
+hipError_t launch_encode_bitslice_ragged(const rsmi_group *groups, const uint32_t *colmap,
+                                         const uint32_t *waves, uint32_t nwaves, uint8_t *base,
+                                         uint32_t bytes, hipStream_t s);
 
 constexpr int kPtabDwords = 8;  // per coefficient: T0lo T0hi T1lo T1hi | T2 pad pad pad
 

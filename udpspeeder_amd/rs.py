@@ -257,6 +257,39 @@ def encode_ragged(base, groups, stream=None) -> None:
                                    _stream_handle(stream)), "rsmi_encode_ragged")
 
 
+class RaggedPlan:
+    """A device-resident plan for one ragged batch layout (rsmi_ragged_plan)."""
+
+    def __init__(self, groups):
+        self._h = C.c_void_p()
+        self.ngroups = len(groups)
+        check(lib().rsmi_ragged_plan_create(C.cast(groups, C.c_void_p), len(groups),
+                                            C.byref(self._h)), "rsmi_ragged_plan_create")
+
+    @property
+    def bitslice(self) -> bool:
+        return bool(lib().rsmi_ragged_plan_uses_bitslice(self._h))
+
+    def encode(self, base, stream=None) -> None:
+        _check_dev(base, "base")
+        check(lib().rsmi_encode_ragged_plan(self._h, base.data_ptr(), _stream_handle(stream)),
+              "rsmi_encode_ragged_plan")
+
+    def close(self) -> None:
+        if self._h:
+            import torch
+            torch.cuda.synchronize()
+            lib().rsmi_ragged_plan_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            if self._h:
+                lib().rsmi_ragged_plan_destroy(self._h)
+        except Exception:
+            pass
+
+
 def encode_ragged_dev(base, dev_groups, ngroups: int, stream=None) -> None:
     """Graph-capturable ragged encode with a device descriptor tensor (uint8,
     24 bytes per group); codes must be resident (prepare_code)."""
