@@ -22,6 +22,12 @@
 #ifndef BS_OCC
 #define BS_OCC 3
 #endif
+#ifndef BS_LD_AUX
+#define BS_LD_AUX 2  // cache-policy bits of the streaming loads (2 = nt: read once)
+#endif
+#ifndef BS_ST_AUX
+#define BS_ST_AUX 2  // cache-policy bits of the parity stores (2 = nt)
+#endif
 #define BS_ACC3(acc, a, b) ((acc) = __builtin_amdgcn_bitop3_b32((acc), (a), (b), 0x96))
 #define BS_ACC2(acc, a) ((acc) ^= (a))
 // keep the generated shard blocks in order so the raw-load ring bounds the
@@ -47,8 +53,8 @@ struct DevIO {
     uint32_t ss;
     __device__ __forceinline__ void load(int j, uint32_t (&p)[8]) const {
         typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-        const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rsrc, v0, j * ss, 0);
-        const u32x4 y = __builtin_amdgcn_raw_buffer_load_b128(rsrc, v1, j * ss, 0);
+        const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rsrc, v0, j * ss, BS_LD_AUX);
+        const u32x4 y = __builtin_amdgcn_raw_buffer_load_b128(rsrc, v1, j * ss, BS_LD_AUX);
         p[0] = x.x; p[1] = x.y; p[2] = x.z; p[3] = x.w;
         p[4] = y.x; p[5] = y.y; p[6] = y.z; p[7] = y.w;
     }
@@ -56,8 +62,8 @@ struct DevIO {
         typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
         const u32x4 x = {q[0], q[1], q[2], q[3]};
         const u32x4 y = {q[4], q[5], q[6], q[7]};
-        __builtin_amdgcn_raw_buffer_store_b128(x, rsrc, v0, j * ss, 0);
-        __builtin_amdgcn_raw_buffer_store_b128(y, rsrc, v1, j * ss, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(x, rsrc, v0, j * ss, BS_ST_AUX);
+        __builtin_amdgcn_raw_buffer_store_b128(y, rsrc, v1, j * ss, BS_ST_AUX);
     }
 };
 

@@ -27,7 +27,16 @@ namespace rsmi {
 namespace {
 
 constexpr int kWaves = 4;      // waves per block (one group each)
-constexpr int kRing = 4;       // survivors in flight per wave
+#ifndef DEC_RING
+#define DEC_RING 4
+#endif
+#ifndef DEC_LD_AUX
+#define DEC_LD_AUX 0           // cache policy of the survivor loads (2 = nt)
+#endif
+#ifndef DEC_ST_AUX
+#define DEC_ST_AUX 0           // cache policy of the rebuilt-row stores
+#endif
+constexpr int kRing = DEC_RING;  // survivors in flight per wave
 constexpr int kRows = 10;      // max e handled by the fused kernel (emax <= kRows)
 constexpr int kPass = 5;       // rows accumulated per pass over the survivors
 constexpr int kTile = 1280;    // bytes per lane-tile pass (64 x 16 + 64 x 4)
@@ -73,7 +82,9 @@ __global__ __launch_bounds__(256, DEC_OCC) void k_decode_fused(UniformArgs a, co
     const int wbytes = wave_lds_bytes(k);
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
-    uint8_t *wl = smem + 5888 + wid * wbytes;
+    const int rows_bytes = ((n - k) * k + 15) & ~15;
+    uint8_t *lrows = smem + 5888;  // the code's parity rows, (n-k) x k
+    uint8_t *wl = smem + 5888 + rows_bytes + wid * wbytes;
     WaveLds L{wl, wl + 256, wl + 512,
               reinterpret_cast<uint32_t *>(wl + 512 + ((kRows * (kRows + k) + 15) & ~15))};
 
@@ -82,6 +93,7 @@ __global__ __launch_bounds__(256, DEC_OCC) void k_decode_fused(UniformArgs a, co
         s2[i] = ptab[i * kPtabDwords + 4];
     }
     for (int i = threadIdx.x; i < 768; i += blockDim.x) smem[5120 + i] = gftab[i];
+    for (int i = threadIdx.x; i < (n - k) * k; i += blockDim.x) lrows[i] = prows[i];
     __syncthreads();
 
     const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
@@ -149,8 +161,8 @@ __global__ __launch_bounds__(256, DEC_OCC) void k_decode_fused(UniformArgs a, co
             for (int q = 0; q < kRing; ++q) {
                 if (q < k) {
                     const uint32_t so = __builtin_amdgcn_readfirstlane(L.sel[q]) * ss;
-                    rq[q] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, v16, so, 0);
-                    rd[q] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, v4, so, 0);
+                    rq[q] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, v16, so, DEC_LD_AUX);
+                    rd[q] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, v4, so, DEC_LD_AUX);
                 }
             }
         };
@@ -161,7 +173,7 @@ __global__ __launch_bounds__(256, DEC_OCC) void k_decode_fused(UniformArgs a, co
         for (int t = lane; t < e * W; t += 64) {
             const int r = t / W, c = t - r * W;
             const int R = L.sel[k - e + r];
-            const uint8_t *prow = prows + (size_t)(R - k) * k;
+            const uint8_t *prow = lrows + (R - k) * k;
             uint8_t v;
             if (c < e) {
                 v = prow[L.miss[c]];
@@ -233,8 +245,8 @@ __global__ __launch_bounds__(256, DEC_OCC) void k_decode_fused(UniformArgs a, co
                             if (j + kRing < k) {
                                 const uint32_t so =
                                     __builtin_amdgcn_readfirstlane(L.sel[j + kRing]) * ss;
-                                rq[q] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, v16, so, 0);
-                                rd[q] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, v4, so, 0);
+                                rq[q] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, v16, so, DEC_LD_AUX);
+                                rd[q] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, v4, so, DEC_LD_AUX);
                             }
                             const uint32_t *tj = L.tab + (j * kRows + rb) * 8;
 #pragma unroll
@@ -259,8 +271,8 @@ __global__ __launch_bounds__(256, DEC_OCC) void k_decode_fused(UniformArgs a, co
                     if (rb + r < e) {
                         const uint32_t so = __builtin_amdgcn_readfirstlane(L.miss[rb + r]) * ss;
                         const u32x4 v = {acc[r][0], acc[r][1], acc[r][2], acc[r][3]};
-                        __builtin_amdgcn_raw_buffer_store_b128(v, rsrc, v16, so, 0);
-                        __builtin_amdgcn_raw_buffer_store_b32(acc[r][4], rsrc, v4, so, 0);
+                        __builtin_amdgcn_raw_buffer_store_b128(v, rsrc, v16, so, DEC_ST_AUX);
+                        __builtin_amdgcn_raw_buffer_store_b32(acc[r][4], rsrc, v4, so, DEC_ST_AUX);
                     }
                 }
             }
@@ -276,13 +288,15 @@ bool decode_fused_ok(int k, int n, int64_t group_stride, int64_t shard_stride, i
     const int m = n - k;
     const int emax = k < m ? k : m;
     return emax <= kRows && n * shard_stride < (int64_t(1) << 31) && len > 0 &&
-           5888 + kWaves * wave_lds_bytes(k) <= 64 * 1024 && group_stride >= n * shard_stride;
+           5888 + ((m * k + 15) & ~15) + kWaves * wave_lds_bytes(k) <= 64 * 1024 &&
+           group_stride >= n * shard_stride;
 }
 
 hipError_t launch_decode_fused(const UniformArgs &a, const uint8_t *present,
                                const uint8_t *parity_rows, int32_t *status,
                                const uint32_t *ptab, const uint8_t *gftab, hipStream_t s) {
-    const size_t lds = 5888 + (size_t)kWaves * wave_lds_bytes(a.k);
+    const size_t lds = 5888 + (size_t)(((a.n - a.k) * a.k + 15) & ~15) +
+                       (size_t)kWaves * wave_lds_bytes(a.k);
     int64_t blocks = (a.ngroups + kWaves - 1) / kWaves;
     const int64_t cap = 256 * 8;
     if (blocks > cap) blocks = cap;
