@@ -41,6 +41,7 @@ def parse():
     p.add_argument("--total-groups", type=int, default=1 << 20, help="strong scaling total (C4)")
     p.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cores)")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-extras", action="store_true", help="skip the C2-worst / C3 lines")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                    help="per-launch HBM bytes from a rocprofv3 --pmc pass (optional)")
     return p.parse_args()
@@ -135,7 +136,18 @@ def main():
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                 "kernel": "encode RS(20,10)", "alg_bytes_per_launch": alg_bytes,
                 "avg_launch_ms": round(enc_ms, 4)}
-    dec_alg = None
+    # decode roofline: k*len read + e*len written for every group with e > 0
+    pres_np = present.cpu().numpy()
+    e_rows = (pres_np[:, :K] == 0).sum(1)
+    dec_alg = int(((e_rows > 0) * K * LEN).sum() + (e_rows * LEN).sum())
+    dec_achieved = dec_alg / (dec_ms * 1e-3) / 1e9
+    roofline_decode = {"bound": "hbm", "achieved": round(dec_achieved, 1), "peak": HBM_PEAK_GBS,
+                       "unit": "GB/s", "frac": round(dec_achieved / HBM_PEAK_GBS, 4),
+                       "kernel": "fused decode RS(20,10), 5 random erasures",
+                       "alg_bytes_per_launch": dec_alg, "avg_launch_ms": round(dec_ms, 4)}
+    extras = None
+    if rank == 0 and world == 1 and not args.no_extras:
+        extras = extra_configs(u, synth, torch, dev, buf, G)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -157,11 +169,62 @@ def main():
             "encode_ms": round(enc_ms, 4), "decode_ms": round(dec_ms, 4),
             "decode_failures": bad,
             "roofline": roofline,
+            "roofline_decode": roofline_decode,
             "cpu_baseline": cpu,
+            "other_configs": extras,
         }
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def _time_ms(torch, fn, reps=10, warm=2):
+    import statistics as st
+    ts = []
+    for i in range(reps + warm):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        fn()
+        b.record()
+        torch.cuda.synchronize()
+        if i >= warm:
+            ts.append(a.elapsed_time(b))
+    return st.median(ts)
+
+
+def extra_configs(u, synth, torch, dev, buf, G):
+    """BASELINE configs beside the headline step (device-resident, N=1):
+    C2 worst case (5 data erasures) and C3 (ragged mode-0 mix)."""
+    n = K + M
+    out = {}
+    # C2 worst case: every group loses 5 data shards
+    pres = torch.from_numpy(synth.erasure_present(synth.ERASE_SEED + 1, 0, G, n, ERASURES,
+                                                  limit=K)).to(dev)
+    st = torch.empty(G, dtype=torch.int32, device=dev)
+    ms = _time_ms(torch, lambda: u.decode(buf, pres, K, n, LEN, status=st))
+    alg = G * (K + ERASURES) * LEN
+    out["c2_worst_5_data_erasures"] = {
+        "decode_ms": round(ms, 4), "groups": G,
+        "payload_GiBps": round(G * K * LEN / (ms * 1e-3) / 2**30, 1),
+        "alg_GBps": round(alg / (ms * 1e-3) / 1e9, 1), "failures": int((st != 0).sum().item())}
+    # C3: ragged mix from -f 1:3,2:4,10:6,20:10, len 64..1250, one bucketed launch
+    table = u.rs_from_str(synth.C3_FEC)
+    ks, ms_, ls = synth.ragged_mix(synth.RAGGED_SEED, 0, G, [y for _, y in table])
+    groups, total = u.make_groups(ks, ks + ms_, ls)
+    base = torch.zeros(total, dtype=torch.uint8, device=dev)
+    dg = u.rs.groups_to_device(groups, dev)
+    u.rs.fill_ragged(base, dg, G, synth.DATA_SEED)
+    plan = u.rs.RaggedPlan(groups)
+    t = _time_ms(torch, lambda: plan.encode(base))
+    alg = int(((ks + ms_) * ls).sum())
+    out["c3_ragged_encode"] = {
+        "encode_ms": round(t, 4), "groups": G, "bitslice_plan": plan.bitslice,
+        "payload_GiBps": round(float((ks * ls).sum()) / (t * 1e-3) / 2**30, 1),
+        "alg_GBps": round(alg / (t * 1e-3) / 1e9, 1), "alg_bytes": alg,
+        "roofline_frac": round(alg / (t * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+    plan.close()
+    del base
+    return out
 
 
 def cpu_baseline(buf, present, G, threads):
