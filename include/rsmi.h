@@ -16,8 +16,11 @@
  * Data shards are j < k, parity shards k <= j < n (same order as the char*
  * data[] array of rs_encode2, lib/rs.h:41).  Each shard holds len payload
  * bytes.  shard_stride must be a multiple of 16 and >= len; group_stride a
- * multiple of 16.  The kernels may read and overwrite the slot padding bytes
- * [len, round_up(len,16)) of a shard slot, never anything beyond it.
+ * multiple of 16.  Slot padding: the kernels may read the bytes
+ * [len, pad_end) of any shard slot and overwrite them in the slots they write
+ * (parity slots for encode, rebuilt data slots for decode), where
+ * pad_end = min(shard_stride, round_up(len, 128)) -- whole cache lines when
+ * the stride has room -- and never touch anything at or beyond pad_end.
  *
  * Every call is asynchronous on `stream` (NULL = the default stream) of the
  * current HIP device, and graph-capturable once the (k,n) code is resident

@@ -21,6 +21,11 @@ def stride_for(ln):
     return max(16, (ln + 15) // 16 * 16)
 
 
+def pad_end(ln, stride):
+    """rsmi.h slot-padding rule: kernels may touch [len, pad_end) only."""
+    return min(stride, (ln + 127) // 128 * 128)
+
+
 def upload(buf, device):
     import torch
     return torch.from_numpy(np.ascontiguousarray(buf)).to(device)
@@ -74,8 +79,8 @@ def test_encode_vs_oracle(gpu, oracle, k, n, ln):
     oracle.encode_batch(k, n, buf.reshape(-1), n * S, S, ln, G)
     out = t.cpu().numpy()
     assert (out[:, :, :ln] == buf[:, :, :ln]).all()
-    # bytes past round_up(len,16) in every slot are never written
-    pad = (ln + 15) // 16 * 16
+    # bytes past the padding bound in every slot are never written
+    pad = pad_end(ln, S)
     assert (out[:, :, pad:] == buf[:, :, pad:]).all()
 
 
@@ -118,7 +123,7 @@ def test_encode_paths_agree(gpu, oracle, bitslice, k, n, ln):
     oracle.encode_batch(k, n, buf.reshape(-1), n * S, S, ln, G)
     out = t.cpu().numpy()
     assert (out[:, :, :ln] == buf[:, :, :ln]).all()
-    pad = (ln + 15) // 16 * 16
+    pad = pad_end(ln, S)
     assert (out[:, :, pad:] == buf[:, :, pad:]).all()
 
 
@@ -232,7 +237,7 @@ def test_decode_paths_agree(gpu, oracle, fused, k, n, ln):
     out = t.cpu().numpy()
     assert (out[:, :k, :ln] == ref[:, :k, :ln]).all()
     assert (out[:, k:] == buf[:, k:]).all()
-    pad = (ln + 15) // 16 * 16
+    pad = pad_end(ln, S)
     assert (out[:, :, pad:] == buf[:, :, pad:]).all()
 
 
@@ -347,7 +352,7 @@ def test_ragged_bitslice_plan_vs_oracle(gpu, oracle):
         got = out[d.offset:d.offset + d.n * d.shard_stride].reshape(d.n, d.shard_stride)
         exp = seg.reshape(d.n, d.shard_stride)
         assert (got[:, :d.len] == exp[:, :d.len]).all(), i
-        pad = (d.len + 15) // 16 * 16
+        pad = pad_end(d.len, d.shard_stride)
         assert (got[:, pad:] == host[d.offset:d.offset + d.n * d.shard_stride]
                 .reshape(d.n, d.shard_stride)[:, pad:]).all(), i
 

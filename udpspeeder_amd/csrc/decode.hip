@@ -153,8 +153,11 @@ __global__ __launch_bounds__(256, DEC_OCC) void k_decode_fused(UniformArgs a, co
         u32x4 rq[kRing];
         uint32_t rd[kRing];
         uint32_t v16, v4;
+        // whole cache lines where the slot has room (rsmi.h padding rule)
+        const int lpad = (int)((a.len + 127) / 128 * 128 < a.shard_stride
+                                   ? (a.len + 127) / 128 * 128 : a.shard_stride);
         auto start_tile = [&](int toff) {
-            const int tlen = a.len - toff;
+            const int tlen = lpad - toff;
             v16 = (16 * lane < tlen) ? (uint32_t)(toff + 16 * lane) : 0x80000000u;
             v4 = (1024 + 4 * lane < tlen) ? (uint32_t)(toff + 1024 + 4 * lane) : 0x80000000u;
 #pragma unroll
