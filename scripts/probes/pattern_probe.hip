@@ -56,6 +56,44 @@ __global__ void copy4(const uint4 *__restrict__ src, uint4 *__restrict__ dst, si
         dst[i] = src[i];
 }
 
+// decode-shaped probe: one wave per group, 20 survivor rows of 1280 B read with a
+// ring of RING rows (dwordx4 for bytes 0..1023 + dword for 1024..1279), E rows written
+template <int RING, int E, int OCC>
+__global__ __launch_bounds__(256, OCC) void dprobe(uint8_t *base, uint32_t G, uint32_t gs, uint32_t ss) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    for (uint32_t g = blockIdx.x * 4u + wid; g < G; g += gridDim.x * 4u) {
+        auto rsrc = __builtin_amdgcn_make_buffer_rsrc(base + (uint64_t)g * gs, 0, (int)gs, 0x00020000);
+        const uint32_t v16 = lane * 16, v4 = 1024 + lane * 4;
+        u32x4 rq[RING];
+        uint32_t rd[RING];
+#pragma unroll
+        for (int q = 0; q < RING; ++q) {
+            rq[q] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, v16, (q + (g & 7)) * ss, 0);
+            rd[q] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, v4, (q + (g & 7)) * ss, 0);
+        }
+        u32x4 acc = {0, 0, 0, 0};
+        uint32_t accd = 0;
+        for (int jb = 0; jb < 20; jb += RING) {
+#pragma unroll
+            for (int q = 0; q < RING; ++q) {
+                const int j = jb + q;
+                acc ^= rq[q];
+                accd ^= rd[q];
+                if (j + RING < 20) {
+                    rq[q] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, v16, (j + RING + (g & 7)) * ss, 0);
+                    rd[q] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, v4, (j + RING + (g & 7)) * ss, 0);
+                }
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < E; ++r) {
+            __builtin_amdgcn_raw_buffer_store_b128(acc + r, rsrc, v16, r * ss, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(accd + r, rsrc, v4, r * ss, 0);
+        }
+    }
+}
+
 template <int U, int AUX>
 __global__ __launch_bounds__(256) void copy_nt(uint8_t *src, uint8_t *dst, uint32_t chunks) {
     // each wave moves U x 1 KiB per step with buffer ops; grid-stride over chunks of U KiB
@@ -153,6 +191,18 @@ int main() {
         });
         printf("copy4 grid %-5d        %.4f ms  %.0f GB/s (read+write)\n", grid, ms,
                2.0 * n4 * 16 / ms / 1e6);
+    }
+    {
+        const double dalg = (double)G * (20 + 3) * 1250;
+        auto drun = [&](const char *name, auto kern, int grid) {
+            float ms = time_ms([&] { kern<<<grid, 256>>>(buf, G, n * S, S); });
+            printf("%-28s %.4f ms  %.0f GB/s alg\n", name, ms, dalg / ms / 1e6);
+        };
+        drun("dprobe ring4 occ4 grid2048", dprobe<4, 3, 4>, 2048);
+        drun("dprobe ring4 occ4 grid4096", dprobe<4, 3, 4>, 4096);
+        drun("dprobe ring4 occ4 grid16384", dprobe<4, 3, 4>, 16384);
+        drun("dprobe ring8 occ4 grid4096", dprobe<8, 3, 4>, 4096);
+        drun("dprobe ring2 occ8 grid8192", dprobe<2, 3, 8>, 8192);
     }
     const uint32_t half = (uint32_t)(bytes / 2);
     uint32_t *sink;

@@ -149,6 +149,10 @@ __global__ __launch_bounds__(256, DEC_OCC) void k_decode_fused(UniformArgs a, co
         const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
             reinterpret_cast<uint8_t *>(gbu), 0, (int)(a.n * a.shard_stride), 0x00020000);
         const uint32_t ss = (uint32_t)a.shard_stride;
+        // survivor j's shard offset lives in lane j (k <= 64 on this path):
+        // v_readlane gives the scalar soffset without an LDS round trip
+        const uint32_t so_lane = (lane < k ? (uint32_t)L.sel[lane] : 0u) * ss;
+        const uint32_t mo_lane = (lane < e ? (uint32_t)L.miss[lane] : 0u) * ss;
         typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
         u32x4 rq[kRing];
         uint32_t rd[kRing];
@@ -163,7 +167,7 @@ __global__ __launch_bounds__(256, DEC_OCC) void k_decode_fused(UniformArgs a, co
 #pragma unroll
             for (int q = 0; q < kRing; ++q) {
                 if (q < k) {
-                    const uint32_t so = __builtin_amdgcn_readfirstlane(L.sel[q]) * ss;
+                    const uint32_t so = __builtin_amdgcn_readlane(so_lane, q);
                     rq[q] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, v16, so, DEC_LD_AUX);
                     rd[q] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, v4, so, DEC_LD_AUX);
                 }
@@ -246,8 +250,7 @@ __global__ __launch_bounds__(256, DEC_OCC) void k_decode_fused(UniformArgs a, co
                                 q2[w] = (x[w] >> 6) & 0x03030303u;
                             }
                             if (j + kRing < k) {
-                                const uint32_t so =
-                                    __builtin_amdgcn_readfirstlane(L.sel[j + kRing]) * ss;
+                                const uint32_t so = __builtin_amdgcn_readlane(so_lane, j + kRing);
                                 rq[q] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, v16, so, DEC_LD_AUX);
                                 rd[q] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, v4, so, DEC_LD_AUX);
                             }
@@ -272,7 +275,7 @@ __global__ __launch_bounds__(256, DEC_OCC) void k_decode_fused(UniformArgs a, co
 #pragma unroll
                 for (int r = 0; r < kPass; ++r) {
                     if (rb + r < e) {
-                        const uint32_t so = __builtin_amdgcn_readfirstlane(L.miss[rb + r]) * ss;
+                        const uint32_t so = __builtin_amdgcn_readlane(mo_lane, rb + r);
                         const u32x4 v = {acc[r][0], acc[r][1], acc[r][2], acc[r][3]};
                         __builtin_amdgcn_raw_buffer_store_b128(v, rsrc, v16, so, DEC_ST_AUX);
                         __builtin_amdgcn_raw_buffer_store_b32(acc[r][4], rsrc, v4, so, DEC_ST_AUX);
@@ -290,7 +293,7 @@ __global__ __launch_bounds__(256, DEC_OCC) void k_decode_fused(UniformArgs a, co
 bool decode_fused_ok(int k, int n, int64_t group_stride, int64_t shard_stride, int len) {
     const int m = n - k;
     const int emax = k < m ? k : m;
-    return emax <= kRows && n * shard_stride < (int64_t(1) << 31) && len > 0 &&
+    return emax <= kRows && k <= 64 && n * shard_stride < (int64_t(1) << 31) && len > 0 &&
            5888 + ((m * k + 15) & ~15) + kWaves * wave_lds_bytes(k) <= 64 * 1024 &&
            group_stride >= n * shard_stride;
 }
