@@ -42,6 +42,9 @@ def parse():
     p.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cores)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-extras", action="store_true", help="skip the C2-worst / C3 lines")
+    p.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL)")
+    p.add_argument("--share-device", action="store_true",
+                   help="map every rank to cuda:0 (rehearsing N>1 on a 1-GPU box, gloo only)")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                    help="per-launch HBM bytes from a rocprofv3 --pmc pass (optional)")
     return p.parse_args()
@@ -61,11 +64,15 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and rank == 0:
         print(f"warning: WORLD_SIZE={world} but --gpus={args.gpus}", file=sys.stderr)
+    if args.share_device:
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", rank=rank, world_size=world,
-                                device_id=dev)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        else:
+            dist.init_process_group(args.backend, rank=rank, world_size=world)
 
     if args.scaling == "weak":
         g0, g1 = shard.weak_range(rank, args.groups)
@@ -109,7 +116,9 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        # max over ranks: the job is as slow as its slowest GPU
+        t = torch.tensor([elapsed], dtype=torch.float64,
+                         device=dev if args.backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     bad = int((status != 0).sum().item())
