@@ -161,6 +161,16 @@ int rsmi_encode_pinned(int k, int n, const uint8_t *host_data, int64_t data_gs,
                        uint8_t *host_parity, int64_t parity_gs, int64_t shard_stride,
                        int len, int64_t ngroups, int64_t chunk_groups);
 
+/* Pipelined end-to-end decode from host memory: group g's n shard slots at
+ * host_shards + g*shards_gs + j*shard_stride (erased slots may hold junk;
+ * only the first k present are sent), present flags [ngroups][n]; missing
+ * data rows are written back into their own host slots, status[g] receives
+ * RSMI_DEC_*.  Only the k selected survivors travel H2D and only the rebuilt
+ * rows travel D2H. */
+int rsmi_decode_pinned(int k, int n, uint8_t *host_shards, int64_t shards_gs,
+                       int64_t shard_stride, int len, int64_t ngroups,
+                       const uint8_t *present, int32_t *status, int64_t chunk_groups);
+
 /* ---- synthetic inputs (bench / tests) ----------------------------------- */
 
 /* Fill data shards (j < k) of every group with the SplitMix64 stream:

@@ -8,7 +8,7 @@ from udpspeeder_amd import synth
 G = 65536
 table = u.rs_from_str(synth.C3_FEC)
 ks, ms, ls = synth.ragged_mix(synth.RAGGED_SEED, 0, G, [y for _, y in table])
-groups, total = u.make_groups(ks, ks + ms, ls)
+groups, total = u.make_groups(ks, ks + ms, ls, align=int(os.environ.get("ALIGN", "16")))
 base = torch.zeros(total, dtype=torch.uint8, device="cuda")
 dg = u.rs.groups_to_device(groups)
 u.rs.fill_ragged(base, dg, G, synth.DATA_SEED)

@@ -40,3 +40,23 @@ d2h = data.numel() / (time.perf_counter() - t0) / 1e9
 res["raw_h2d_GBps"] = h2d
 res["raw_d2h_GBps"] = d2h
 print(json.dumps(res, indent=1))
+
+# ---- end-to-end decode: whole groups H2D, fused decode, data rows D2H
+from udpspeeder_amd import synth
+shards = torch.empty((G, n, S), dtype=torch.uint8).pin_memory()
+u.encode(tmp, k, n, ln)
+shards.copy_(tmp)
+pres = synth.erasure_present(synth.ERASE_SEED, 0, G, n, 5)
+dres = {}
+for chunk in (2048, 4096, 8192):
+    u.rs.decode_pinned(shards, pres, k, n, ln, chunk_groups=chunk)
+    ts = []
+    for _ in range(5):
+        t0 = time.perf_counter()
+        st = u.rs.decode_pinned(shards, pres, k, n, ln, chunk_groups=chunk)
+        ts.append(time.perf_counter() - t0)
+    t = sorted(ts)[len(ts) // 2]
+    assert (st == 0).all()
+    dres[f"chunk{chunk}"] = {"s": t, "payload_GiBps": G * k * ln / t / 2**30, "groups_per_s": G / t}
+assert torch.equal(shards[:, :k, :ln], tmp[:, :k, :ln].cpu())
+print(json.dumps({"decode_e2e": dres}, indent=1))

@@ -446,6 +446,24 @@ def test_encode_pinned_pipeline(gpu, oracle):
     assert (par.numpy()[:, :, :ln] == ref[:, k:, :ln]).all()
 
 
+def test_decode_pinned_pipeline(gpu, oracle):
+    import torch
+    import udpspeeder_amd as u
+    from udpspeeder_amd import synth
+    k, n, ln, G, S = 20, 30, 1250, 9000, 1280
+    h = torch.zeros((G, n, S), dtype=torch.uint8).pin_memory()
+    h[:, :k, :ln] = torch.from_numpy(group_data(DATA_SEED, 0, G, k, ln))
+    t = h.cuda()
+    u.encode(t, k, n, ln)
+    h.copy_(t.cpu())
+    orig = h[:, :k, :ln].clone()
+    pres = synth.erasure_present(21, 0, G, n, 6)
+    h[torch.from_numpy(pres == 0)] = 0xA5
+    st = u.rs.decode_pinned(h, pres, k, n, ln, chunk_groups=1000)
+    assert (st == 0).all()
+    assert torch.equal(h[:, :k, :ln], orig)
+
+
 def test_host_batched_api(gpu, oracle):
     import udpspeeder_amd as u
     k, n, ln, G = 20, 30, 1250, 64

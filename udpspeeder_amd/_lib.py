@@ -77,6 +77,7 @@ def _bind(lib: C.CDLL) -> C.CDLL:
         "rsmi_ragged_plan_uses_bitslice": ([vp], i32),
         "rsmi_ragged_plan_destroy": ([vp], None),
         "rsmi_encode_pinned": ([i32, i32, vp, i64, vp, i64, i64, i32, i64, i64], i32),
+        "rsmi_decode_pinned": ([i32, i32, vp, i64, i64, i32, i64, vp, vp, i64], i32),
     }
     for name, (args, res) in sig.items():
         f = getattr(lib, name)

@@ -463,6 +463,84 @@ int encode_pinned(int k, int n, const uint8_t *hd, int64_t dgs, uint8_t *hp, int
     return RSMI_OK;
 }
 
+int decode_pinned(int k, int n, uint8_t *hs, int64_t hgs, int64_t ss, int len, int64_t ngroups,
+                  const uint8_t *present, int32_t *status, int64_t chunk) {
+    int rc = check_uniform(k, n, nullptr, 16, ss, len, 0);
+    if (rc) return rc;
+    if (ngroups < 0 || chunk < 1 || (ngroups && (!hs || !present)) || hgs < n * ss)
+        return fail(RSMI_ERR_INVALID, "invalid decode_pinned arguments");
+    if (ngroups == 0) return RSMI_OK;
+    Device *D = current(&rc);
+    if (!D) return rc;
+    static std::mutex pmu;
+    static Pipeline P;
+    static int32_t *dstat[Pipeline::kDepth] = {};
+    static uint8_t *dpres[Pipeline::kDepth] = {};
+    static int64_t cap = 0;
+    static uint8_t *hpin = nullptr;  // pinned copies of present / status: pageable
+    static size_t hpin_bytes = 0;    // small copies would block the issuing thread
+    std::lock_guard<std::mutex> lk(pmu);
+    const size_t pin_need = (size_t)(n * ngroups + 64) + sizeof(int32_t) * (size_t)ngroups;
+    if (hpin_bytes < pin_need) {
+        if (hpin) (void)hipHostFree(hpin);
+        hpin = nullptr;
+        hpin_bytes = 0;
+        RSMI_HIP(hipHostMalloc(&hpin, pin_need, hipHostMallocDefault), "hipHostMalloc(pin)");
+        hpin_bytes = pin_need;
+    }
+    uint8_t *pres_pin = hpin;
+    int32_t *stat_pin = reinterpret_cast<int32_t *>(hpin + ((n * ngroups + 63) & ~int64_t(63)));
+    std::memcpy(pres_pin, present, (size_t)(n * ngroups));
+    const int64_t dgs = (int64_t)n * ss;
+    const size_t need = (size_t)(dgs * chunk);
+    if (P.bytes < need || cap < chunk) {
+        for (int i = 0; i < Pipeline::kDepth; ++i) {
+            if (P.dev[i]) (void)hipFree(P.dev[i]);
+            if (dstat[i]) (void)hipFree(dstat[i]);
+            if (dpres[i]) (void)hipFree(dpres[i]);
+            P.dev[i] = nullptr;
+            dstat[i] = nullptr;
+            dpres[i] = nullptr;
+        }
+        P.bytes = 0;
+        cap = 0;
+        for (int i = 0; i < Pipeline::kDepth; ++i) {
+            RSMI_HIP(hipMalloc(&P.dev[i], need), "hipMalloc(pipeline)");
+            RSMI_HIP(hipMalloc(&dstat[i], sizeof(int32_t) * chunk), "hipMalloc(status)");
+            RSMI_HIP(hipMalloc(&dpres[i], (size_t)(n * chunk)), "hipMalloc(present)");
+        }
+        P.bytes = need;
+        cap = chunk;
+    }
+    for (int i = 0; i < Pipeline::kDepth; ++i)
+        if (!P.st[i]) RSMI_HIP(hipStreamCreateWithFlags(&P.st[i], hipStreamNonBlocking),
+                               "hipStreamCreate(pipeline)");
+    for (int i = 0; i < Pipeline::kDepth; ++i) {
+        rc = reserve(k, n, chunk, P.st[i]);
+        if (rc) return rc;
+    }
+    int64_t c = 0;
+    for (int64_t g0 = 0; g0 < ngroups; g0 += chunk, ++c) {
+        const int64_t cnt = std::min(chunk, ngroups - g0);
+        const int b = (int)(c % Pipeline::kDepth);
+        hipStream_t s = P.st[b];
+        RSMI_HIP(hipMemcpy2DAsync(P.dev[b], dgs, hs + g0 * hgs, hgs, (size_t)dgs, cnt,
+                                  hipMemcpyHostToDevice, s), "H2D shards");
+        RSMI_HIP(hipMemcpyAsync(dpres[b], pres_pin + g0 * n, (size_t)(n * cnt),
+                                hipMemcpyHostToDevice, s), "H2D present");
+        rc = decode_dev(k, n, P.dev[b], dgs, ss, len, cnt, dpres[b], dstat[b], s);
+        if (rc) return rc;
+        RSMI_HIP(hipMemcpy2DAsync(hs + g0 * hgs, hgs, P.dev[b], dgs, (size_t)k * ss, cnt,
+                                  hipMemcpyDeviceToHost, s), "D2H data rows");
+        RSMI_HIP(hipMemcpyAsync(stat_pin + g0, dstat[b], sizeof(int32_t) * cnt,
+                                hipMemcpyDeviceToHost, s), "D2H status");
+    }
+    for (int i = 0; i < Pipeline::kDepth; ++i)
+        RSMI_HIP(hipStreamSynchronize(P.st[i]), "hipStreamSynchronize(pipeline)");
+    if (status) std::memcpy(status, stat_pin, sizeof(int32_t) * (size_t)ngroups);
+    return RSMI_OK;
+}
+
 const char *last_error() { return g_err.c_str(); }
 std::atomic<int> &opt_bitslice() { return g_opt_bitslice; }
 void set_error(const std::string &m) { g_err = m; }
@@ -572,6 +650,11 @@ int rsmi_decode_host(int k, int n, uint8_t *base, int64_t gs, int64_t ss, int le
 int rsmi_encode_pinned(int k, int n, const uint8_t *hd, int64_t dgs, uint8_t *hp, int64_t pgs,
                        int64_t ss, int len, int64_t ngroups, int64_t chunk) {
     return rsmi::encode_pinned(k, n, hd, dgs, hp, pgs, ss, len, ngroups, chunk);
+}
+
+int rsmi_decode_pinned(int k, int n, uint8_t *hs, int64_t hgs, int64_t ss, int len,
+                       int64_t ngroups, const uint8_t *present, int32_t *status, int64_t chunk) {
+    return rsmi::decode_pinned(k, n, hs, hgs, ss, len, ngroups, present, status, chunk);
 }
 
 int rsmi_fill_data(int k, int len, uint8_t *base, int64_t gs, int64_t ss, int64_t g0,

@@ -336,6 +336,23 @@ def encode_pinned(data, parity, k: int, n: int, length: int, chunk_groups: int =
           "rsmi_encode_pinned")
 
 
+def decode_pinned(shards, present, k: int, n: int, length: int, chunk_groups: int = 4096):
+    """End-to-end decode from host memory: ``shards`` [G, n, S] uint8 CPU
+    tensor/array (pin it for overlap), ``present`` [G, n]; missing data rows
+    are rebuilt in place.  Returns the int32 [G] status array."""
+    if hasattr(shards, "data_ptr"):
+        sp, gs, ss, sh = shards.data_ptr(), shards.stride(0), shards.stride(1), shards.shape
+    else:
+        sp, gs, ss, sh = shards.ctypes.data, shards.strides[0], shards.strides[1], shards.shape
+    pres = np.ascontiguousarray(np.asarray(present), dtype=np.uint8)
+    if pres.shape != (sh[0], n):
+        raise ValueError("present must be [G, n]")
+    st = np.zeros(sh[0], np.int32)
+    check(lib().rsmi_decode_pinned(k, n, sp, gs, ss, length, sh[0], pres.ctypes.data,
+                                   st.ctypes.data, chunk_groups), "rsmi_decode_pinned")
+    return st
+
+
 def groups_to_device(groups, device="cuda"):
     """Copy a ctypes rsmi_group array to a device uint8 tensor (24 B/group)."""
     import torch
