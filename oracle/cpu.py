@@ -221,3 +221,151 @@ class Reference(_Lib):
         self.encode_batch(k, n, buf, n, 1, 1, k)
         out[k:, :] = buf.reshape(k, n)[:, k:].T
         return out
+
+
+# --------------------------------------------------------------------------
+# Packet cook / de_cook (SURVEY §8f row f2)
+# --------------------------------------------------------------------------
+COOK_ORACLE_SO = os.path.join(HERE, "libcookoracle.so")
+REF_COOK_SO = os.path.join(HERE, "_ref", "libref_cook.so")
+
+NO_CHECKSUM, NO_OBSCURE, NO_XOR = 1, 2, 4
+IV_MAX = 32          # packet.cpp:14 iv_max; the IV array stride of the batch API
+COOK_SEED = 0xC00C1E5
+
+
+def cook_payloads(seed: int, p0: int, npk: int, lens: np.ndarray, stride: int) -> np.ndarray:
+    """[npk, stride] uint8: packet i's bytes 0..lens[i]-1 are SplitMix64 stream
+    seed^(p0+i) (byte q = byte q%8 of word q//8), the rest zero."""
+    lmax = int(lens.max()) if npk else 0
+    words = splitmix_words(seed, np.arange(p0, p0 + npk, dtype=np.uint64), (lmax + 7) // 8)
+    b = words.view(np.uint8).reshape(npk, -1)[:, :lmax]
+    out = np.zeros((npk, stride), np.uint8)
+    out[:, :lmax] = b
+    out[np.arange(stride)[None, :] >= lens[:, None]] = 0
+    return out
+
+
+def cook_ivs(seed: int, p0: int, npk: int, iv_min: int = 4, iv_max: int = 32):
+    """(iv [npk, 32] uint8, iv_len [npk] uint8): iv_len = random_between(iv_min,
+    iv_max) as packet.cpp:81 draws it, bytes from a SplitMix64 stream."""
+    r = splitmix_words(seed ^ 0x1F, np.arange(p0, p0 + npk, dtype=np.uint64), 5)
+    iv_len = (iv_min + (r[:, 0] % np.uint64(iv_max - iv_min + 1))).astype(np.uint8)
+    iv = np.ascontiguousarray(r[:, 1:5]).view(np.uint8).reshape(npk, 32).copy()
+    return iv, iv_len
+
+
+class CookOracle(_Lib):
+    """Our C restatement of packet.cpp's cook (oracle/cook_oracle.c)."""
+
+    def __init__(self, path: str = COOK_ORACLE_SO):
+        super().__init__(path)
+        L = self.lib
+        L.co_crc32h.argtypes = [C.c_void_p, C.c_int]
+        L.co_crc32h.restype = C.c_uint32
+        L.co_do_cook.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_char_p, C.c_int]
+        L.co_de_cook.argtypes = [C.c_void_p, C.c_void_p, C.c_char_p, C.c_int]
+        L.co_cook_batch.argtypes = [C.c_void_p, C.c_int64, C.c_int64, C.c_void_p, C.c_void_p,
+                                    C.c_void_p, C.c_char_p, C.c_int, C.c_void_p]
+        L.co_decook_batch.argtypes = [C.c_void_p, C.c_int64, C.c_int64, C.c_void_p, C.c_char_p,
+                                      C.c_int, C.c_void_p]
+
+    def crc32h(self, data: bytes) -> int:
+        b = np.frombuffer(bytes(data), np.uint8) if len(data) else np.zeros(1, np.uint8)
+        return int(self.lib.co_crc32h(_p(b), len(data)))
+
+    def do_cook(self, data: bytes, iv: bytes, key: bytes = b"", flags: int = 0) -> bytes:
+        buf = np.zeros(len(data) + 4 + len(iv) + 1 + 16, np.uint8)
+        buf[:len(data)] = np.frombuffer(bytes(data), np.uint8)
+        ivb = np.frombuffer(bytes(iv) + b"\0", np.uint8)
+        n = self.lib.co_do_cook(_p(buf), len(data), _p(ivb), len(iv), key, flags)
+        return buf[:n].tobytes()
+
+    def de_cook(self, data: bytes, key: bytes = b"", flags: int = 0):
+        """(status, bytes of the whole input buffer after the call, new len)."""
+        buf = np.frombuffer(bytes(data) + b"\0", np.uint8).copy()
+        ln = C.c_int(len(data))
+        rc = self.lib.co_de_cook(_p(buf), C.byref(ln), key, flags)
+        return rc, buf[:len(data)].tobytes(), ln.value
+
+    def cook_batch(self, buf, stride, lens, iv, iv_len, key=b"", flags=0):
+        npk = len(lens)
+        lens = np.ascontiguousarray(lens, np.int32)
+        out = np.zeros(npk, np.int32)
+        self.lib.co_cook_batch(_p(buf), npk, stride, _p(lens), _p(np.ascontiguousarray(iv)),
+                               _p(np.ascontiguousarray(iv_len, np.uint8)), key, flags, _p(out))
+        return out
+
+    def decook_batch(self, buf, stride, lens, key=b"", flags=0):
+        npk = len(lens)
+        lens = np.ascontiguousarray(lens, np.int32)
+        out = np.zeros(npk, np.int32)
+        self.lib.co_decook_batch(_p(buf), npk, stride, _p(lens), key, flags, _p(out))
+        return out
+
+
+class CookReference(_Lib):
+    """The real reference packet.cpp (oracle/_ref/libref_cook.so), if built.
+    Its transform state lives in process globals, so every call sets them."""
+
+    def __init__(self, path: str = REF_COOK_SO):
+        super().__init__(path)
+        L = self.lib
+        L.ref_cook_config.argtypes = [C.c_int, C.c_int, C.c_int, C.c_char_p, C.c_int, C.c_int]
+        L.ref_crc32h.argtypes = [C.c_void_p, C.c_int]
+        L.ref_crc32h.restype = C.c_uint32
+        L.ref_do_cook.argtypes = [C.c_void_p, C.c_int]
+        L.ref_de_cook.argtypes = [C.c_void_p, C.c_void_p]
+        L.ref_de_cook_batch.argtypes = [C.c_void_p, C.c_int64, C.c_int64, C.c_void_p, C.c_void_p,
+                                        C.c_int]
+        L.ref_do_cook_batch.argtypes = [C.c_void_p, C.c_int64, C.c_int64, C.c_void_p, C.c_void_p]
+
+    @staticmethod
+    def available(path: str = REF_COOK_SO) -> bool:
+        return os.path.exists(path)
+
+    def config(self, key: bytes = b"", flags: int = 0, iv_min: int = 4, iv_max: int = 32):
+        self.lib.ref_cook_config(flags & 1, (flags >> 1) & 1, (flags >> 2) & 1, key, iv_min, iv_max)
+
+    def crc32h(self, data: bytes) -> int:
+        b = np.frombuffer(bytes(data) + b"\0", np.uint8)
+        return int(self.lib.ref_crc32h(_p(b), len(data)))
+
+    def do_cook(self, data: bytes) -> bytes:
+        buf = np.zeros(len(data) + 64, np.uint8)
+        buf[:len(data)] = np.frombuffer(bytes(data), np.uint8)
+        n = self.lib.ref_do_cook(_p(buf), len(data))
+        return buf[:n].tobytes()
+
+    def de_cook(self, data: bytes):
+        buf = np.frombuffer(bytes(data) + b"\0", np.uint8).copy()
+        ln = C.c_int(len(data))
+        rc = self.lib.ref_de_cook(_p(buf), C.byref(ln))
+        return rc, buf[:len(data)].tobytes(), ln.value
+
+    def decook_batch(self, buf, stride, lens, nthreads=1):
+        npk = len(lens)
+        lens = np.ascontiguousarray(lens, np.int32)
+        out = np.zeros(npk, np.int32)
+        self.lib.ref_de_cook_batch(_p(buf), npk, stride, _p(lens), _p(out), nthreads)
+        return out
+
+    def cook_batch(self, buf, stride, lens):
+        npk = len(lens)
+        lens = np.ascontiguousarray(lens, np.int32)
+        out = np.zeros(npk, np.int32)
+        self.lib.ref_do_cook_batch(_p(buf), npk, stride, _p(lens), _p(out))
+        return out
+
+
+def recover_iv(cooked: bytes, plain_len: int, key: bytes = b"", flags: int = 0):
+    """(iv, iv_len) a reference do_cook drew, read back from its output."""
+    if flags & NO_OBSCURE:
+        return b"", 0
+    d = bytearray(cooked)
+    if not (flags & NO_XOR) and key:
+        for i in range(len(d)):
+            d[i] ^= key[i % len(key)]
+    ivl = d[-1]
+    start = plain_len + (0 if flags & NO_CHECKSUM else 4)
+    return bytes(d[start:start + ivl]), ivl
