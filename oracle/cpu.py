@@ -255,6 +255,16 @@ def cook_ivs(seed: int, p0: int, npk: int, iv_min: int = 4, iv_max: int = 32):
     return iv, iv_len
 
 
+def device_ivs(seed: int, p0: int, npk: int):
+    """The IVs rsmi_cook_dev draws when given none (cook.hip): words
+    w_j = mix((seed ^ p) + (j+1)*GAMMA) of packet p; iv_len = 4 + w_0 % 29,
+    iv byte j = byte j%8 of w_{1 + j//8}."""
+    w = splitmix_words(seed, np.arange(p0, p0 + npk, dtype=np.uint64), 5)
+    iv_len = (4 + (w[:, 0] % np.uint64(29))).astype(np.uint8)
+    iv = np.ascontiguousarray(w[:, 1:5]).view(np.uint8).reshape(npk, 32).copy()
+    return iv, iv_len
+
+
 class CookOracle(_Lib):
     """Our C restatement of packet.cpp's cook (oracle/cook_oracle.c)."""
 

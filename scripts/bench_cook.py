@@ -1,0 +1,66 @@
+"""Time the cook / de_cook kernels on framed FEC packets.
+
+Workload: every packet RS(20,10) emits for G groups -- 8-byte header + 1250-byte
+shard = 1258-byte packets, n = 30 per group -- in 1312-byte slots, cooked with
+device-drawn IVs under a key, then de_cooked.  Prints one JSON line.
+
+    python scripts/bench_cook.py [--groups 65536] [--iters 20]
+"""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from udpspeeder_amd.cook import CookContext  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--groups", type=int, default=65536)
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--len", type=int, default=1258)
+    ap.add_argument("--stride", type=int, default=1312)
+    ap.add_argument("--key", default="bench-key")
+    ap.add_argument("--flags", type=int, default=0)
+    args = ap.parse_args()
+    dev = torch.device("cuda:0")
+    npk = args.groups * 30
+    buf = torch.randint(0, 256, (npk, args.stride), dtype=torch.uint8, device=dev)
+    orig = buf[:, :args.len].clone()
+    lens = torch.full((npk,), args.len, dtype=torch.int32, device=dev)
+    out = torch.empty_like(lens)
+    back = torch.empty_like(lens)
+    ctx = CookContext(args.key.encode(), args.flags)
+    s = torch.cuda.current_stream()
+    e = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+    tc = td = 0.0
+    for it in range(args.iters + 2):
+        e[0].record(s)
+        ctx.cook(buf, lens, cap=args.stride, out_len=out, seed=it)
+        e[1].record(s)
+        ctx.decook(buf, out, cap=args.stride, out_len=back)
+        e[2].record(s)
+        torch.cuda.synchronize()
+        if it >= 2:
+            tc += e[0].elapsed_time(e[1])
+            td += e[1].elapsed_time(e[2])
+    assert bool((back == args.len).all()) and torch.equal(buf[:, :args.len], orig)
+    tc /= args.iters
+    td /= args.iters
+    olen = float(out.float().mean())
+    # algorithmic bytes: cook reads len, writes the cooked packet; de_cook reads
+    # the cooked packet, writes len
+    cb = npk * (args.len + olen)
+    print(json.dumps({
+        "packets": npk, "len": args.len, "mean_cooked_len": round(olen, 2),
+        "cook_ms": round(tc, 4), "decook_ms": round(td, 4),
+        "cook_GBps": round(cb / tc / 1e6, 1), "decook_GBps": round(cb / td / 1e6, 1),
+        "cook_Mpps": round(npk / tc / 1e3, 1), "decook_Mpps": round(npk / td / 1e3, 1),
+        "key": args.key, "flags": args.flags}))
+
+
+if __name__ == "__main__":
+    main()

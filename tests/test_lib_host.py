@@ -43,6 +43,19 @@ def test_exports_rsmi_h():
     assert not missing, missing
 
 
+def test_exports_rsmi_cook_h():
+    ex = _exports()
+    decl = _declared("rsmi_cook.h")
+    assert "rsmi_cook_dev" in decl and "rsmi_decook_dev" in decl
+    missing = [d for d in decl if d not in ex]
+    assert not missing, missing
+
+
+def test_every_header_is_checked():
+    assert sorted(os.listdir(os.path.join(ROOT, "include"))) == ["rs_compat.h", "rsmi.h",
+                                                                 "rsmi_cook.h"]
+
+
 def test_exports_rs_compat_h_mangled():
     ex = _exports()
     decl = _declared("rs_compat.h")

@@ -49,6 +49,17 @@ class rsmi_group(C.Structure):
                 ("k", C.c_uint16), ("n", C.c_uint16), ("reserved", C.c_uint32)]
 
 
+class rsmi_packet_batch(C.Structure):  # include/rsmi_cook.h
+    _fields_ = [("base", C.c_void_p), ("offset", C.c_void_p), ("stride", C.c_int64),
+                ("count", C.c_int64), ("cap", C.c_int32), ("reserved", C.c_int32),
+                ("len", C.c_void_p), ("out_len", C.c_void_p)]
+
+
+RSMI_COOK_NO_CHECKSUM, RSMI_COOK_NO_OBSCURE, RSMI_COOK_NO_XOR = 1, 2, 4
+RSMI_COOK_IV_MAX = 32
+RSMI_COOK_MAX_LEN = 65535
+
+
 _lock = threading.Lock()
 _lib = None
 
@@ -78,6 +89,12 @@ def _bind(lib: C.CDLL) -> C.CDLL:
         "rsmi_ragged_plan_destroy": ([vp], None),
         "rsmi_encode_pinned": ([i32, i32, vp, i64, vp, i64, i64, i32, i64, i64], i32),
         "rsmi_decode_pinned": ([i32, i32, vp, i64, i64, i32, i64, vp, vp, i64], i32),
+        "rsmi_cook_ctx_create": ([C.c_char_p, i32, vp], i32),
+        "rsmi_cook_ctx_destroy": ([vp], None),
+        "rsmi_cook_dev": ([vp, vp, vp, vp, C.c_uint64, vp], i32),
+        "rsmi_decook_dev": ([vp, vp, vp], i32),
+        "rsmi_cook_host": ([vp, vp, i64, i64, C.c_int32, vp, vp, vp, vp, C.c_uint64], i32),
+        "rsmi_decook_host": ([vp, vp, i64, i64, C.c_int32, vp, vp], i32),
     }
     for name, (args, res) in sig.items():
         f = getattr(lib, name)
