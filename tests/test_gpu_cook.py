@@ -161,7 +161,9 @@ def test_corruption_vs_oracle(gpu, cook_oracle, flags):
     st = ctx.decook(t, ln, cap=stride).cpu().numpy()
     assert (st == wst).all()
     assert (t.cpu().numpy() == want).all()
-    assert (wst < 0).sum() > npk // 4 and (wst >= 0).sum() > npk // 8
+    assert (wst >= 0).sum() > npk // 8 and (wst < 0).sum() > 0
+    if not flags & NO_CHECKSUM:                  # the crc catches flips and truncations
+        assert (wst < 0).sum() > npk // 4
 
 
 def test_offsets_and_alignment(gpu, cook_oracle):

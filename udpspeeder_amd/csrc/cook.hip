@@ -212,9 +212,10 @@ __global__ __launch_bounds__(kThreads) void k_cook(CookArgs a) {
                     st_piece(pkt + P, d ^ m);
                 }
             }
-            if (ck) {
+            if (ck) {  // the partner packet may need more rounds: only own rounds count
                 c = half_xor(nib_map(T + kCookLane + 128 * hl, c));
-                acc = nib_map(T + kCookRound, acc) ^ c;
+                const uint32_t nacc = nib_map(T + kCookRound, acc) ^ c;
+                acc = r < nr ? nacc : acc;
             }
         }
         uint32_t crc = 0;
@@ -338,9 +339,10 @@ __global__ __launch_bounds__(kThreads) void k_decook(CookArgs a) {
                     c = slice8(T, c, ci.z, ci.w);
                 }
             }
-            if (ck) {
+            if (ck) {  // the partner packet may need more rounds: only own rounds count
                 c = half_xor(nib_map(T + kCookLane + 128 * hl, c));
-                acc = nib_map(T + kCookRound, acc) ^ c;
+                const uint32_t nacc = nib_map(T + kCookRound, acc) ^ c;
+                acc = r < nr ? nacc : acc;
             }
         }
         if (crc_on && ~unshift(T + kCookUns, acc, (uint32_t)(nr * kRound - Lc)) != crc_in) status = -1;
