@@ -1,32 +1,34 @@
 // cook.hip -- batched packet cook / de_cook for gfx950.
 //
 // Semantics: packet.cpp do_cook (:303-308) and de_cook (:310-326), see
-// include/rsmi_cook.h.  One half-wave (32 lanes) owns one packet; a lane owns a
-// 48-byte chunk (three 16-byte pieces) of each 1536-byte round of it.
+// include/rsmi_cook.h.  One half-wave (32 lanes) owns one packet.  A packet is
+// walked in rounds of 96 16-byte pieces (1536 B); in a round lane l owns pieces
+// l, l+32, l+64, so every load and store instruction covers 512 contiguous
+// bytes of each of the wave's two packets.
 //
-// The transform is byte-parallel: piece P of the output is the input piece
-// XOR a key-stream window (KS[p] = key[p % strlen(key)], precomputed per
-// context, read 16-B aligned from L1/L2) XOR an IV window (the packet's IV
-// repeated in LDS, read as five dwords and funnel-shifted by P mod iv_len).
+// The transform is byte-parallel: an output piece is the input piece XOR a
+// key-stream window (KS[p] = key[p % strlen(key)], precomputed per context,
+// read 16-B aligned from L1/L2) XOR an IV window (the packet's IV repeated in
+// LDS, read as five dwords and funnel-shifted by P mod iv_len).
 //
 // CRC-32 (packet.cpp:236-257) is the only serial part.  Raw CRC (register init
 // 0, no final xor) is linear, with Z_d = "feed d zero bytes" a linear map on
-// the 32-bit register:
-//   * each lane folds its chunk with slicing-by-8 (8 x 256-word LDS tables);
-//   * lane l's value is shifted to the round end by Z_{48(31-l)} and the 32
-//     lanes XOR-reduce with ds_swizzle (no lookups in the reduction);
-//   * rounds chain through Z_1536;
-//   * the message is zero-padded to whole rounds, so the result is finally
-//     un-shifted by Z_{-z} (z = padded - len) -- three nibble-table maps for
-//     the three hex digits of z.
+// the 32-bit register.  The message is zero-padded to Q whole pieces; then
+//   * each piece's raw CRC comes from slicing-by-8 (8 x 256-word LDS tables);
+//   * a lane folds its pieces Horner-style, h = Z_512(h) ^ crc(piece);
+//   * h is shifted to the end of the round's data by Z_{16k}, k = pieces after
+//     the lane's last piece (always 0..31: 32 nibble-table maps), and the 32
+//     lanes XOR-reduce with ds_swizzle;
+//   * rounds chain as acc = Z_{16 Q_r}(acc) ^ round, Z_{16 Q_r} being Z_512
+//     applied Q_r/32 times and one lane map;
+//   * the < 16 bytes of zero padding are removed with Z_{-z} (two nibble maps).
 // crc32h's init ~0 is folded in by complementing the first 4 bytes of the
-// zero-padded message, its final ~ at the end.  Linear maps are applied as
-// eight 16-entry nibble tables (512 B per map) so all of them fit in LDS.
+// padded message, its final ~ at the end.
 //
-// Cook writes pieces wholly below len as it goes; the (at most four) pieces
-// that hold the appended crc/iv/iv_len tail are rebuilt after the CRC is known,
-// from a 64-byte per-packet overlay in LDS.  De_cook reads the IV and the
-// stored crc first, then writes every piece in its single pass.
+// Cook keeps the (at most one per lane) piece that holds part of the appended
+// crc/iv/iv_len tail in registers and rebuilds it after the CRC is known from a
+// 64-byte per-packet overlay in LDS.  De_cook issues its first round of loads,
+// then reads iv_len, the IV and the stored crc, then writes every piece.
 #include "rsmi_internal.hpp"
 #include "../../include/rsmi_cook.h"
 
@@ -34,9 +36,9 @@ namespace rsmi {
 namespace {
 
 constexpr int kThreads = 512;           // 8 waves = 16 packets in flight per block
-constexpr int kChunk = 48;              // bytes per lane per round
-constexpr int kRound = 32 * kChunk;     // 1536
-constexpr int kScr = 368;               // per-packet LDS: iv2[288] | overlay[64] | misc[16]
+constexpr int kRound = 1536;            // 96 pieces: 3 per lane
+constexpr int kScrCook = 144;           // per-packet LDS: iv2[64] | overlay[64] | misc[16]
+constexpr int kScrDecook = 304;         // iv2[288] (iv_len up to 255) | misc[16]
 
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
     return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
@@ -121,10 +123,54 @@ __device__ __forceinline__ uint64_t splitmix(uint64_t seed, uint64_t idx, uint64
     return z ^ (z >> 31);
 }
 
-__device__ __forceinline__ uint32_t unshift(const uint32_t *U, uint32_t c, uint32_t z) {
-    c = nib_map(U + 128 * (z & 15), c);
-    c = nib_map(U + 128 * (16 + ((z >> 4) & 15)), c);
-    return nib_map(U + 128 * (32 + (z >> 8)), c);
+// Z_512 as four byte tables.
+__device__ __forceinline__ uint32_t z512(const uint32_t *B, uint32_t c) {
+    return xor3(B[c & 0xff], B[256 + ((c >> 8) & 0xff)], B[512 + ((c >> 16) & 0xff)]) ^
+           B[768 + (c >> 24)];
+}
+
+// Raw CRC of one 16-byte piece.
+__device__ __forceinline__ uint32_t crc16(const uint32_t *T, u32x4 v) {
+    return slice8(T, slice8(T, 0u, v.x, v.y), v.z, v.w);
+}
+
+// Remove z < 16 trailing zero bytes: Z_{-z} = Z_{-(z&3)} o Z_{-4(z>>2)}.
+__device__ __forceinline__ uint32_t unshift(const uint32_t *T, uint32_t c, uint32_t z) {
+    const uint32_t *U = T + kCookUns;
+    const uint32_t lo = z & 3, hi = z >> 2;
+    const uint32_t c1 = nib_map(U + 128 * (lo ? lo - 1 : 0), c);
+    c = lo ? c1 : c;
+    const uint32_t c2 = nib_map(U + 128 * (hi ? hi + 2 : 0), c);
+    return hi ? c2 : c;
+}
+
+// CRC of a round, folded one piece at a time: piece q (= 32p + lane) of the
+// round, crc input v; qr = data pieces of the packet in this round (0..96).
+struct RoundCrc {
+    uint32_t h = 0;
+    int last = -1;
+    __device__ __forceinline__ void add(const uint32_t *T, u32x4 v, int q, int qr) {
+        const uint32_t hn = z512(T + kCookZ512, h) ^ crc16(T, v);
+        h = q < qr ? hn : h;
+        last = q < qr ? q : last;
+    }
+    // The round's raw CRC relative to the end of its data, in all 32 lanes.
+    __device__ __forceinline__ uint32_t finish(const uint32_t *T, int qr) const {
+        int k = qr - 1 - last;
+        k = (last >= 0 && k >= 0 && k < 32) ? k : 0;
+        const uint32_t c = nib_map(T + kCookLane + 128 * k, h);
+        return half_xor(last >= 0 ? c : 0u);
+    }
+};
+
+// acc = Z_{16 qr}(acc): Z_512 (qr / 32) times, then the lane map Z_{16 (qr % 32)}.
+__device__ __forceinline__ uint32_t shift_pieces(const uint32_t *T, uint32_t acc, int qr) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const uint32_t n = z512(T + kCookZ512, acc);
+        acc = i < (qr >> 5) ? n : acc;
+    }
+    return nib_map(T + kCookLane + 128 * (qr & 31), acc);
 }
 
 __device__ __forceinline__ int round16(int x) { return (x + 15) & ~15; }
@@ -141,16 +187,40 @@ __device__ __forceinline__ int wave_max(int v) {
     return a > b ? a : b;
 }
 
+__device__ __forceinline__ uint8_t *packet_ptr(const CookArgs &a, int64_t pk) {
+    return a.base + (a.offset ? a.offset[pk] : (uint64_t)pk * (uint64_t)a.stride);
+}
+
+// The three pieces of round r owned by lane hl: zeros past ext.
+__device__ __forceinline__ void load_round(u32x4 (&d)[3], const uint8_t *pkt, int r, int hl,
+                                           int ext) {
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+        const int P = r * kRound + 16 * (32 * p + hl);
+        d[p] = P < ext ? ld_piece(pkt + P) : u32x4{0, 0, 0, 0};
+    }
+}
+
+__device__ __forceinline__ u32x4 ks_piece(const CookArgs &a, int P) {
+    return a.ks ? *reinterpret_cast<const u32x4 *>(a.ks + P) : u32x4{0, 0, 0, 0};
+}
+
+// CRC input of piece P: bytes below n, the first 4 bytes complemented (init ~0).
+__device__ __forceinline__ u32x4 crc_in(u32x4 v, int P, int n) {
+    u32x4 c = v & piece_mask(n - P);
+    if (P == 0) c.x = ~c.x;
+    return c;
+}
+
 __global__ __launch_bounds__(kThreads) void k_cook(CookArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const bool ck = !(a.flags & RSMI_COOK_NO_CHECKSUM);
     const bool obs = !(a.flags & RSMI_COOK_NO_OBSCURE);
-    const bool kx = a.ks != nullptr;
     if (ck) load_tables(lds, a.tabs);
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63, half = lane >> 5, hl = lane & 31;
-    uint8_t *scr = reinterpret_cast<uint8_t *>(lds + kCookTabWords) + (wid * 2 + half) * kScr;
+    uint8_t *scr = reinterpret_cast<uint8_t *>(lds + kCookTabWords) + (wid * 2 + half) * kScrCook;
     uint32_t *iv2w = reinterpret_cast<uint32_t *>(scr);
-    uint8_t *ovl = scr + 288;
+    uint8_t *ovl = scr + 64;
     const uint32_t *T = lds;
     const int64_t npairs = (a.count + 1) >> 1;
 
@@ -160,68 +230,59 @@ __global__ __launch_bounds__(kThreads) void k_cook(CookArgs a) {
         const bool have = pk < a.count;
         int L = -1, ivl = 0;
         uint8_t *pkt = nullptr;
-        uint64_t iw0 = 0;
         if (have) {
             L = a.len[pk];
-            pkt = a.base + (a.offset ? a.offset[pk] : (uint64_t)pk * (uint64_t)a.stride);
-            if (obs) {
-                if (a.iv) {
-                    ivl = a.iv_len[pk];
-                } else {
-                    iw0 = splitmix(a.seed, (uint64_t)pk, 0);
-                    ivl = 4 + (int)(iw0 % 29u);
-                }
-            }
+            pkt = packet_ptr(a, pk);
+            if (obs) ivl = a.iv ? a.iv_len[pk] : 4 + (int)(splitmix(a.seed, (uint64_t)pk, 0) % 29u);
         }
         const int out = L + (ck ? 4 : 0) + (obs ? ivl + 1 : 0);
         const bool ok = have && L >= 0 && L <= RSMI_COOK_MAX_LEN && ivl <= RSMI_COOK_IV_MAX &&
                         round16(out) <= a.cap && ((uintptr_t)pkt & 3) == 0;
         const int ext = ok ? round16(out) : 0;
-        if (ok && ivl) {  // iv repeated: iv2[t] = iv[t % ivl], t < ivl + 20
+        u32x4 cur[3];
+        load_round(cur, pkt, 0, hl, ext);
+        if (ok && ivl) {  // iv repeated: iv2[t] = iv[t % ivl], t < ivl + 20 (<= 52)
             for (int t = hl; t < ivl + 20; t += 32) {
                 const int j = t % ivl;
-                uint8_t b;
-                if (a.iv)
-                    b = a.iv[pk * RSMI_COOK_IV_MAX + j];
-                else
-                    b = (uint8_t)(splitmix(a.seed, (uint64_t)pk, 1 + (j >> 3)) >> (8 * (j & 7)));
-                scr[t] = b;
+                scr[t] = a.iv ? a.iv[pk * RSMI_COOK_IV_MAX + j]
+                              : (uint8_t)(splitmix(a.seed, (uint64_t)pk, 1 + (j >> 3)) >> (8 * (j & 7)));
             }
         }
         wave_sync();
         const uint32_t magic = ivl ? 0xFFFFFFFFu / (uint32_t)ivl : 0u;
-        const int nr = (ext + kRound - 1) / kRound;
-        const int nrm = wave_max(nr);
+        const int Q = (L + 15) >> 4;            // pieces holding payload (crc input)
+        const int P0 = L & ~15;                 // first piece that holds tail bytes
+        const int nrm = wave_max((ext + kRound - 1) / kRound);
         uint32_t acc = 0;
+        u32x4 dt = {0, 0, 0, 0};                // this lane's tail piece, if any
+        int Pt = -1;
         for (int r = 0; r < nrm; ++r) {
-            uint32_t c = 0;
+            if (r) load_round(cur, pkt, r, hl, ext);   // rounds past the first (long packets)
+            const int qr = min(max(Q - 96 * r, 0), 96);
+            RoundCrc rc;
 #pragma unroll
             for (int p = 0; p < 3; ++p) {
-                const int P = r * kRound + hl * kChunk + p * 16;
-                u32x4 d = {0, 0, 0, 0};
-                if (P < ext) d = ld_piece(pkt + P);
-                if (ck) {
-                    u32x4 ci = d & piece_mask(L - P);
-                    if (P == 0) ci.x = ~ci.x;
-                    c = slice8(T, c, ci.x, ci.y);
-                    c = slice8(T, c, ci.z, ci.w);
-                }
+                const int P = r * kRound + 16 * (32 * p + hl);
+                if (ck) rc.add(T, crc_in(cur[p], P, L), 32 * p + hl, qr);
                 if (P < ext && P + 16 <= L) {  // wholly payload: obscure + xor, store now
-                    u32x4 m = kx ? *reinterpret_cast<const u32x4 *>(a.ks + P) : u32x4{0, 0, 0, 0};
+                    u32x4 m = ks_piece(a, P);
                     if (ivl) m ^= iv_window(iv2w, (uint32_t)P, (uint32_t)ivl, magic);
-                    st_piece(pkt + P, d ^ m);
+                    st_piece(pkt + P, cur[p] ^ m);
+                } else if (P < ext && P >= P0) {
+                    dt = cur[p];
+                    Pt = P;
                 }
+                __builtin_amdgcn_sched_barrier(0);  // one piece's lookups at a time
             }
-            if (ck) {  // the partner packet may need more rounds: only own rounds count
-                c = half_xor(nib_map(T + kCookLane + 128 * hl, c));
-                const uint32_t nacc = nib_map(T + kCookRound, acc) ^ c;
-                acc = r < nr ? nacc : acc;
+            if (ck) {
+                const uint32_t c = rc.finish(T, qr);
+                const uint32_t nacc = (r ? shift_pieces(T, acc, qr) : 0u) ^ c;
+                acc = qr > 0 ? nacc : acc;
             }
         }
         uint32_t crc = 0;
-        if (ck) crc = ~unshift(T + kCookUns, acc, (uint32_t)(nr * kRound - L));
+        if (ck && L > 0) crc = ~unshift(T, acc, (uint32_t)(16 * Q - L));
         // ---- tail: crc (BE), iv, iv_len appended after the payload -------------
-        const int P0 = L & ~15;
         if (ok) {
             for (int t = hl; t < 64; t += 32) {
                 const int pos = P0 + t;
@@ -235,22 +296,18 @@ __global__ __launch_bounds__(kThreads) void k_cook(CookArgs a) {
                         const int w = u - (ck ? 4 : 0);
                         v = w < ivl ? scr[w] : (uint32_t)ivl;
                     }
-                    if (kx) v ^= a.ks[pos];
+                    if (a.ks) v ^= a.ks[pos];
                 }
                 ovl[t] = (uint8_t)v;
             }
         }
         wave_sync();
-        if (ok && hl < 4) {
-            const int P = P0 + 16 * hl;
-            if (P < ext) {
-                const u32x4 d = ld_piece(pkt + P);
-                u32x4 m = kx ? *reinterpret_cast<const u32x4 *>(a.ks + P) : u32x4{0, 0, 0, 0};
-                if (ivl) m ^= iv_window(iv2w, (uint32_t)P, (uint32_t)ivl, magic);
-                const u32x4 o = *reinterpret_cast<const u32x4 *>(ovl + 16 * hl);
-                const u32x4 lo = piece_mask(L - P), hi = piece_mask(out - P);
-                st_piece(pkt + P, ((d ^ m) & lo) | (o & hi & ~lo) | (d & ~hi));
-            }
+        if (Pt >= 0) {
+            u32x4 m = ks_piece(a, Pt);
+            if (ivl) m ^= iv_window(iv2w, (uint32_t)Pt, (uint32_t)ivl, magic);
+            const u32x4 o = *reinterpret_cast<const u32x4 *>(ovl + (Pt - P0));
+            const u32x4 lo = piece_mask(L - Pt), hi = piece_mask(out - Pt);
+            st_piece(pkt + Pt, ((dt ^ m) & lo) | (o & hi & ~lo) | (dt & ~hi));
         }
         if (have && hl == 0) a.out_len[pk] = ok ? out : -1;
         wave_sync();  // the scratch slice is rewritten by the next packet
@@ -261,12 +318,11 @@ __global__ __launch_bounds__(kThreads) void k_decook(CookArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const bool ck = !(a.flags & RSMI_COOK_NO_CHECKSUM);
     const bool obs = !(a.flags & RSMI_COOK_NO_OBSCURE);
-    const bool kx = a.ks != nullptr;
     if (ck) load_tables(lds, a.tabs);
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63, half = lane >> 5, hl = lane & 31;
-    uint8_t *scr = reinterpret_cast<uint8_t *>(lds + kCookTabWords) + (wid * 2 + half) * kScr;
+    uint8_t *scr = reinterpret_cast<uint8_t *>(lds + kCookTabWords) + (wid * 2 + half) * kScrDecook;
     uint32_t *iv2w = reinterpret_cast<uint32_t *>(scr);
-    uint8_t *misc = scr + 352;
+    uint8_t *misc = scr + 288;
     const uint32_t *T = lds;
     const int64_t npairs = (a.count + 1) >> 1;
 
@@ -278,17 +334,20 @@ __global__ __launch_bounds__(kThreads) void k_decook(CookArgs a) {
         uint8_t *pkt = nullptr;
         if (have) {
             L = a.len[pk];
-            pkt = a.base + (a.offset ? a.offset[pk] : (uint64_t)pk * (uint64_t)a.stride);
+            pkt = packet_ptr(a, pk);
         }
         const bool ok = have && L >= 0 && L <= RSMI_COOK_MAX_LEN && round16(L) <= a.cap &&
                         ((uintptr_t)pkt & 3) == 0;
+        const int ext = ok ? round16(L) : 0;
+        u32x4 cur[3];
+        load_round(cur, pkt, 0, hl, ext);       // in flight while the tail is parsed
         // ---- de_obscure bounds (packet.cpp:93-100), read before any store ------
         int status = 0, ivl = 0, L1 = L;
         if (ok && obs) {
             if (L < 1) {
                 status = -1;
             } else {
-                const int v = pkt[L - 1] ^ (kx ? a.ks[L - 1] : 0);
+                const int v = pkt[L - 1] ^ (a.ks ? a.ks[L - 1] : 0);
                 if (L < 1 + v) status = -1;
                 else { ivl = v; L1 = L - 1 - v; }
             }
@@ -297,7 +356,7 @@ __global__ __launch_bounds__(kThreads) void k_decook(CookArgs a) {
         if (ok && ivl) {
             for (int t = hl; t < ivl + 20; t += 32) {
                 const int pos = L1 + t % ivl;
-                scr[t] = pkt[pos] ^ (kx ? a.ks[pos] : 0);
+                scr[t] = pkt[pos] ^ (a.ks ? a.ks[pos] : 0);
             }
         }
         wave_sync();
@@ -307,45 +366,44 @@ __global__ __launch_bounds__(kThreads) void k_decook(CookArgs a) {
         if (ok && ck && status == 0 && Lc < 0) status = -1;
         if (crc_on && hl < 4) {
             const int pos = Lc + hl;
-            uint32_t b = pkt[pos] ^ (kx ? a.ks[pos] : 0);
+            uint32_t b = pkt[pos] ^ (a.ks ? a.ks[pos] : 0);
             if (ivl) b ^= scr[mod_ivl((uint32_t)pos, (uint32_t)ivl, magic)];
             misc[hl] = (uint8_t)b;
         }
         wave_sync();
-        const uint32_t crc_in = crc_on ? __builtin_bswap32(*reinterpret_cast<const uint32_t *>(misc)) : 0u;
-        const int ext = ok ? round16(L) : 0;
-        const int nr = (ext + kRound - 1) / kRound;
-        const int nrm = wave_max(nr);
+        const uint32_t want = crc_on ? __builtin_bswap32(*reinterpret_cast<const uint32_t *>(misc)) : 0u;
+        const int Q = (Lc + 15) >> 4;
+        const int nrm = wave_max((ext + kRound - 1) / kRound);
         uint32_t acc = 0;
         for (int r = 0; r < nrm; ++r) {
-            uint32_t c = 0;
+            if (r) load_round(cur, pkt, r, hl, ext);   // rounds past the first (long packets)
+            const int qr = crc_on ? min(max(Q - 96 * r, 0), 96) : 0;
+            RoundCrc rc;
 #pragma unroll
             for (int p = 0; p < 3; ++p) {
-                const int P = r * kRound + hl * kChunk + p * 16;
+                const int P = r * kRound + 16 * (32 * p + hl);
                 u32x4 o = {0, 0, 0, 0};
                 if (P < ext) {
-                    const u32x4 d = ld_piece(pkt + P);
-                    const u32x4 mk = kx ? *reinterpret_cast<const u32x4 *>(a.ks + P) : u32x4{0, 0, 0, 0};
+                    const u32x4 mk = ks_piece(a, P);
                     const u32x4 mi = ivl ? iv_window(iv2w, (uint32_t)P, (uint32_t)ivl, magic)
                                          : u32x4{0, 0, 0, 0};
-                    if (P + 16 <= L1) o = d ^ mk ^ mi;
-                    else o = d ^ (mk & piece_mask(L - P)) ^ (mi & piece_mask(L1 - P));
+                    if (P + 16 <= L1) o = cur[p] ^ mk ^ mi;
+                    else o = cur[p] ^ (mk & piece_mask(L - P)) ^ (mi & piece_mask(L1 - P));
                     st_piece(pkt + P, o);
                 }
-                if (ck) {
-                    u32x4 ci = o & piece_mask(Lc - P);
-                    if (P == 0) ci.x = ~ci.x;
-                    c = slice8(T, c, ci.x, ci.y);
-                    c = slice8(T, c, ci.z, ci.w);
-                }
+                if (ck) rc.add(T, crc_in(o, P, Lc), 32 * p + hl, qr);
+                __builtin_amdgcn_sched_barrier(0);
             }
-            if (ck) {  // the partner packet may need more rounds: only own rounds count
-                c = half_xor(nib_map(T + kCookLane + 128 * hl, c));
-                const uint32_t nacc = nib_map(T + kCookRound, acc) ^ c;
-                acc = r < nr ? nacc : acc;
+            if (ck) {
+                const uint32_t c = rc.finish(T, qr);
+                const uint32_t nacc = (r ? shift_pieces(T, acc, qr) : 0u) ^ c;
+                acc = qr > 0 ? nacc : acc;
             }
         }
-        if (crc_on && ~unshift(T + kCookUns, acc, (uint32_t)(nr * kRound - Lc)) != crc_in) status = -1;
+        if (crc_on) {
+            const uint32_t got = Lc > 0 ? ~unshift(T, acc, (uint32_t)(16 * Q - Lc)) : 0u;
+            if (got != want) status = -1;
+        }
         if (have && hl == 0) a.out_len[pk] = (!ok || status) ? -1 : (ck ? Lc : L1);
         wave_sync();
     }
@@ -353,14 +411,16 @@ __global__ __launch_bounds__(kThreads) void k_decook(CookArgs a) {
 
 }  // namespace
 
-size_t cook_lds_bytes() { return (size_t)kCookTabWords * 4 + (size_t)(kThreads / 32) * kScr; }
+size_t cook_lds_bytes(bool decook) {
+    return (size_t)kCookTabWords * 4 + (size_t)(kThreads / 32) * (decook ? kScrDecook : kScrCook);
+}
 
 hipError_t launch_cook(const CookArgs &a, bool decook, int max_blocks, hipStream_t s) {
     if (a.count <= 0) return hipSuccess;
     const int64_t pairs = (a.count + 1) / 2;
     int64_t blocks = (pairs + kThreads / 64 - 1) / (kThreads / 64);
     if (blocks > max_blocks) blocks = max_blocks;
-    const size_t lds = cook_lds_bytes();
+    const size_t lds = cook_lds_bytes(decook);
     if (decook)
         k_decook<<<(unsigned)blocks, kThreads, lds, s>>>(a);
     else

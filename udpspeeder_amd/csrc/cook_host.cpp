@@ -76,11 +76,23 @@ struct CrcTables {
         for (int v = 0; v < 256; ++v) blob[v] = t0[v];
         for (int k = 1; k < 8; ++k)
             for (int v = 0; v < 256; ++v) blob[256 * k + v] = feed0(blob[256 * (k - 1) + v]);
-        for (int l = 0; l < 32; ++l) put_map(&blob[rsmi::kCookLane + 128 * l], 48 * (31 - l));
-        put_map(&blob[rsmi::kCookRound], 1536);
-        for (int c = 0; c < 16; ++c) put_map(&blob[rsmi::kCookUns + 128 * c], -c);
-        for (int b = 0; b < 16; ++b) put_map(&blob[rsmi::kCookUns + 128 * (16 + b)], -16 * b);
-        for (int a = 0; a < 8; ++a) put_map(&blob[rsmi::kCookUns + 128 * (32 + a)], -256 * a);
+        for (int k = 0; k < 32; ++k) put_map(&blob[rsmi::kCookLane + 128 * k], 16 * k);
+        // Z_512 as four byte tables: Z(c) = B0[c & 255] ^ B1[c >> 8 & 255] ^ ...
+        uint32_t basis[32];
+        for (int b = 0; b < 32; ++b) {
+            uint32_t c = 1u << b;
+            for (int i = 0; i < 512; ++i) c = feed0(c);
+            basis[b] = c;
+        }
+        for (int t = 0; t < 4; ++t)
+            for (int v = 0; v < 256; ++v) {
+                uint32_t r = 0;
+                for (int b = 0; b < 8; ++b)
+                    if (v >> b & 1) r ^= basis[8 * t + b];
+                blob[rsmi::kCookZ512 + 256 * t + v] = r;
+            }
+        for (int c = 1; c < 4; ++c) put_map(&blob[rsmi::kCookUns + 128 * (c - 1)], -c);
+        for (int c = 1; c < 4; ++c) put_map(&blob[rsmi::kCookUns + 128 * (2 + c)], -4 * c);
     }
 };
 
@@ -135,7 +147,7 @@ extern "C" int rsmi_cook_ctx_create(const char *key, int flags, rsmi_cook_ctx **
         return fail(RSMI_ERR_HIP, "hipGetDevice (no usable GPU?)");
     }
     // LDS per block bounds residency: as many blocks per CU as 160 KiB holds
-    const int per_cu = (int)((160 * 1024) / rsmi::cook_lds_bytes());
+    const int per_cu = (int)((160 * 1024) / rsmi::cook_lds_bytes(true));
     c->max_blocks = cus * (per_cu > 0 ? per_cu : 1) * 2;
     const CrcTables &t = crc_tables();
     hipError_t e = hipMalloc(&c->tabs, sizeof(uint32_t) * t.blob.size());

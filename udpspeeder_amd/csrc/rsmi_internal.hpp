@@ -71,13 +71,13 @@ constexpr int kPtabDwords = 8;  // per coefficient: T0lo T0hi T1lo T1hi | T2 pad
 // ---- packet cook / de_cook (cook.hip, cook_host.cpp) -------------------------------
 // CRC table blob (u32 words), built on the host by cook_host.cpp:
 //   [0, 2048)        slicing-by-8 tables T_k[256], k = 0..7
-//   kCookLane + 128l nibble map of Z_{48(31-l)}, l = 0..31 (lane -> round end)
-//   kCookRound       nibble map of Z_1536 (one round)
-//   kCookUns + 128i  nibble maps of Z_{-c}, Z_{-16b}, Z_{-256a} (i = c, 16+b, 32+a)
+//   kCookLane + 128k nibble map of Z_{16k}, k = 0..31 (k = 0: identity)
+//   kCookZ512        byte map of Z_512 (4 tables of 256 words)
+//   kCookUns + 128i  nibble maps of Z_{-c}, c = 1..3, then Z_{-4c}, c = 1..3
 constexpr int kCookLane = 2048;
-constexpr int kCookRound = kCookLane + 32 * 128;
-constexpr int kCookUns = kCookRound + 128;
-constexpr int kCookTabWords = kCookUns + 40 * 128;
+constexpr int kCookZ512 = kCookLane + 32 * 128;
+constexpr int kCookUns = kCookZ512 + 1024;
+constexpr int kCookTabWords = kCookUns + 6 * 128;
 constexpr int kCookKsBytes = 65536 + 128;  // key stream covers every byte position used
 
 struct CookArgs {
@@ -92,7 +92,7 @@ struct CookArgs {
     const uint32_t *tabs;        // device CRC blob
     const uint8_t *ks;           // device key stream, NULL when there is no XOR stage
 };
-size_t cook_lds_bytes();
+size_t cook_lds_bytes(bool decook);
 hipError_t launch_cook(const CookArgs &a, bool decook, int max_blocks, hipStream_t s);
 
 }  // namespace rsmi
