@@ -1,0 +1,21 @@
+"""Average PMC counters per dispatch for kernels matching a substring:
+    python scripts/pmc_summary.py gpurun_out/pmc_cook cook decook"""
+import collections
+import csv
+import glob
+import sys
+
+root, names = sys.argv[1], sys.argv[2:]
+for p in sorted(glob.glob(f"{root}/p*/run_counter_collection.csv")):
+    agg = collections.defaultdict(lambda: collections.defaultdict(float))
+    for row in csv.DictReader(open(p)):
+        k = row["Kernel_Name"]
+        hit = [n for n in names if ("::" + n + "(") in k]
+        if not hit:
+            continue
+        agg[hit[-1]][(row["Dispatch_Id"], row["Counter_Name"])] += float(row["Counter_Value"])
+    for kn, d in agg.items():
+        per = collections.defaultdict(list)
+        for (disp, c), v in d.items():
+            per[c].append(v)
+        print(p.split("/")[-2], kn, {c: round(sum(v) / len(v)) for c, v in per.items()})

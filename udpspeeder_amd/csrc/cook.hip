@@ -99,11 +99,8 @@ __device__ __forceinline__ u32x4 piece_mask(int v) {
     return m;
 }
 
-// IV bytes iv[(pos + t) % ivl], t = 0..15, from the repeated IV in LDS.
-__device__ __forceinline__ u32x4 iv_window(const uint32_t *iv2w, uint32_t pos, uint32_t ivl,
-                                           uint32_t magic) {
-    uint32_t r = pos - __umulhi(pos, magic) * ivl;
-    if (r >= ivl) r -= ivl;
+// IV bytes iv[(r + t) % ivl], t = 0..15, from the repeated IV in LDS (r < ivl).
+__device__ __forceinline__ u32x4 iv_window_at(const uint32_t *iv2w, uint32_t r) {
     const uint32_t *w = iv2w + (r >> 2);
     const uint32_t sh = r & 3;
     const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3], w4 = w[4];
@@ -113,6 +110,17 @@ __device__ __forceinline__ u32x4 iv_window(const uint32_t *iv2w, uint32_t pos, u
 
 __device__ __forceinline__ uint32_t mod_ivl(uint32_t pos, uint32_t ivl, uint32_t magic) {
     uint32_t r = pos - __umulhi(pos, magic) * ivl;
+    return r >= ivl ? r - ivl : r;
+}
+
+__device__ __forceinline__ u32x4 iv_window(const uint32_t *iv2w, uint32_t pos, uint32_t ivl,
+                                           uint32_t magic) {
+    return iv_window_at(iv2w, mod_ivl(pos, ivl, magic));
+}
+
+// Position of the IV cycle at the next piece a lane owns (512 bytes further).
+__device__ __forceinline__ uint32_t iv_step(uint32_t r, uint32_t s512, uint32_t ivl) {
+    r += s512;
     return r >= ivl ? r - ivl : r;
 }
 
@@ -206,13 +214,15 @@ __device__ __forceinline__ u32x4 ks_piece(const CookArgs &a, int P) {
 }
 
 // CRC input of piece P: bytes below n, the first 4 bytes complemented (init ~0).
+// The byte mask is built only when some lane of the wave holds a piece that
+// ends past n (a wave-uniform branch): most pieces are whole.
 __device__ __forceinline__ u32x4 crc_in(u32x4 v, int P, int n) {
-    u32x4 c = v & piece_mask(n - P);
-    if (P == 0) c.x = ~c.x;
-    return c;
+    if (__ballot(P + 16 > n)) v &= piece_mask(n - P);
+    if (P == 0) v.x = ~v.x;
+    return v;
 }
 
-__global__ __launch_bounds__(kThreads) void k_cook(CookArgs a) {
+__global__ __launch_bounds__(kThreads, 6) void k_cook(CookArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const bool ck = !(a.flags & RSMI_COOK_NO_CHECKSUM);
     const bool obs = !(a.flags & RSMI_COOK_NO_OBSCURE);
@@ -250,6 +260,7 @@ __global__ __launch_bounds__(kThreads) void k_cook(CookArgs a) {
         }
         wave_sync();
         const uint32_t magic = ivl ? 0xFFFFFFFFu / (uint32_t)ivl : 0u;
+        const uint32_t s512 = ivl ? mod_ivl(512u, (uint32_t)ivl, magic) : 0u;
         const int Q = (L + 15) >> 4;            // pieces holding payload (crc input)
         const int P0 = L & ~15;                 // first piece that holds tail bytes
         const int nrm = wave_max((ext + kRound - 1) / kRound);
@@ -260,18 +271,20 @@ __global__ __launch_bounds__(kThreads) void k_cook(CookArgs a) {
             if (r) load_round(cur, pkt, r, hl, ext);   // rounds past the first (long packets)
             const int qr = min(max(Q - 96 * r, 0), 96);
             RoundCrc rc;
+            uint32_t ivr = ivl ? mod_ivl((uint32_t)(r * kRound + 16 * hl), (uint32_t)ivl, magic) : 0u;
 #pragma unroll
             for (int p = 0; p < 3; ++p) {
                 const int P = r * kRound + 16 * (32 * p + hl);
                 if (ck) rc.add(T, crc_in(cur[p], P, L), 32 * p + hl, qr);
                 if (P < ext && P + 16 <= L) {  // wholly payload: obscure + xor, store now
                     u32x4 m = ks_piece(a, P);
-                    if (ivl) m ^= iv_window(iv2w, (uint32_t)P, (uint32_t)ivl, magic);
+                    if (ivl) m ^= iv_window_at(iv2w, ivr);
                     st_piece(pkt + P, cur[p] ^ m);
                 } else if (P < ext && P >= P0) {
                     dt = cur[p];
                     Pt = P;
                 }
+                if (ivl) ivr = iv_step(ivr, s512, (uint32_t)ivl);
                 __builtin_amdgcn_sched_barrier(0);  // one piece's lookups at a time
             }
             if (ck) {
@@ -314,7 +327,7 @@ __global__ __launch_bounds__(kThreads) void k_cook(CookArgs a) {
     }
 }
 
-__global__ __launch_bounds__(kThreads) void k_decook(CookArgs a) {
+__global__ __launch_bounds__(kThreads, 6) void k_decook(CookArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const bool ck = !(a.flags & RSMI_COOK_NO_CHECKSUM);
     const bool obs = !(a.flags & RSMI_COOK_NO_OBSCURE);
@@ -353,6 +366,7 @@ __global__ __launch_bounds__(kThreads) void k_decook(CookArgs a) {
             }
         }
         const uint32_t magic = ivl ? 0xFFFFFFFFu / (uint32_t)ivl : 0u;
+        const uint32_t s512 = ivl ? mod_ivl(512u, (uint32_t)ivl, magic) : 0u;
         if (ok && ivl) {
             for (int t = hl; t < ivl + 20; t += 32) {
                 const int pos = L1 + t % ivl;
@@ -379,19 +393,20 @@ __global__ __launch_bounds__(kThreads) void k_decook(CookArgs a) {
             if (r) load_round(cur, pkt, r, hl, ext);   // rounds past the first (long packets)
             const int qr = crc_on ? min(max(Q - 96 * r, 0), 96) : 0;
             RoundCrc rc;
+            uint32_t ivr = ivl ? mod_ivl((uint32_t)(r * kRound + 16 * hl), (uint32_t)ivl, magic) : 0u;
 #pragma unroll
             for (int p = 0; p < 3; ++p) {
                 const int P = r * kRound + 16 * (32 * p + hl);
                 u32x4 o = {0, 0, 0, 0};
                 if (P < ext) {
                     const u32x4 mk = ks_piece(a, P);
-                    const u32x4 mi = ivl ? iv_window(iv2w, (uint32_t)P, (uint32_t)ivl, magic)
-                                         : u32x4{0, 0, 0, 0};
+                    const u32x4 mi = ivl ? iv_window_at(iv2w, ivr) : u32x4{0, 0, 0, 0};
                     if (P + 16 <= L1) o = cur[p] ^ mk ^ mi;
                     else o = cur[p] ^ (mk & piece_mask(L - P)) ^ (mi & piece_mask(L1 - P));
                     st_piece(pkt + P, o);
                 }
                 if (ck) rc.add(T, crc_in(o, P, Lc), 32 * p + hl, qr);
+                if (ivl) ivr = iv_step(ivr, s512, (uint32_t)ivl);
                 __builtin_amdgcn_sched_barrier(0);
             }
             if (ck) {
