@@ -233,6 +233,43 @@ def extra_configs(u, synth, torch, dev, buf, G):
         "roofline_frac": round(alg / (t * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
     plan.close()
     del base
+    # f2: cook + de_cook of every packet C1 emits (8-B header + 1250-B shard)
+    from udpspeeder_amd.cook import CookContext
+    plen, pstride = 8 + LEN, 1312
+    npk = G * n
+    pk = torch.empty((npk, pstride), dtype=torch.uint8, device=dev)
+    pk[:, :8] = 0x5A
+    pk.view(G, n, pstride)[:, :, 8:8 + LEN] = buf[:, :, :LEN]
+    lens = torch.full((npk,), plen, dtype=torch.int32, device=dev)
+    olen = torch.empty_like(lens)
+    back = torch.empty_like(lens)
+    ctx = CookContext(b"bench-key", 0)
+    tcs, tds = [], []
+    for i in range(6):  # refill, cook, de_cook: the round trip must restore the packets
+        pk.view(G, n, pstride)[:, :, 8:8 + LEN] = buf[:, :, :LEN]
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+        e[0].record()
+        ctx.cook(pk, lens, cap=pstride, out_len=olen, seed=7 + i)
+        e[1].record()
+        ctx.decook(pk, olen, cap=pstride, out_len=back)
+        e[2].record()
+        torch.cuda.synchronize()
+        if i:
+            tcs.append(e[0].elapsed_time(e[1]))
+            tds.append(e[1].elapsed_time(e[2]))
+    tc, td = statistics.median(tcs), statistics.median(tds)
+    ok = bool((back == plen).all()) and torch.equal(
+        pk.view(G, n, pstride)[:, :, 8:8 + LEN], buf[:, :, :LEN])
+    cooked = float(olen.float().mean())
+    alg = npk * (plen + cooked)
+    out["f2_cook_decook"] = {
+        "packets": npk, "len": plen, "key": True, "cook_ms": round(tc, 4),
+        "decook_ms": round(td, 4), "cook_Mpps": round(npk / tc / 1e3, 1),
+        "decook_Mpps": round(npk / td / 1e3, 1),
+        "cook_frac": round(alg / (tc * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+        "decook_frac": round(alg / (td * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "roundtrip_ok": ok}
+    ctx.close()
+    del pk
     return out
 
 

@@ -7,6 +7,7 @@ set -e
 R=$PWD
 cd /tmp && export TMPDIR=/tmp
 SETS=${PMC_SETS:-"FETCH_SIZE;WRITE_SIZE;SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT;SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVES;SQ_BUSY_CYCLES SQ_WAVE_CYCLES"}
+mkdir -p $R/gpurun_out/pmc_cook
 IFS=';' read -ra ARR <<< "$SETS"
 i=0
 for set in "${ARR[@]}"; do
