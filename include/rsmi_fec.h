@@ -1,0 +1,114 @@
+/*
+ * rsmi_fec.h -- batched FEC framing on MI355X.
+ *
+ * UDPspeeder's fec_encode_manager_t (fec_manager.h:271-365,
+ * fec_manager.cpp:174-447) turns the packets a connection sends into FEC
+ * groups: it collects them (mode 0: a length-prefixed "blob" split into k
+ * equal shards, fec_manager.cpp:35-75; mode 1: one packet per data shard,
+ * zero-padded to the longest), picks (k, m) (short_packet_optimize,
+ * fec_manager.cpp:267-288), prefixes every shard with the 8-byte header
+ *     seq (u32 big-endian) | mode | k | m | index      (fec_manager.cpp:318-333)
+ * and calls rs_encode2 once per group (fec_manager.cpp:364).
+ *
+ * Here one rsmi_fenc object holds one manager's state.  A batch of input()
+ * calls is planned on the host -- the exact decisions of
+ * fec_encode_manager_t::input/output, which need only packet lengths -- and
+ * the byte work (blob assembly, padding, headers, the RS encode of every
+ * group) runs on the GPU in a few launches over a slot array:
+ *
+ *   slot s occupies [s*slot_stride, (s+1)*slot_stride) of slots_base;
+ *   its packet starts at +8 (8-byte header) and its shard at +16.
+ *
+ * Every packet the reference's output() would return is listed, in the
+ * reference's order, as (slot, length); packet bytes are slots_base +
+ * slot*slot_stride + 8 .. + length.  Results are byte-identical to the
+ * reference's packets, with one documented difference: in mode 0 the bytes of
+ * the last data shard past the blob's end are zero here, where the reference
+ * sends whatever its blob buffer held there before (stale bytes of earlier
+ * groups, fec_manager.cpp:67-75); the parity covers the zeros.  The receiver
+ * never reads those bytes (blob_decode_t::output, fec_manager.cpp:97-129).
+ *
+ * Packets still waiting for their group at the end of a batch (the
+ * reference's pending input_buf / blob) are copied into a device carry area
+ * owned by the encoder, so the caller may reuse its input buffer once the
+ * batch's work on the stream has completed.
+ */
+#ifndef RSMI_FEC_H_
+#define RSMI_FEC_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RSMI_FEC_MAX_PACKETS 255 /* max_fec_packet_num (fec_manager.h:18) */
+#define RSMI_FEC_HEADER 8        /* u32 seq + mode + k + m + index        */
+
+/* fec_parameter_t (fec_manager.h:26-180) without the timer fields. */
+typedef struct rsmi_fec_config {
+    int32_t mode;      /* 0 or 1 (-f mode, fec_parameter_t::mode)          */
+    int32_t mtu;       /* fec_parameter_t::mtu, default 1250 (common.h:105) */
+    int32_t queue_len; /* fec_parameter_t::queue_len, default 200          */
+    int32_t short_packet_optimize; /* the global of fec_manager.cpp:30 (1) */
+    int32_t header_overhead;       /* the global of fec_manager.cpp:31 (40) */
+    int32_t rs_cnt;    /* x of the last -f point (get_tail().x)            */
+    uint8_t rs_y[RSMI_FEC_MAX_PACKETS + 1]; /* rs_par[x-1].y, x = 1..rs_cnt  */
+} rsmi_fec_config;
+
+/* fec_parameter_t::rs_from_str (fec_manager.h:40-136) plus the defaults
+ * above: "20:10" or "1:3,2:4,10:6,20:10".  Returns RSMI_OK, or
+ * RSMI_ERR_INVALID where the reference returns -1. */
+int rsmi_fec_config_init(rsmi_fec_config *cfg, const char *rs_str, int mode, int mtu,
+                         int queue_len);
+
+typedef struct rsmi_fenc rsmi_fenc;
+
+/* A manager with the given config whose first group gets sequence number
+ * seq0 (the reference draws it, get_fake_random_number, fec_manager.h:327). */
+int rsmi_fenc_create(const rsmi_fec_config *cfg, uint32_t seq0, rsmi_fenc **out);
+void rsmi_fenc_destroy(rsmi_fenc *enc);
+
+/* New parameters, taken up when the next group starts -- the reference's
+ * fec_par.clone(g_fec_par) at counter == 0 (fec_manager.cpp:207-209). */
+int rsmi_fenc_set_config(rsmi_fenc *enc, const rsmi_fec_config *cfg);
+
+/* One emitted packet: output() after input() call `event` returned it. */
+typedef struct rsmi_fenc_packet {
+    int64_t slot;   /* slot index in the batch's slot array                */
+    int32_t len;    /* bytes from slot start + 8 (header included)         */
+    int32_t event;  /* index of the input() call in the batch              */
+} rsmi_fenc_packet;
+
+/* Plan a batch of input() calls on the host.  len[i] >= 0 is input(s, len[i])
+ * with the packet at in_base + in_off[i] (device memory; the buffer needs 16
+ * readable bytes past every packet); len[i] < 0 is input(0, 0), the timer
+ * flush (tunnel_client.cpp:41).  ret[i] (host, may be NULL) receives input()'s
+ * return value (0, or -1 where the reference logs and drops the packet).
+ * Afterwards *n_slots, *n_packets give the sizes of the batch and
+ * *slot_stride_min the least slot_stride rsmi_fenc_run_dev accepts.
+ * The plan replaces the previous one; state advances as if input() had been
+ * called for every event. */
+int rsmi_fenc_plan(rsmi_fenc *enc, int64_t n_events, const int32_t *len, const uint64_t *in_off,
+                   const uint8_t *in_base, int32_t *ret, int64_t *n_slots, int64_t *n_packets,
+                   int32_t *slot_stride_min);
+
+/* Copy the planned packet list (n_packets entries, host). */
+int rsmi_fenc_packets(const rsmi_fenc *enc, rsmi_fenc_packet *out);
+
+/* Per-group view of the plan (host arrays of n_groups entries, any may be
+ * NULL): first slot, k, m, shard length (fec_len) and sequence number. */
+int rsmi_fenc_groups(const rsmi_fenc *enc, int64_t *n_groups, int64_t *slot0, int32_t *k,
+                     int32_t *m, int32_t *fec_len, uint32_t *seq);
+
+/* Run the planned batch on `stream`: frame every group (headers, blob or
+ * padded shards) and the mode-1 packets sent ahead of their group, RS-encode
+ * every group's parity slots, and move still-pending packets into the carry
+ * area.  slots_base: device, 16-aligned, n_slots * slot_stride bytes;
+ * slot_stride: a multiple of 16, >= slot_stride_min.  Asynchronous. */
+int rsmi_fenc_run_dev(rsmi_fenc *enc, uint8_t *slots_base, int64_t slot_stride, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RSMI_FEC_H_ */

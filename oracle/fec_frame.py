@@ -1,0 +1,246 @@
+"""TEST INFRASTRUCTURE ONLY -- a CPU restatement of UDPspeeder's FEC framing
+(SURVEY §8f row f1), the checker for include/rsmi_fec.h.  Nothing here is
+shipped or called by the product path.
+
+* :class:`EncodeManager` restates ``fec_encode_manager_t::input`` / ``output``
+  (fec_manager.cpp:174-460) and ``blob_encode_t`` (:35-75) in plain Python;
+  parity comes from the C restatement of lib/fec.cpp (oracle/rs_oracle.c).
+  One deliberate difference from the reference, the same as the GPU path's:
+  in mode 0 the bytes of the last data shard past the blob's end are zero,
+  where the reference sends stale bytes of earlier blobs.
+* :class:`FecReference` drives the REAL reference managers
+  (oracle/_ref/libref_fec.so, fec_manager.cpp compiled unmodified), for the
+  golden generator and for pinning this restatement.
+* :func:`zero_stale_tail` rewrites a reference mode-0 group the way the
+  restatement frames it (stale bytes zeroed, parity recomputed by the
+  reference codec), which is what tests/golden/fec_encode.npz stores.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from typing import List, Optional, Tuple
+
+import numpy as np
+
+from oracle.cpu import Oracle
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REF_FEC_SO = os.path.join(HERE, "_ref", "libref_fec.so")
+HEADER = 8
+MAX_FEC_PACKET_NUM = 255
+
+
+def rs_table(rs_str: str) -> List[int]:
+    """rs_par[x-1].y for x = 1..rs_cnt (fec_manager.h:40-136)."""
+    from udpspeeder_amd.fec_param import rs_from_str
+    t = rs_from_str(rs_str)
+    if t is None:
+        raise ValueError(rs_str)
+    return [y for _, y in t]
+
+
+def _round_up_div(a: int, b: int) -> int:  # common.cpp:747-749
+    return (a + b - 1) // b
+
+
+def _hdr(seq: int, mode: int, k: int, m: int, idx: int) -> bytes:  # fec_manager.cpp:318-333
+    return seq.to_bytes(4, "big") + bytes([mode, k, m, idx & 0xFF])
+
+
+class EncodeManager:
+    """fec_encode_manager_t restated.  input(None) is input(0, 0)."""
+
+    def __init__(self, rs_str: str, mode: int, mtu: int, queue_len: int, seq0: int,
+                 short_packet_optimize: int = 1, header_overhead: int = 40,
+                 oracle: Optional[Oracle] = None):
+        self.y = rs_table(rs_str)
+        self.mode, self.mtu, self.queue_len = mode, mtu, queue_len
+        self.spo, self.overhead = short_packet_optimize, header_overhead
+        self.seq = seq0 & 0xFFFFFFFF
+        self.pend: List[bytes] = []
+        self.blob_len = 4
+        self.ready: List[bytes] = []
+        self.oracle = oracle or Oracle()
+
+    @property
+    def tail_x(self) -> int:
+        return len(self.y)
+
+    def _shard_len(self, n: int, nxt: int) -> int:  # blob_encode_t::get_shard_len :51-53
+        return _round_up_div(self.blob_len + 2 + nxt, n)
+
+    def _append(self, s: bytes):  # :174-204
+        self.pend.append(bytes(s))
+        if self.mode == 0:
+            self.blob_len += 2 + len(s)
+
+    def _parity(self, shards: List[bytes], k: int, n: int, ln: int) -> List[bytes]:
+        stride = max(16, (ln + 15) // 16 * 16)
+        buf = np.zeros(n * stride, np.uint8)
+        for i, s in enumerate(shards):
+            buf[i * stride:i * stride + ln] = np.frombuffer(s, np.uint8)
+        self.oracle.encode_batch(k, n, buf, n * stride, stride, ln, 1)
+        return [buf[j * stride:j * stride + ln].tobytes() for j in range(k, n)]
+
+    def input(self, s: Optional[bytes]) -> int:
+        mode = self.mode
+        has = s is not None
+        ln = len(s) if has else 0
+        if has and ln > 65535:
+            return -1
+        if mode == 0 and has and not self.pend:
+            if self._shard_len(self.tail_x, ln) > self.mtu:  # :217-223
+                return -1
+        if not has and not self.pend:  # :228-231
+            return -1
+        about = not has
+        delayed = False
+        if mode == 0 and self._shard_len(self.tail_x, ln) > self.mtu:  # :235-238
+            about = delayed = True
+        if has and not delayed:
+            self._append(s)
+        counter = len(self.pend)
+        if mode == 0 and counter == self.queue_len:
+            about = True
+        if mode == 1 and counter == self.tail_x:
+            about = True
+        out: List[bytes] = []
+        if about:
+            if mode == 0:
+                tx = self.tail_x
+                k, m = tx, self.y[tx - 1]
+                if self.spo:  # short_packet_optimize :264-288
+                    best_len = (self._shard_len(tx, 0) + self.overhead) * (tx + m)
+                    best = tx
+                    for i in range(1, tx):
+                        sl = self._shard_len(i, 0)
+                        if sl > self.mtu:
+                            continue
+                        nl = (sl + self.overhead) * (i + self.y[i - 1])
+                        if nl < best_len:
+                            best_len, best = nl, i
+                    k, m = best, self.y[best - 1]
+                fec_len = _round_up_div(self.blob_len, k)
+                blob = bytearray(len(self.pend).to_bytes(4, "big"))
+                for p in self.pend:
+                    blob += len(p).to_bytes(2, "big") + p
+                blob += bytes(k * fec_len - len(blob))  # zero tail (the reference: stale)
+                data = [bytes(blob[i * fec_len:(i + 1) * fec_len]) for i in range(k)]
+                par = self._parity(data, k, k + m, fec_len)
+                for i in range(k + m):
+                    out.append(_hdr(self.seq, 0, k, m, i) + (data + par)[i])
+            else:
+                k = counter
+                m = self.y[counter - 1]
+                fec_len = max(len(p) + 2 for p in self.pend)
+                data = [(len(p).to_bytes(2, "big") + p).ljust(fec_len, b"\0") for p in self.pend]
+                par = self._parity(data, k, k + m, fec_len)
+                if has:  # fast send: the last data packet goes with the parity
+                    out.append(_hdr(self.seq, 1, 0, 0, k - 1) + data[k - 1][:len(self.pend[-1]) + 2])
+                for i in range(k, k + m):
+                    out.append(_hdr(self.seq, 1, k, m, i) + par[i - k])
+            self.seq = (self.seq + 1) & 0xFFFFFFFF
+            self.pend = []
+            self.blob_len = 4
+        elif has and mode == 1:  # encode_fast_send :394-429
+            i = counter - 1
+            out.append(_hdr(self.seq, 1, 0, 0, i) + len(s).to_bytes(2, "big") + bytes(s))
+        if has and delayed:
+            self._append(s)
+        self.ready = out
+        return 0
+
+    def output(self) -> List[bytes]:
+        r, self.ready = self.ready, []
+        return r
+
+
+def zero_stale_tail(packets: List[bytes], ref_rs) -> Tuple[List[bytes], int]:
+    """A reference mode-0 group (all k+m packets) with the stale bytes past the
+    blob's end zeroed and the parity recomputed by the reference codec
+    (oracle/_ref/libref_rs.so).  Returns (packets, number of nonzero stale
+    bytes replaced)."""
+    k, m = packets[0][5], packets[0][6]
+    n = k + m
+    fec_len = len(packets[0]) - HEADER
+    blob = b"".join(p[HEADER:] for p in packets[:k])
+    cnt = int.from_bytes(blob[:4], "big")
+    pos = 4
+    for _ in range(cnt):
+        pos += 2 + int.from_bytes(blob[pos:pos + 2], "big")
+    stale = sum(1 for b in blob[pos:] if b)
+    blob = blob[:pos] + bytes(len(blob) - pos)
+    stride = max(16, (fec_len + 15) // 16 * 16)
+    buf = np.zeros(n * stride, np.uint8)
+    for i in range(k):
+        buf[i * stride:i * stride + fec_len] = np.frombuffer(blob[i * fec_len:(i + 1) * fec_len], np.uint8)
+    ref_rs.encode_batch(k, n, buf, n * stride, stride, fec_len, 1)
+    out = [packets[i][:HEADER] + buf[i * stride:i * stride + fec_len].tobytes() for i in range(n)]
+    return out, stale
+
+
+class FecReference:
+    """The real reference managers (oracle/_ref/libref_fec.so).  The managers'
+    parameters live in the process-global g_fec_par; config() sets them and
+    managers created afterwards copy them (fec_manager.cpp:154)."""
+
+    def __init__(self, path: str = REF_FEC_SO):
+        self.lib = C.CDLL(path)
+        L = self.lib
+        L.ref_fec_config.argtypes = [C.c_char_p, C.c_int, C.c_int, C.c_int]
+        L.ref_fenc_new.restype = C.c_void_p
+        L.ref_fenc_free.argtypes = [C.c_void_p]
+        L.ref_fdec_new.restype = C.c_void_p
+        L.ref_fdec_free.argtypes = [C.c_void_p]
+        for f in (L.ref_fenc_run, L.ref_fdec_run):
+            f.argtypes = [C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                          C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64]
+            f.restype = C.c_int64
+
+    @staticmethod
+    def available(path: str = REF_FEC_SO) -> bool:
+        return os.path.exists(path)
+
+    def config(self, rs_str: str, mode: int, mtu: int = 1250, queue_len: int = 200):
+        if self.lib.ref_fec_config(rs_str.encode(), mode, mtu, queue_len) != 0:
+            raise ValueError(rs_str)
+
+    def _run(self, fn, h, events: List[Optional[bytes]]):
+        n = len(events)
+        lens = np.array([-1 if e is None else len(e) for e in events], np.int32)
+        offs = np.zeros(n, np.uint64)
+        o = 0
+        for i, e in enumerate(events):
+            offs[i] = o
+            o += 0 if e is None else len(e)
+        buf = np.frombuffer(b"".join(e for e in events if e is not None) + bytes(16), np.uint8).copy()
+        ret = np.zeros(n, np.int32)
+        cap = max(1 << 20, 64 * (o + 1) + 4096 * n)
+        maxo = 300 * n + 16
+        out = np.zeros(cap, np.uint8)
+        pos = np.zeros(maxo, np.int64)
+        ol = np.zeros(maxo, np.int32)
+        ev = np.zeros(maxo, np.int32)
+        p = lambda a: a.ctypes.data_as(C.c_void_p)
+        np_ = fn(h, n, p(lens), p(offs), p(buf), p(ret), p(out), cap, p(pos), p(ol), p(ev), maxo)
+        if np_ < 0:
+            raise RuntimeError("reference output overflow")
+        pk = [out[pos[j]:pos[j] + ol[j]].tobytes() for j in range(np_)]
+        return ret, pk, ev[:np_].copy()
+
+    def encode(self, events: List[Optional[bytes]]):
+        """Feed a fresh fec_encode_manager_t; returns (ret[], packets[], event[])."""
+        h = self.lib.ref_fenc_new()
+        try:
+            return self._run(self.lib.ref_fenc_run, h, events)
+        finally:
+            self.lib.ref_fenc_free(h)
+
+    def decode(self, packets: List[bytes]):
+        """Feed a fresh fec_decode_manager_t; returns (ret[], outputs[], event[])."""
+        h = self.lib.ref_fdec_new()
+        try:
+            return self._run(self.lib.ref_fdec_run, h, packets)
+        finally:
+            self.lib.ref_fdec_free(h)

@@ -1,0 +1,97 @@
+"""TEST INFRASTRUCTURE ONLY -- regenerate tests/golden/fec_encode.npz from the
+REAL reference fec_encode_manager_t.
+
+Run in the build container (where /root/reference exists):
+
+    make -C oracle && python -m oracle.gen_golden_fec
+
+Each case sets g_fec_par (-f string, mode, mtu, queue_len), feeds a fresh
+reference manager a seeded event sequence -- packets of seeded lengths whose
+bytes are the SplitMix64 stream of (seed, event index) (oracle.cpu.cook_payloads),
+and input(0, 0) timer flushes -- and records every input() return value and
+every packet output() returned, with the event it followed.  Mode-0 groups are
+stored as oracle.fec_frame.zero_stale_tail rewrites them: the reference's stale
+bytes past the blob's end zeroed and the parity recomputed by the reference
+codec (the count of nonzero stale bytes replaced is recorded).  The encoder's
+first sequence number (random in the reference) is read from its first header.
+
+Fixtures are data only: lengths, return codes, packet lengths / events, the
+packet bytes themselves for the small cases and a sha256 of all of them.
+"""
+from __future__ import annotations
+
+import hashlib
+import os
+
+import numpy as np
+
+from oracle.cpu import Reference, cook_payloads, splitmix_words
+from oracle.fec_frame import FecReference, zero_stale_tail
+
+OUT = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "golden")
+FEC_SEED = 0xFEC0
+FULL_BYTES_MAX = 120_000
+
+# name, -f, mode, mtu, queue_len, events, max len, flush per mille, zero-len per mille
+CASES = [
+    ("m0_20_10", "20:10", 0, 1250, 200, 400, 1300, 20, 10),
+    ("m0_c3", "1:3,2:4,10:6,20:10", 0, 1250, 200, 400, 400, 50, 20),
+    ("m0_small_queue", "3:2", 0, 100, 5, 300, 60, 100, 50),
+    ("m0_queue3", "20:10", 0, 1250, 3, 200, 500, 30, 0),
+    ("m0_no_parity", "4:0", 0, 300, 200, 150, 200, 50, 50),
+    ("m0_tiny", "2:1,8:4", 0, 40, 200, 300, 30, 60, 300),
+    ("m1_20_10", "20:10", 1, 1250, 200, 300, 1200, 50, 10),
+    ("m1_c3", "1:3,2:4,10:6,20:10", 1, 1250, 200, 400, 300, 100, 20),
+    ("m1_no_parity", "5:0", 1, 1250, 200, 150, 100, 80, 50),
+    ("m1_long", "3:2", 1, 1250, 200, 60, 3600, 100, 0),
+]
+
+
+def case_events(ci: int, n: int, lmax: int, flush_pm: int, zero_pm: int):
+    r = splitmix_words(FEC_SEED ^ (ci << 20), np.arange(n, dtype=np.uint64), 3)
+    lens = (r[:, 0] % np.uint64(lmax + 1)).astype(np.int64)
+    lens[(r[:, 1] % np.uint64(1000)) < np.uint64(zero_pm)] = 0
+    lens[(r[:, 2] % np.uint64(1000)) < np.uint64(flush_pm)] = -1
+    lens = lens.astype(np.int32)
+    pay = cook_payloads(FEC_SEED + ci, 0, n, np.maximum(lens, 0), max(1, int(lens.max(initial=0))))
+    ev = [None if lens[i] < 0 else pay[i, :lens[i]].tobytes() for i in range(n)]
+    return lens, ev
+
+
+def main():
+    fr, rr = FecReference(), Reference()
+    arrays = {}
+    names = []
+    for ci, (name, rs, mode, mtu, ql, n, lmax, fpm, zpm) in enumerate(CASES):
+        fr.config(rs, mode, mtu, ql)
+        lens, ev = case_events(ci, n, lmax, fpm, zpm)
+        ret, pk, pev = fr.encode(ev)
+        stale = 0
+        if mode == 0:
+            fixed, j = [], 0
+            while j < len(pk):
+                k, m = pk[j][5], pk[j][6]
+                g, s = zero_stale_tail(pk[j:j + k + m], rr)
+                fixed += g
+                stale += s
+                j += k + m
+            pk = fixed
+        blob = b"".join(pk)
+        seq0 = int.from_bytes(pk[0][:4], "big") if pk else 0
+        arrays[f"{name}__lens"] = lens
+        arrays[f"{name}__ret"] = np.asarray(ret, np.int32)
+        arrays[f"{name}__pk_len"] = np.array([len(p) for p in pk], np.int32)
+        arrays[f"{name}__pk_event"] = np.asarray(pev, np.int32)
+        arrays[f"{name}__meta"] = np.array([ci, mode, mtu, ql, seq0, stale], np.int64)
+        arrays[f"{name}__rs"] = np.frombuffer(rs.encode(), np.uint8)
+        arrays[f"{name}__sha256"] = np.frombuffer(hashlib.sha256(blob).digest(), np.uint8)
+        if len(blob) <= FULL_BYTES_MAX:
+            arrays[f"{name}__pk_bytes"] = np.frombuffer(blob, np.uint8)
+        names.append(name)
+        print(f"{name}: {n} events, {len(pk)} packets, {len(blob)} B, stale bytes zeroed {stale}")
+    arrays["cases"] = np.array(names)
+    np.savez_compressed(os.path.join(OUT, "fec_encode.npz"), **arrays)
+
+
+if __name__ == "__main__":
+    main()

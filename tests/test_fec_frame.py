@@ -1,0 +1,182 @@
+"""FEC framing: fec_encode_manager_t batched on the GPU.
+
+CPU tests pin the Python restatement (oracle/fec_frame.py) to the fixtures the
+REAL reference manager produced (tests/golden/fec_encode.npz, written by
+oracle/gen_golden_fec.py), and check librsmi.so's host planner -- return codes,
+packet lengths, output() order, group boundaries -- against them without a GPU.
+GPU tests frame + encode through the C ABI and compare every packet byte with
+the fixtures and, at larger sizes, with the restatement; batches are cut at
+arbitrary event boundaries so groups straddle batches (the carry area).
+"""
+import hashlib
+import os
+
+import numpy as np
+import pytest
+
+from oracle.cpu import cook_payloads
+from oracle.fec_frame import EncodeManager
+from oracle.gen_golden_fec import CASES, case_events
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "fec_encode.npz")
+
+
+@pytest.fixture(scope="module")
+def fx():
+    return dict(np.load(GOLDEN))
+
+
+def _case(fx, name):
+    ci = [c[0] for c in CASES].index(name)
+    _, rs, mode, mtu, ql, n, lmax, fpm, zpm = CASES[ci]
+    lens, ev = case_events(ci, n, lmax, fpm, zpm)
+    assert (lens == fx[f"{name}__lens"]).all()
+    meta = fx[f"{name}__meta"]
+    return dict(rs=rs, mode=mode, mtu=mtu, ql=ql, lens=lens, ev=ev, seq0=int(meta[4]),
+                ret=fx[f"{name}__ret"], pk_len=fx[f"{name}__pk_len"],
+                pk_event=fx[f"{name}__pk_event"], sha=fx[f"{name}__sha256"].tobytes(),
+                full=fx.get(f"{name}__pk_bytes"))
+
+
+def _expected_packets(c):
+    if c["full"] is None:
+        return None
+    off = np.concatenate([[0], np.cumsum(c["pk_len"])])
+    b = c["full"].tobytes()
+    return [b[off[i]:off[i + 1]] for i in range(len(c["pk_len"]))]
+
+
+NAMES = [c[0] for c in CASES]
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_oracle_matches_reference_fixtures(fx, name):
+    c = _case(fx, name)
+    em = EncodeManager(c["rs"], c["mode"], c["mtu"], c["ql"], c["seq0"])
+    ret, pk, pev = [], [], []
+    for i, e in enumerate(c["ev"]):
+        ret.append(em.input(e))
+        o = em.output()
+        pk += o
+        pev += [i] * len(o)
+    assert ret == list(c["ret"])
+    assert pev == list(c["pk_event"])
+    assert [len(p) for p in pk] == list(c["pk_len"])
+    assert hashlib.sha256(b"".join(pk)).digest() == c["sha"]
+    exp = _expected_packets(c)
+    if exp is not None:
+        assert pk == exp
+
+
+@pytest.mark.parametrize("name", NAMES)
+@pytest.mark.parametrize("nbatch", [1, 3])
+def test_planner_matches_reference_fixtures(fx, name, nbatch):
+    """librsmi.so's planner (no GPU): ret, packet lengths and events, group headers."""
+    from udpspeeder_amd.fec import FecEncoder
+    c = _case(fx, name)
+    enc = FecEncoder(c["rs"], c["mode"], c["mtu"], c["ql"], seq0=c["seq0"])
+    lens = c["lens"]
+    cuts = np.linspace(0, len(lens), nbatch + 1).astype(int)
+    ret, plen, pev, nslot = [], [], [], 0
+    for a, b in zip(cuts[:-1], cuts[1:]):
+        offs = np.zeros(b - a, np.uint64)
+        p = enc.plan_host(lens[a:b], offs)
+        ret += list(p.ret)
+        plen += list(p.packets["len"])
+        pev += list(p.packets["event"] + a)
+        assert (p.packets["slot"] >= 0).all() and (p.packets["slot"] < p.n_slots).all()
+        nslot += p.n_slots
+    assert ret == list(c["ret"])
+    assert plen == list(c["pk_len"])
+    assert pev == list(c["pk_event"])
+    enc.close()
+
+
+def _run_gpu(enc, lens, ev, cuts, torch):
+    """Run the events through the GPU in batches; returns the emitted packets."""
+    out = []
+    for a, b in zip(cuts[:-1], cuts[1:]):
+        ln = lens[a:b]
+        offs = np.zeros(b - a, np.uint64)
+        o = 0
+        chunks = []
+        for i in range(a, b):
+            offs[i - a] = o
+            if ev[i] is not None:
+                chunks.append(ev[i])
+                o += len(ev[i])
+        host = np.frombuffer(b"".join(chunks) + bytes(32), np.uint8)
+        inbuf = torch.from_numpy(host.copy()).cuda()
+        p = enc.plan(ln, offs, inbuf)
+        S = max(p.slot_stride_min, 16)
+        slots = torch.full((max(1, p.n_slots) * S,), 0xEE, dtype=torch.uint8, device="cuda")
+        enc.run(slots, S)
+        h = slots.cpu().numpy()
+        del inbuf  # the carry area holds what the next batch needs
+        out += [(h[s * S + 8:s * S + 8 + l].tobytes(), int(e) + a) for s, l, e in p.packets]
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", NAMES)
+@pytest.mark.parametrize("nbatch", [1, 4])
+def test_gpu_frames_match_reference(fx, gpu, name, nbatch):
+    import torch
+    from udpspeeder_amd.fec import FecEncoder
+    c = _case(fx, name)
+    enc = FecEncoder(c["rs"], c["mode"], c["mtu"], c["ql"], seq0=c["seq0"])
+    rng = np.random.default_rng(len(name) * 7 + nbatch)
+    n = len(c["lens"])
+    cuts = np.unique(np.concatenate([[0, n], rng.integers(0, n, nbatch - 1)])) if nbatch > 1 \
+        else np.array([0, n])
+    out = _run_gpu(enc, c["lens"], c["ev"], cuts, torch)
+    pk = [p for p, _ in out]
+    assert [e for _, e in out] == list(c["pk_event"])
+    assert [len(p) for p in pk] == list(c["pk_len"])
+    exp = _expected_packets(c)
+    if exp is not None:
+        bad = [i for i, (a, b) in enumerate(zip(pk, exp)) if a != b]
+        assert not bad, (len(bad), bad[:5])
+    assert hashlib.sha256(b"".join(pk)).digest() == c["sha"]
+    enc.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rs,mode,mtu,ql,lmax", [
+    ("20:10", 0, 1250, 200, 1250), ("1:3,2:4,10:6,20:10", 0, 1250, 200, 700),
+    ("20:10", 1, 1250, 200, 1250), ("10:5,40:20", 0, 1400, 200, 1400),
+    ("1:3,2:4,10:6,20:10", 1, 1250, 200, 900)])
+def test_gpu_frames_match_oracle_large(gpu, rs, mode, mtu, ql, lmax):
+    """Thousands of groups per batch, several batches, against the restatement."""
+    import torch
+    from udpspeeder_amd.fec import FecEncoder
+    rng = np.random.default_rng(mtu + lmax + mode)
+    n = 12000
+    lens = rng.integers(0, lmax + 1, n).astype(np.int32)
+    lens[rng.random(n) < 0.01] = -1
+    pay = cook_payloads(0xF00D + mode, 0, n, np.maximum(lens, 0), lmax)
+    ev = [None if lens[i] < 0 else pay[i, :lens[i]].tobytes() for i in range(n)]
+    enc = FecEncoder(rs, mode, mtu, ql, seq0=0xFFFFFFF0)
+    em = EncodeManager(rs, mode, mtu, ql, 0xFFFFFFF0)
+    exp = []
+    for i, e in enumerate(ev):
+        em.input(e)
+        exp += [(p, i) for p in em.output()]
+    out = _run_gpu(enc, lens, ev, np.array([0, 5000, 5001, n]), torch)
+    assert len(out) == len(exp)
+    bad = [i for i, (a, b) in enumerate(zip(out, exp)) if a != b]
+    assert not bad, (len(bad), bad[:5])
+    enc.close()
+
+
+@pytest.mark.gpu
+def test_gpu_per_call_interface(gpu):
+    """input()/output() one event at a time, as fec_manager's callers use it
+    (misc.cpp:401-411: three packets then the timer flush)."""
+    from udpspeeder_amd.fec import FecEncoder
+    enc = FecEncoder("20:10", 0, 1250, 200, seq0=77)
+    em = EncodeManager("20:10", 0, 1250, 200, 77)
+    for d in [b"11111", b"22", b"33333333", None, b"a" * 7, b"b" * 13, b"ccc", None]:
+        assert enc.input(d) == em.input(d)
+        assert enc.output() == em.output()
+    enc.close()

@@ -51,9 +51,17 @@ def test_exports_rsmi_cook_h():
     assert not missing, missing
 
 
+def test_exports_rsmi_fec_h():
+    ex = _exports()
+    decl = _declared("rsmi_fec.h")
+    assert "rsmi_fenc_plan" in decl and "rsmi_fenc_run_dev" in decl
+    missing = [d for d in decl if d not in ex]
+    assert not missing, missing
+
+
 def test_every_header_is_checked():
     assert sorted(os.listdir(os.path.join(ROOT, "include"))) == ["rs_compat.h", "rsmi.h",
-                                                                 "rsmi_cook.h"]
+                                                                 "rsmi_cook.h", "rsmi_fec.h"]
 
 
 def test_exports_rs_compat_h_mangled():

@@ -55,6 +55,16 @@ class rsmi_packet_batch(C.Structure):  # include/rsmi_cook.h
                 ("len", C.c_void_p), ("out_len", C.c_void_p)]
 
 
+class rsmi_fec_config(C.Structure):  # include/rsmi_fec.h
+    _fields_ = [("mode", C.c_int32), ("mtu", C.c_int32), ("queue_len", C.c_int32),
+                ("short_packet_optimize", C.c_int32), ("header_overhead", C.c_int32),
+                ("rs_cnt", C.c_int32), ("rs_y", C.c_uint8 * 256)]
+
+
+class rsmi_fenc_packet(C.Structure):
+    _fields_ = [("slot", C.c_int64), ("len", C.c_int32), ("event", C.c_int32)]
+
+
 RSMI_COOK_NO_CHECKSUM, RSMI_COOK_NO_OBSCURE, RSMI_COOK_NO_XOR = 1, 2, 4
 RSMI_COOK_IV_MAX = 32
 RSMI_COOK_MAX_LEN = 65535
@@ -95,6 +105,14 @@ def _bind(lib: C.CDLL) -> C.CDLL:
         "rsmi_decook_dev": ([vp, vp, vp], i32),
         "rsmi_cook_host": ([vp, vp, i64, i64, C.c_int32, vp, vp, vp, vp, C.c_uint64], i32),
         "rsmi_decook_host": ([vp, vp, i64, i64, C.c_int32, vp, vp], i32),
+        "rsmi_fec_config_init": ([vp, C.c_char_p, i32, i32, i32], i32),
+        "rsmi_fenc_create": ([vp, C.c_uint32, vp], i32),
+        "rsmi_fenc_set_config": ([vp, vp], i32),
+        "rsmi_fenc_destroy": ([vp], None),
+        "rsmi_fenc_plan": ([vp, i64, vp, vp, vp, vp, vp, vp, vp], i32),
+        "rsmi_fenc_packets": ([vp, vp], i32),
+        "rsmi_fenc_groups": ([vp, vp, vp, vp, vp, vp, vp], i32),
+        "rsmi_fenc_run_dev": ([vp, vp, i64, vp], i32),
     }
     for name, (args, res) in sig.items():
         f = getattr(lib, name)

@@ -1,0 +1,481 @@
+// fec_enc.cpp -- host side of the batched FEC framing (include/rsmi_fec.h).
+//
+// The planner replays fec_encode_manager_t::input() and ::output()
+// (fec_manager.cpp:174-460) event by event.  Every decision there depends only
+// on packet lengths, so it runs here without touching payload bytes.  It emits
+// framing jobs for the GPU (frame.hip), the list of packets the reference's
+// output() would have returned, and the encode launches.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "rsmi_internal.hpp"
+#include "../../include/rsmi_fec.h"
+
+namespace rsmi {
+void set_error(const std::string &m);
+}
+
+using rsmi::CarryCopy;
+using rsmi::FrameGroup;
+using rsmi::FrameSrc;
+
+namespace {
+
+int fail(int code, const std::string &m) {
+    rsmi::set_error(m);
+    return code;
+}
+
+int round_up_div(int a, int b) { return (a + b - 1) / b; }  // common.cpp:747-749
+
+// Payload addresses in a plan: a device address in the batch input, or (tag
+// bit set) an offset in carry buffer 0 / 1, resolved when the batch runs so
+// that planning needs no device.
+constexpr uint64_t kCarryTag = 1ull << 63, kCarryBuf1 = 1ull << 62, kCarryOff = kCarryBuf1 - 1;
+
+struct Pending {
+    uint64_t addr;  // batch-input device address or tagged carry offset
+    uint32_t len;
+    int64_t emitted;  // mode 1: index in this batch's packet list of its early send, -1 if none
+};
+
+// One encode launch over a run of consecutive groups with the same code and
+// shard length.
+struct Run {
+    int64_t slot0, count;
+    int k, n, len;
+};
+
+}  // namespace
+
+struct rsmi_fenc {
+    rsmi_fec_config cfg;
+    rsmi_fec_config next_cfg;
+    bool has_next = false;
+    uint32_t seq;
+    int blob_len = 4;  // blob_encode_t::current_len (starts at sizeof(u32), :38-42)
+    std::vector<Pending> pend;  // the open group's inputs, in order
+
+    // ---- last plan
+    std::vector<FrameGroup> jobs;
+    std::vector<FrameSrc> srcs;
+    std::vector<CarryCopy> carry;
+    std::vector<rsmi_fenc_packet> packets;
+    std::vector<int64_t> g_slot0;
+    std::vector<int32_t> g_k, g_m, g_len;
+    std::vector<uint32_t> g_seq;
+    std::vector<Run> runs;
+    int64_t n_slots = 0;
+    int32_t stride_min = 16;
+    bool planned = false;
+
+    // ---- device side
+    int device = -1;
+    uint8_t *dplan = nullptr, *hplan = nullptr;
+    size_t plan_cap = 0, hplan_cap = 0;
+    uint8_t *dcarry[2] = {nullptr, nullptr};
+    size_t carry_cap[2] = {0, 0};
+    int carry_cur = 0;  // pending packets live in dcarry[carry_cur] (or the batch input)
+    size_t carry_need = 0;  // bytes of dcarry[carry_cur] the last plan fills
+    hipEvent_t done = nullptr;
+    bool in_flight = false;
+
+    int tail_x() const { return cfg.rs_cnt; }
+    int y_of(int x) const { return cfg.rs_y[x - 1]; }
+    // blob_encode_t::get_shard_len(n, next_packet_len), fec_manager.cpp:51-53
+    int shard_len(int n, int next) const { return round_up_div(blob_len + 2 + next, n); }
+};
+
+namespace {
+
+int wait_idle(rsmi_fenc *E) {
+    if (E->in_flight) {
+        hipError_t e = hipEventSynchronize(E->done);
+        if (e != hipSuccess) return fail(RSMI_ERR_HIP, std::string("fenc wait: ") + hipGetErrorString(e));
+        E->in_flight = false;
+    }
+    return RSMI_OK;
+}
+
+int grow(uint8_t **p, size_t *cap, size_t need, bool pinned) {
+    if (need <= *cap) return RSMI_OK;
+    size_t c = std::max(need, *cap * 2);
+    c = (c + 4095) & ~size_t(4095);
+    if (*p) (void)(pinned ? hipHostFree(*p) : hipFree(*p));
+    *p = nullptr;
+    *cap = 0;
+    hipError_t e = pinned ? hipHostMalloc((void **)p, c, hipHostMallocDefault) : hipMalloc((void **)p, c);
+    if (e != hipSuccess) return fail(RSMI_ERR_NOMEM, "fenc allocation failed");
+    *cap = c;
+    return RSMI_OK;
+}
+
+// Close the open group (the about_to_fec branch, fec_manager.cpp:248-367).
+// Early-sent mode-1 packets of the group are pointed at their group slots.
+void close_group(rsmi_fenc *E, int k, int m, int fec_len) {
+    const int64_t slot0 = E->n_slots;
+    const int n = k + m;
+    E->n_slots += n;
+    FrameGroup G{};
+    G.slot0 = (uint64_t)slot0;
+    G.seq = E->seq;
+    G.fec_len = (uint32_t)fec_len;
+    G.src0 = (uint32_t)E->srcs.size();
+    G.nsrc = (uint32_t)E->pend.size();
+    G.blob_len = (uint32_t)E->blob_len;
+    G.nslots = (uint16_t)n;
+    G.nframe = (uint16_t)k;
+    G.mode = (uint8_t)E->cfg.mode;
+    G.k = (uint8_t)k;
+    G.m = (uint8_t)m;
+    G.idx0 = 0;
+    uint32_t off = 4;
+    for (size_t j = 0; j < E->pend.size(); ++j) {
+        const Pending &p = E->pend[j];
+        E->srcs.push_back(FrameSrc{p.addr, p.len, E->cfg.mode == 0 ? off : 0u});
+        off += 2 + p.len;
+        if (p.emitted >= 0) E->packets[(size_t)p.emitted].slot = slot0 + (int64_t)j;
+    }
+    E->jobs.push_back(G);
+    E->g_slot0.push_back(slot0);
+    E->g_k.push_back(k);
+    E->g_m.push_back(m);
+    E->g_len.push_back(fec_len);
+    E->g_seq.push_back(E->seq);
+    // pad_end of the encode kernels must stay inside the slot (rsmi.h padding rule)
+    const int need = 16 + ((fec_len + 127) & ~127);
+    E->stride_min = std::max(E->stride_min, (need + 15) & ~15);
+    if (m > 0) {
+        const bool extend = !E->runs.empty() && E->runs.back().k == k && E->runs.back().n == n &&
+                            E->runs.back().len == fec_len &&
+                            E->runs.back().slot0 + E->runs.back().count * n == slot0;
+        if (!extend) E->runs.push_back(Run{slot0, 0, k, n, fec_len});
+        E->runs.back().count += 1;
+    }
+}
+
+// fec_encode_manager_t::input (fec_manager.cpp:206-447) for one event,
+// followed by output() (:448-460): appends the packets output() would return.
+int input_event(rsmi_fenc *E, int32_t event, bool has, int len, uint64_t addr) {
+    if (E->pend.empty() && E->has_next) {  // fec_par.clone(g_fec_par) at counter 0 (:207-209)
+        E->cfg = E->next_cfg;
+        E->has_next = false;
+    }
+    const rsmi_fec_config &P = E->cfg;
+    const int mode = P.mode;
+    if (has && (len < 0 || len > 65535)) return -1;  // the reference asserts (:187, :57)
+    if (mode == 0 && has && E->pend.empty()) {
+        if (E->shard_len(E->tail_x(), len) > P.mtu) return -1;  // :217-223, "message too long"
+    }
+    const int cnt = (int)E->pend.size();
+    if (!has && cnt == 0) return -1;  // :228-231
+    bool about = !has;
+    bool delayed = false;
+    // :235-238 (input(0,0) passes len 0)
+    if (mode == 0 && E->shard_len(E->tail_x(), has ? len : 0) > P.mtu) {
+        about = true;
+        delayed = true;
+    }
+    auto append = [&]() {  // fec_encode_manager_t::append (:174-204)
+        E->pend.push_back(Pending{addr, (uint32_t)len, -1});
+        if (mode == 0) E->blob_len += 2 + len;
+    };
+    if (has && !delayed) append();
+    const int counter = (int)E->pend.size();
+    if (mode == 0 && counter == P.queue_len) about = true;
+    if (mode == 1 && counter == E->tail_x()) about = true;
+
+    if (about) {
+        if (counter == 0) return -1;  // :252-255
+        int k, m, fec_len;
+        if (mode == 0) {
+            const int tx = E->tail_x(), ty = E->y_of(tx);
+            k = tx;
+            m = ty;
+            if (P.short_packet_optimize) {  // :264-288
+                uint32_t best_len = (uint32_t)(E->shard_len(tx, 0) + P.header_overhead) * (uint32_t)(tx + ty);
+                int best = tx;
+                for (int i = 1; i < tx; ++i) {
+                    const uint32_t sl = (uint32_t)E->shard_len(i, 0);
+                    if (sl > (uint32_t)P.mtu) continue;
+                    const uint32_t nl = (sl + (uint32_t)P.header_overhead) * (uint32_t)(i + E->y_of(i));
+                    if (nl < best_len) {
+                        best_len = nl;
+                        best = i;
+                    }
+                }
+                k = best;
+                m = E->y_of(best);
+            }
+            fec_len = round_up_div(E->blob_len, k);  // blob_encode_t::output (:67-75)
+        } else {
+            k = counter;
+            m = E->y_of(counter);
+            fec_len = -1;
+            for (const Pending &p : E->pend) fec_len = std::max(fec_len, (int)p.len + 2);
+        }
+        const int64_t first_pk = (int64_t)E->packets.size();
+        // the packets output() returns (:318-346, fast send :376-393)
+        if (mode == 0) {
+            for (int i = 0; i < k + m; ++i)
+                E->packets.push_back(rsmi_fenc_packet{-1, 8 + fec_len, event});
+        } else {
+            if (has) {  // the packet that completed the group goes with the parity (:376-381)
+                E->pend.back().emitted = (int64_t)E->packets.size();
+                E->packets.push_back(rsmi_fenc_packet{-1, 8 + (int)E->pend.back().len + 2, event});
+            }
+            for (int i = k; i < k + m; ++i)
+                E->packets.push_back(rsmi_fenc_packet{-1, 8 + fec_len, event});
+        }
+        const int64_t slot0 = E->n_slots;
+        close_group(E, k, m, fec_len);
+        if (mode == 0) {
+            for (int i = 0; i < k + m; ++i) E->packets[(size_t)(first_pk + i)].slot = slot0 + i;
+        } else {
+            int64_t q = first_pk + (has ? 1 : 0);
+            for (int i = k; i < k + m; ++i) E->packets[(size_t)q++].slot = slot0 + i;
+        }
+        E->seq++;
+        E->pend.clear();
+        E->blob_len = 4;
+    } else if (has && mode == 1) {  // encode_fast_send (:394-429): the data packet goes now
+        E->pend.back().emitted = (int64_t)E->packets.size();
+        E->packets.push_back(rsmi_fenc_packet{-1, 8 + len + 2, event});
+    }
+    if (has && delayed) append();  // :436-439
+    return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int rsmi_fec_config_init(rsmi_fec_config *cfg, const char *s, int mode, int mtu, int queue_len) {
+    if (!cfg || !s) return fail(RSMI_ERR_INVALID, "null config/string");
+    if (mode != 0 && mode != 1) return fail(RSMI_ERR_INVALID, "mode must be 0 or 1");
+    if (mtu < 1 || queue_len < 1) return fail(RSMI_ERR_INVALID, "bad mtu/queue_len");
+    // rs_from_str (fec_manager.h:40-136)
+    std::vector<std::pair<int, int>> pv;
+    std::string str(s);
+    size_t pos = 0;
+    while (true) {
+        size_t c = str.find(',', pos);
+        std::string tok = str.substr(pos, c == std::string::npos ? std::string::npos : c - pos);
+        int x, y;
+        if (std::sscanf(tok.c_str(), "%d:%d", &x, &y) != 2)
+            return fail(RSMI_ERR_INVALID, "failed to parse [" + tok + "]");
+        if (x < 1 || y < 0 || x + y > RSMI_FEC_MAX_PACKETS)
+            return fail(RSMI_ERR_INVALID, "invalid x:y in [" + tok + "]");
+        pv.emplace_back(x, y);
+        if (c == std::string::npos) break;
+        pos = c + 1;
+    }
+    for (size_t i = 1; i < pv.size(); ++i)
+        if (pv[i].first <= pv[i - 1].first)
+            return fail(RSMI_ERR_INVALID, "x in x:y should be in ascend order");
+    std::memset(cfg, 0, sizeof(*cfg));
+    cfg->mode = mode;
+    cfg->mtu = mtu;
+    cfg->queue_len = queue_len;
+    cfg->short_packet_optimize = 1;
+    cfg->header_overhead = 40;
+    for (int i = 1; i <= pv[0].first; ++i) cfg->rs_y[i - 1] = (uint8_t)pv[0].second;
+    for (size_t i = 1; i < pv.size(); ++i) {
+        const int now_x = pv[i].first, now_y = pv[i].second;
+        const int pre_x = pv[i - 1].first, pre_y = pv[i - 1].second;
+        cfg->rs_y[now_x - 1] = (uint8_t)now_y;
+        for (int j = pre_x + 1; j <= now_x - 1; ++j) {
+            const double distance = now_x - pre_x;
+            int in_y = (int)(pre_y + (now_y - pre_y) * (j - pre_x) / distance + 0.9999);
+            if (j + in_y > RSMI_FEC_MAX_PACKETS) in_y = RSMI_FEC_MAX_PACKETS - j;
+            cfg->rs_y[j - 1] = (uint8_t)in_y;
+        }
+    }
+    cfg->rs_cnt = pv.back().first;
+    return RSMI_OK;
+}
+
+int rsmi_fenc_create(const rsmi_fec_config *cfg, uint32_t seq0, rsmi_fenc **out) {
+    if (!cfg || !out) return fail(RSMI_ERR_INVALID, "null config/out");
+    *out = nullptr;
+    if ((cfg->mode != 0 && cfg->mode != 1) || cfg->rs_cnt < 1 || cfg->rs_cnt > RSMI_FEC_MAX_PACKETS ||
+        cfg->mtu < 1 || cfg->queue_len < 1)
+        return fail(RSMI_ERR_INVALID, "invalid fec config");
+    for (int x = 1; x <= cfg->rs_cnt; ++x)
+        if (x + cfg->rs_y[x - 1] > RSMI_FEC_MAX_PACKETS) return fail(RSMI_ERR_INVALID, "x + y > 255");
+    rsmi_fenc *E = new rsmi_fenc();
+    E->cfg = *cfg;
+    E->seq = seq0;
+    *out = E;  // the device is bound at the first rsmi_fenc_run_dev
+    return RSMI_OK;
+}
+
+int rsmi_fenc_set_config(rsmi_fenc *E, const rsmi_fec_config *cfg) {
+    if (!E || !cfg) return fail(RSMI_ERR_INVALID, "null encoder/config");
+    if ((cfg->mode != 0 && cfg->mode != 1) || cfg->rs_cnt < 1 || cfg->rs_cnt > RSMI_FEC_MAX_PACKETS ||
+        cfg->mtu < 1 || cfg->queue_len < 1)
+        return fail(RSMI_ERR_INVALID, "invalid fec config");
+    E->next_cfg = *cfg;
+    E->has_next = true;
+    return RSMI_OK;
+}
+
+void rsmi_fenc_destroy(rsmi_fenc *E) {
+    if (!E) return;
+    (void)wait_idle(E);
+    if (E->dplan) (void)hipFree(E->dplan);
+    if (E->hplan) (void)hipHostFree(E->hplan);
+    for (int i = 0; i < 2; ++i)
+        if (E->dcarry[i]) (void)hipFree(E->dcarry[i]);
+    if (E->done) (void)hipEventDestroy(E->done);
+    delete E;
+}
+
+int rsmi_fenc_plan(rsmi_fenc *E, int64_t n_events, const int32_t *len, const uint64_t *in_off,
+                   const uint8_t *in_base, int32_t *ret, int64_t *n_slots, int64_t *n_packets,
+                   int32_t *slot_stride_min) {
+    if (!E || n_events < 0 || (n_events && !len)) return fail(RSMI_ERR_INVALID, "bad fenc_plan args");
+    int rc = wait_idle(E);  // the previous batch still reads the plan buffers and carry area
+    if (rc) return rc;
+    E->jobs.clear();
+    E->srcs.clear();
+    E->carry.clear();
+    E->packets.clear();
+    E->g_slot0.clear();
+    E->g_k.clear();
+    E->g_m.clear();
+    E->g_len.clear();
+    E->g_seq.clear();
+    E->runs.clear();
+    E->n_slots = 0;
+    E->stride_min = 16;
+    for (Pending &p : E->pend) p.emitted = -1;  // sent in an earlier batch
+    for (int64_t i = 0; i < n_events; ++i) {
+        const bool has = len[i] >= 0;
+        if (has && (!in_off || !in_base)) return fail(RSMI_ERR_INVALID, "packet without in_off/in_base");
+        const uint64_t addr = has ? (uint64_t)(uintptr_t)(in_base + in_off[i]) : 0;
+        const int r = input_event(E, (int32_t)i, has, has ? len[i] : 0, addr);
+        if (ret) ret[i] = r;
+    }
+    // mode-1 packets sent ahead of a group that is still open: a slot of their own
+    for (size_t j = 0; j < E->pend.size(); ++j) {
+        const Pending &p = E->pend[j];
+        if (p.emitted < 0) continue;
+        const int64_t slot = E->n_slots++;
+        FrameGroup G{};
+        G.slot0 = (uint64_t)slot;
+        G.seq = E->seq;
+        G.fec_len = p.len + 2;
+        G.src0 = (uint32_t)E->srcs.size();
+        G.nsrc = 1;
+        G.nslots = 1;
+        G.nframe = 1;
+        G.mode = 1;
+        G.idx0 = (uint8_t)j;
+        E->srcs.push_back(FrameSrc{p.addr, p.len, 0});
+        E->jobs.push_back(G);
+        E->packets[(size_t)p.emitted].slot = slot;
+        E->stride_min = std::max(E->stride_min, (int32_t)((16 + p.len + 2 + 15) & ~15u));
+    }
+    // the open group's payloads move to the other carry buffer
+    size_t cbytes = 0;
+    for (const Pending &p : E->pend) cbytes += (p.len + 15) & ~15u;
+    const int nxt = E->carry_cur ^ 1;
+    E->carry_need = cbytes + 16;
+    size_t co = 0;
+    for (Pending &p : E->pend) {
+        const uint64_t dst = kCarryTag | (nxt ? kCarryBuf1 : 0) | (uint64_t)co;
+        if (p.len) E->carry.push_back(CarryCopy{p.addr, dst, p.len, 0});
+        p.addr = dst;
+        co += (p.len + 15) & ~15u;
+    }
+    E->carry_cur = nxt;
+    E->planned = true;
+    if (n_slots) *n_slots = E->n_slots;
+    if (n_packets) *n_packets = (int64_t)E->packets.size();
+    if (slot_stride_min) *slot_stride_min = E->stride_min;
+    return RSMI_OK;
+}
+
+int rsmi_fenc_packets(const rsmi_fenc *E, rsmi_fenc_packet *out) {
+    if (!E || (!out && !E->packets.empty())) return fail(RSMI_ERR_INVALID, "bad fenc_packets args");
+    if (!E->packets.empty()) std::memcpy(out, E->packets.data(), E->packets.size() * sizeof(rsmi_fenc_packet));
+    return RSMI_OK;
+}
+
+int rsmi_fenc_groups(const rsmi_fenc *E, int64_t *n, int64_t *slot0, int32_t *k, int32_t *m,
+                     int32_t *fec_len, uint32_t *seq) {
+    if (!E) return fail(RSMI_ERR_INVALID, "null encoder");
+    const size_t g = E->g_k.size();
+    if (n) *n = (int64_t)g;
+    if (slot0) std::copy(E->g_slot0.begin(), E->g_slot0.end(), slot0);
+    if (k) std::copy(E->g_k.begin(), E->g_k.end(), k);
+    if (m) std::copy(E->g_m.begin(), E->g_m.end(), m);
+    if (fec_len) std::copy(E->g_len.begin(), E->g_len.end(), fec_len);
+    if (seq) std::copy(E->g_seq.begin(), E->g_seq.end(), seq);
+    return RSMI_OK;
+}
+
+int rsmi_fenc_run_dev(rsmi_fenc *E, uint8_t *slots, int64_t S, void *stream) {
+    if (!E || !E->planned) return fail(RSMI_ERR_INVALID, "rsmi_fenc_run_dev without a plan");
+    if (E->n_slots && (!slots || ((uintptr_t)slots & 15)))
+        return fail(RSMI_ERR_INVALID, "slots_base must be 16-aligned");
+    if (S % 16 || S < E->stride_min)
+        return fail(RSMI_ERR_INVALID, "slot_stride must be a multiple of 16 >= slot_stride_min (" +
+                                          std::to_string(E->stride_min) + ")");
+    int cur;
+    if (hipGetDevice(&cur) != hipSuccess) return fail(RSMI_ERR_HIP, "fenc: no usable GPU");
+    if (E->device < 0) {
+        if (hipEventCreateWithFlags(&E->done, hipEventDisableTiming) != hipSuccess)
+            return fail(RSMI_ERR_HIP, "fenc: hipEventCreate");
+        E->device = cur;
+    } else if (cur != E->device) {
+        return fail(RSMI_ERR_INVALID, "rsmi_fenc_run_dev on another device than the encoder's");
+    }
+    hipStream_t s = (hipStream_t)stream;
+    // carry buffer this batch fills; resolve tagged carry offsets
+    int rc0 = grow(&E->dcarry[E->carry_cur], &E->carry_cap[E->carry_cur], E->carry_need, false);
+    if (rc0) return rc0;
+    auto resolve = [E](uint64_t a) -> uint64_t {
+        if (!(a & kCarryTag)) return a;
+        return (uint64_t)(uintptr_t)(E->dcarry[(a & kCarryBuf1) ? 1 : 0] + (a & kCarryOff));
+    };
+    for (FrameSrc &f : E->srcs) f.addr = resolve(f.addr);
+    for (CarryCopy &c : E->carry) {
+        c.src = resolve(c.src);
+        c.dst = resolve(c.dst);
+    }
+    const size_t gb = E->jobs.size() * sizeof(FrameGroup), sb = E->srcs.size() * sizeof(FrameSrc),
+                 cb = E->carry.size() * sizeof(CarryCopy);
+    const size_t go = 0, so = (gb + 255) & ~size_t(255), co = (so + sb + 255) & ~size_t(255);
+    const size_t all = co + cb + 16;
+    int rc = grow(&E->dplan, &E->plan_cap, all, false);
+    if (!rc) rc = grow(&E->hplan, &E->hplan_cap, all, true);
+    if (rc) return rc;
+    if (gb) std::memcpy(E->hplan + go, E->jobs.data(), gb);
+    if (sb) std::memcpy(E->hplan + so, E->srcs.data(), sb);
+    if (cb) std::memcpy(E->hplan + co, E->carry.data(), cb);
+    hipError_t e = hipMemcpyAsync(E->dplan, E->hplan, all, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess)
+        e = rsmi::launch_frame(reinterpret_cast<const FrameGroup *>(E->dplan + go), (int64_t)E->jobs.size(),
+                               reinterpret_cast<const FrameSrc *>(E->dplan + so), slots, S, s);
+    if (e != hipSuccess) return fail(RSMI_ERR_HIP, std::string("fenc frame: ") + hipGetErrorString(e));
+    // parity of every group
+    for (const Run &r : E->runs) {
+        rc = rsmi_encode_dev(r.k, r.n, slots + r.slot0 * S + 16, (int64_t)r.n * S, S, r.len, r.count, stream);
+        if (rc) return rc;
+    }
+    e = rsmi::launch_carry(reinterpret_cast<const CarryCopy *>(E->dplan + co), (int64_t)E->carry.size(), s);
+    if (e == hipSuccess) e = hipEventRecord(E->done, s);
+    if (e != hipSuccess) return fail(RSMI_ERR_HIP, std::string("fenc carry: ") + hipGetErrorString(e));
+    E->in_flight = true;
+    E->planned = false;
+    return RSMI_OK;
+}
+
+}  // extern "C"

@@ -95,4 +95,32 @@ struct CookArgs {
 size_t cook_lds_bytes(bool decook);
 hipError_t launch_cook(const CookArgs &a, bool decook, int max_blocks, hipStream_t s);
 
+
+
+// ---- FEC framing (frame.hip, fec_enc.cpp) --------------------------------------
+// One framing job: a completed FEC group (nslots = k + m slots, nframe = k data
+// shards) or a mode-1 packet sent ahead of its group (nslots = nframe = 1).
+struct FrameGroup {
+    uint64_t slot0;     // first slot
+    uint32_t seq;
+    uint32_t fec_len;   // shard bytes
+    uint32_t src0;      // first FrameSrc of the job
+    uint32_t nsrc;      // mode 0: blob records (the blob's u32 count); mode 1: = nframe
+    uint32_t blob_len;  // mode 0: blob bytes (blob_encode_t::current_len)
+    uint16_t nslots, nframe;
+    uint8_t mode, k, m, idx0;  // header bytes; idx0 = index of slot 0
+};
+struct FrameSrc {
+    uint64_t addr;      // device address of the payload
+    uint32_t len;
+    uint32_t off;       // mode 0: blob offset of the record's u16 length; mode 1: 0
+};
+struct CarryCopy {
+    uint64_t src, dst;  // dst 16-aligned, room for round_up(len, 16)
+    uint32_t len, pad;
+};
+hipError_t launch_frame(const FrameGroup *groups, int64_t ngroups, const FrameSrc *srcs,
+                        uint8_t *slots, int64_t slot_stride, hipStream_t s);
+hipError_t launch_carry(const CarryCopy *jobs, int64_t njobs, hipStream_t s);
+
 }  // namespace rsmi

@@ -1,0 +1,165 @@
+"""Batched FEC framing on the GPU (include/rsmi_fec.h).
+
+UDPspeeder's ``fec_encode_manager_t`` (fec_manager.cpp:174-460) turns a
+connection's packets into FEC groups: mode 0 packs them into a length-prefixed
+blob cut into k shards, mode 1 sends each packet as one zero-padded shard;
+every packet gets the 8-byte header ``seq | mode | k | m | index`` and parity
+comes from rs_encode2.  :class:`FecEncoder` holds one manager's state; a batch
+of ``input()`` calls is planned on the host (lengths only) and framed, encoded
+and carried over on the GPU:
+
+    enc = FecEncoder("20:10", mode=0, mtu=1250, queue_len=200, seq0=1)
+    plan = enc.plan(lens, offsets, in_buf)          # host lists, device input
+    slots = torch.empty(plan.n_slots * S, dtype=torch.uint8, device="cuda")
+    enc.run(slots, S)                                # frame + encode + carry
+    for slot, length, event in plan.packets: ...     # output() order
+
+``input`` / ``output`` keep the reference's per-call interface (one GPU batch
+per call) for callers and tests that think in single packets.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from typing import List, Optional
+
+import numpy as np
+
+from ._lib import check, lib, rsmi_fec_config, rsmi_fenc_packet
+
+HEADER = 8
+
+
+def fec_config(rs_str: str, mode: int = 0, mtu: int = 1250, queue_len: int = 200,
+               short_packet_optimize: int = 1, header_overhead: int = 40) -> rsmi_fec_config:
+    """fec_parameter_t from a -f string (rs_from_str, fec_manager.h:40-136)."""
+    cfg = rsmi_fec_config()
+    check(lib().rsmi_fec_config_init(C.byref(cfg), rs_str.encode(), mode, mtu, queue_len),
+          "rsmi_fec_config_init")
+    cfg.short_packet_optimize = short_packet_optimize
+    cfg.header_overhead = header_overhead
+    return cfg
+
+
+@dataclass
+class FencPlan:
+    n_slots: int
+    slot_stride_min: int
+    ret: np.ndarray          # input() return value per event
+    packets: np.ndarray      # structured: slot, len, event (output() order)
+    groups: dict             # slot0, k, m, fec_len, seq per completed group
+
+
+class FecEncoder:
+    """One fec_encode_manager_t; its device state lives on the current device."""
+
+    def __init__(self, rs_str: str = "20:10", mode: int = 0, mtu: int = 1250,
+                 queue_len: int = 200, seq0: int = 0, **kw):
+        self.cfg = fec_config(rs_str, mode, mtu, queue_len, **kw)
+        h = C.c_void_p()
+        check(lib().rsmi_fenc_create(C.byref(self.cfg), C.c_uint32(seq0 & 0xFFFFFFFF), C.byref(h)),
+              "rsmi_fenc_create")
+        self._h = h
+        self._keep = None
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().rsmi_fenc_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_config(self, rs_str: str, mode: int = 0, mtu: int = 1250, queue_len: int = 200):
+        """g_fec_par update: taken up at the next group start (fec_manager.cpp:207-209)."""
+        cfg = fec_config(rs_str, mode, mtu, queue_len)
+        check(lib().rsmi_fenc_set_config(self._h, C.byref(cfg)), "rsmi_fenc_set_config")
+
+    def plan(self, lens, offsets=None, in_buf=None) -> FencPlan:
+        """Plan input() for every event: lens[i] >= 0 is a packet of that many
+        bytes at in_buf + offsets[i] (in_buf: CUDA uint8 tensor with 16 spare
+        bytes after every packet), lens[i] < 0 is the timer flush input(0, 0)."""
+        lens = np.ascontiguousarray(lens, np.int32)
+        n = len(lens)
+        offp = basep = None
+        if offsets is not None:
+            offsets = np.ascontiguousarray(offsets, np.uint64)
+            offp = offsets.ctypes.data
+        if isinstance(in_buf, int):
+            basep = in_buf
+        elif in_buf is not None:
+            basep = in_buf.data_ptr()
+        ret = np.zeros(n, np.int32)
+        ns, npk, smin = C.c_int64(), C.c_int64(), C.c_int32()
+        check(lib().rsmi_fenc_plan(self._h, n, lens.ctypes.data if n else None, offp, basep,
+                                   ret.ctypes.data if n else None, C.byref(ns), C.byref(npk),
+                                   C.byref(smin)), "rsmi_fenc_plan")
+        pk = (rsmi_fenc_packet * max(1, npk.value))()
+        check(lib().rsmi_fenc_packets(self._h, pk), "rsmi_fenc_packets")
+        dt = np.dtype([("slot", np.int64), ("len", np.int32), ("event", np.int32)])
+        packets = np.frombuffer(bytes(pk), dt)[:npk.value].copy()
+        ng = C.c_int64()
+        check(lib().rsmi_fenc_groups(self._h, C.byref(ng), None, None, None, None, None),
+              "rsmi_fenc_groups")
+        g = {"slot0": np.zeros(ng.value, np.int64), "k": np.zeros(ng.value, np.int32),
+             "m": np.zeros(ng.value, np.int32), "fec_len": np.zeros(ng.value, np.int32),
+             "seq": np.zeros(ng.value, np.uint32)}
+        if ng.value:
+            check(lib().rsmi_fenc_groups(self._h, None, g["slot0"].ctypes.data, g["k"].ctypes.data,
+                                         g["m"].ctypes.data, g["fec_len"].ctypes.data,
+                                         g["seq"].ctypes.data), "rsmi_fenc_groups")
+        self._keep = in_buf  # the input must outlive the run
+        return FencPlan(ns.value, smin.value, ret, packets, g)
+
+    def plan_host(self, lens, offsets) -> FencPlan:
+        """Plan only (no device): decisions, packet list and groups for a batch
+        whose payloads are never framed -- for inspecting the schedule."""
+        return self.plan(lens, offsets, 0x10000)
+
+    def run(self, slots, slot_stride: int, stream=None):
+        """Frame + encode + carry the planned batch into `slots` (CUDA uint8,
+        >= n_slots * slot_stride bytes); asynchronous on `stream`."""
+        import torch
+        s = stream if stream is not None else torch.cuda.current_stream()
+        check(lib().rsmi_fenc_run_dev(self._h, slots.data_ptr() if slots.numel() else None,
+                                      int(slot_stride), s.cuda_stream), "rsmi_fenc_run_dev")
+
+    @staticmethod
+    def slot_stride_for(fec_len_max: int) -> int:
+        """A slot stride that fits fec_len_max-byte shards and do_cook's tail
+        (rsmi_cook.h) in place: 16 + round_up(fec_len_max, 128), + 128."""
+        return 16 + (fec_len_max + 127) // 128 * 128 + 128
+
+    # ---- the reference's per-call interface (one GPU batch per call) ---------
+    def input(self, data: Optional[bytes]) -> int:
+        """fec_encode_manager_t::input(s, len); data None is input(0, 0)."""
+        import torch
+        if data is None:
+            p = self.plan([-1])
+            buf = torch.zeros(16, dtype=torch.uint8, device="cuda")
+        else:
+            buf = torch.zeros(len(data) + 16, dtype=torch.uint8)
+            buf[:len(data)] = torch.frombuffer(bytearray(data), dtype=torch.uint8) if data else buf[:0]
+            buf = buf.cuda()
+            p = self.plan([len(data)], [0], buf)
+        stride = max(p.slot_stride_min, 16)
+        slots = torch.zeros(max(1, p.n_slots) * stride, dtype=torch.uint8, device="cuda")
+        self.run(slots, stride)
+        host = slots.cpu().numpy()
+        self._ready = [host[s * stride + HEADER:s * stride + HEADER + ln].tobytes()
+                       for s, ln, _ in p.packets]
+        return int(p.ret[0])
+
+    def output(self) -> List[bytes]:
+        """fec_encode_manager_t::output: the packets the last input() produced."""
+        r, self._ready = getattr(self, "_ready", []), []
+        return r
+
+
+def packets_bytes(plan: FencPlan, slots_host: np.ndarray, slot_stride: int) -> List[bytes]:
+    """The emitted packets of a run, as bytes (slots_host: the slot array on the host)."""
+    return [slots_host[s * slot_stride + HEADER:s * slot_stride + HEADER + ln].tobytes()
+            for s, ln, _ in plan.packets]
