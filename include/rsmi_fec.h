@@ -17,11 +17,13 @@
  * group) runs on the GPU in a few launches over a slot array:
  *
  *   slot s occupies [s*slot_stride, (s+1)*slot_stride) of slots_base;
- *   its packet starts at +8 (8-byte header) and its shard at +16.
+ *   its packet starts at +RSMI_FEC_SLOT_PACKET (120: the 8-byte header) and
+ *   its shard at +RSMI_FEC_SLOT_SHARD (128), so with a slot_stride that is a
+ *   multiple of 128 every shard row is cache-line aligned for the encoder.
  *
  * Every packet the reference's output() would return is listed, in the
  * reference's order, as (slot, length); packet bytes are slots_base +
- * slot*slot_stride + 8 .. + length.  Results are byte-identical to the
+ * slot*slot_stride + RSMI_FEC_SLOT_PACKET .. + length.  Results are byte-identical to the
  * reference's packets, with one documented difference: in mode 0 the bytes of
  * the last data shard past the blob's end are zero here, where the reference
  * sends whatever its blob buffer held there before (stale bytes of earlier
@@ -44,6 +46,8 @@ extern "C" {
 
 #define RSMI_FEC_MAX_PACKETS 255 /* max_fec_packet_num (fec_manager.h:18) */
 #define RSMI_FEC_HEADER 8        /* u32 seq + mode + k + m + index        */
+#define RSMI_FEC_SLOT_PACKET 120 /* packet offset in a slot                */
+#define RSMI_FEC_SLOT_SHARD 128  /* shard offset in a slot                 */
 
 /* fec_parameter_t (fec_manager.h:26-180) without the timer fields. */
 typedef struct rsmi_fec_config {
@@ -76,7 +80,7 @@ int rsmi_fenc_set_config(rsmi_fenc *enc, const rsmi_fec_config *cfg);
 /* One emitted packet: output() after input() call `event` returned it. */
 typedef struct rsmi_fenc_packet {
     int64_t slot;   /* slot index in the batch's slot array                */
-    int32_t len;    /* bytes from slot start + 8 (header included)         */
+    int32_t len;    /* packet bytes from the slot start + RSMI_FEC_SLOT_PACKET, header included */
     int32_t event;  /* index of the input() call in the batch              */
 } rsmi_fenc_packet;
 
@@ -92,6 +96,10 @@ typedef struct rsmi_fenc_packet {
 int rsmi_fenc_plan(rsmi_fenc *enc, int64_t n_events, const int32_t *len, const uint64_t *in_off,
                    const uint8_t *in_base, int32_t *ret, int64_t *n_slots, int64_t *n_packets,
                    int32_t *slot_stride_min);
+/* slot_stride_min = RSMI_FEC_SLOT_SHARD + round_up(fec_len, 128) over the
+ * batch's groups (the encoders may touch a parity row's padding up to the
+ * next 128-byte line, rsmi.h).  A caller that cooks packets in place
+ * (rsmi_cook.h) adds room for do_cook's tail: 37 bytes, whole 16-byte pieces. */
 
 /* Copy the planned packet list (n_packets entries, host). */
 int rsmi_fenc_packets(const rsmi_fenc *enc, rsmi_fenc_packet *out);
@@ -105,7 +113,8 @@ int rsmi_fenc_groups(const rsmi_fenc *enc, int64_t *n_groups, int64_t *slot0, in
  * padded shards) and the mode-1 packets sent ahead of their group, RS-encode
  * every group's parity slots, and move still-pending packets into the carry
  * area.  slots_base: device, 16-aligned, n_slots * slot_stride bytes;
- * slot_stride: a multiple of 16, >= slot_stride_min.  Asynchronous. */
+ * slot_stride: a multiple of 16, >= slot_stride_min (a multiple of 128 keeps
+ * the shard rows line-aligned).  Asynchronous. */
 int rsmi_fenc_run_dev(rsmi_fenc *enc, uint8_t *slots_base, int64_t slot_stride, void *stream);
 
 #ifdef __cplusplus

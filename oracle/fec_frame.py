@@ -244,3 +244,203 @@ class FecReference:
             return self._run(self.lib.ref_fdec_run, h, packets)
         finally:
             self.lib.ref_fdec_free(h)
+
+
+# --------------------------------------------------------------------------
+# fec_decode_manager_t (fec_manager.cpp:469-797, fec_manager.h:185-235, 366-435)
+FEC_BUFF_NUM = 2000              # fec_manager.cpp:33
+ANTI_REPLAY_BUFF_SIZE = 30000    # fec_manager.h:16
+ANTI_REPLAY_TIMEOUT = 120 * 1000  # fec_manager.h:185 (ms)
+MAX_DATA_LEN = 3600              # common.h:102
+
+
+class AntiReplay:
+    """anti_replay_t (fec_manager.h:187-235); time in ms from the caller."""
+
+    def __init__(self):
+        self.buf = [-1] * ANTI_REPLAY_BUFF_SIZE
+        self.mp = {}  # seq -> [time, index]
+        self.index = 0
+
+    def is_valid(self, seq: int, now: int) -> bool:
+        e = self.mp.get(seq)
+        if e is None:
+            return True
+        if now - e[0] > ANTI_REPLAY_TIMEOUT:
+            self.buf[e[1]] = -1
+            del self.mp[seq]
+            return True
+        return False
+
+    def set_invalid(self, seq: int, now: int):
+        if not self.is_valid(seq, now):
+            return
+        old = self.buf[self.index]
+        if old != -1:
+            del self.mp[old]
+        self.buf[self.index] = seq
+        self.mp[seq] = [now, self.index]
+        self.index = (self.index + 1) % ANTI_REPLAY_BUFF_SIZE
+
+
+class _Group:  # fec_group_t (fec_manager.h:376-384)
+    __slots__ = ("type", "data_num", "redundant_num", "len", "fec_done", "group_mp")
+
+    def __init__(self):
+        self.type = self.data_num = self.redundant_num = self.len = -1
+        self.fec_done = 0
+        self.group_mp = {}  # inner index -> ring slot
+
+
+class DecodeManager:
+    """fec_decode_manager_t restated; parity via the C restatement of
+    rs_decode2.  input(packet) -> return value; output() -> list of bytes."""
+
+    def __init__(self, oracle: Optional[Oracle] = None):
+        self.oracle = oracle or Oracle()
+        self.ar = AntiReplay()
+        self.mp = {}
+        self.ring = [None] * FEC_BUFF_NUM  # (seq, payload bytes) per slot
+        self.index = 0
+        self.ready: List[bytes] = []
+        self.now = 0  # ms
+
+    def _g(self, seq) -> _Group:  # unordered_map::operator[] inserts
+        g = self.mp.get(seq)
+        if g is None:
+            g = self.mp[seq] = _Group()
+        return g
+
+    def input(self, s: bytes) -> int:
+        self.ready = []
+        r = self._input(bytes(s))
+        return r
+
+    def _input(self, s: bytes) -> int:
+        if len(s) < HEADER:
+            return -1
+        seq = int.from_bytes(s[:4], "big")
+        typ, data_num, red_num, inner = s[4], s[5], s[6], s[7]
+        pay = s[HEADER:]
+        ln = len(pay)
+        if typ == 1:
+            if ln < 2:
+                return -1
+            if data_num == 0 and int.from_bytes(pay[:2], "big") + 2 != ln:
+                return -1
+        if typ == 0 and data_num == 0:
+            return -1
+        if data_num + red_num >= MAX_FEC_PACKET_NUM:
+            return -1
+        if not self.ar.is_valid(seq, self.now):
+            return 0
+        g = self._g(seq)
+        if g.fec_done:
+            return -1
+        if inner in g.group_mp:
+            return -1
+        if g.type == -1:
+            g.type = typ
+        elif g.type != typ:
+            return -1
+        if data_num != 0:
+            if g.data_num == -1:
+                g.data_num, g.redundant_num, g.len = data_num, red_num, ln
+            elif (g.data_num, g.redundant_num, g.len) != (data_num, red_num, ln):
+                return -1
+        old = self.ring[self.index]
+        if old is not None:
+            tmp_seq = old[0]
+            self.ar.set_invalid(tmp_seq, self.now)
+            self.mp.pop(tmp_seq, None)
+            if tmp_seq == seq:
+                return -1
+        self.ring[self.index] = (seq, pay)
+        g = self._g(seq)
+        g.group_mp[inner] = self.index
+        size = len(g.group_mp)
+        about = False
+        end = False
+        if typ == 0:
+            if size > data_num:
+                self.ar.set_invalid(seq, self.now)
+                end = True
+            elif size == data_num:
+                about = True
+        elif g.data_num != -1:
+            if size > g.data_num + 1:
+                self.ar.set_invalid(seq, self.now)
+                end = True
+            elif size >= g.data_num:
+                about = True
+        if not end:
+            if about:
+                self._decode(seq, g, typ, inner, ln)
+            elif typ == 1 and data_num == 0:  # decode_fast_send (:760-776)
+                self.ready = [pay[2:]]
+        self.index = (self.index + 1) % FEC_BUFF_NUM
+        return 0
+
+    def _decode(self, seq, g: _Group, typ, inner, ln):
+        k, m = g.data_num, g.redundant_num
+        n = k + m
+        if typ == 0:
+            shards = [None] * n
+            for idx, slot in g.group_mp.items():
+                if idx < n:
+                    shards[idx] = self.ring[slot][1]
+            bad_index = any(idx >= n for idx in g.group_mp)
+            rc, out, bufs = self.oracle.decode_ptrs(k, n, shards, ln) if not bad_index else (1, None, None)
+            g.fec_done = 1
+            if rc != 0:  # the reference asserts here (fec_manager.cpp:632)
+                self.ar.set_invalid(seq, self.now)
+                return
+            blob = b"".join(bufs[out[i]] for i in range(k))
+            if len(blob) < 4:
+                self.ar.set_invalid(seq, self.now)
+                return
+            cnt = int.from_bytes(blob[:4], "big")
+            if cnt > 30000:  # max_blob_packet_num (fec_manager.h:15)
+                self.ar.set_invalid(seq, self.now)
+                return
+            pos, res = 4, []
+            for _ in range(cnt):  # blob_decode_t::output (:97-129)
+                if pos + 2 > len(blob):
+                    self.ar.set_invalid(seq, self.now)
+                    return
+                l = int.from_bytes(blob[pos:pos + 2], "big")
+                pos += 2
+                if pos + l > len(blob):
+                    self.ar.set_invalid(seq, self.now)
+                    return
+                res.append(blob[pos:pos + l])
+                pos += l
+            self.ready = res
+            self.ar.set_invalid(seq, self.now)
+        else:
+            items = sorted(g.group_mp.items())
+            lens = [len(self.ring[slot][1]) for _, slot in items]
+            max_len = max(lens)
+            if min(lens) < 2 or max_len != g.len:
+                self.ar.set_invalid(seq, self.now)
+                return
+            shards = [None] * n
+            for idx, slot in items:
+                if idx < n:
+                    shards[idx] = self.ring[slot][1].ljust(max_len, b"\0")
+            missed = [i for i in range(k) if shards[i] is None or i == inner]
+            bad_index = any(idx >= n for idx, _ in items)
+            rc, out, bufs = self.oracle.decode_ptrs(k, n, shards, max_len) if not bad_index else (1, None, None)
+            g.fec_done = 1
+            if rc != 0:  # the reference asserts here (fec_manager.cpp:710)
+                self.ar.set_invalid(seq, self.now)
+                return
+            data = [bufs[out[i]] for i in range(k)]
+            lens_i = [int.from_bytes(d[:2], "big") for d in data]
+            if all(l <= MAX_DATA_LEN for l in lens_i):
+                self.ready = [data[i][2:2 + lens_i[i]] for i in missed]
+            self.ar.set_invalid(seq, self.now)
+
+    def output(self) -> List[bytes]:
+        r, self.ready = self.ready, []
+        return r

@@ -108,12 +108,12 @@ def _run_gpu(enc, lens, ev, cuts, torch):
         host = np.frombuffer(b"".join(chunks) + bytes(32), np.uint8)
         inbuf = torch.from_numpy(host.copy()).cuda()
         p = enc.plan(ln, offs, inbuf)
-        S = max(p.slot_stride_min, 16)
+        S = (p.slot_stride_min + 127) // 128 * 128
         slots = torch.full((max(1, p.n_slots) * S,), 0xEE, dtype=torch.uint8, device="cuda")
         enc.run(slots, S)
         h = slots.cpu().numpy()
         del inbuf  # the carry area holds what the next batch needs
-        out += [(h[s * S + 8:s * S + 8 + l].tobytes(), int(e) + a) for s, l, e in p.packets]
+        out += [(h[s * S + 120:s * S + 120 + l].tobytes(), int(e) + a) for s, l, e in p.packets]
     return out
 
 

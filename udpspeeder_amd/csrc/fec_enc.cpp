@@ -8,6 +8,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
+#include <new>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -33,15 +35,58 @@ int fail(int code, const std::string &m) {
 
 int round_up_div(int a, int b) { return (a + b - 1) / b; }  // common.cpp:747-749
 
-// Payload addresses in a plan: a device address in the batch input, or (tag
-// bit set) an offset in carry buffer 0 / 1, resolved when the batch runs so
-// that planning needs no device.
-constexpr uint64_t kCarryTag = 1ull << 63, kCarryBuf1 = 1ull << 62, kCarryOff = kCarryBuf1 - 1;
+// Payload addresses in a plan: a device address in the batch input, or a
+// carry-tagged offset (rsmi::kCarryTag), resolved by the kernels, so planning
+// needs no device.
+using rsmi::kCarryBuf1;
+using rsmi::kCarryTag;
 
 struct Pending {
     uint64_t addr;  // batch-input device address or tagged carry offset
     uint32_t len;
     int64_t emitted;  // mode 1: index in this batch's packet list of its early send, -1 if none
+};
+
+// A growable array in pinned host memory (plain memory when no device is
+// usable, e.g. planning-only on a CPU host), so a plan is uploaded straight
+// from where the planner wrote it.
+template <class T>
+struct HostArr {
+    T *p = nullptr;
+    size_t n = 0, cap = 0;
+    bool pinned = false;
+    HostArr() = default;
+    HostArr(const HostArr &) = delete;
+    HostArr &operator=(const HostArr &) = delete;
+    ~HostArr() { release(p, pinned); }
+    static void release(T *q, bool pin) {
+        if (!q) return;
+        if (pin) (void)hipHostFree(q);
+        else std::free(q);
+    }
+    void push_back(const T &v) {
+        if (n == cap) reserve(cap ? 2 * cap : 1024);
+        p[n++] = v;
+    }
+    void reserve(size_t c) {
+        if (c <= cap) return;
+        T *q = nullptr;
+        bool pin = hipHostMalloc((void **)&q, c * sizeof(T), hipHostMallocDefault) == hipSuccess;
+        if (!pin) {
+            q = static_cast<T *>(std::malloc(c * sizeof(T)));
+            if (!q) throw std::bad_alloc();
+        }
+        if (n) std::memcpy(q, p, n * sizeof(T));
+        release(p, pinned);
+        p = q;
+        pinned = pin;
+        cap = c;
+    }
+    void clear() { n = 0; }
+    size_t size() const { return n; }
+    T *begin() { return p; }
+    T *end() { return p + n; }
+    T &operator[](size_t i) { return p[i]; }
 };
 
 // One encode launch over a run of consecutive groups with the same code and
@@ -62,22 +107,22 @@ struct rsmi_fenc {
     std::vector<Pending> pend;  // the open group's inputs, in order
 
     // ---- last plan
-    std::vector<FrameGroup> jobs;
-    std::vector<FrameSrc> srcs;
-    std::vector<CarryCopy> carry;
+    HostArr<FrameGroup> jobs;
+    HostArr<FrameSrc> srcs;
+    HostArr<CarryCopy> carry;
     std::vector<rsmi_fenc_packet> packets;
     std::vector<int64_t> g_slot0;
     std::vector<int32_t> g_k, g_m, g_len;
     std::vector<uint32_t> g_seq;
     std::vector<Run> runs;
     int64_t n_slots = 0;
-    int32_t stride_min = 16;
+    int32_t stride_min = rsmi::kSlotShard;
     bool planned = false;
 
     // ---- device side
     int device = -1;
-    uint8_t *dplan = nullptr, *hplan = nullptr;
-    size_t plan_cap = 0, hplan_cap = 0;
+    uint8_t *dplan = nullptr;
+    size_t plan_cap = 0;
     uint8_t *dcarry[2] = {nullptr, nullptr};
     size_t carry_cap[2] = {0, 0};
     int carry_cur = 0;  // pending packets live in dcarry[carry_cur] (or the batch input)
@@ -148,8 +193,7 @@ void close_group(rsmi_fenc *E, int k, int m, int fec_len) {
     E->g_len.push_back(fec_len);
     E->g_seq.push_back(E->seq);
     // pad_end of the encode kernels must stay inside the slot (rsmi.h padding rule)
-    const int need = 16 + ((fec_len + 127) & ~127);
-    E->stride_min = std::max(E->stride_min, (need + 15) & ~15);
+    E->stride_min = std::max(E->stride_min, rsmi::kSlotShard + ((fec_len + 127) & ~127));
     if (m > 0) {
         const bool extend = !E->runs.empty() && E->runs.back().k == k && E->runs.back().n == n &&
                             E->runs.back().len == fec_len &&
@@ -329,7 +373,6 @@ void rsmi_fenc_destroy(rsmi_fenc *E) {
     if (!E) return;
     (void)wait_idle(E);
     if (E->dplan) (void)hipFree(E->dplan);
-    if (E->hplan) (void)hipHostFree(E->hplan);
     for (int i = 0; i < 2; ++i)
         if (E->dcarry[i]) (void)hipFree(E->dcarry[i]);
     if (E->done) (void)hipEventDestroy(E->done);
@@ -353,7 +396,7 @@ int rsmi_fenc_plan(rsmi_fenc *E, int64_t n_events, const int32_t *len, const uin
     E->g_seq.clear();
     E->runs.clear();
     E->n_slots = 0;
-    E->stride_min = 16;
+    E->stride_min = rsmi::kSlotShard;
     for (Pending &p : E->pend) p.emitted = -1;  // sent in an earlier batch
     for (int64_t i = 0; i < n_events; ++i) {
         const bool has = len[i] >= 0;
@@ -380,7 +423,7 @@ int rsmi_fenc_plan(rsmi_fenc *E, int64_t n_events, const int32_t *len, const uin
         E->srcs.push_back(FrameSrc{p.addr, p.len, 0});
         E->jobs.push_back(G);
         E->packets[(size_t)p.emitted].slot = slot;
-        E->stride_min = std::max(E->stride_min, (int32_t)((16 + p.len + 2 + 15) & ~15u));
+        E->stride_min = std::max(E->stride_min, (int32_t)((rsmi::kSlotShard + p.len + 2 + 15) & ~15u));
     }
     // the open group's payloads move to the other carry buffer
     size_t cbytes = 0;
@@ -441,36 +484,29 @@ int rsmi_fenc_run_dev(rsmi_fenc *E, uint8_t *slots, int64_t S, void *stream) {
     // carry buffer this batch fills; resolve tagged carry offsets
     int rc0 = grow(&E->dcarry[E->carry_cur], &E->carry_cap[E->carry_cur], E->carry_need, false);
     if (rc0) return rc0;
-    auto resolve = [E](uint64_t a) -> uint64_t {
-        if (!(a & kCarryTag)) return a;
-        return (uint64_t)(uintptr_t)(E->dcarry[(a & kCarryBuf1) ? 1 : 0] + (a & kCarryOff));
-    };
-    for (FrameSrc &f : E->srcs) f.addr = resolve(f.addr);
-    for (CarryCopy &c : E->carry) {
-        c.src = resolve(c.src);
-        c.dst = resolve(c.dst);
-    }
+    const rsmi::CarryBase carry{{E->dcarry[0], E->dcarry[1]}};
     const size_t gb = E->jobs.size() * sizeof(FrameGroup), sb = E->srcs.size() * sizeof(FrameSrc),
                  cb = E->carry.size() * sizeof(CarryCopy);
     const size_t go = 0, so = (gb + 255) & ~size_t(255), co = (so + sb + 255) & ~size_t(255);
     const size_t all = co + cb + 16;
     int rc = grow(&E->dplan, &E->plan_cap, all, false);
-    if (!rc) rc = grow(&E->hplan, &E->hplan_cap, all, true);
     if (rc) return rc;
-    if (gb) std::memcpy(E->hplan + go, E->jobs.data(), gb);
-    if (sb) std::memcpy(E->hplan + so, E->srcs.data(), sb);
-    if (cb) std::memcpy(E->hplan + co, E->carry.data(), cb);
-    hipError_t e = hipMemcpyAsync(E->dplan, E->hplan, all, hipMemcpyHostToDevice, s);
+    hipError_t e = hipSuccess;
+    if (gb) e = hipMemcpyAsync(E->dplan + go, E->jobs.p, gb, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess && sb) e = hipMemcpyAsync(E->dplan + so, E->srcs.p, sb, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess && cb) e = hipMemcpyAsync(E->dplan + co, E->carry.p, cb, hipMemcpyHostToDevice, s);
     if (e == hipSuccess)
         e = rsmi::launch_frame(reinterpret_cast<const FrameGroup *>(E->dplan + go), (int64_t)E->jobs.size(),
-                               reinterpret_cast<const FrameSrc *>(E->dplan + so), slots, S, s);
+                               reinterpret_cast<const FrameSrc *>(E->dplan + so), carry, slots, S, s);
     if (e != hipSuccess) return fail(RSMI_ERR_HIP, std::string("fenc frame: ") + hipGetErrorString(e));
     // parity of every group
     for (const Run &r : E->runs) {
-        rc = rsmi_encode_dev(r.k, r.n, slots + r.slot0 * S + 16, (int64_t)r.n * S, S, r.len, r.count, stream);
+        rc = rsmi_encode_dev(r.k, r.n, slots + r.slot0 * S + rsmi::kSlotShard, (int64_t)r.n * S, S,
+                             r.len, r.count, stream);
         if (rc) return rc;
     }
-    e = rsmi::launch_carry(reinterpret_cast<const CarryCopy *>(E->dplan + co), (int64_t)E->carry.size(), s);
+    e = rsmi::launch_carry(reinterpret_cast<const CarryCopy *>(E->dplan + co), (int64_t)E->carry.size(),
+                           carry, s);
     if (e == hipSuccess) e = hipEventRecord(E->done, s);
     if (e != hipSuccess) return fail(RSMI_ERR_HIP, std::string("fenc carry: ") + hipGetErrorString(e));
     E->in_flight = true;

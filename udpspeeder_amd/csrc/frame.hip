@@ -91,36 +91,35 @@ __device__ __forceinline__ u32x4 konst(uint32_t c, int nb, int64_t s0, int64_t b
     return r;
 }
 
-struct Src {
-    const uint8_t *addr;
-    uint32_t len, off;
+// Source records of the job being framed, staged in LDS (structure of arrays).
+struct LdsSrc {
+    uint64_t addr[kLdsSrc];
+    uint32_t off[kLdsSrc];
+    uint32_t len[kLdsSrc];
 };
 
-__device__ __forceinline__ Src get_src(const FrameSrc *g, const FrameSrc *lds, uint32_t j,
-                                       uint32_t nlds) {
-    const FrameSrc &s = j < nlds ? lds[j] : g[j];
-    return Src{reinterpret_cast<const uint8_t *>(s.addr), s.len, s.off};
-}
-
-// Largest j in [0, n) with off_j <= pos (off_0 <= pos is guaranteed).
-__device__ __forceinline__ uint32_t find_src(const FrameSrc *g, const FrameSrc *lds, uint32_t n,
-                                             uint32_t nlds, int64_t pos) {
-    uint32_t lo = 0, hi = n;  // invariant: off_lo <= pos, answer < hi
-    while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) >> 1;
-        const uint32_t o = mid < nlds ? lds[mid].off : g[mid].off;
-        if ((int64_t)o <= pos) lo = mid;
-        else hi = mid;
+// Read access to a job's source records: from LDS, or straight from global
+// memory for the rare job with more than kLdsSrc records (tiny packets, long
+// queue_len), so that the LDS path holds no global loads a wait could join.
+template <bool kGlobal>
+struct View {
+    const FrameSrc *g;
+    const LdsSrc *l;
+    CarryBase carry;
+    __device__ __forceinline__ uint32_t off(uint32_t j) const { return kGlobal ? g[j].off : l->off[j]; }
+    __device__ __forceinline__ uint32_t len(uint32_t j) const { return kGlobal ? g[j].len : l->len[j]; }
+    __device__ __forceinline__ const uint8_t *addr(uint32_t j) const {
+        return kGlobal ? carry.resolve(g[j].addr) : reinterpret_cast<const uint8_t *>(l->addr[j]);
     }
-    return lo;
-}
+};
 
 // The 16 stream bytes at [b, b+16) of a stream made of: an optional 4-byte
-// big-endian count at [0, 4), then source records [u16 len BE][payload] at
-// their offsets, then zeros from stream_len on.
-__device__ u32x4 stream_piece(const FrameSrc *g, const FrameSrc *lds, uint32_t j0, uint32_t n,
-                              uint32_t nlds, int64_t b, int64_t stream_len, bool count_hdr,
-                              uint32_t count) {
+// big-endian count at [0, 4), then records j0.. [u16 len BE][payload] at their
+// offsets, then zeros from stream_len on.  j is a record with off_j <= max(b, 4)
+// whose successor starts beyond it (the search result).
+template <class V>
+__device__ u32x4 stream_piece(const V &src, uint32_t j, uint32_t jend, int64_t b, int64_t stream_len,
+                              bool count_hdr, uint32_t count) {
     u32x4 acc = {0, 0, 0, 0};
     const int64_t end = min(b + 16, stream_len);
     int64_t pos = b;
@@ -129,20 +128,16 @@ __device__ u32x4 stream_piece(const FrameSrc *g, const FrameSrc *lds, uint32_t j
         acc |= konst(count, 4, 0, b);
         pos = 4;
     }
-    if (pos >= end || n == 0) return acc;
-    uint32_t j = j0 + find_src(g + j0, lds + j0, n, nlds > j0 ? nlds - j0 : 0, pos);
-    const uint32_t jend = j0 + n;
     while (pos < end && j < jend) {
-        const Src s = get_src(g, lds, j, nlds);
-        const int64_t p0 = s.off, q0 = p0 + 2, q1 = q0 + s.len;
+        const int64_t p0 = src.off(j), q0 = p0 + 2, q1 = q0 + src.len(j);
         if (pos < q0) {
-            acc |= konst(s.len & 0xffffu, 2, p0, b);
+            acc |= konst(src.len(j) & 0xffffu, 2, p0, b);
             pos = min(q0, end);
         }
         if (pos < end && pos < q1) {
             const int64_t e = min(q1, end);
             const int lo = (int)(pos - b), hi = (int)(e - b);
-            acc |= keep(window(s.addr + (pos - q0), lo, hi), lo, hi);
+            acc |= keep(window(src.addr(j) + (pos - q0), lo, hi), lo, hi);
             pos = e;
         }
         if (pos >= q1) ++j;
@@ -150,54 +145,174 @@ __device__ u32x4 stream_piece(const FrameSrc *g, const FrameSrc *lds, uint32_t j
     return acc;
 }
 
+constexpr int kBatch = 4;     // pieces per thread per step: their loads are in flight together
+constexpr int kSlowMax = 1024;  // boundary pieces queued per job (more are assembled in place)
+
+struct Piece {
+    uint32_t i, q, j;
+    int64_t b;
+};
+
+// Piece t = shard i * pps + piece q, its stream position b, and (mode 0) the
+// record j holding stream byte max(b, 4) is found by the caller.
+__device__ __forceinline__ Piece piece_at(const FrameGroup &G, uint32_t t, uint32_t pps,
+                                          uint32_t magic) {
+    uint32_t i = pps == 1 ? t : __umulhi(t, magic);  // t / pps, corrected below
+    if (i * pps > t) --i;
+    if ((i + 1) * pps <= t) ++i;
+    Piece P;
+    P.i = i;
+    P.q = t - i * pps;
+    P.b = G.mode == 0 ? (int64_t)i * G.fec_len + 16 * (int64_t)P.q : 16 * (int64_t)P.q;
+    P.j = G.mode == 0 ? 0u : i;
+    return P;
+}
+
+template <class V>
+__device__ __forceinline__ uint32_t find_record(const V &src, uint32_t n, int64_t b) {
+    uint32_t j = 0;
+    const int64_t pos = max(b, (int64_t)4);
+    while (n > 1) {
+        const uint32_t h = n >> 1;
+        j = (int64_t)src.off(j + h) <= pos ? j + h : j;
+        n -= h;
+    }
+    return j;
+}
+
+template <class V>
+__device__ __forceinline__ u32x4 slow_piece(const FrameGroup &G, const V &src, uint32_t nsrc,
+                                            const Piece &P) {
+    if (G.mode == 0) return stream_piece(src, P.j, nsrc, P.b, G.blob_len, true, G.nsrc);
+    return stream_piece(src, P.j, P.j + 1, P.b, (int64_t)src.len(P.j) + 2, false, 0);
+}
+
+__device__ __forceinline__ void put_piece(uint8_t *s0, int64_t slot_stride, const Piece &P, u32x4 v) {
+    *reinterpret_cast<u32x4 *>(s0 + (int64_t)P.i * slot_stride + kSlotShard + 16 * (int64_t)P.q) = v;
+}
+
+// Frame one job with kThreads threads.  Phase 1 takes kBatch pieces per thread
+// per step: the record searches run interleaved and the 16-byte loads of the
+// pieces that lie inside one payload are issued together (straight-line, every
+// lane loads: the others read a dummy address) and stored.  Pieces that cross
+// a record or stream boundary (a few per record) are queued in LDS; phase 2
+// assembles them segment by segment, one per lane, so no wave runs the segment
+// loop for a single lane of its 64.
+template <bool kGlobal>
+__device__ __forceinline__ void frame_job(const FrameGroup &G, const View<kGlobal> &src,
+                                          uint8_t *s0, int64_t slot_stride, const uint8_t *dummy,
+                                          uint32_t *slow, uint32_t *nslow) {
+    const uint32_t nsrc = G.mode == 0 ? G.nsrc : G.nframe;
+    const uint32_t pps = (G.fec_len + 15) >> 4;
+    const uint32_t total = pps * G.nframe;
+    const uint32_t magic = pps == 1 ? 0u : (uint32_t)(0xFFFFFFFFu / pps) + 1u;
+    for (uint32_t t0 = threadIdx.x; t0 < total; t0 += kBatch * kThreads) {
+        Piece P[kBatch];
+#pragma unroll
+        for (int u = 0; u < kBatch; ++u) P[u] = piece_at(G, min(t0 + u * kThreads, total - 1), pps, magic);
+        if (G.mode == 0) {  // kBatch interleaved searches (same trip count)
+            uint32_t n = nsrc;
+            while (n > 1) {
+                const uint32_t h = n >> 1;
+#pragma unroll
+                for (int u = 0; u < kBatch; ++u)
+                    P[u].j = (int64_t)src.off(P[u].j + h) <= max(P[u].b, (int64_t)4) ? P[u].j + h : P[u].j;
+                n -= h;
+            }
+        }
+        const uint8_t *A[kBatch];
+        bool fast[kBatch];
+#pragma unroll
+        for (int u = 0; u < kBatch; ++u) {
+            const int64_t q0 = G.mode == 0 ? (int64_t)src.off(P[u].j) + 2 : 2;
+            const int64_t q1 = q0 + src.len(P[u].j);
+            fast[u] = P[u].b >= q0 && P[u].b + 16 <= q1;
+            A[u] = fast[u] ? src.addr(P[u].j) + (P[u].b - q0) : dummy;
+        }
+        u32x4 v[kBatch];
+#pragma unroll
+        for (int u = 0; u < kBatch; ++u) v[u] = window(A[u], 0, 16);
+#pragma unroll
+        for (int u = 0; u < kBatch; ++u) {
+            const uint32_t t = t0 + u * kThreads;
+            if (t >= total) continue;
+            if (fast[u]) {
+                put_piece(s0, slot_stride, P[u], v[u]);
+            } else {
+                const uint32_t k = atomicAdd(nslow, 1u);
+                if (k < (uint32_t)kSlowMax) slow[k] = t;
+            }
+        }
+    }
+    __syncthreads();
+    const uint32_t nq = *nslow;
+    if (nq <= (uint32_t)kSlowMax) {
+        for (uint32_t k = threadIdx.x; k < nq; k += kThreads) {
+            Piece Q = piece_at(G, slow[k], pps, magic);
+            if (G.mode == 0) Q.j = find_record(src, nsrc, Q.b);
+            put_piece(s0, slot_stride, Q, slow_piece(G, src, nsrc, Q));
+        }
+    } else {  // queue overflow (thousands of tiny records): every boundary piece in place
+        for (uint32_t t = threadIdx.x; t < total; t += kThreads) {
+            Piece Q = piece_at(G, t, pps, magic);
+            if (G.mode == 0) Q.j = find_record(src, nsrc, Q.b);
+            const int64_t q0 = G.mode == 0 ? (int64_t)src.off(Q.j) + 2 : 2;
+            if (Q.b >= q0 && Q.b + 16 <= q0 + src.len(Q.j)) continue;
+            put_piece(s0, slot_stride, Q, slow_piece(G, src, nsrc, Q));
+        }
+    }
+}
+
 __global__ __launch_bounds__(kThreads) void k_frame(const FrameGroup *groups, int64_t ngroups,
-                                                     const FrameSrc *srcs, uint8_t *slots,
-                                                     int64_t slot_stride) {
-    __shared__ FrameSrc lsrc[kLdsSrc];
+                                                     const FrameSrc *srcs, CarryBase carry,
+                                                     uint8_t *slots, int64_t slot_stride) {
+    __shared__ LdsSrc lsrc;
+    __shared__ uint32_t slow[kSlowMax];
+    __shared__ uint32_t nslow;
+    const uint8_t *dummy = reinterpret_cast<const uint8_t *>(groups);  // >= 20 readable bytes
     for (int64_t gi = blockIdx.x; gi < ngroups; gi += gridDim.x) {
         const FrameGroup G = groups[gi];
         const FrameSrc *gs = srcs + G.src0;
         const uint32_t nsrc = G.mode == 0 ? G.nsrc : G.nframe;
-        const uint32_t nl = min(nsrc, (uint32_t)kLdsSrc);
-        for (uint32_t t = threadIdx.x; t < nl; t += kThreads) lsrc[t] = gs[t];
+        const bool in_lds = nsrc <= (uint32_t)kLdsSrc;
+        if (in_lds)
+            for (uint32_t t = threadIdx.x; t < nsrc; t += kThreads) {
+                const FrameSrc f = gs[t];
+                lsrc.addr[t] = (uint64_t)(uintptr_t)carry.resolve(f.addr);
+                lsrc.off[t] = f.off;
+                lsrc.len[t] = f.len;
+            }
+        if (threadIdx.x == 0) nslow = 0;
         __syncthreads();
         uint8_t *s0 = slots + (int64_t)G.slot0 * slot_stride;
         // headers: seq | mode | k | m | index (fec_manager.cpp:318-333); mode-1
         // data packets carry k = m = 0 (:321-323)
         for (uint32_t j = threadIdx.x; j < G.nslots; j += kThreads) {
             const bool zero_km = G.mode == 1 && j < G.nframe;
-            const uint32_t w1 = (uint32_t)G.mode | (zero_km ? 0u : ((uint32_t)G.k << 8 | (uint32_t)G.m << 16)) |
+            const uint32_t w1 = (uint32_t)G.mode |
+                                (zero_km ? 0u : ((uint32_t)G.k << 8 | (uint32_t)G.m << 16)) |
                                 ((G.idx0 + j) & 0xffu) << 24;
-            *reinterpret_cast<u32x2 *>(s0 + (int64_t)j * slot_stride + 8) = u32x2{bswap32(G.seq), w1};
+            *reinterpret_cast<u32x2 *>(s0 + (int64_t)j * slot_stride + kSlotHeader) =
+                u32x2{bswap32(G.seq), w1};
         }
-        // data shards, whole 16-byte pieces
-        const uint32_t pps = (G.fec_len + 15) >> 4;
-        const uint32_t total = pps * G.nframe;
-        for (uint32_t t = threadIdx.x; t < total; t += kThreads) {
-            const uint32_t i = t / pps, q = t - i * pps;
-            u32x4 v;
-            if (G.mode == 0) {
-                const int64_t b = (int64_t)i * G.fec_len + 16 * (int64_t)q;
-                v = stream_piece(gs, lsrc, 0, nsrc, nl, b, G.blob_len, true, G.nsrc);
-            } else {
-                const Src s = get_src(gs, lsrc, i, nl);
-                v = stream_piece(gs, lsrc, i, 1, nl, 16 * (int64_t)q, (int64_t)s.len + 2, false, 0);
-            }
-            *reinterpret_cast<u32x4 *>(s0 + (int64_t)i * slot_stride + 16 + 16 * (int64_t)q) = v;
-        }
-        __syncthreads();  // lsrc is restaged for the next group
+        if (in_lds)
+            frame_job(G, View<false>{gs, &lsrc, carry}, s0, slot_stride, dummy, slow, &nslow);
+        else
+            frame_job(G, View<true>{gs, &lsrc, carry}, s0, slot_stride, dummy, slow, &nslow);
+        __syncthreads();  // lsrc and the queue are reset for the next group
     }
 }
 
 // Pending packets -> carry area: dst (16-aligned) gets len bytes of src, whole
 // pieces (bytes past len inside the last piece are zero).
-__global__ __launch_bounds__(kThreads) void k_carry(const CarryCopy *jobs, int64_t njobs) {
+__global__ __launch_bounds__(kThreads) void k_carry(const CarryCopy *jobs, int64_t njobs,
+                                                     CarryBase carry) {
     const int lane = threadIdx.x & 63;
     const int64_t w0 = (int64_t)blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
     for (int64_t w = w0; w < njobs; w += (int64_t)gridDim.x * (kThreads / 64)) {
         const CarryCopy J = jobs[w];
-        const uint8_t *src = reinterpret_cast<const uint8_t *>(J.src);
-        uint8_t *dst = reinterpret_cast<uint8_t *>(J.dst);
+        const uint8_t *src = carry.resolve(J.src);
+        uint8_t *dst = const_cast<uint8_t *>(carry.resolve(J.dst));
         for (uint32_t q = lane; 16 * q < J.len; q += 64) {
             const int hi = (int)min(16u, J.len - 16 * q);
             *reinterpret_cast<u32x4 *>(dst + 16 * (int64_t)q) = keep(window(src + 16 * q, 0, hi), 0, hi);
@@ -208,18 +323,18 @@ __global__ __launch_bounds__(kThreads) void k_carry(const CarryCopy *jobs, int64
 }  // namespace
 
 hipError_t launch_frame(const FrameGroup *groups, int64_t ngroups, const FrameSrc *srcs,
-                        uint8_t *slots, int64_t slot_stride, hipStream_t s) {
+                        CarryBase carry, uint8_t *slots, int64_t slot_stride, hipStream_t s) {
     if (ngroups <= 0) return hipSuccess;
     const int64_t blocks = ngroups < 65536 ? ngroups : 65536;
-    k_frame<<<(unsigned)blocks, kThreads, 0, s>>>(groups, ngroups, srcs, slots, slot_stride);
+    k_frame<<<(unsigned)blocks, kThreads, 0, s>>>(groups, ngroups, srcs, carry, slots, slot_stride);
     return hipGetLastError();
 }
 
-hipError_t launch_carry(const CarryCopy *jobs, int64_t njobs, hipStream_t s) {
+hipError_t launch_carry(const CarryCopy *jobs, int64_t njobs, CarryBase carry, hipStream_t s) {
     if (njobs <= 0) return hipSuccess;
     int64_t blocks = (njobs + kThreads / 64 - 1) / (kThreads / 64);
     if (blocks > 8192) blocks = 8192;
-    k_carry<<<(unsigned)blocks, kThreads, 0, s>>>(jobs, njobs);
+    k_carry<<<(unsigned)blocks, kThreads, 0, s>>>(jobs, njobs, carry);
     return hipGetLastError();
 }
 

@@ -6,6 +6,7 @@
 #include <cstdint>
 
 #include "../../include/rsmi.h"
+#include "../../include/rsmi_fec.h"
 
 namespace rsmi {
 
@@ -98,6 +99,8 @@ hipError_t launch_cook(const CookArgs &a, bool decook, int max_blocks, hipStream
 
 
 // ---- FEC framing (frame.hip, fec_enc.cpp) --------------------------------------
+constexpr int kSlotHeader = RSMI_FEC_SLOT_PACKET;  // packet (8-byte header) offset in a slot
+constexpr int kSlotShard = RSMI_FEC_SLOT_SHARD;    // shard offset: 128-byte aligned rows
 // One framing job: a completed FEC group (nslots = k + m slots, nframe = k data
 // shards) or a mode-1 packet sent ahead of its group (nslots = nframe = 1).
 struct FrameGroup {
@@ -110,17 +113,27 @@ struct FrameGroup {
     uint16_t nslots, nframe;
     uint8_t mode, k, m, idx0;  // header bytes; idx0 = index of slot 0
 };
+// A payload address in a plan: a device address, or (kCarryTag set) an offset
+// into carry buffer 0 or 1 (kCarryBuf1), resolved by the kernels.
+constexpr uint64_t kCarryTag = 1ull << 63, kCarryBuf1 = 1ull << 62, kCarryOff = kCarryBuf1 - 1;
+struct CarryBase {
+    const uint8_t *buf[2];
+    __host__ __device__ const uint8_t *resolve(uint64_t a) const {
+        return (a & kCarryTag) ? buf[(a & kCarryBuf1) ? 1 : 0] + (a & kCarryOff)
+                               : reinterpret_cast<const uint8_t *>(a);
+    }
+};
 struct FrameSrc {
-    uint64_t addr;      // device address of the payload
+    uint64_t addr;      // payload address (carry-tagged or device)
     uint32_t len;
     uint32_t off;       // mode 0: blob offset of the record's u16 length; mode 1: 0
 };
 struct CarryCopy {
-    uint64_t src, dst;  // dst 16-aligned, room for round_up(len, 16)
+    uint64_t src, dst;  // carry-tagged or device addresses; dst 16-aligned, room for round_up(len, 16)
     uint32_t len, pad;
 };
 hipError_t launch_frame(const FrameGroup *groups, int64_t ngroups, const FrameSrc *srcs,
-                        uint8_t *slots, int64_t slot_stride, hipStream_t s);
-hipError_t launch_carry(const CarryCopy *jobs, int64_t njobs, hipStream_t s);
+                        CarryBase carry, uint8_t *slots, int64_t slot_stride, hipStream_t s);
+hipError_t launch_carry(const CarryCopy *jobs, int64_t njobs, CarryBase carry, hipStream_t s);
 
 }  // namespace rsmi

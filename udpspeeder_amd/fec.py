@@ -28,6 +28,8 @@ import numpy as np
 from ._lib import check, lib, rsmi_fec_config, rsmi_fenc_packet
 
 HEADER = 8
+SLOT_PACKET = 120   # RSMI_FEC_SLOT_PACKET: packet offset in a slot
+SLOT_SHARD = 128    # RSMI_FEC_SLOT_SHARD: shard offset (128-byte aligned rows)
 
 
 def fec_config(rs_str: str, mode: int = 0, mtu: int = 1250, queue_len: int = 200,
@@ -129,9 +131,9 @@ class FecEncoder:
 
     @staticmethod
     def slot_stride_for(fec_len_max: int) -> int:
-        """A slot stride that fits fec_len_max-byte shards and do_cook's tail
-        (rsmi_cook.h) in place: 16 + round_up(fec_len_max, 128), + 128."""
-        return 16 + (fec_len_max + 127) // 128 * 128 + 128
+        """A multiple of 128 that fits fec_len_max-byte shards and do_cook's
+        tail (rsmi_cook.h) in place: SLOT_SHARD + round_up(fec_len_max + 37, 128)."""
+        return SLOT_SHARD + (fec_len_max + 37 + 127) // 128 * 128
 
     # ---- the reference's per-call interface (one GPU batch per call) ---------
     def input(self, data: Optional[bytes]) -> int:
@@ -145,11 +147,11 @@ class FecEncoder:
             buf[:len(data)] = torch.frombuffer(bytearray(data), dtype=torch.uint8) if data else buf[:0]
             buf = buf.cuda()
             p = self.plan([len(data)], [0], buf)
-        stride = max(p.slot_stride_min, 16)
+        stride = p.slot_stride_min
         slots = torch.zeros(max(1, p.n_slots) * stride, dtype=torch.uint8, device="cuda")
         self.run(slots, stride)
         host = slots.cpu().numpy()
-        self._ready = [host[s * stride + HEADER:s * stride + HEADER + ln].tobytes()
+        self._ready = [host[s * stride + SLOT_PACKET:s * stride + SLOT_PACKET + ln].tobytes()
                        for s, ln, _ in p.packets]
         return int(p.ret[0])
 
@@ -161,5 +163,5 @@ class FecEncoder:
 
 def packets_bytes(plan: FencPlan, slots_host: np.ndarray, slot_stride: int) -> List[bytes]:
     """The emitted packets of a run, as bytes (slots_host: the slot array on the host)."""
-    return [slots_host[s * slot_stride + HEADER:s * slot_stride + HEADER + ln].tobytes()
+    return [slots_host[s * slot_stride + SLOT_PACKET:s * slot_stride + SLOT_PACKET + ln].tobytes()
             for s, ln, _ in plan.packets]
