@@ -92,7 +92,9 @@ typedef struct rsmi_fenc_packet {
  * Afterwards *n_slots, *n_packets give the sizes of the batch and
  * *slot_stride_min the least slot_stride rsmi_fenc_run_dev accepts.
  * The plan replaces the previous one; state advances as if input() had been
- * called for every event. */
+ * called for every event.  Run every plan (its carry copies keep open groups)
+ * before the next.  in_base NULL plans decisions only: such an encoder never
+ * runs on a device. */
 int rsmi_fenc_plan(rsmi_fenc *enc, int64_t n_events, const int32_t *len, const uint64_t *in_off,
                    const uint8_t *in_base, int32_t *ret, int64_t *n_slots, int64_t *n_packets,
                    int32_t *slot_stride_min);
@@ -116,6 +118,61 @@ int rsmi_fenc_groups(const rsmi_fenc *enc, int64_t *n_groups, int64_t *slot0, in
  * slot_stride: a multiple of 16, >= slot_stride_min (a multiple of 128 keeps
  * the shard rows line-aligned).  Asynchronous. */
 int rsmi_fenc_run_dev(rsmi_fenc *enc, uint8_t *slots_base, int64_t slot_stride, void *stream);
+
+/* ---- receive side: fec_decode_manager_t ------------------
+ *
+ * fec_decode_manager_t::input / output (fec_manager.cpp:469-797) take every
+ * received packet (after de_cook): header checks, the anti-replay window of
+ * anti_replay_t (fec_manager.h:187-235), the per-seq group map, the ring of
+ * fec_buff_num packet buffers whose reuse evicts old groups (:554-576), and --
+ * once a group has enough shards -- rs_decode2 plus blob_decode (mode 0) or
+ * the length-prefixed data shards (mode 1), with mode-1 data packets passed
+ * straight through (decode_fast_send, :760-776).
+ *
+ * rsmi_fdec_plan replays those decisions for a batch of packets on the host
+ * (they need only headers, lengths and the mode-1 length prefixes).
+ * rsmi_fdec_run_dev gathers every completed group's first k shards into
+ * per-(k,n) staging batches on the device, decodes them with rsmi_decode_dev,
+ * packs each group's k data rows contiguously and copies them to pinned host
+ * memory.  rsmi_fdec_outputs then lists, per input event and in the
+ * reference's order, the packets output() would return.  Received shards of
+ * groups still open at the end of a batch are kept in a device carry area
+ * indexed like the reference's ring, so groups straddle batches.
+ *
+ * Differences from the reference: a group whose shard indices include one
+ * >= k + m makes the reference abort (assert on rs_decode2, :632 and :710);
+ * here that group is dropped like a failed decode (no output, anti-replay
+ * marked).  Nothing else differs. */
+typedef struct rsmi_fdec rsmi_fdec;
+
+/* buff_num: fec_buff_num (fec_manager.cpp:33), 0 for the default 2000. */
+int rsmi_fdec_create(int32_t buff_num, rsmi_fdec **out);
+void rsmi_fdec_destroy(rsmi_fdec *dec);
+
+/* Plan input() for n received packets: packet i is len[i] bytes at
+ * host_base + off[i] (host memory, read for headers and mode-1 length
+ * prefixes) and at dev_base + off[i] (the same bytes on the device, 16
+ * readable bytes after every packet).  now_ms is get_current_time() for the
+ * anti-replay timeout (anti_replay_timeout = 120 s, fec_manager.h:185).
+ * ret[i] (may be NULL) receives input()'s return value.  *n_decodes: groups
+ * this batch decodes.  Run every plan before the next.  dev_base NULL plans
+ * decisions only (return codes): such a decoder never runs on a device. */
+int rsmi_fdec_plan(rsmi_fdec *dec, int64_t n, const int32_t *len, const uint64_t *off,
+                   const uint8_t *host_base, const uint8_t *dev_base, int64_t now_ms,
+                   int32_t *ret, int64_t *n_decodes);
+
+/* Gather, decode, pack and copy back the planned groups on `stream`
+ * (asynchronous; dev_base must stay valid until it completes). */
+int rsmi_fdec_run_dev(rsmi_fdec *dec, void *stream);
+
+/* Wait for the run and resolve the output list: *n_out packets. */
+int rsmi_fdec_outputs(rsmi_fdec *dec, int64_t *n_out);
+
+/* The resolved outputs (arrays of n_out entries, any may be NULL): host
+ * pointer and length of each packet and the index of the input() call whose
+ * output() returned it.  Pointers stay valid until the next plan; a
+ * pass-through packet points into host_base. */
+int rsmi_fdec_output_list(const rsmi_fdec *dec, const uint8_t **ptr, int32_t *len, int32_t *event);
 
 #ifdef __cplusplus
 }

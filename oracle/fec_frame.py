@@ -444,3 +444,46 @@ class DecodeManager:
     def output(self) -> List[bytes]:
         r, self.ready = self.ready, []
         return r
+
+
+def lossy_channel(packets: List[bytes], seed: int, loss=0.1, dup=0.02, swap=0.05, delay=0.0,
+                  delay_by=2500, replay=0.0, trunc=0.0, garbage=0.0) -> List[bytes]:
+    """A seeded unreliable channel for decode tests: drops, duplicates, swaps
+    neighbours, delays packets by ~delay_by positions (past the reference's
+    2000-buffer ring), replays old packets (anti-replay), truncates mode-1
+    packets by 1..3 bytes and injects short / out-of-range garbage headers.
+    Deterministic in (packets, seed)."""
+    rng = np.random.default_rng(seed)
+    out: List[bytes] = []
+    held: List[Tuple[int, bytes]] = []
+    for p in packets:
+        while held and held[0][0] <= len(out):
+            out.append(held.pop(0)[1])
+        r = rng.random(8)
+        if r[0] < loss:
+            continue
+        q = p
+        if r[1] < trunc and len(q) > HEADER + 3 and q[4] == 1:
+            q = q[:len(q) - 1 - int(rng.integers(0, 3))]
+        if r[2] < delay:
+            held.append((len(out) + delay_by + int(rng.integers(0, 500)), q))
+            held.sort(key=lambda t: t[0])
+        else:
+            out.append(q)
+        if r[3] < dup:
+            out.append(q)
+        if r[4] < replay and len(out) > 50:
+            out.append(out[int(rng.integers(0, len(out) - 50))])
+        if r[5] < garbage:
+            kind = int(rng.integers(0, 3))
+            if kind == 0:
+                out.append(bytes(rng.integers(0, 256, int(rng.integers(0, 8)), dtype=np.uint8)))
+            elif kind == 1:  # data_num + redundant_num >= 255
+                out.append(q[:5] + bytes([200, 60]) + q[7:])
+            else:  # type 0 with data_num 0
+                out.append(q[:4] + bytes([0, 0]) + q[6:])
+    out += [p for _, p in held]
+    for i in range(len(out) - 1):
+        if rng.random() < swap:
+            out[i], out[i + 1] = out[i + 1], out[i]
+    return out

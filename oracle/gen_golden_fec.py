@@ -26,7 +26,7 @@ import os
 import numpy as np
 
 from oracle.cpu import Reference, cook_payloads, splitmix_words
-from oracle.fec_frame import FecReference, zero_stale_tail
+from oracle.fec_frame import EncodeManager, FecReference, lossy_channel, zero_stale_tail
 
 OUT = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "golden")
 FEC_SEED = 0xFEC0
@@ -56,6 +56,38 @@ def case_events(ci: int, n: int, lmax: int, flush_pm: int, zero_pm: int):
     pay = cook_payloads(FEC_SEED + ci, 0, n, np.maximum(lens, 0), max(1, int(lens.max(initial=0))))
     ev = [None if lens[i] < 0 else pay[i, :lens[i]].tobytes() for i in range(n)]
     return lens, ev
+
+
+# Receive side (fec_decode_manager_t): the packets EncodeManager (pinned to the
+# reference encoder above) frames for an encode case, seq0 fixed, through a
+# seeded lossy channel, fed to the REAL reference decoder.
+# name, encode case, seq0, channel kwargs
+DEC_CASES = [
+    ("d_m0_20_10", "m0_20_10", 0x10, dict(loss=0.15, dup=0.03, swap=0.1)),
+    ("d_m0_c3", "m0_c3", 0xFFFFFFF8, dict(loss=0.3, dup=0.05, swap=0.2, replay=0.02)),
+    ("d_m0_small_queue", "m0_small_queue", 7, dict(loss=0.2, swap=0.3, garbage=0.05)),
+    ("d_m0_queue3", "m0_queue3", 99, dict(loss=0.25, dup=0.1, delay=0.02, delay_by=2100)),
+    ("d_m0_tiny", "m0_tiny", 5, dict(loss=0.4, dup=0.1, swap=0.3, garbage=0.1)),
+    ("d_m1_20_10", "m1_20_10", 0x20, dict(loss=0.15, dup=0.03, swap=0.1, trunc=0.02)),
+    ("d_m1_c3", "m1_c3", 0xABCDEF, dict(loss=0.3, dup=0.05, swap=0.2, replay=0.03, trunc=0.03)),
+    ("d_m1_no_parity", "m1_no_parity", 3, dict(loss=0.1, dup=0.1, garbage=0.05)),
+    ("d_m1_long", "m1_long", 11, dict(loss=0.2, swap=0.2)),
+]
+
+
+def dec_channel(name: str):
+    """The channel packets of a decode case (deterministic)."""
+    ci = [c[0] for c in DEC_CASES].index(name)
+    _, ename, seq0, kw = DEC_CASES[ci]
+    ei = [c[0] for c in CASES].index(ename)
+    _, rs, mode, mtu, ql, n, lmax, fpm, zpm = CASES[ei]
+    lens, ev = case_events(ei, n, lmax, fpm, zpm)
+    em = EncodeManager(rs, mode, mtu, ql, seq0)
+    pk = []
+    for e in ev:
+        em.input(e)
+        pk += em.output()
+    return lossy_channel(pk, 0xC4A7 + ci, **kw)
 
 
 def main():
@@ -91,6 +123,26 @@ def main():
         print(f"{name}: {n} events, {len(pk)} packets, {len(blob)} B, stale bytes zeroed {stale}")
     arrays["cases"] = np.array(names)
     np.savez_compressed(os.path.join(OUT, "fec_encode.npz"), **arrays)
+
+    arrays, names = {}, []
+    for name, _, _, _ in DEC_CASES:
+        chan = dec_channel(name)
+        ret, out, oev = fr.decode(chan)
+        blob = b"".join(out)
+        arrays[f"{name}__chan_sha256"] = np.frombuffer(hashlib.sha256(b"".join(
+            len(p).to_bytes(4, "little") + p for p in chan)).digest(), np.uint8)
+        arrays[f"{name}__ret"] = np.asarray(ret, np.int32)
+        arrays[f"{name}__out_len"] = np.array([len(p) for p in out], np.int32)
+        arrays[f"{name}__out_event"] = np.asarray(oev, np.int32)
+        arrays[f"{name}__sha256"] = np.frombuffer(hashlib.sha256(blob).digest(), np.uint8)
+        if len(blob) <= FULL_BYTES_MAX:
+            arrays[f"{name}__out_bytes"] = np.frombuffer(blob, np.uint8)
+        names.append(name)
+        rv = np.asarray(ret)
+        print(f"{name}: {len(chan)} packets in, {len(out)} out ({len(blob)} B), "
+              f"ret -1: {(rv == -1).sum()}, ret 0: {(rv == 0).sum()}")
+    arrays["cases"] = np.array(names)
+    np.savez_compressed(os.path.join(OUT, "fec_decode.npz"), **arrays)
 
 
 if __name__ == "__main__":

@@ -1,0 +1,204 @@
+"""Receive side of the FEC framing: fec_decode_manager_t.
+
+CPU tests pin the Python restatement (oracle/fec_frame.py:DecodeManager) to the
+REAL reference decoder -- through the committed fixtures
+(tests/golden/fec_decode.npz, oracle/gen_golden_fec.py) and, where the
+reference build is present, live on long runs whose delays exceed the
+2000-buffer ring -- and check librsmi.so's host planner (return codes) without
+a GPU.  GPU tests run the batched decoder (plan -> gather/decode/pack on the
+GPU -> outputs) and compare every output packet with the fixtures and the
+restatement, with batches cut at arbitrary packets so groups straddle batches.
+"""
+import hashlib
+import os
+
+import numpy as np
+import pytest
+
+from oracle.fec_frame import DecodeManager, EncodeManager, FecReference, lossy_channel
+from oracle.gen_golden_fec import DEC_CASES, dec_channel
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "fec_decode.npz")
+NAMES = [c[0] for c in DEC_CASES]
+
+
+@pytest.fixture(scope="module")
+def fx():
+    return dict(np.load(GOLDEN))
+
+
+def _case(fx, name):
+    chan = dec_channel(name)
+    h = hashlib.sha256(b"".join(len(p).to_bytes(4, "little") + p for p in chan)).digest()
+    assert h == fx[f"{name}__chan_sha256"].tobytes(), "channel regeneration drifted"
+    full = fx.get(f"{name}__out_bytes")
+    exp = None
+    if full is not None:
+        off = np.concatenate([[0], np.cumsum(fx[f"{name}__out_len"])])
+        b = full.tobytes()
+        exp = [b[off[i]:off[i + 1]] for i in range(len(off) - 1)]
+    return dict(chan=chan, ret=list(fx[f"{name}__ret"]), out_len=list(fx[f"{name}__out_len"]),
+                out_event=list(fx[f"{name}__out_event"]), sha=fx[f"{name}__sha256"].tobytes(),
+                exp=exp)
+
+
+def _oracle_run(chan, now=None):
+    dm = DecodeManager()
+    ret, out, ev = [], [], []
+    for i, p in enumerate(chan):
+        if now is not None:
+            dm.now = now[i]
+        ret.append(dm.input(p))
+        o = dm.output()
+        out += o
+        ev += [i] * len(o)
+    return ret, out, ev
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_oracle_matches_reference_fixtures(fx, name):
+    c = _case(fx, name)
+    ret, out, ev = _oracle_run(c["chan"])
+    assert ret == c["ret"]
+    assert ev == c["out_event"]
+    assert [len(p) for p in out] == c["out_len"]
+    assert hashlib.sha256(b"".join(out)).digest() == c["sha"]
+    if c["exp"] is not None:
+        assert out == c["exp"]
+
+
+def _pack(chan):
+    lens = np.array([len(p) for p in chan], np.int32)
+    offs = np.zeros(len(chan), np.uint64)
+    o = 0
+    for i, p in enumerate(chan):
+        offs[i] = o
+        o += (len(p) + 15) // 16 * 16 + 16
+    host = np.zeros(o + 64, np.uint8)
+    for i, p in enumerate(chan):
+        host[offs[i]:offs[i] + len(p)] = np.frombuffer(p, np.uint8)
+    return host, lens, offs
+
+
+@pytest.mark.parametrize("name", NAMES)
+@pytest.mark.parametrize("nbatch", [1, 3])
+def test_planner_ret_matches_reference(fx, name, nbatch):
+    """librsmi.so's planner without a GPU: every input() return value."""
+    from udpspeeder_amd.fec import FecDecoder
+    c = _case(fx, name)
+    host, lens, offs = _pack(c["chan"])
+    dec = FecDecoder()
+    cuts = np.linspace(0, len(lens), nbatch + 1).astype(int)
+    ret = []
+    for a, b in zip(cuts[:-1], cuts[1:]):
+        ret += list(dec.plan(host, lens[a:b], offs[a:b]).ret)
+    assert ret == c["ret"]
+    dec.close()
+
+
+def _long_run(mode, rs, seed, n=6000, lmax=900):
+    rng = np.random.default_rng(seed)
+    em = EncodeManager(rs, mode, 1250, 200, seed)
+    pk = []
+    for i in range(n):
+        if rng.random() < 0.02:
+            em.input(None)
+        else:
+            em.input(rng.integers(0, 256, int(rng.integers(0, lmax + 1)), dtype=np.uint8).tobytes())
+        pk += em.output()
+    return lossy_channel(pk, seed, loss=0.2, dup=0.05, swap=0.1, delay=0.01, delay_by=2100,
+                         replay=0.01, trunc=0.01, garbage=0.01)
+
+
+@pytest.mark.skipif(not FecReference.available(), reason="reference build absent")
+@pytest.mark.parametrize("mode,rs", [(0, "20:10"), (1, "1:3,2:4,10:6,20:10")])
+def test_oracle_matches_live_reference_with_ring_evictions(mode, rs):
+    chan = _long_run(mode, rs, 31 + mode)
+    fr = FecReference()
+    r_ret, r_out, r_ev = fr.decode(chan)
+    ret, out, ev = _oracle_run(chan)
+    assert ret == list(r_ret) and ev == list(r_ev) and out == r_out
+
+
+def test_planner_anti_replay_timeout_matches_oracle():
+    """anti_replay_timeout (120 s): replays older than it are accepted again."""
+    from udpspeeder_amd.fec import FecDecoder
+    chan = _long_run(1, "20:10", 5, n=1500)
+    chan = chan + chan[:400]  # replayed, some after the window
+    now = np.zeros(len(chan), np.int64)
+    now[len(chan) - 400:] = np.linspace(60_000, 300_000, 400).astype(np.int64)
+    ret, _, _ = _oracle_run(chan, now)
+    host, lens, offs = _pack(chan)
+    dec = FecDecoder()
+    got = []
+    # one packet per plan where the clock moves, as the reference reads it per input()
+    got += list(dec.plan(host, lens[:len(chan) - 400], offs[:len(chan) - 400], now_ms=0).ret)
+    for i in range(len(chan) - 400, len(chan)):
+        got += list(dec.plan(host, lens[i:i + 1], offs[i:i + 1], now_ms=int(now[i])).ret)
+    assert got == ret
+    dec.close()
+
+
+def _gpu_run(chan, cuts, torch):
+    from udpspeeder_amd.fec import FecDecoder
+    host, lens, offs = _pack(chan)
+    dev = torch.from_numpy(host).cuda()
+    dec = FecDecoder()
+    ret, out = [], []
+    for a, b in zip(cuts[:-1], cuts[1:]):
+        p = dec.plan(host, lens[a:b], offs[a:b], dev)
+        ret += list(p.ret)
+        dec.run()
+        out += [(bts, e + a) for bts, e in dec.outputs()]
+    dec.close()
+    return ret, out
+
+
+def _cuts(n, nbatch, seed):
+    rng = np.random.default_rng(seed)
+    if nbatch == 1:
+        return np.array([0, n])
+    return np.unique(np.concatenate([[0, n], rng.integers(0, n, nbatch - 1)]))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", NAMES)
+@pytest.mark.parametrize("nbatch", [1, 4])
+def test_gpu_decoder_matches_reference(fx, gpu, name, nbatch):
+    import torch
+    c = _case(fx, name)
+    ret, out = _gpu_run(c["chan"], _cuts(len(c["chan"]), nbatch, len(name)), torch)
+    assert ret == c["ret"]
+    assert [e for _, e in out] == c["out_event"]
+    assert [len(b) for b, _ in out] == c["out_len"]
+    if c["exp"] is not None:
+        bad = [i for i, ((b, _), x) in enumerate(zip(out, c["exp"])) if b != x]
+        assert not bad, (len(bad), bad[:5])
+    assert hashlib.sha256(b"".join(b for b, _ in out)).digest() == c["sha"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode,rs", [(0, "20:10"), (0, "1:3,2:4,10:6,20:10"), (1, "20:10"),
+                                     (1, "1:3,2:4,10:6,20:10")])
+def test_gpu_decoder_matches_oracle_long(gpu, mode, rs):
+    import torch
+    chan = _long_run(mode, rs, 77 + mode)
+    ret, out, ev = _oracle_run(chan)
+    g_ret, g_out = _gpu_run(chan, _cuts(len(chan), 5, 3), torch)
+    assert g_ret == ret
+    assert [e for _, e in g_out] == ev
+    bad = [i for i, ((b, _), x) in enumerate(zip(g_out, out)) if b != x]
+    assert not bad, (len(bad), bad[:5])
+
+
+@pytest.mark.gpu
+def test_gpu_per_call_interface(gpu):
+    """input()/output() one packet at a time (misc.cpp:409-425's loop)."""
+    from udpspeeder_amd.fec import FecDecoder
+    chan = _long_run(0, "3:2", 9, n=300, lmax=50)
+    dm = DecodeManager()
+    dec = FecDecoder()
+    for p in chan:
+        assert dec.input(p) == dm.input(p)
+        assert dec.output() == dm.output()
+    dec.close()

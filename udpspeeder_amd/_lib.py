@@ -113,6 +113,12 @@ def _bind(lib: C.CDLL) -> C.CDLL:
         "rsmi_fenc_packets": ([vp, vp], i32),
         "rsmi_fenc_groups": ([vp, vp, vp, vp, vp, vp, vp], i32),
         "rsmi_fenc_run_dev": ([vp, vp, i64, vp], i32),
+        "rsmi_fdec_create": ([C.c_int32, vp], i32),
+        "rsmi_fdec_destroy": ([vp], None),
+        "rsmi_fdec_plan": ([vp, i64, vp, vp, vp, vp, i64, vp, vp], i32),
+        "rsmi_fdec_run_dev": ([vp, vp], i32),
+        "rsmi_fdec_outputs": ([vp, vp], i32),
+        "rsmi_fdec_output_list": ([vp, vp, vp, vp], i32),
     }
     for name, (args, res) in sig.items():
         f = getattr(lib, name)

@@ -1,0 +1,560 @@
+// fec_dec.cpp -- receive side of the batched FEC framing (include/rsmi_fec.h,
+// SURVEY §8f row f3).
+//
+// The planner replays fec_decode_manager_t::input (fec_manager.cpp:469-784)
+// packet by packet: header checks, anti_replay_t (fec_manager.h:187-235), the
+// seq -> group map with unordered_map::operator[]'s insert-on-read, the ring
+// of fec_buff_num buffers whose reuse evicts old groups, and the decisions of
+// when a group decodes.  None of them depends on decoded bytes, so the decodes
+// of a whole batch run afterwards on the GPU (gather -> rsmi_decode_dev per
+// (k,n) -> pack -> one D2H), and the outputs -- blob_decode's records (mode
+// 0) or the missed data shards (mode 1), which do depend on decoded bytes --
+// are resolved on the host from the copied-back rows.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <new>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "rsmi_internal.hpp"
+#include "../../include/rsmi_fec.h"
+
+namespace rsmi {
+void set_error(const std::string &m);
+}
+
+using rsmi::GatherCopy;
+using rsmi::PackJob;
+using rsmi::CarryCopy;
+
+namespace {
+
+int fail(int code, const std::string &m) {
+    rsmi::set_error(m);
+    return code;
+}
+
+constexpr uint32_t kAntiReplaySize = 30000;      // anti_replay_buff_size (fec_manager.h:16)
+constexpr int64_t kAntiReplayTimeout = 120000;   // anti_replay_timeout, ms (fec_manager.h:185)
+constexpr int kMaxBlobPackets = 30000;           // max_blob_packet_num (fec_manager.h:15)
+constexpr int kMaxDataLen = 3600;                // max_data_len (common.h:102)
+constexpr int kBufLen = kMaxDataLen + 200;       // buf_len (common.h:103)
+constexpr int kRingBytes = (kBufLen + 15) & ~15; // carry bytes per ring slot
+
+uint32_t rd_u32(const uint8_t *p) { return (uint32_t)p[0] << 24 | (uint32_t)p[1] << 16 | (uint32_t)p[2] << 8 | p[3]; }
+uint32_t rd_u16(const uint8_t *p) { return (uint32_t)p[0] << 8 | p[1]; }
+
+// anti_replay_t (fec_manager.h:187-235)
+struct AntiReplay {
+    struct Info {
+        int64_t time;
+        uint32_t index;
+    };
+    std::vector<int64_t> buf = std::vector<int64_t>(kAntiReplaySize, -1);
+    std::unordered_map<uint32_t, Info> mp;
+    uint32_t index = 0;
+    AntiReplay() { mp.reserve(kAntiReplaySize * 3); }
+    bool valid(uint32_t seq, int64_t now) {
+        auto it = mp.find(seq);
+        if (it == mp.end()) return true;
+        if (now - it->second.time > kAntiReplayTimeout) {
+            buf[it->second.index] = -1;
+            mp.erase(it);
+            return true;
+        }
+        return false;
+    }
+    void set_invalid(uint32_t seq, int64_t now) {
+        if (!valid(seq, now)) return;
+        if (buf[index] != -1) mp.erase((uint32_t)buf[index]);
+        buf[index] = seq;
+        mp[seq] = Info{now, index};
+        if (++index == kAntiReplaySize) index = 0;
+    }
+};
+
+struct Group {  // fec_group_t (fec_manager.h:376-384)
+    int type = -1, data_num = -1, red = -1, len = -1, fec_done = 0;
+    std::map<int, int> gm;  // inner index -> ring slot
+};
+
+struct RingEnt {  // fec_data_t (fec_manager.h:366-375), bytes on the device
+    bool used = false;
+    uint32_t seq = 0;
+    int len = 0;
+    uint64_t src = 0;  // payload: device address in the batch, or carry-tagged slot
+    bool in_batch = false;
+};
+
+struct Job {  // one group decoded in this batch
+    int type, k, n, len, inner;
+    int32_t event;
+    int bucket;
+    int64_t row;        // group row in its bucket's staging
+    int64_t blob_off;   // its k data rows, packed, in the host blob
+};
+
+struct Bucket {
+    int k, n, len = 0;
+    int64_t rows = 0, stride = 0, staging_off = 0, present_off = 0;
+};
+
+struct Out {
+    int32_t event;
+    int64_t job;        // -1: pass-through packet
+    const uint8_t *ptr;
+    int32_t len;
+};
+
+template <class T>
+int dev_grow(T **p, size_t *cap, size_t need) {
+    if (need <= *cap) return RSMI_OK;
+    size_t c = std::max(need, *cap * 2);
+    c = (c + 4095) & ~size_t(4095);
+    if (*p) (void)hipFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    if (hipMalloc((void **)p, c) != hipSuccess) return fail(RSMI_ERR_NOMEM, "fdec device allocation failed");
+    *cap = c;
+    return RSMI_OK;
+}
+
+int host_grow(uint8_t **p, size_t *cap, size_t need) {
+    if (need <= *cap) return RSMI_OK;
+    size_t c = std::max(need, *cap * 2);
+    c = (c + 4095) & ~size_t(4095);
+    if (*p) (void)hipHostFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    if (hipHostMalloc((void **)p, c, hipHostMallocDefault) != hipSuccess)
+        return fail(RSMI_ERR_NOMEM, "fdec pinned allocation failed");
+    *cap = c;
+    return RSMI_OK;
+}
+
+}  // namespace
+
+struct rsmi_fdec {
+    int buff_num = 2000;
+    AntiReplay ar;
+    std::unordered_map<uint32_t, Group> mp;
+    std::vector<RingEnt> ring;
+    int index = 0;
+
+    // ---- last plan
+    std::vector<Job> jobs;
+    std::vector<Bucket> buckets;
+    std::map<int, int> bucket_of;  // k*257+n -> bucket
+    std::vector<GatherCopy> gathers;
+    std::vector<CarryCopy> carries;
+    std::vector<Out> outs;
+    std::vector<uint8_t> present;  // all buckets' present flags
+    int64_t staging_bytes = 0, blob_bytes = 0;
+    const uint8_t *host_base = nullptr;
+    bool planned = false, ran = false, resolved = false, plan_only = false;
+
+    // ---- device side
+    int device = -1;
+    uint8_t *dcarry = nullptr;  // buff_num x kRingBytes, indexed by ring slot
+    size_t dcarry_cap = 0;
+    uint8_t *dstage = nullptr, *dmeta = nullptr, *dblob = nullptr;
+    size_t stage_cap = 0, meta_cap = 0, blob_cap = 0;
+    uint8_t *hmeta = nullptr, *hblob = nullptr;
+    size_t hmeta_cap = 0, hblob_cap = 0;
+    int32_t *dstatus = nullptr;
+    size_t status_cap = 0;
+    hipEvent_t done = nullptr;
+    bool in_flight = false;
+
+    Group &group(uint32_t seq) { return mp[seq]; }  // operator[] inserts, as the reference
+};
+
+namespace {
+
+int wait_idle(rsmi_fdec *D) {
+    if (D->in_flight) {
+        hipError_t e = hipEventSynchronize(D->done);
+        D->in_flight = false;
+        if (e != hipSuccess) return fail(RSMI_ERR_HIP, std::string("fdec wait: ") + hipGetErrorString(e));
+    }
+    return RSMI_OK;
+}
+
+// The about_to_fec branch (fec_manager.cpp:616-757) up to the byte work:
+// queue the decode job; its outputs are resolved after the run.
+void plan_decode(rsmi_fdec *D, uint32_t seq, Group &g, int type, int inner, int len, int32_t event,
+                 int64_t now) {
+    const int k = g.data_num, m = g.red, n = k + m;
+    int dlen = len;
+    if (type == 1) {  // data_check (:671-695): every shard >= 2 bytes, the longest == the group's len
+        int max_len = -1;
+        bool ok = true;
+        for (auto &kv : g.gm) {
+            const int l = D->ring[(size_t)kv.second].len;
+            if (l < 2) ok = false;
+            max_len = std::max(max_len, l);
+        }
+        if (max_len != g.len) ok = false;
+        if (!ok) {
+            D->ar.set_invalid(seq, now);
+            return;
+        }
+        dlen = max_len;
+    }
+    g.fec_done = 1;
+    // rs_decode2's survivors: the first k present indices below n (rs.cpp:24-39)
+    std::vector<std::pair<int, int>> sel;
+    bool bad = false;
+    for (auto &kv : g.gm) {
+        if (kv.first >= n) bad = true;
+        else if ((int)sel.size() < k) sel.emplace_back(kv.first, kv.second);
+    }
+    if (bad || (int)sel.size() < k) {  // the reference aborts on its assert here
+        D->ar.set_invalid(seq, now);
+        return;
+    }
+    const int key = k * 257 + n;
+    auto it = D->bucket_of.find(key);
+    int b;
+    if (it == D->bucket_of.end()) {
+        b = (int)D->buckets.size();
+        D->bucket_of[key] = b;
+        Bucket B;
+        B.k = k;
+        B.n = n;
+        D->buckets.push_back(B);
+    } else {
+        b = it->second;
+    }
+    Bucket &B = D->buckets[(size_t)b];
+    B.len = std::max(B.len, dlen);
+    Job J;
+    J.type = type;
+    J.k = k;
+    J.n = n;
+    J.len = dlen;
+    J.inner = inner;
+    J.event = event;
+    J.bucket = b;
+    J.row = B.rows++;
+    J.blob_off = D->blob_bytes;
+    D->blob_bytes += (int64_t)k * dlen + 16;
+    // survivor copies: dst is patched once the bucket strides are known
+    for (auto &sv : sel) {
+        const RingEnt &r = D->ring[(size_t)sv.second];
+        GatherCopy G;
+        G.src = r.src;
+        G.dst = ((uint64_t)D->jobs.size() << 8) | (uint64_t)sv.first;  // (job, index) until patched
+        G.len = (uint32_t)r.len;
+        G.dst_len = 0;
+        D->gathers.push_back(G);
+    }
+    D->outs.push_back(Out{event, (int64_t)D->jobs.size(), nullptr, 0});
+    D->jobs.push_back(J);
+    D->ar.set_invalid(seq, now);
+}
+
+// fec_decode_manager_t::input (fec_manager.cpp:469-784) for one packet.
+int input_packet(rsmi_fdec *D, const uint8_t *s, int len, uint64_t dsrc, int32_t event, int64_t now) {
+    if (len < 8) return -1;
+    const uint32_t seq = rd_u32(s);
+    const int type = s[4], data_num = s[5], red = s[6], inner = s[7];
+    const uint8_t *pay = s + 8;
+    len -= 8;
+    if (type == 1) {
+        if (len < 2) return -1;
+        if (data_num == 0 && (int)rd_u16(pay) + 2 != len) return -1;
+    }
+    if (type == 0 && data_num == 0) return -1;
+    if (data_num + red >= RSMI_FEC_MAX_PACKETS) return -1;
+    if (!D->ar.valid(seq, now)) return 0;
+    {
+        Group &g = D->group(seq);
+        if (g.fec_done) return -1;
+        if (g.gm.count(inner)) return -1;
+        if (g.type == -1) g.type = type;
+        else if (g.type != type) return -1;
+        if (data_num != 0) {
+            if (g.data_num == -1) {
+                g.data_num = data_num;
+                g.red = red;
+                g.len = len;
+            } else if (g.data_num != data_num || g.red != red || g.len != len) {
+                return -1;
+            }
+        }
+    }
+    RingEnt &slot = D->ring[(size_t)D->index];
+    if (slot.used) {  // ring reuse evicts the slot's group (:554-576)
+        const uint32_t tmp_seq = slot.seq;
+        D->ar.set_invalid(tmp_seq, now);
+        auto it = D->mp.find(tmp_seq);
+        if (it != D->mp.end()) D->mp.erase(it);
+        if (tmp_seq == seq) return -1;
+    }
+    slot.used = true;
+    slot.seq = seq;
+    slot.len = len;
+    slot.src = dsrc;
+    slot.in_batch = true;
+    Group &g = D->group(seq);
+    g.gm[inner] = D->index;
+    const int size = (int)g.gm.size();
+    bool about = false, end = false;
+    if (type == 0) {
+        if (size > data_num) {
+            D->ar.set_invalid(seq, now);
+            end = true;
+        } else if (size == data_num) {
+            about = true;
+        }
+    } else if (g.data_num != -1) {
+        if (size > g.data_num + 1) {
+            D->ar.set_invalid(seq, now);
+            end = true;
+        } else if (size >= g.data_num) {
+            about = true;
+        }
+    }
+    if (!end) {
+        if (about) plan_decode(D, seq, g, type, inner, len, event, now);
+        else if (type == 1 && data_num == 0)  // decode_fast_send (:760-776)
+            D->outs.push_back(Out{event, -1, pay + 2, len - 2});
+    }
+    if (++D->index == D->buff_num) D->index = 0;
+    return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int rsmi_fdec_create(int32_t buff_num, rsmi_fdec **out) {
+    if (!out || buff_num < 0) return fail(RSMI_ERR_INVALID, "bad fdec_create args");
+    rsmi_fdec *D = new rsmi_fdec();
+    if (buff_num) D->buff_num = buff_num;
+    D->ring.assign((size_t)D->buff_num, RingEnt{});
+    D->mp.reserve((size_t)D->buff_num * 3);
+    *out = D;
+    return RSMI_OK;
+}
+
+void rsmi_fdec_destroy(rsmi_fdec *D) {
+    if (!D) return;
+    (void)wait_idle(D);
+    for (uint8_t *p : {D->dcarry, D->dstage, D->dmeta, D->dblob}) if (p) (void)hipFree(p);
+    if (D->dstatus) (void)hipFree(D->dstatus);
+    for (uint8_t *p : {D->hmeta, D->hblob}) if (p) (void)hipHostFree(p);
+    if (D->done) (void)hipEventDestroy(D->done);
+    delete D;
+}
+
+int rsmi_fdec_plan(rsmi_fdec *D, int64_t n, const int32_t *len, const uint64_t *off,
+                   const uint8_t *host_base, const uint8_t *dev_base, int64_t now_ms, int32_t *ret,
+                   int64_t *n_decodes) {
+    if (!D || n < 0 || (n && (!len || !off || !host_base))) return fail(RSMI_ERR_INVALID, "bad fdec_plan args");
+    if (D->planned && !D->plan_only)
+        return fail(RSMI_ERR_INVALID, "rsmi_fdec_plan: run the previous plan first (its carry copies)");
+    if (!dev_base) {
+        D->plan_only = true;  // decisions only; this decoder never runs on a device
+    } else if (D->plan_only) {
+        return fail(RSMI_ERR_INVALID, "rsmi_fdec_plan: decoder was used plan-only (dev_base NULL)");
+    }
+    int rc = wait_idle(D);
+    if (rc) return rc;
+    D->jobs.clear();
+    D->buckets.clear();
+    D->bucket_of.clear();
+    D->gathers.clear();
+    D->carries.clear();
+    D->outs.clear();
+    D->present.clear();
+    D->staging_bytes = D->blob_bytes = 0;
+    D->host_base = host_base;
+    for (int64_t i = 0; i < n; ++i) {
+        int r;
+        if (len[i] < 0 || len[i] + 100 >= kBufLen) {
+            r = -1;  // the reference asserts len + 100 < buf_len (:471)
+        } else {
+            const uint64_t dsrc = dev_base ? (uint64_t)(uintptr_t)(dev_base + off[i]) + 8 : 0;
+            r = input_packet(D, host_base + off[i], len[i], dsrc, (int32_t)i, now_ms);
+        }
+        if (ret) ret[i] = r;
+    }
+    // staging layout per bucket: rows x n shards x stride, present flags rows x n
+    int64_t so = 0, po = 0;
+    for (Bucket &B : D->buckets) {
+        B.stride = (B.len + 127) & ~127;
+        B.staging_off = so;
+        B.present_off = po;
+        so += B.rows * B.n * B.stride;
+        po += (B.rows * B.n + 15) & ~int64_t(15);
+    }
+    D->staging_bytes = so;
+    D->present.assign((size_t)po, 0);
+    for (GatherCopy &G : D->gathers) {
+        const Job &J = D->jobs[(size_t)(G.dst >> 8)];
+        const int idx = (int)(G.dst & 0xff);
+        const Bucket &B = D->buckets[(size_t)J.bucket];
+        G.dst = (uint64_t)(B.staging_off + (J.row * B.n + idx) * B.stride);  // offset; based at run time
+        G.dst_len = (uint32_t)B.stride;
+        D->present[(size_t)(B.present_off + J.row * B.n + idx)] = 1;
+    }
+    // live shards of the batch move to the carry area, at their ring slot (:587)
+    for (int sidx = 0; sidx < D->buff_num; ++sidx) {
+        RingEnt &r = D->ring[(size_t)sidx];
+        if (!r.used || !r.in_batch) continue;
+        r.in_batch = false;
+        auto it = D->mp.find(r.seq);
+        const bool live = it != D->mp.end() && !it->second.fec_done;
+        const uint64_t dst = rsmi::kCarryTag | (uint64_t)sidx * kRingBytes;
+        if (live && r.len > 0) D->carries.push_back(CarryCopy{r.src, dst, (uint32_t)r.len, 0});
+        r.src = dst;
+    }
+    D->planned = true;
+    D->ran = D->resolved = false;
+    if (n_decodes) *n_decodes = (int64_t)D->jobs.size();
+    return RSMI_OK;
+}
+
+int rsmi_fdec_run_dev(rsmi_fdec *D, void *stream) {
+    if (!D || !D->planned) return fail(RSMI_ERR_INVALID, "rsmi_fdec_run_dev without a plan");
+    if (D->plan_only) return fail(RSMI_ERR_INVALID, "rsmi_fdec_run_dev on a plan-only decoder");
+    int cur;
+    if (hipGetDevice(&cur) != hipSuccess) return fail(RSMI_ERR_HIP, "fdec: no usable GPU");
+    if (D->device < 0) {
+        if (hipEventCreateWithFlags(&D->done, hipEventDisableTiming) != hipSuccess)
+            return fail(RSMI_ERR_HIP, "fdec: hipEventCreate");
+        D->device = cur;
+    } else if (cur != D->device) {
+        return fail(RSMI_ERR_INVALID, "rsmi_fdec_run_dev on another device than the decoder's");
+    }
+    hipStream_t s = (hipStream_t)stream;
+    int rc = dev_grow(&D->dcarry, &D->dcarry_cap, (size_t)D->buff_num * kRingBytes);
+    if (!rc) rc = dev_grow(&D->dstage, &D->stage_cap, (size_t)D->staging_bytes + 16);
+    if (!rc) rc = dev_grow(&D->dblob, &D->blob_cap, (size_t)D->blob_bytes + 16);
+    if (!rc) rc = host_grow(&D->hblob, &D->hblob_cap, (size_t)D->blob_bytes + 16);
+    int64_t max_rows = 0;
+    for (const Bucket &B : D->buckets) max_rows = std::max(max_rows, B.rows);
+    if (!rc) rc = dev_grow(&D->dstatus, &D->status_cap, (size_t)max_rows * 4 + 16);
+    if (rc) return rc;
+    // metadata: gathers | present | packs | carries, one upload
+    std::vector<PackJob> packs(D->jobs.size());
+    for (size_t j = 0; j < D->jobs.size(); ++j) {
+        const Job &J = D->jobs[j];
+        const Bucket &B = D->buckets[(size_t)J.bucket];
+        packs[j] = PackJob{(uint64_t)(uintptr_t)(D->dstage + B.staging_off + J.row * B.n * B.stride),
+                           (uint64_t)(uintptr_t)(D->dblob + J.blob_off), (uint32_t)J.k, (uint32_t)J.len,
+                           (uint32_t)B.stride, 0};
+    }
+    const size_t gb = D->gathers.size() * sizeof(GatherCopy), pb = D->present.size(),
+                 kb = packs.size() * sizeof(PackJob), cb = D->carries.size() * sizeof(CarryCopy);
+    const size_t go = 0, po = (gb + 255) & ~size_t(255), ko = (po + pb + 255) & ~size_t(255),
+                 co = (ko + kb + 255) & ~size_t(255), all = co + cb + 16;
+    rc = dev_grow(&D->dmeta, &D->meta_cap, all);
+    if (!rc) rc = host_grow(&D->hmeta, &D->hmeta_cap, all);
+    if (rc) return rc;
+    GatherCopy *hg = reinterpret_cast<GatherCopy *>(D->hmeta + go);
+    for (size_t i = 0; i < D->gathers.size(); ++i) {
+        hg[i] = D->gathers[i];
+        hg[i].dst += (uint64_t)(uintptr_t)D->dstage;
+    }
+    if (pb) std::memcpy(D->hmeta + po, D->present.data(), pb);
+    if (kb) std::memcpy(D->hmeta + ko, packs.data(), kb);
+    if (cb) std::memcpy(D->hmeta + co, D->carries.data(), cb);
+    const rsmi::CarryBase carry{{D->dcarry, D->dcarry}};
+    hipError_t e = hipMemcpyAsync(D->dmeta, D->hmeta, all, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess)
+        e = rsmi::launch_gather(reinterpret_cast<const GatherCopy *>(D->dmeta + go),
+                                (int64_t)D->gathers.size(), carry, s);
+    if (e != hipSuccess) return fail(RSMI_ERR_HIP, std::string("fdec gather: ") + hipGetErrorString(e));
+    for (const Bucket &B : D->buckets) {
+        rc = rsmi_decode_dev(B.k, B.n, D->dstage + B.staging_off, (int64_t)B.n * B.stride, B.stride,
+                             B.len, B.rows, D->dmeta + po + B.present_off, D->dstatus, stream);
+        if (rc) return rc;
+    }
+    e = rsmi::launch_pack(reinterpret_cast<const PackJob *>(D->dmeta + ko), (int64_t)packs.size(), s);
+    if (e == hipSuccess)
+        e = rsmi::launch_carry(reinterpret_cast<const CarryCopy *>(D->dmeta + co),
+                               (int64_t)D->carries.size(), carry, s);
+    if (e == hipSuccess && D->blob_bytes)
+        e = hipMemcpyAsync(D->hblob, D->dblob, (size_t)D->blob_bytes, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipEventRecord(D->done, s);
+    if (e != hipSuccess) return fail(RSMI_ERR_HIP, std::string("fdec run: ") + hipGetErrorString(e));
+    D->in_flight = true;
+    D->planned = false;
+    D->ran = true;
+    return RSMI_OK;
+}
+
+int rsmi_fdec_outputs(rsmi_fdec *D, int64_t *n_out) {
+    if (!D) return fail(RSMI_ERR_INVALID, "null decoder");
+    if (!D->resolved) {
+        bool any_job = !D->jobs.empty();
+        if (any_job && !D->ran) return fail(RSMI_ERR_INVALID, "rsmi_fdec_outputs before rsmi_fdec_run_dev");
+        int rc = wait_idle(D);
+        if (rc) return rc;
+        std::vector<Out> res;
+        res.reserve(D->outs.size() * 2);
+        for (const Out &o : D->outs) {
+            if (o.job < 0) {
+                res.push_back(o);
+                continue;
+            }
+            const Job &J = D->jobs[(size_t)o.job];
+            const uint8_t *blob = D->hblob + J.blob_off;
+            if (J.type == 0) {  // blob_decode_t::output (fec_manager.cpp:97-129)
+                const int64_t cur = (int64_t)J.k * J.len;
+                if (cur < 4) continue;
+                const uint32_t cnt = rd_u32(blob);
+                if (cnt > (uint32_t)kMaxBlobPackets) continue;
+                int64_t pos = 4;
+                const size_t mark = res.size();
+                bool ok = true;
+                for (uint32_t i = 0; i < cnt; ++i) {
+                    if (pos + 2 > cur) { ok = false; break; }
+                    const int l = (int)rd_u16(blob + pos);
+                    pos += 2;
+                    if (pos + l > cur) { ok = false; break; }
+                    res.push_back(Out{o.event, o.job, blob + pos, l});
+                    pos += l;
+                }
+                if (!ok) res.resize(mark);
+            } else {  // mode 1 (:713-755): every data row's u16 <= max_data_len, then the missed rows
+                bool ok = true;
+                for (int i = 0; i < J.k; ++i)
+                    if ((int)rd_u16(blob + (int64_t)i * J.len) > kMaxDataLen) ok = false;
+                if (!ok) continue;
+                // missed = rows not received + the packet that completed the group
+                const Bucket &B = D->buckets[(size_t)J.bucket];
+                const uint8_t *pres = D->present.data() + B.present_off + J.row * B.n;
+                for (int i = 0; i < J.k; ++i) {
+                    if (pres[i] && i != J.inner) continue;
+                    const uint8_t *r = blob + (int64_t)i * J.len;
+                    res.push_back(Out{o.event, o.job, r + 2, (int32_t)rd_u16(r)});
+                }
+            }
+        }
+        D->outs.swap(res);
+        D->resolved = true;
+    }
+    if (n_out) *n_out = (int64_t)D->outs.size();
+    return RSMI_OK;
+}
+
+int rsmi_fdec_output_list(const rsmi_fdec *D, const uint8_t **ptr, int32_t *len, int32_t *event) {
+    if (!D || !D->resolved) return fail(RSMI_ERR_INVALID, "call rsmi_fdec_outputs first");
+    for (size_t i = 0; i < D->outs.size(); ++i) {
+        if (ptr) ptr[i] = D->outs[i].ptr;
+        if (len) len[i] = D->outs[i].len;
+        if (event) event[i] = D->outs[i].event;
+    }
+    return RSMI_OK;
+}
+
+}  // extern "C"

@@ -118,6 +118,7 @@ struct rsmi_fenc {
     int64_t n_slots = 0;
     int32_t stride_min = rsmi::kSlotShard;
     bool planned = false;
+    bool plan_only = false;
 
     // ---- device side
     int device = -1;
@@ -383,6 +384,15 @@ int rsmi_fenc_plan(rsmi_fenc *E, int64_t n_events, const int32_t *len, const uin
                    const uint8_t *in_base, int32_t *ret, int64_t *n_slots, int64_t *n_packets,
                    int32_t *slot_stride_min) {
     if (!E || n_events < 0 || (n_events && !len)) return fail(RSMI_ERR_INVALID, "bad fenc_plan args");
+    if (E->planned && !E->plan_only && E->carry.size())
+        return fail(RSMI_ERR_INVALID, "rsmi_fenc_plan: run the previous plan first (its carry copies)");
+    bool any_packet = false;
+    for (int64_t i = 0; i < n_events && !any_packet; ++i) any_packet = len[i] >= 0;
+    if (!in_base && any_packet) {
+        E->plan_only = true;  // decisions only; this encoder never runs on a device
+    } else if (E->plan_only && any_packet) {
+        return fail(RSMI_ERR_INVALID, "rsmi_fenc_plan: encoder was used plan-only (in_base NULL)");
+    }
     int rc = wait_idle(E);  // the previous batch still reads the plan buffers and carry area
     if (rc) return rc;
     E->jobs.clear();
@@ -400,8 +410,8 @@ int rsmi_fenc_plan(rsmi_fenc *E, int64_t n_events, const int32_t *len, const uin
     for (Pending &p : E->pend) p.emitted = -1;  // sent in an earlier batch
     for (int64_t i = 0; i < n_events; ++i) {
         const bool has = len[i] >= 0;
-        if (has && (!in_off || !in_base)) return fail(RSMI_ERR_INVALID, "packet without in_off/in_base");
-        const uint64_t addr = has ? (uint64_t)(uintptr_t)(in_base + in_off[i]) : 0;
+        if (has && !in_off) return fail(RSMI_ERR_INVALID, "packet without in_off");
+        const uint64_t addr = has && in_base ? (uint64_t)(uintptr_t)(in_base + in_off[i]) : 0;
         const int r = input_event(E, (int32_t)i, has, has ? len[i] : 0, addr);
         if (ret) ret[i] = r;
     }
@@ -466,6 +476,7 @@ int rsmi_fenc_groups(const rsmi_fenc *E, int64_t *n, int64_t *slot0, int32_t *k,
 
 int rsmi_fenc_run_dev(rsmi_fenc *E, uint8_t *slots, int64_t S, void *stream) {
     if (!E || !E->planned) return fail(RSMI_ERR_INVALID, "rsmi_fenc_run_dev without a plan");
+    if (E->plan_only) return fail(RSMI_ERR_INVALID, "rsmi_fenc_run_dev on a plan-only encoder");
     if (E->n_slots && (!slots || ((uintptr_t)slots & 15)))
         return fail(RSMI_ERR_INVALID, "slots_base must be 16-aligned");
     if (S % 16 || S < E->stride_min)

@@ -91,7 +91,7 @@ class FecEncoder:
             offsets = np.ascontiguousarray(offsets, np.uint64)
             offp = offsets.ctypes.data
         if isinstance(in_buf, int):
-            basep = in_buf
+            basep = in_buf or None
         elif in_buf is not None:
             basep = in_buf.data_ptr()
         ret = np.zeros(n, np.int32)
@@ -119,7 +119,7 @@ class FecEncoder:
     def plan_host(self, lens, offsets) -> FencPlan:
         """Plan only (no device): decisions, packet list and groups for a batch
         whose payloads are never framed -- for inspecting the schedule."""
-        return self.plan(lens, offsets, 0x10000)
+        return self.plan(lens, offsets, 0)
 
     def run(self, slots, slot_stride: int, stream=None):
         """Frame + encode + carry the planned batch into `slots` (CUDA uint8,
@@ -165,3 +165,81 @@ def packets_bytes(plan: FencPlan, slots_host: np.ndarray, slot_stride: int) -> L
     """The emitted packets of a run, as bytes (slots_host: the slot array on the host)."""
     return [slots_host[s * slot_stride + SLOT_PACKET:s * slot_stride + SLOT_PACKET + ln].tobytes()
             for s, ln, _ in plan.packets]
+
+
+@dataclass
+class FdecPlan:
+    ret: np.ndarray      # input() return value per packet
+    n_decodes: int       # groups the batch decodes
+
+
+class FecDecoder:
+    """One fec_decode_manager_t (fec_manager.cpp:469-797): received packets in,
+    the packets output() returns out.  Decodes run batched on the GPU."""
+
+    def __init__(self, buff_num: int = 0):
+        h = C.c_void_p()
+        check(lib().rsmi_fdec_create(int(buff_num), C.byref(h)), "rsmi_fdec_create")
+        self._h = h
+        self._keep = None
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().rsmi_fdec_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def plan(self, host_buf: np.ndarray, lens, offsets, dev_buf=None, now_ms: int = 0) -> FdecPlan:
+        """Plan input() for every packet: packet i is lens[i] bytes at
+        host_buf[offsets[i]:] (host uint8 array) and at the same offset of
+        dev_buf (CUDA uint8 tensor with the same bytes, 16 spare after each)."""
+        lens = np.ascontiguousarray(lens, np.int32)
+        offsets = np.ascontiguousarray(offsets, np.uint64)
+        n = len(lens)
+        ret = np.zeros(n, np.int32)
+        nd = C.c_int64()
+        devp = dev_buf.data_ptr() if dev_buf is not None else None  # None: plan only
+        check(lib().rsmi_fdec_plan(self._h, n, lens.ctypes.data, offsets.ctypes.data,
+                                   host_buf.ctypes.data, devp, int(now_ms), ret.ctypes.data,
+                                   C.byref(nd)), "rsmi_fdec_plan")
+        self._keep = (host_buf, dev_buf)
+        return FdecPlan(ret, nd.value)
+
+    def run(self, stream=None):
+        import torch
+        s = stream if stream is not None else torch.cuda.current_stream()
+        check(lib().rsmi_fdec_run_dev(self._h, s.cuda_stream), "rsmi_fdec_run_dev")
+
+    def outputs(self):
+        """[(bytes, event)] in the reference's output() order (waits for the run)."""
+        n = C.c_int64()
+        check(lib().rsmi_fdec_outputs(self._h, C.byref(n)), "rsmi_fdec_outputs")
+        ptr = (C.c_void_p * max(1, n.value))()
+        ln = np.zeros(max(1, n.value), np.int32)
+        ev = np.zeros(max(1, n.value), np.int32)
+        check(lib().rsmi_fdec_output_list(self._h, ptr, ln.ctypes.data, ev.ctypes.data),
+              "rsmi_fdec_output_list")
+        return [(C.string_at(ptr[i], int(ln[i])) if ln[i] else b"", int(ev[i]))
+                for i in range(n.value)]
+
+    # ---- the reference's per-call interface ------------------------------------
+    def input(self, packet: bytes, now_ms: int = 0) -> int:
+        """fec_decode_manager_t::input(s, len) for one packet (one GPU batch)."""
+        import torch
+        host = np.zeros(len(packet) + 16, np.uint8)
+        host[:len(packet)] = np.frombuffer(bytes(packet), np.uint8)
+        dev = torch.from_numpy(host).cuda()
+        p = self.plan(host, [len(packet)], [0], dev, now_ms)
+        self.run()
+        self._ready = [b for b, _ in self.outputs()]
+        return int(p.ret[0])
+
+    def output(self) -> List[bytes]:
+        """fec_decode_manager_t::output: the packets the last input() produced."""
+        r, self._ready = getattr(self, "_ready", []), []
+        return r
