@@ -22,6 +22,9 @@
 #ifndef BS_OCC
 #define BS_OCC 3
 #endif
+#ifndef BS_PERSIST
+#define BS_PERSIST 0  // 1: balanced persistent grid (measured 5 % slower than one wave per chunk)
+#endif
 #ifndef BS_LD_AUX
 #define BS_LD_AUX 2  // cache-policy bits of the streaming loads (2 = nt: read once)
 #endif
@@ -67,8 +70,8 @@ struct DevIO {
     }
 };
 
-__device__ __forceinline__ DevIO make_io(const UniformArgs &a, uint32_t cols, uint32_t P) {
-    const uint32_t wave = blockIdx.x * 4u + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+__device__ __forceinline__ DevIO make_io(const UniformArgs &a, uint32_t cols, uint32_t P,
+                                         uint32_t wave) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t cfirst = wave * 128u;
     const uint32_t clast = (cfirst + 127u < cols) ? cfirst + 127u : cols - 1u;
@@ -87,15 +90,17 @@ __device__ __forceinline__ DevIO make_io(const UniformArgs &a, uint32_t cols, ui
     return io;
 }
 
-// Waves whose first column is past the end exit before touching memory
-// (a grid is rounded up to whole 4-wave blocks).
+// A wave encodes 128-column chunks w, w + wstep, ...: the launch sizes the grid
+// so every resident wave gets the same number of chunks (no partly filled last
+// round of waves).  Waves past the end exit before touching memory.
 #define BS_KERNEL(K, N)                                                                   \
     __global__ __launch_bounds__(256, BS_OCC) void k_bs_##K##_##N(UniformArgs a, uint32_t cols,     \
-                                                          uint32_t P) {                    \
-        const uint32_t wave = blockIdx.x * 4u + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); \
-        if (wave * 128u >= cols) return;                                                  \
-        DevIO io = make_io(a, cols, P);                                                   \
-        bs_code_##K##_##N(io);                                                            \
+                                                          uint32_t P, uint32_t wstep) {    \
+        for (uint32_t wave = blockIdx.x * 4u + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); \
+             wave * 128u < cols; wave += wstep) {                                          \
+            DevIO io = make_io(a, cols, P, wave);                                         \
+            bs_code_##K##_##N(io);                                                        \
+        }                                                                                 \
     }
 BS_FOR_EACH_CODE(BS_KERNEL)
 #undef BS_KERNEL
@@ -208,13 +213,29 @@ hipError_t launch_encode_bitslice(const UniformArgs &a, hipStream_t s) {
     if (cols >= (int64_t(1) << 31) || a.shard_stride < P * 16 || span >= (int64_t(1) << 31) ||
         a.group_stride < a.n * a.shard_stride)
         return hipErrorNotSupported;
-    const int64_t waves = (cols + 127) / 128;
+    const int64_t chunks = (cols + 127) / 128;
+    int64_t waves = chunks;
+#if BS_PERSIST
+    // balanced persistent grid: every resident wave slot takes ceil(chunks /
+    // slots) chunks, and only as many waves run as that needs
+    static int cus = 0;
+    if (!cus) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            cus = 256;
+    }
+    const int64_t slots = (int64_t)cus * 4 * BS_OCC;
+    const int64_t per = (chunks + slots - 1) / slots;
+    waves = (chunks + per - 1) / per;
+#endif
     const int64_t blocks = (waves + 3) / 4;
     if (blocks > 0x7fffffff) return hipErrorNotSupported;
+    const uint32_t wstep = (uint32_t)(blocks * 4);
     switch (a.k * 257 + a.n) {
 #define BS_LAUNCH(K, N)                                                                 \
     case K * 257 + N:                                                                   \
-        k_bs_##K##_##N<<<(unsigned)blocks, 256, 0, s>>>(a, (uint32_t)cols, (uint32_t)P); \
+        k_bs_##K##_##N<<<(unsigned)blocks, 256, 0, s>>>(a, (uint32_t)cols, (uint32_t)P, wstep); \
         return hipGetLastError();
         BS_FOR_EACH_CODE(BS_LAUNCH)
 #undef BS_LAUNCH

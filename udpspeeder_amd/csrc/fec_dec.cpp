@@ -16,6 +16,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <memory>
 #include <new>
 #include <string>
 #include <unordered_map>
@@ -29,7 +30,6 @@ void set_error(const std::string &m);
 }
 
 using rsmi::GatherCopy;
-using rsmi::PackJob;
 using rsmi::CarryCopy;
 
 namespace {
@@ -88,7 +88,15 @@ struct RingEnt {  // fec_data_t (fec_manager.h:366-375), bytes on the device
     uint32_t seq = 0;
     int len = 0;
     uint64_t src = 0;  // payload: device address in the batch, or carry-tagged slot
+    const uint8_t *host = nullptr;  // payload in the caller's host buffer (this batch only)
     bool in_batch = false;
+};
+
+// Where the host finds data row i of a decoded group: the received packet in
+// the caller's host buffer, or row `d2h` of the rows copied back.
+struct RowRef {
+    const uint8_t *host;
+    int64_t d2h;
 };
 
 struct Job {  // one group decoded in this batch
@@ -96,7 +104,7 @@ struct Job {  // one group decoded in this batch
     int32_t event;
     int bucket;
     int64_t row;        // group row in its bucket's staging
-    int64_t blob_off;   // its k data rows, packed, in the host blob
+    int64_t rows0;      // its k RowRefs in rsmi_fdec::rows
 };
 
 struct Bucket {
@@ -154,7 +162,27 @@ struct rsmi_fdec {
     std::vector<CarryCopy> carries;
     std::vector<Out> outs;
     std::vector<uint8_t> present;  // all buckets' present flags
-    int64_t staging_bytes = 0, blob_bytes = 0;
+    std::vector<RowRef> rows;      // k per job
+    std::vector<std::pair<int64_t, int>> d2h_rows;  // (job, row) copied back, in d2h order
+    // outputs that straddle two rows, copied into bump-allocated chunks that are
+    // kept from batch to batch (fresh pages would cost a fault per 4 KiB)
+    std::vector<std::pair<std::unique_ptr<uint8_t[]>, size_t>> spill;
+    size_t spill_chunk = 0, spill_used = 0;
+    uint8_t *spill_alloc(size_t n) {
+        while (spill_chunk < spill.size() && spill_used + n > spill[spill_chunk].second) {
+            ++spill_chunk;
+            spill_used = 0;
+        }
+        if (spill_chunk == spill.size()) {
+            const size_t c = std::max<size_t>(n, size_t(64) << 20);
+            spill.emplace_back(std::unique_ptr<uint8_t[]>(new uint8_t[c]), c);
+            spill_used = 0;
+        }
+        uint8_t *p = spill[spill_chunk].first.get() + spill_used;
+        spill_used += n;
+        return p;
+    }
+    int64_t staging_bytes = 0, d2h_bytes = 0;
     const uint8_t *host_base = nullptr;
     bool planned = false, ran = false, resolved = false, plan_only = false;
 
@@ -242,8 +270,20 @@ void plan_decode(rsmi_fdec *D, uint32_t seq, Group &g, int type, int inner, int 
     J.event = event;
     J.bucket = b;
     J.row = B.rows++;
-    J.blob_off = D->blob_bytes;
-    D->blob_bytes += (int64_t)k * dlen + 16;
+    J.rows0 = (int64_t)D->rows.size();
+    // data rows the host will read: the received packet when this batch's host
+    // buffer holds it, else the decoded (or carried) row, copied back
+    const int64_t job = (int64_t)D->jobs.size();
+    for (int i = 0; i < k; ++i) {
+        auto f = g.gm.find(i);
+        const RingEnt *r = f != g.gm.end() ? &D->ring[(size_t)f->second] : nullptr;
+        if (r && r->host && r->in_batch) {
+            D->rows.push_back(RowRef{r->host, -1});
+        } else {
+            D->rows.push_back(RowRef{nullptr, (int64_t)D->d2h_rows.size()});
+            D->d2h_rows.emplace_back(job, i);
+        }
+    }
     // survivor copies: dst is patched once the bucket strides are known
     for (auto &sv : sel) {
         const RingEnt &r = D->ring[(size_t)sv.second];
@@ -301,6 +341,7 @@ int input_packet(rsmi_fdec *D, const uint8_t *s, int len, uint64_t dsrc, int32_t
     slot.seq = seq;
     slot.len = len;
     slot.src = dsrc;
+    slot.host = pay;
     slot.in_batch = true;
     Group &g = D->group(seq);
     g.gm[inner] = D->index;
@@ -374,7 +415,10 @@ int rsmi_fdec_plan(rsmi_fdec *D, int64_t n, const int32_t *len, const uint64_t *
     D->carries.clear();
     D->outs.clear();
     D->present.clear();
-    D->staging_bytes = D->blob_bytes = 0;
+    D->rows.clear();
+    D->d2h_rows.clear();
+    D->spill_chunk = D->spill_used = 0;  // the chunks are reused
+    D->staging_bytes = D->d2h_bytes = 0;
     D->host_base = host_base;
     for (int64_t i = 0; i < n; ++i) {
         int r;
@@ -415,6 +459,12 @@ int rsmi_fdec_plan(rsmi_fdec *D, int64_t n, const int32_t *len, const uint64_t *
         const uint64_t dst = rsmi::kCarryTag | (uint64_t)sidx * kRingBytes;
         if (live && r.len > 0) D->carries.push_back(CarryCopy{r.src, dst, (uint32_t)r.len, 0});
         r.src = dst;
+        r.host = nullptr;
+    }
+    for (auto &jr : D->d2h_rows) {  // byte offsets of the rows copied back
+        const Job &J = D->jobs[(size_t)jr.first];
+        D->rows[(size_t)(J.rows0 + jr.second)].d2h = D->d2h_bytes;
+        D->d2h_bytes += (J.len + 15) & ~15;
     }
     D->planned = true;
     D->ran = D->resolved = false;
@@ -437,23 +487,24 @@ int rsmi_fdec_run_dev(rsmi_fdec *D, void *stream) {
     hipStream_t s = (hipStream_t)stream;
     int rc = dev_grow(&D->dcarry, &D->dcarry_cap, (size_t)D->buff_num * kRingBytes);
     if (!rc) rc = dev_grow(&D->dstage, &D->stage_cap, (size_t)D->staging_bytes + 16);
-    if (!rc) rc = dev_grow(&D->dblob, &D->blob_cap, (size_t)D->blob_bytes + 16);
-    if (!rc) rc = host_grow(&D->hblob, &D->hblob_cap, (size_t)D->blob_bytes + 16);
+    if (!rc) rc = dev_grow(&D->dblob, &D->blob_cap, (size_t)D->d2h_bytes + 16);
+    if (!rc) rc = host_grow(&D->hblob, &D->hblob_cap, (size_t)D->d2h_bytes + 16);
     int64_t max_rows = 0;
     for (const Bucket &B : D->buckets) max_rows = std::max(max_rows, B.rows);
     if (!rc) rc = dev_grow(&D->dstatus, &D->status_cap, (size_t)max_rows * 4 + 16);
     if (rc) return rc;
-    // metadata: gathers | present | packs | carries, one upload
-    std::vector<PackJob> packs(D->jobs.size());
-    for (size_t j = 0; j < D->jobs.size(); ++j) {
-        const Job &J = D->jobs[j];
+    // metadata: gathers | present | row copies back | carries, one upload
+    std::vector<CarryCopy> packs(D->d2h_rows.size());
+    int64_t ro = 0;
+    for (size_t j = 0; j < D->d2h_rows.size(); ++j) {
+        const Job &J = D->jobs[(size_t)D->d2h_rows[j].first];
         const Bucket &B = D->buckets[(size_t)J.bucket];
-        packs[j] = PackJob{(uint64_t)(uintptr_t)(D->dstage + B.staging_off + J.row * B.n * B.stride),
-                           (uint64_t)(uintptr_t)(D->dblob + J.blob_off), (uint32_t)J.k, (uint32_t)J.len,
-                           (uint32_t)B.stride, 0};
+        const uint8_t *row = D->dstage + B.staging_off + (J.row * B.n + D->d2h_rows[j].second) * B.stride;
+        packs[j] = CarryCopy{(uint64_t)(uintptr_t)row, (uint64_t)(uintptr_t)(D->dblob + ro), (uint32_t)J.len, 0};
+        ro += (J.len + 15) & ~15;
     }
     const size_t gb = D->gathers.size() * sizeof(GatherCopy), pb = D->present.size(),
-                 kb = packs.size() * sizeof(PackJob), cb = D->carries.size() * sizeof(CarryCopy);
+                 kb = packs.size() * sizeof(CarryCopy), cb = D->carries.size() * sizeof(CarryCopy);
     const size_t go = 0, po = (gb + 255) & ~size_t(255), ko = (po + pb + 255) & ~size_t(255),
                  co = (ko + kb + 255) & ~size_t(255), all = co + cb + 16;
     rc = dev_grow(&D->dmeta, &D->meta_cap, all);
@@ -474,16 +525,18 @@ int rsmi_fdec_run_dev(rsmi_fdec *D, void *stream) {
                                 (int64_t)D->gathers.size(), carry, s);
     if (e != hipSuccess) return fail(RSMI_ERR_HIP, std::string("fdec gather: ") + hipGetErrorString(e));
     for (const Bucket &B : D->buckets) {
+        if (B.len == 0) continue;  // empty shards: nothing to rebuild
         rc = rsmi_decode_dev(B.k, B.n, D->dstage + B.staging_off, (int64_t)B.n * B.stride, B.stride,
                              B.len, B.rows, D->dmeta + po + B.present_off, D->dstatus, stream);
         if (rc) return rc;
     }
-    e = rsmi::launch_pack(reinterpret_cast<const PackJob *>(D->dmeta + ko), (int64_t)packs.size(), s);
+    e = rsmi::launch_carry(reinterpret_cast<const CarryCopy *>(D->dmeta + ko), (int64_t)packs.size(),
+                           carry, s);
     if (e == hipSuccess)
         e = rsmi::launch_carry(reinterpret_cast<const CarryCopy *>(D->dmeta + co),
                                (int64_t)D->carries.size(), carry, s);
-    if (e == hipSuccess && D->blob_bytes)
-        e = hipMemcpyAsync(D->hblob, D->dblob, (size_t)D->blob_bytes, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess && D->d2h_bytes)
+        e = hipMemcpyAsync(D->hblob, D->dblob, (size_t)D->d2h_bytes, hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipEventRecord(D->done, s);
     if (e != hipSuccess) return fail(RSMI_ERR_HIP, std::string("fdec run: ") + hipGetErrorString(e));
     D->in_flight = true;
@@ -507,36 +560,52 @@ int rsmi_fdec_outputs(rsmi_fdec *D, int64_t *n_out) {
                 continue;
             }
             const Job &J = D->jobs[(size_t)o.job];
-            const uint8_t *blob = D->hblob + J.blob_off;
+            const RowRef *rr = D->rows.data() + J.rows0;
+            auto row = [&](int i) -> const uint8_t * {
+                return rr[i].host ? rr[i].host : D->hblob + rr[i].d2h;
+            };
+            const int64_t L = J.len;
+            const int64_t cur = (int64_t)J.k * L;  // the blob: the k data rows back to back
+            // n bytes of the blob at pos: a pointer into one row, or a spilled copy
+            auto span = [&](int64_t pos, int64_t n) -> const uint8_t * {
+                const int64_t r = pos / L, o0 = pos - r * L;
+                if (o0 + n <= L) return row((int)r) + o0;
+                uint8_t *buf = D->spill_alloc((size_t)n);
+                for (int64_t c = 0; c < n;) {
+                    const int64_t rr2 = (pos + c) / L, oo = pos + c - rr2 * L;
+                    const int64_t t = std::min(n - c, L - oo);
+                    std::memcpy(buf + c, row((int)rr2) + oo, (size_t)t);
+                    c += t;
+                }
+                return buf;
+            };
             if (J.type == 0) {  // blob_decode_t::output (fec_manager.cpp:97-129)
-                const int64_t cur = (int64_t)J.k * J.len;
                 if (cur < 4) continue;
-                const uint32_t cnt = rd_u32(blob);
+                const uint32_t cnt = rd_u32(span(0, 4));
                 if (cnt > (uint32_t)kMaxBlobPackets) continue;
                 int64_t pos = 4;
                 const size_t mark = res.size();
                 bool ok = true;
                 for (uint32_t i = 0; i < cnt; ++i) {
                     if (pos + 2 > cur) { ok = false; break; }
-                    const int l = (int)rd_u16(blob + pos);
+                    const int l = (int)rd_u16(span(pos, 2));
                     pos += 2;
                     if (pos + l > cur) { ok = false; break; }
-                    res.push_back(Out{o.event, o.job, blob + pos, l});
+                    res.push_back(Out{o.event, o.job, l ? span(pos, l) : row(0), l});
                     pos += l;
                 }
                 if (!ok) res.resize(mark);
             } else {  // mode 1 (:713-755): every data row's u16 <= max_data_len, then the missed rows
                 bool ok = true;
                 for (int i = 0; i < J.k; ++i)
-                    if ((int)rd_u16(blob + (int64_t)i * J.len) > kMaxDataLen) ok = false;
+                    if ((int)rd_u16(row(i)) > kMaxDataLen) ok = false;
                 if (!ok) continue;
                 // missed = rows not received + the packet that completed the group
                 const Bucket &B = D->buckets[(size_t)J.bucket];
                 const uint8_t *pres = D->present.data() + B.present_off + J.row * B.n;
                 for (int i = 0; i < J.k; ++i) {
                     if (pres[i] && i != J.inner) continue;
-                    const uint8_t *r = blob + (int64_t)i * J.len;
-                    res.push_back(Out{o.event, o.job, r + 2, (int32_t)rd_u16(r)});
+                    res.push_back(Out{o.event, o.job, row(i) + 2, (int32_t)rd_u16(row(i))});
                 }
             }
         }

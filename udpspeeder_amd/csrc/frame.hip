@@ -340,43 +340,6 @@ __global__ __launch_bounds__(kThreads) void k_gather(const GatherCopy *jobs, int
     }
 }
 
-// k rows of len bytes (stride apart, 16-aligned) -> one contiguous blob at an
-// arbitrary address: one wave per group; dword stores, each dword built from
-// the (at most two) rows it spans.
-__global__ __launch_bounds__(kThreads) void k_pack(const PackJob *jobs, int64_t njobs) {
-    const int lane = threadIdx.x & 63;
-    const int64_t w0 = (int64_t)blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
-    for (int64_t w = w0; w < njobs; w += (int64_t)gridDim.x * (kThreads / 64)) {
-        const PackJob J = jobs[w];
-        const uint8_t *src = reinterpret_cast<const uint8_t *>(J.src);
-        uint8_t *dst = reinterpret_cast<uint8_t *>(J.dst);
-        const uint64_t total = (uint64_t)J.k * J.len;
-        // head bytes up to the first 4-aligned dst address, then whole dwords, then the tail
-        const uint32_t head = (uint32_t)((4 - ((uintptr_t)dst & 3)) & 3);
-        auto byte_at = [&](uint64_t b) -> uint32_t {
-            const uint32_t r = (uint32_t)(b / J.len);
-            return src[(uint64_t)r * J.stride + (b - (uint64_t)r * J.len)];
-        };
-        if (lane < (int)head && lane < (int)total) dst[lane] = (uint8_t)byte_at(lane);
-        const uint64_t nd = total > head ? (total - head) / 4 : 0;
-        for (uint64_t d = lane; d < nd; d += 64) {
-            const uint64_t b = head + 4 * d;
-            const uint32_t r = (uint32_t)(b / J.len);
-            const uint64_t o = b - (uint64_t)r * J.len;  // offset in row r
-            uint32_t v;
-            if (o + 4 <= J.len) {
-                v = keep(window(src + (uint64_t)r * J.stride + o, 0, 4), 0, 4).x;
-            } else {
-                v = 0;
-                for (int t = 0; t < 4; ++t) v |= byte_at(b + t) << (8 * t);
-            }
-            *reinterpret_cast<uint32_t *>(dst + b) = v;
-        }
-        const uint64_t tail0 = head + 4 * nd;
-        if (tail0 + lane < total && lane < 4) dst[tail0 + lane] = (uint8_t)byte_at(tail0 + lane);
-    }
-}
-
 }  // namespace
 
 hipError_t launch_gather(const GatherCopy *jobs, int64_t njobs, CarryBase carry, hipStream_t s) {
@@ -384,14 +347,6 @@ hipError_t launch_gather(const GatherCopy *jobs, int64_t njobs, CarryBase carry,
     int64_t blocks = (njobs + kThreads / 64 - 1) / (kThreads / 64);
     if (blocks > 16384) blocks = 16384;
     k_gather<<<(unsigned)blocks, kThreads, 0, s>>>(jobs, njobs, carry);
-    return hipGetLastError();
-}
-
-hipError_t launch_pack(const PackJob *jobs, int64_t njobs, hipStream_t s) {
-    if (njobs <= 0) return hipSuccess;
-    int64_t blocks = (njobs + kThreads / 64 - 1) / (kThreads / 64);
-    if (blocks > 16384) blocks = 16384;
-    k_pack<<<(unsigned)blocks, kThreads, 0, s>>>(jobs, njobs);
     return hipGetLastError();
 }
 

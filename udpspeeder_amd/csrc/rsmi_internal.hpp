@@ -139,14 +139,7 @@ struct GatherCopy {
     uint64_t dst;
     uint32_t len, dst_len;
 };
-// The k data rows of one decoded group (row r at src + r*stride, 16-aligned)
-// concatenated into dst (any alignment; the output blob).
-struct PackJob {
-    uint64_t src, dst;
-    uint32_t k, len, stride, pad;
-};
 hipError_t launch_gather(const GatherCopy *jobs, int64_t njobs, CarryBase carry, hipStream_t s);
-hipError_t launch_pack(const PackJob *jobs, int64_t njobs, hipStream_t s);
 hipError_t launch_frame(const FrameGroup *groups, int64_t ngroups, const FrameSrc *srcs,
                         CarryBase carry, uint8_t *slots, int64_t slot_stride, hipStream_t s);
 hipError_t launch_carry(const CarryCopy *jobs, int64_t njobs, CarryBase carry, hipStream_t s);

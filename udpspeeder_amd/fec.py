@@ -215,17 +215,23 @@ class FecDecoder:
         s = stream if stream is not None else torch.cuda.current_stream()
         check(lib().rsmi_fdec_run_dev(self._h, s.cuda_stream), "rsmi_fdec_run_dev")
 
-    def outputs(self):
-        """[(bytes, event)] in the reference's output() order (waits for the run)."""
+    def outputs_raw(self):
+        """(ptr, len, event) arrays of the outputs, in output() order, without
+        copying the bytes (waits for the run; pointers live until the next plan)."""
         n = C.c_int64()
         check(lib().rsmi_fdec_outputs(self._h, C.byref(n)), "rsmi_fdec_outputs")
-        ptr = (C.c_void_p * max(1, n.value))()
+        ptr = np.zeros(max(1, n.value), np.uint64)
         ln = np.zeros(max(1, n.value), np.int32)
         ev = np.zeros(max(1, n.value), np.int32)
-        check(lib().rsmi_fdec_output_list(self._h, ptr, ln.ctypes.data, ev.ctypes.data),
-              "rsmi_fdec_output_list")
-        return [(C.string_at(ptr[i], int(ln[i])) if ln[i] else b"", int(ev[i]))
-                for i in range(n.value)]
+        check(lib().rsmi_fdec_output_list(self._h, ptr.ctypes.data, ln.ctypes.data,
+                                          ev.ctypes.data), "rsmi_fdec_output_list")
+        return ptr[:n.value], ln[:n.value], ev[:n.value]
+
+    def outputs(self):
+        """[(bytes, event)] in the reference's output() order (waits for the run)."""
+        ptr, ln, ev = self.outputs_raw()
+        return [(C.string_at(int(ptr[i]), int(ln[i])) if ln[i] else b"", int(ev[i]))
+                for i in range(len(ln))]
 
     # ---- the reference's per-call interface ------------------------------------
     def input(self, packet: bytes, now_ms: int = 0) -> int:
