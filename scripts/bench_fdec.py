@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--erase", type=int, default=5)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--mode", type=int, default=0)
+    ap.add_argument("--cpu-sample", type=int, default=100000, help="0 = no CPU baseline")
     args = ap.parse_args()
     plen = 1200 if args.mode == 0 else 1250
     npk = args.groups * 20
@@ -83,7 +84,22 @@ def main():
         outs = n_out
     med = lambda i: float(np.median([r[i] for r in res]))
     payload = int(npk) * plen
+    cpu = None
+    if args.cpu_sample:
+        # the reference's fec_decode_manager_t (oracle/_ref) on one thread -- its
+        # libev thread -- over the first packets of the same stream
+        from oracle.fec_frame import FecReference
+        if FecReference.available():
+            n = min(args.cpu_sample, len(lens))
+            chan = [host_all[int(oi[i]):int(oi[i]) + int(lens[i])].tobytes() for i in range(n)]
+            t0 = time.perf_counter()
+            _, rout, _ = FecReference().decode(chan)
+            dt = time.perf_counter() - t0
+            cpu = {"kind": "reference", "threads": 1, "sample_packets": n,
+                   "packets_in_per_s": round(n / dt, 1), "outputs": len(rout),
+                   "note": "includes the driver's copy of each packet in and out"}
     print(json.dumps({
+        "cpu_baseline": cpu,
         "mode": args.mode, "groups": int(len(g0)), "packets_in": int(len(kept)),
         "erased_per_group": args.erase, "decoded_groups": int(dp.n_decodes), "outputs": outs,
         "plan_ms": round(med(0) * 1e3, 3), "run_ms": round(med(1), 4),

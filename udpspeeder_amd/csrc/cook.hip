@@ -209,6 +209,13 @@ __device__ __forceinline__ void load_round(u32x4 (&d)[3], const uint8_t *pkt, in
     }
 }
 
+// Bytes of round 0 that may be read before the packet's length is known:
+// whole pieces within its cap (the packet owns them), none if misaligned.
+// Pieces past the packet's extent are loaded but never stored.
+__device__ __forceinline__ int cap_extent(const CookArgs &a, const uint8_t *pkt, bool have) {
+    return (have && ((uintptr_t)pkt & 3) == 0) ? min(a.cap & ~15, kRound) : 0;
+}
+
 __device__ __forceinline__ u32x4 ks_piece(const CookArgs &a, int P) {
     return a.ks ? *reinterpret_cast<const u32x4 *>(a.ks + P) : u32x4{0, 0, 0, 0};
 }
@@ -239,18 +246,19 @@ __global__ __launch_bounds__(kThreads, 6) void k_cook(CookArgs a) {
         const int64_t pk = 2 * pw + half;
         const bool have = pk < a.count;
         int L = -1, ivl = 0;
-        uint8_t *pkt = nullptr;
+        uint8_t *pkt = have ? packet_ptr(a, pk) : nullptr;
+        // round 0 is read up to the packet's cap (every packet owns cap bytes), so
+        // these loads fly together with the length load instead of after it
+        u32x4 cur[3];
+        load_round(cur, pkt, 0, hl, cap_extent(a, pkt, have));
         if (have) {
             L = a.len[pk];
-            pkt = packet_ptr(a, pk);
             if (obs) ivl = a.iv ? a.iv_len[pk] : 4 + (int)(splitmix(a.seed, (uint64_t)pk, 0) % 29u);
         }
         const int out = L + (ck ? 4 : 0) + (obs ? ivl + 1 : 0);
         const bool ok = have && L >= 0 && L <= RSMI_COOK_MAX_LEN && ivl <= RSMI_COOK_IV_MAX &&
                         round16(out) <= a.cap && ((uintptr_t)pkt & 3) == 0;
         const int ext = ok ? round16(out) : 0;
-        u32x4 cur[3];
-        load_round(cur, pkt, 0, hl, ext);
         if (ok && ivl) {  // iv repeated: iv2[t] = iv[t % ivl], t < ivl + 20 (<= 52)
             for (int t = hl; t < ivl + 20; t += 32) {
                 const int j = t % ivl;
@@ -343,6 +351,8 @@ __global__ __launch_bounds__(kThreads, 6) void k_decook(CookArgs a) {
          pw += (int64_t)gridDim.x * (kThreads / 64)) {
         const int64_t pk = 2 * pw + half;
         const bool have = pk < a.count;
+        // (de_cook keeps its round-0 loads behind the length: loading up to the
+        // cap here spills registers and measured slower)
         int L = -1;
         uint8_t *pkt = nullptr;
         if (have) {
