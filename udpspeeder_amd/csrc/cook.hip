@@ -1,10 +1,11 @@
 // cook.hip -- batched packet cook / de_cook for gfx950.
 //
 // Semantics: packet.cpp do_cook (:303-308) and de_cook (:310-326), see
-// include/rsmi_cook.h.  One half-wave (32 lanes) owns one packet.  A packet is
-// walked in rounds of 96 16-byte pieces (1536 B); in a round lane l owns pieces
-// l, l+32, l+64, so every load and store instruction covers 512 contiguous
-// bytes of each of the wave's two packets.
+// include/rsmi_cook.h.  kLpp lanes (16 by default, a quarter wave) own one
+// packet, so a wave works on 64/kLpp packets at once.  A packet is walked in
+// rounds of 96 16-byte pieces (1536 B); in a round lane l owns pieces l,
+// l+kLpp, l+2kLpp, ..., so every load and store instruction covers 16*kLpp
+// contiguous bytes of each of the wave's packets.
 //
 // The transform is byte-parallel: an output piece is the input piece XOR a
 // key-stream window (KS[p] = key[p % strlen(key)], precomputed per context,
@@ -15,12 +16,12 @@
 // 0, no final xor) is linear, with Z_d = "feed d zero bytes" a linear map on
 // the 32-bit register.  The message is zero-padded to Q whole pieces; then
 //   * each piece's raw CRC comes from slicing-by-8 (8 x 256-word LDS tables);
-//   * a lane folds its pieces Horner-style, h = Z_512(h) ^ crc(piece);
+//   * a lane folds its pieces Horner-style, h = Z_{16 kLpp}(h) ^ crc(piece);
 //   * h is shifted to the end of the round's data by Z_{16k}, k = pieces after
-//     the lane's last piece (always 0..31: 32 nibble-table maps), and the 32
-//     lanes XOR-reduce with ds_swizzle;
-//   * rounds chain as acc = Z_{16 Q_r}(acc) ^ round, Z_{16 Q_r} being Z_512
-//     applied Q_r/32 times and one lane map;
+//     the lane's last piece (always 0..kLpp-1: kLpp nibble-table maps), and the
+//     packet's kLpp lanes XOR-reduce with ds_swizzle;
+//   * rounds chain as acc = Z_{16 Q_r}(acc) ^ round, Z_{16 Q_r} being
+//     Z_{16 kLpp} applied Q_r/kLpp times and one lane map;
 //   * the < 16 bytes of zero padding are removed with Z_{-z} (two nibble maps).
 // crc32h's init ~0 is folded in by complementing the first 4 bytes of the
 // padded message, its final ~ at the end.
@@ -35,8 +36,14 @@
 namespace rsmi {
 namespace {
 
-constexpr int kThreads = 512;           // 8 waves = 16 packets in flight per block
-constexpr int kRound = 1536;            // 96 pieces: 3 per lane
+constexpr int kLpp = kCookLpp;          // lanes per packet
+constexpr int kPpw = 64 / kLpp;         // packets per wave
+constexpr int kPpl = 96 / kLpp;         // pieces per lane per round
+#ifndef COOK_OCC
+#define COOK_OCC (kLpp == 16 ? 5 : 6)   // waves per SIMD the register budget is cut for
+#endif
+constexpr int kThreads = kLpp == 16 ? 256 : 512;  // LDS (tables per block) bounds residency
+constexpr int kRound = 1536;            // 96 pieces per packet per round
 constexpr int kScrCook = 144;           // per-packet LDS: iv2[64] | overlay[64] | misc[16]
 constexpr int kScrDecook = 304;         // iv2[288] (iv_len up to 255) | misc[16]
 
@@ -78,13 +85,13 @@ __device__ __forceinline__ uint32_t nib_map(const uint32_t *M, uint32_t c) {
     return r ^ M[112 + (c >> 28)];
 }
 
-// XOR over the 32 lanes of this half-wave (ds_swizzle xor-mode stays in 32 lanes).
-__device__ __forceinline__ uint32_t half_xor(uint32_t c) {
+// XOR over the kLpp lanes of one packet (ds_swizzle xor-mode, xor masks < kLpp).
+__device__ __forceinline__ uint32_t group_xor(uint32_t c) {
     c ^= (uint32_t)__builtin_amdgcn_ds_swizzle((int)c, 0x041F);
     c ^= (uint32_t)__builtin_amdgcn_ds_swizzle((int)c, 0x081F);
     c ^= (uint32_t)__builtin_amdgcn_ds_swizzle((int)c, 0x101F);
     c ^= (uint32_t)__builtin_amdgcn_ds_swizzle((int)c, 0x201F);
-    c ^= (uint32_t)__builtin_amdgcn_ds_swizzle((int)c, 0x401F);
+    if (kLpp == 32) c ^= (uint32_t)__builtin_amdgcn_ds_swizzle((int)c, 0x401F);
     return c;
 }
 
@@ -118,7 +125,7 @@ __device__ __forceinline__ u32x4 iv_window(const uint32_t *iv2w, uint32_t pos, u
     return iv_window_at(iv2w, mod_ivl(pos, ivl, magic));
 }
 
-// Position of the IV cycle at the next piece a lane owns (512 bytes further).
+// Position of the IV cycle at the next piece a lane owns (16 kLpp bytes further).
 __device__ __forceinline__ uint32_t iv_step(uint32_t r, uint32_t s512, uint32_t ivl) {
     r += s512;
     return r >= ivl ? r - ivl : r;
@@ -131,8 +138,8 @@ __device__ __forceinline__ uint64_t splitmix(uint64_t seed, uint64_t idx, uint64
     return z ^ (z >> 31);
 }
 
-// Z_512 as four byte tables.
-__device__ __forceinline__ uint32_t z512(const uint32_t *B, uint32_t c) {
+// Z_{16 kLpp} as four byte tables.
+__device__ __forceinline__ uint32_t zh(const uint32_t *B, uint32_t c) {
     return xor3(B[c & 0xff], B[256 + ((c >> 8) & 0xff)], B[512 + ((c >> 16) & 0xff)]) ^
            B[768 + (c >> 24)];
 }
@@ -152,33 +159,34 @@ __device__ __forceinline__ uint32_t unshift(const uint32_t *T, uint32_t c, uint3
     return hi ? c2 : c;
 }
 
-// CRC of a round, folded one piece at a time: piece q (= 32p + lane) of the
+// CRC of a round, folded one piece at a time: piece q (= kLpp p + lane) of the
 // round, crc input v; qr = data pieces of the packet in this round (0..96).
 struct RoundCrc {
     uint32_t h = 0;
     int last = -1;
     __device__ __forceinline__ void add(const uint32_t *T, u32x4 v, int q, int qr) {
-        const uint32_t hn = z512(T + kCookZ512, h) ^ crc16(T, v);
+        const uint32_t hn = zh(T + kCookZH, h) ^ crc16(T, v);
         h = q < qr ? hn : h;
         last = q < qr ? q : last;
     }
-    // The round's raw CRC relative to the end of its data, in all 32 lanes.
+    // The round's raw CRC relative to the end of its data, in all kLpp lanes.
     __device__ __forceinline__ uint32_t finish(const uint32_t *T, int qr) const {
         int k = qr - 1 - last;
-        k = (last >= 0 && k >= 0 && k < 32) ? k : 0;
+        k = (last >= 0 && k >= 0 && k < kLpp) ? k : 0;
         const uint32_t c = nib_map(T + kCookLane + 128 * k, h);
-        return half_xor(last >= 0 ? c : 0u);
+        return group_xor(last >= 0 ? c : 0u);
     }
 };
 
-// acc = Z_{16 qr}(acc): Z_512 (qr / 32) times, then the lane map Z_{16 (qr % 32)}.
+// acc = Z_{16 qr}(acc): Z_{16 kLpp} (qr / kLpp) times, then the lane map
+// Z_{16 (qr % kLpp)}.
 __device__ __forceinline__ uint32_t shift_pieces(const uint32_t *T, uint32_t acc, int qr) {
 #pragma unroll
-    for (int i = 0; i < 3; ++i) {
-        const uint32_t n = z512(T + kCookZ512, acc);
-        acc = i < (qr >> 5) ? n : acc;
+    for (int i = 0; i < kPpl; ++i) {
+        const uint32_t n = zh(T + kCookZH, acc);
+        acc = i < qr / kLpp ? n : acc;
     }
-    return nib_map(T + kCookLane + 128 * (qr & 31), acc);
+    return nib_map(T + kCookLane + 128 * (qr % kLpp), acc);
 }
 
 __device__ __forceinline__ int round16(int x) { return (x + 15) & ~15; }
@@ -189,22 +197,24 @@ __device__ __forceinline__ void load_tables(uint32_t *lds, const uint32_t *tabs)
     __syncthreads();
 }
 
-// Uniform loop bound for the two packets of a wave.
+// Uniform loop bound for the packets of a wave.
 __device__ __forceinline__ int wave_max(int v) {
-    const int a = __builtin_amdgcn_readlane(v, 0), b = __builtin_amdgcn_readlane(v, 32);
-    return a > b ? a : b;
+    int m = __builtin_amdgcn_readlane(v, 0);
+#pragma unroll
+    for (int s = 1; s < kPpw; ++s) m = max(m, __builtin_amdgcn_readlane(v, s * kLpp));
+    return m;
 }
 
 __device__ __forceinline__ uint8_t *packet_ptr(const CookArgs &a, int64_t pk) {
     return a.base + (a.offset ? a.offset[pk] : (uint64_t)pk * (uint64_t)a.stride);
 }
 
-// The three pieces of round r owned by lane hl: zeros past ext.
-__device__ __forceinline__ void load_round(u32x4 (&d)[3], const uint8_t *pkt, int r, int hl,
+// The kPpl pieces of round r owned by lane hl: zeros past ext.
+__device__ __forceinline__ void load_round(u32x4 (&d)[kPpl], const uint8_t *pkt, int r, int hl,
                                            int ext) {
 #pragma unroll
-    for (int p = 0; p < 3; ++p) {
-        const int P = r * kRound + 16 * (32 * p + hl);
+    for (int p = 0; p < kPpl; ++p) {
+        const int P = r * kRound + 16 * (kLpp * p + hl);
         d[p] = P < ext ? ld_piece(pkt + P) : u32x4{0, 0, 0, 0};
     }
 }
@@ -229,27 +239,27 @@ __device__ __forceinline__ u32x4 crc_in(u32x4 v, int P, int n) {
     return v;
 }
 
-__global__ __launch_bounds__(kThreads, 6) void k_cook(CookArgs a) {
+__global__ __launch_bounds__(kThreads, COOK_OCC) void k_cook(CookArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const bool ck = !(a.flags & RSMI_COOK_NO_CHECKSUM);
     const bool obs = !(a.flags & RSMI_COOK_NO_OBSCURE);
     if (ck) load_tables(lds, a.tabs);
-    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63, half = lane >> 5, hl = lane & 31;
-    uint8_t *scr = reinterpret_cast<uint8_t *>(lds + kCookTabWords) + (wid * 2 + half) * kScrCook;
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63, sub = lane / kLpp, hl = lane % kLpp;
+    uint8_t *scr = reinterpret_cast<uint8_t *>(lds + kCookTabWords) + (wid * kPpw + sub) * kScrCook;
     uint32_t *iv2w = reinterpret_cast<uint32_t *>(scr);
     uint8_t *ovl = scr + 64;
     const uint32_t *T = lds;
-    const int64_t npairs = (a.count + 1) >> 1;
+    const int64_t nunits = (a.count + kPpw - 1) / kPpw;  // kPpw packets per wave step
 
-    for (int64_t pw = (int64_t)blockIdx.x * (kThreads / 64) + wid; pw < npairs;
+    for (int64_t pw = (int64_t)blockIdx.x * (kThreads / 64) + wid; pw < nunits;
          pw += (int64_t)gridDim.x * (kThreads / 64)) {
-        const int64_t pk = 2 * pw + half;
+        const int64_t pk = kPpw * pw + sub;
         const bool have = pk < a.count;
         int L = -1, ivl = 0;
         uint8_t *pkt = have ? packet_ptr(a, pk) : nullptr;
         // round 0 is read up to the packet's cap (every packet owns cap bytes), so
         // these loads fly together with the length load instead of after it
-        u32x4 cur[3];
+        u32x4 cur[kPpl];
         load_round(cur, pkt, 0, hl, cap_extent(a, pkt, have));
         if (have) {
             L = a.len[pk];
@@ -260,7 +270,7 @@ __global__ __launch_bounds__(kThreads, 6) void k_cook(CookArgs a) {
                         round16(out) <= a.cap && ((uintptr_t)pkt & 3) == 0;
         const int ext = ok ? round16(out) : 0;
         if (ok && ivl) {  // iv repeated: iv2[t] = iv[t % ivl], t < ivl + 20 (<= 52)
-            for (int t = hl; t < ivl + 20; t += 32) {
+            for (int t = hl; t < ivl + 20; t += kLpp) {
                 const int j = t % ivl;
                 scr[t] = a.iv ? a.iv[pk * RSMI_COOK_IV_MAX + j]
                               : (uint8_t)(splitmix(a.seed, (uint64_t)pk, 1 + (j >> 3)) >> (8 * (j & 7)));
@@ -268,7 +278,7 @@ __global__ __launch_bounds__(kThreads, 6) void k_cook(CookArgs a) {
         }
         wave_sync();
         const uint32_t magic = ivl ? 0xFFFFFFFFu / (uint32_t)ivl : 0u;
-        const uint32_t s512 = ivl ? mod_ivl(512u, (uint32_t)ivl, magic) : 0u;
+        const uint32_t sstep = ivl ? mod_ivl(16u * kLpp, (uint32_t)ivl, magic) : 0u;
         const int Q = (L + 15) >> 4;            // pieces holding payload (crc input)
         const int P0 = L & ~15;                 // first piece that holds tail bytes
         const int nrm = wave_max((ext + kRound - 1) / kRound);
@@ -281,9 +291,9 @@ __global__ __launch_bounds__(kThreads, 6) void k_cook(CookArgs a) {
             RoundCrc rc;
             uint32_t ivr = ivl ? mod_ivl((uint32_t)(r * kRound + 16 * hl), (uint32_t)ivl, magic) : 0u;
 #pragma unroll
-            for (int p = 0; p < 3; ++p) {
-                const int P = r * kRound + 16 * (32 * p + hl);
-                if (ck) rc.add(T, crc_in(cur[p], P, L), 32 * p + hl, qr);
+            for (int p = 0; p < kPpl; ++p) {
+                const int P = r * kRound + 16 * (kLpp * p + hl);
+                if (ck) rc.add(T, crc_in(cur[p], P, L), kLpp * p + hl, qr);
                 if (P < ext && P + 16 <= L) {  // wholly payload: obscure + xor, store now
                     u32x4 m = ks_piece(a, P);
                     if (ivl) m ^= iv_window_at(iv2w, ivr);
@@ -292,7 +302,7 @@ __global__ __launch_bounds__(kThreads, 6) void k_cook(CookArgs a) {
                     dt = cur[p];
                     Pt = P;
                 }
-                if (ivl) ivr = iv_step(ivr, s512, (uint32_t)ivl);
+                if (ivl) ivr = iv_step(ivr, sstep, (uint32_t)ivl);
                 __builtin_amdgcn_sched_barrier(0);  // one piece's lookups at a time
             }
             if (ck) {
@@ -305,7 +315,7 @@ __global__ __launch_bounds__(kThreads, 6) void k_cook(CookArgs a) {
         if (ck && L > 0) crc = ~unshift(T, acc, (uint32_t)(16 * Q - L));
         // ---- tail: crc (BE), iv, iv_len appended after the payload -------------
         if (ok) {
-            for (int t = hl; t < 64; t += 32) {
+            for (int t = hl; t < 64; t += kLpp) {
                 const int pos = P0 + t;
                 uint32_t v = 0;
                 if (pos >= L && pos < out) {
@@ -335,21 +345,21 @@ __global__ __launch_bounds__(kThreads, 6) void k_cook(CookArgs a) {
     }
 }
 
-__global__ __launch_bounds__(kThreads, 6) void k_decook(CookArgs a) {
+__global__ __launch_bounds__(kThreads, COOK_OCC) void k_decook(CookArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const bool ck = !(a.flags & RSMI_COOK_NO_CHECKSUM);
     const bool obs = !(a.flags & RSMI_COOK_NO_OBSCURE);
     if (ck) load_tables(lds, a.tabs);
-    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63, half = lane >> 5, hl = lane & 31;
-    uint8_t *scr = reinterpret_cast<uint8_t *>(lds + kCookTabWords) + (wid * 2 + half) * kScrDecook;
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63, sub = lane / kLpp, hl = lane % kLpp;
+    uint8_t *scr = reinterpret_cast<uint8_t *>(lds + kCookTabWords) + (wid * kPpw + sub) * kScrDecook;
     uint32_t *iv2w = reinterpret_cast<uint32_t *>(scr);
     uint8_t *misc = scr + 288;
     const uint32_t *T = lds;
-    const int64_t npairs = (a.count + 1) >> 1;
+    const int64_t nunits = (a.count + kPpw - 1) / kPpw;  // kPpw packets per wave step
 
-    for (int64_t pw = (int64_t)blockIdx.x * (kThreads / 64) + wid; pw < npairs;
+    for (int64_t pw = (int64_t)blockIdx.x * (kThreads / 64) + wid; pw < nunits;
          pw += (int64_t)gridDim.x * (kThreads / 64)) {
-        const int64_t pk = 2 * pw + half;
+        const int64_t pk = kPpw * pw + sub;
         const bool have = pk < a.count;
         // (de_cook keeps its round-0 loads behind the length: loading up to the
         // cap here spills registers and measured slower)
@@ -362,7 +372,7 @@ __global__ __launch_bounds__(kThreads, 6) void k_decook(CookArgs a) {
         const bool ok = have && L >= 0 && L <= RSMI_COOK_MAX_LEN && round16(L) <= a.cap &&
                         ((uintptr_t)pkt & 3) == 0;
         const int ext = ok ? round16(L) : 0;
-        u32x4 cur[3];
+        u32x4 cur[kPpl];
         load_round(cur, pkt, 0, hl, ext);       // in flight while the tail is parsed
         // ---- de_obscure bounds (packet.cpp:93-100), read before any store ------
         int status = 0, ivl = 0, L1 = L;
@@ -376,9 +386,9 @@ __global__ __launch_bounds__(kThreads, 6) void k_decook(CookArgs a) {
             }
         }
         const uint32_t magic = ivl ? 0xFFFFFFFFu / (uint32_t)ivl : 0u;
-        const uint32_t s512 = ivl ? mod_ivl(512u, (uint32_t)ivl, magic) : 0u;
+        const uint32_t sstep = ivl ? mod_ivl(16u * kLpp, (uint32_t)ivl, magic) : 0u;
         if (ok && ivl) {
-            for (int t = hl; t < ivl + 20; t += 32) {
+            for (int t = hl; t < ivl + 20; t += kLpp) {
                 const int pos = L1 + t % ivl;
                 scr[t] = pkt[pos] ^ (a.ks ? a.ks[pos] : 0);
             }
@@ -405,8 +415,8 @@ __global__ __launch_bounds__(kThreads, 6) void k_decook(CookArgs a) {
             RoundCrc rc;
             uint32_t ivr = ivl ? mod_ivl((uint32_t)(r * kRound + 16 * hl), (uint32_t)ivl, magic) : 0u;
 #pragma unroll
-            for (int p = 0; p < 3; ++p) {
-                const int P = r * kRound + 16 * (32 * p + hl);
+            for (int p = 0; p < kPpl; ++p) {
+                const int P = r * kRound + 16 * (kLpp * p + hl);
                 u32x4 o = {0, 0, 0, 0};
                 if (P < ext) {
                     const u32x4 mk = ks_piece(a, P);
@@ -415,8 +425,8 @@ __global__ __launch_bounds__(kThreads, 6) void k_decook(CookArgs a) {
                     else o = cur[p] ^ (mk & piece_mask(L - P)) ^ (mi & piece_mask(L1 - P));
                     st_piece(pkt + P, o);
                 }
-                if (ck) rc.add(T, crc_in(o, P, Lc), 32 * p + hl, qr);
-                if (ivl) ivr = iv_step(ivr, s512, (uint32_t)ivl);
+                if (ck) rc.add(T, crc_in(o, P, Lc), kLpp * p + hl, qr);
+                if (ivl) ivr = iv_step(ivr, sstep, (uint32_t)ivl);
                 __builtin_amdgcn_sched_barrier(0);
             }
             if (ck) {
@@ -437,13 +447,13 @@ __global__ __launch_bounds__(kThreads, 6) void k_decook(CookArgs a) {
 }  // namespace
 
 size_t cook_lds_bytes(bool decook) {
-    return (size_t)kCookTabWords * 4 + (size_t)(kThreads / 32) * (decook ? kScrDecook : kScrCook);
+    return (size_t)kCookTabWords * 4 + (size_t)(kThreads / kLpp) * (decook ? kScrDecook : kScrCook);
 }
 
 hipError_t launch_cook(const CookArgs &a, bool decook, int max_blocks, hipStream_t s) {
     if (a.count <= 0) return hipSuccess;
-    const int64_t pairs = (a.count + 1) / 2;
-    int64_t blocks = (pairs + kThreads / 64 - 1) / (kThreads / 64);
+    const int64_t units = (a.count + kPpw - 1) / kPpw;
+    int64_t blocks = (units + kThreads / 64 - 1) / (kThreads / 64);
     if (blocks > max_blocks) blocks = max_blocks;
     const size_t lds = cook_lds_bytes(decook);
     if (decook)

@@ -76,12 +76,13 @@ struct CrcTables {
         for (int v = 0; v < 256; ++v) blob[v] = t0[v];
         for (int k = 1; k < 8; ++k)
             for (int v = 0; v < 256; ++v) blob[256 * k + v] = feed0(blob[256 * (k - 1) + v]);
-        for (int k = 0; k < 32; ++k) put_map(&blob[rsmi::kCookLane + 128 * k], 16 * k);
-        // Z_512 as four byte tables: Z(c) = B0[c & 255] ^ B1[c >> 8 & 255] ^ ...
+        for (int k = 0; k < rsmi::kCookLpp; ++k) put_map(&blob[rsmi::kCookLane + 128 * k], 16 * k);
+        // Z_{16 kCookLpp} (a lane's step to its next piece) as four byte tables:
+        // Z(c) = B0[c & 255] ^ B1[c >> 8 & 255] ^ ...
         uint32_t basis[32];
         for (int b = 0; b < 32; ++b) {
             uint32_t c = 1u << b;
-            for (int i = 0; i < 512; ++i) c = feed0(c);
+            for (int i = 0; i < 16 * rsmi::kCookLpp; ++i) c = feed0(c);
             basis[b] = c;
         }
         for (int t = 0; t < 4; ++t)
@@ -89,7 +90,7 @@ struct CrcTables {
                 uint32_t r = 0;
                 for (int b = 0; b < 8; ++b)
                     if (v >> b & 1) r ^= basis[8 * t + b];
-                blob[rsmi::kCookZ512 + 256 * t + v] = r;
+                blob[rsmi::kCookZH + 256 * t + v] = r;
             }
         for (int c = 1; c < 4; ++c) put_map(&blob[rsmi::kCookUns + 128 * (c - 1)], -c);
         for (int c = 1; c < 4; ++c) put_map(&blob[rsmi::kCookUns + 128 * (2 + c)], -4 * c);

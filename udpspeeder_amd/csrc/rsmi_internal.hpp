@@ -70,14 +70,20 @@ hipError_t launch_encode_bitslice_ragged(const rsmi_group *groups, const uint32_
 constexpr int kPtabDwords = 8;  // per coefficient: T0lo T0hi T1lo T1hi | T2 pad pad pad
 
 // ---- packet cook / de_cook (cook.hip, cook_host.cpp) -------------------------------
+// A packet is walked by kCookLpp lanes of a wave (16: four packets per wave,
+// or 32: two), each holding every kCookLpp-th 16-byte piece.
+#ifndef COOK_LPP
+#define COOK_LPP 16
+#endif
+constexpr int kCookLpp = COOK_LPP;
 // CRC table blob (u32 words), built on the host by cook_host.cpp:
 //   [0, 2048)        slicing-by-8 tables T_k[256], k = 0..7
-//   kCookLane + 128k nibble map of Z_{16k}, k = 0..31 (k = 0: identity)
-//   kCookZ512        byte map of Z_512 (4 tables of 256 words)
+//   kCookLane + 128k nibble map of Z_{16k}, k = 0..kCookLpp-1 (k = 0: identity)
+//   kCookZH          byte map of Z_{16 kCookLpp}, a lane's Horner step (4 x 256 words)
 //   kCookUns + 128i  nibble maps of Z_{-c}, c = 1..3, then Z_{-4c}, c = 1..3
 constexpr int kCookLane = 2048;
-constexpr int kCookZ512 = kCookLane + 32 * 128;
-constexpr int kCookUns = kCookZ512 + 1024;
+constexpr int kCookZH = kCookLane + kCookLpp * 128;
+constexpr int kCookUns = kCookZH + 1024;
 constexpr int kCookTabWords = kCookUns + 6 * 128;
 constexpr int kCookKsBytes = 65536 + 128;  // key stream covers every byte position used
 
