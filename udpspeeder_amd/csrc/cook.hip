@@ -42,6 +42,9 @@ constexpr int kPpl = 96 / kLpp;         // pieces per lane per round
 #ifndef COOK_OCC
 #define COOK_OCC (kLpp == 16 ? 5 : 6)   // waves per SIMD the register budget is cut for
 #endif
+#ifndef COOK_SB
+#define COOK_SB 1  // scheduling fence every COOK_SB pieces (0: none), bounds registers
+#endif
 constexpr int kThreads = kLpp == 16 ? 256 : 512;  // LDS (tables per block) bounds residency
 constexpr int kRound = 1536;            // 96 pieces per packet per round
 constexpr int kScrCook = 144;           // per-packet LDS: iv2[64] | overlay[64] | misc[16]
@@ -138,8 +141,37 @@ __device__ __forceinline__ uint64_t splitmix(uint64_t seed, uint64_t idx, uint64
     return z ^ (z >> 31);
 }
 
+// Word at byte offset o of table t (o a multiple of 4).
+__device__ __forceinline__ uint32_t at(const uint32_t *t, uint32_t o) {
+    return *reinterpret_cast<const uint32_t *>(reinterpret_cast<const uint8_t *>(t) + o);
+}
+
+#if COOK_NIB
+// Z_{16 kLpp} as eight nibble tables.
+__device__ __forceinline__ uint32_t zh(const uint32_t *T, uint32_t c) {
+    return nib_map(T + kCookZN, c);
+}
+
+// Raw CRC of one 16-byte piece: 32 nibble lookups, one level deep.
+__device__ __forceinline__ uint32_t crc16(const uint32_t *T, u32x4 v) {
+    const uint32_t *N = T + kCookNib;
+    uint32_t r[4];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+        const uint32_t lo = (v[d] << 2) & 0x3C3C3C3Cu, hi = (v[d] >> 2) & 0x3C3C3C3Cu;
+        const uint32_t *Nd = N + 128 * d;
+        uint32_t x = xor3(at(Nd, lo & 0xff), at(Nd + 16, hi & 0xff),
+                          at(Nd + 32, (lo >> 8) & 0xff));
+        x = xor3(x, at(Nd + 48, (hi >> 8) & 0xff), at(Nd + 64, (lo >> 16) & 0xff));
+        x = xor3(x, at(Nd + 80, (hi >> 16) & 0xff), at(Nd + 96, lo >> 24));
+        r[d] = x ^ at(Nd + 112, hi >> 24);
+    }
+    return xor3(r[0], r[1], r[2]) ^ r[3];
+}
+#else
 // Z_{16 kLpp} as four byte tables.
-__device__ __forceinline__ uint32_t zh(const uint32_t *B, uint32_t c) {
+__device__ __forceinline__ uint32_t zh(const uint32_t *T, uint32_t c) {
+    const uint32_t *B = T + kCookZH;
     return xor3(B[c & 0xff], B[256 + ((c >> 8) & 0xff)], B[512 + ((c >> 16) & 0xff)]) ^
            B[768 + (c >> 24)];
 }
@@ -148,6 +180,7 @@ __device__ __forceinline__ uint32_t zh(const uint32_t *B, uint32_t c) {
 __device__ __forceinline__ uint32_t crc16(const uint32_t *T, u32x4 v) {
     return slice8(T, slice8(T, 0u, v.x, v.y), v.z, v.w);
 }
+#endif
 
 // Remove z < 16 trailing zero bytes: Z_{-z} = Z_{-(z&3)} o Z_{-4(z>>2)}.
 __device__ __forceinline__ uint32_t unshift(const uint32_t *T, uint32_t c, uint32_t z) {
@@ -165,7 +198,7 @@ struct RoundCrc {
     uint32_t h = 0;
     int last = -1;
     __device__ __forceinline__ void add(const uint32_t *T, u32x4 v, int q, int qr) {
-        const uint32_t hn = zh(T + kCookZH, h) ^ crc16(T, v);
+        const uint32_t hn = zh(T, h) ^ crc16(T, v);
         h = q < qr ? hn : h;
         last = q < qr ? q : last;
     }
@@ -183,7 +216,7 @@ struct RoundCrc {
 __device__ __forceinline__ uint32_t shift_pieces(const uint32_t *T, uint32_t acc, int qr) {
 #pragma unroll
     for (int i = 0; i < kPpl; ++i) {
-        const uint32_t n = zh(T + kCookZH, acc);
+        const uint32_t n = zh(T, acc);
         acc = i < qr / kLpp ? n : acc;
     }
     return nib_map(T + kCookLane + 128 * (qr % kLpp), acc);
@@ -303,7 +336,8 @@ __global__ __launch_bounds__(kThreads, COOK_OCC) void k_cook(CookArgs a) {
                     Pt = P;
                 }
                 if (ivl) ivr = iv_step(ivr, sstep, (uint32_t)ivl);
-                __builtin_amdgcn_sched_barrier(0);  // one piece's lookups at a time
+                if (COOK_SB && p % COOK_SB == COOK_SB - 1)
+                    __builtin_amdgcn_sched_barrier(0);  // COOK_SB pieces' lookups at a time
             }
             if (ck) {
                 const uint32_t c = rc.finish(T, qr);
@@ -427,7 +461,7 @@ __global__ __launch_bounds__(kThreads, COOK_OCC) void k_decook(CookArgs a) {
                 }
                 if (ck) rc.add(T, crc_in(o, P, Lc), kLpp * p + hl, qr);
                 if (ivl) ivr = iv_step(ivr, sstep, (uint32_t)ivl);
-                __builtin_amdgcn_sched_barrier(0);
+                if (COOK_SB && p % COOK_SB == COOK_SB - 1) __builtin_amdgcn_sched_barrier(0);
             }
             if (ck) {
                 const uint32_t c = rc.finish(T, qr);

@@ -94,6 +94,15 @@ struct CrcTables {
             }
         for (int c = 1; c < 4; ++c) put_map(&blob[rsmi::kCookUns + 128 * (c - 1)], -c);
         for (int c = 1; c < 4; ++c) put_map(&blob[rsmi::kCookUns + 128 * (2 + c)], -4 * c);
+        // nibble i of a piece is the low (i even) or high nibble of byte i / 2
+        for (int i = 0; i < 32; ++i)
+            for (uint32_t v = 0; v < 16; ++v) {
+                uint32_t c = 0;
+                for (int j = 0; j < 16; ++j)
+                    c = feed0(c ^ (j == i / 2 ? (i & 1 ? v << 4 : v) : 0u));
+                blob[rsmi::kCookNib + 16 * i + v] = c;
+            }
+        put_map(&blob[rsmi::kCookZN], 16 * rsmi::kCookLpp);
     }
 };
 

@@ -81,10 +81,19 @@ constexpr int kCookLpp = COOK_LPP;
 //   kCookLane + 128k nibble map of Z_{16k}, k = 0..kCookLpp-1 (k = 0: identity)
 //   kCookZH          byte map of Z_{16 kCookLpp}, a lane's Horner step (4 x 256 words)
 //   kCookUns + 128i  nibble maps of Z_{-c}, c = 1..3, then Z_{-4c}, c = 1..3
+//   kCookNib + 16i   raw CRC of a 16-byte piece holding nibble i alone, i = 0..31
+//   kCookZN          nibble map of Z_{16 kCookLpp}
+// COOK_NIB selects the nibble forms for the per-piece work: 16-entry tables sit in
+// distinct LDS banks, so a wave's lookups into one never conflict.
+#ifndef COOK_NIB
+#define COOK_NIB 0
+#endif
 constexpr int kCookLane = 2048;
 constexpr int kCookZH = kCookLane + kCookLpp * 128;
 constexpr int kCookUns = kCookZH + 1024;
-constexpr int kCookTabWords = kCookUns + 6 * 128;
+constexpr int kCookNib = kCookUns + 6 * 128;
+constexpr int kCookZN = kCookNib + 512;
+constexpr int kCookTabWords = kCookZN + 128;
 constexpr int kCookKsBytes = 65536 + 128;  // key stream covers every byte position used
 
 struct CookArgs {
