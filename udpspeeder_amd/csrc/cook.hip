@@ -141,12 +141,12 @@ __device__ __forceinline__ uint64_t splitmix(uint64_t seed, uint64_t idx, uint64
     return z ^ (z >> 31);
 }
 
+#if COOK_NIB
 // Word at byte offset o of table t (o a multiple of 4).
 __device__ __forceinline__ uint32_t at(const uint32_t *t, uint32_t o) {
     return *reinterpret_cast<const uint32_t *>(reinterpret_cast<const uint8_t *>(t) + o);
 }
 
-#if COOK_NIB
 // Z_{16 kLpp} as eight nibble tables.
 __device__ __forceinline__ uint32_t zh(const uint32_t *T, uint32_t c) {
     return nib_map(T + kCookZN, c);

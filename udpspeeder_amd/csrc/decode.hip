@@ -14,8 +14,11 @@
 // Per wave:
 //   1. ballot the group's present flags -> sel[k], miss[e], status;
 //   2. issue the first RING survivor loads (they fly during step 3);
-//   3. Gauss-Jordan in the wave's LDS slice; expand every coefficient into its
-//      v_perm split tables (5 dwords, see kernels.hip) in LDS;
+//   3. Gauss-Jordan with column c of [A | M] in lane c (e bytes in registers,
+//      W = e + k <= 64; wider systems use the wave's LDS slice); multiplies by
+//      a wave-uniform factor go through that factor's v_perm split table;
+//      expand every coefficient into its split table (5 dwords, see
+//      kernels.hip) in LDS;
 //   4. stream: per survivor, 5 dwords per lane (one 1-KiB dwordx4 wave-load +
 //      one 256-B dword wave-load cover a 1280-B tile), GF multiply-accumulate
 //      into e row accumulators, prefetch survivor j+RING; store e rows.
@@ -31,15 +34,19 @@ constexpr int kWaves = 4;      // waves per block (one group each)
 #define DEC_RING 4
 #endif
 #ifndef DEC_LD_AUX
-#define DEC_LD_AUX 0           // cache policy of the survivor loads (2 = nt)
+#define DEC_LD_AUX 2           // cache policy of the survivor loads (2 = nt: -6 % decode time)
 #endif
 #ifndef DEC_ST_AUX
 #define DEC_ST_AUX 0           // cache policy of the rebuilt-row stores
 #endif
 constexpr int kRing = DEC_RING;  // survivors in flight per wave
+static_assert(kRing % 2 == 0, "ring slots are consumed in pairs under DEC_PAIR");
 constexpr int kRows = 10;      // max e handled by the fused kernel (emax <= kRows)
 constexpr int kPass = 5;       // rows accumulated per pass over the survivors
 constexpr int kTile = 1280;    // bytes per lane-tile pass (64 x 16 + 64 x 4)
+#ifndef DEC_PAIR
+#define DEC_PAIR 0             // fold survivors in pairs (fewer XORs, more VGPRs)
+#endif
 #ifndef DEC_OCC
 #define DEC_OCC 4              // waves per SIMD the register budget is cut for
 #endif
@@ -52,6 +59,14 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+constexpr int kRowsAt = 6144;  // smem: s01 | s2 | exp | log | inv | parity rows | wave slices
+
+// c * x for a byte x (upper bits zero), c given by its split table (t, t2)
+__device__ __forceinline__ uint32_t gmul_t(uint4 t, uint32_t t2, uint32_t x) {
+    return xor3(__builtin_amdgcn_perm(t.y, t.x, x & 7u), __builtin_amdgcn_perm(t.w, t.z, (x >> 3) & 7u),
+                __builtin_amdgcn_perm(t2, t2, x >> 6));
 }
 
 __device__ __forceinline__ uint32_t gmul(const uint8_t *lexp, const uint8_t *llog, uint32_t a,
@@ -78,13 +93,14 @@ __global__ __launch_bounds__(256, DEC_OCC) void k_decode_fused(UniformArgs a, co
     uint32_t *s2 = reinterpret_cast<uint32_t *>(smem + 4096);      // 256 x 4 B
     uint8_t *lexp = smem + 5120;                                   // 512
     uint8_t *llog = smem + 5632;                                   // 256
+    uint8_t *linv = smem + 5888;                                   // 256: x^-1
     const int k = a.k, n = a.n;
     const int wbytes = wave_lds_bytes(k);
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     const int rows_bytes = ((n - k) * k + 15) & ~15;
-    uint8_t *lrows = smem + 5888;  // the code's parity rows, (n-k) x k
-    uint8_t *wl = smem + 5888 + rows_bytes + wid * wbytes;
+    uint8_t *lrows = smem + kRowsAt;  // the code's parity rows, (n-k) x k
+    uint8_t *wl = smem + kRowsAt + rows_bytes + wid * wbytes;
     WaveLds L{wl, wl + 256, wl + 512,
               reinterpret_cast<uint32_t *>(wl + 512 + ((kRows * (kRows + k) + 15) & ~15))};
 
@@ -93,6 +109,8 @@ __global__ __launch_bounds__(256, DEC_OCC) void k_decode_fused(UniformArgs a, co
         s2[i] = ptab[i * kPtabDwords + 4];
     }
     for (int i = threadIdx.x; i < 768; i += blockDim.x) smem[5120 + i] = gftab[i];
+    for (int i = threadIdx.x; i < 256; i += blockDim.x)
+        linv[i] = i ? gftab[255 - gftab[512 + i]] : 0;  // exp[255 - log x]
     for (int i = threadIdx.x; i < (n - k) * k; i += blockDim.x) lrows[i] = prows[i];
     __syncthreads();
 
@@ -151,7 +169,8 @@ __global__ __launch_bounds__(256, DEC_OCC) void k_decode_fused(UniformArgs a, co
         const uint32_t ss = (uint32_t)a.shard_stride;
         // survivor j's shard offset lives in lane j (k <= 64 on this path):
         // v_readlane gives the scalar soffset without an LDS round trip
-        const uint32_t so_lane = (lane < k ? (uint32_t)L.sel[lane] : 0u) * ss;
+        const uint32_t sel_lane = lane < k ? (uint32_t)L.sel[lane] : 0u;
+        const uint32_t so_lane = sel_lane * ss;
         const uint32_t mo_lane = (lane < e ? (uint32_t)L.miss[lane] : 0u) * ss;
         typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
         u32x4 rq[kRing];
@@ -175,8 +194,61 @@ __global__ __launch_bounds__(256, DEC_OCC) void k_decode_fused(UniformArgs a, co
         };
         start_tile(0);  // the first survivors fly while the matrix is inverted
 
-        // ---- 3. Gauss-Jordan: aug = [A | M], e x (e+k) -------------------------
+        // ---- 3. Gauss-Jordan on [A | M], e x (e+k) ------------------------------
         const int W = e + k;
+        if (W <= 64) {
+            // lane c holds column c: a missing data index (c < e) or survivor c - e
+            const uint32_t col = lane < e ? (uint32_t)L.miss[lane]
+                                          : (lane < W ? (uint32_t)L.sel[lane - e] : 0u);
+            uint32_t a[kRows];
+#pragma unroll
+            for (int r = 0; r < kRows; ++r) {
+                a[r] = 0;
+                if (r < e) {
+                    const uint32_t R = __builtin_amdgcn_readlane(sel_lane, k - e + r);
+                    const uint8_t *prow = lrows + (R - k) * k;
+                    const uint32_t v = prow[col < (uint32_t)k ? col : 0u];
+                    a[r] = (lane >= e && col >= (uint32_t)k) ? (uint32_t)(col == R) : v;
+                }
+            }
+#pragma unroll
+            for (int p = 0; p < kRows; ++p) {
+                if (p < e) {
+                    const uint32_t piv = __builtin_amdgcn_readlane(a[p], p);
+                    if (piv == 0) {
+                        st = RSMI_DEC_SINGULAR;
+                        break;
+                    }
+                    const uint32_t ip = __builtin_amdgcn_readfirstlane(linv[piv]);
+                    a[p] = gmul_t(s01[ip], s2[ip], a[p]);
+#pragma unroll
+                    for (int r = 0; r < kRows; ++r) {
+                        if (r < e && r != p) {
+                            const uint32_t f = __builtin_amdgcn_readlane(a[r], p);
+                            a[r] ^= gmul_t(s01[f], s2[f], a[p]);
+                        }
+                        __builtin_amdgcn_sched_barrier(0);
+                    }
+                }
+            }
+            st = __builtin_amdgcn_readfirstlane(st);
+            if (st != RSMI_DEC_OK) {
+                if (lane == 0 && status_out) status_out[g] = st;
+                continue;
+            }
+            // coef[r][j] sits in lane e + j: expand into split tables tab[j][r]
+            if (lane >= e && lane < W) {
+                uint32_t *dst = L.tab + (lane - e) * kRows * 8;
+#pragma unroll
+                for (int r = 0; r < kRows; ++r) {
+                    if (r < e) {
+                        reinterpret_cast<uint4 *>(dst + r * 8)[0] = s01[a[r]];
+                        dst[r * 8 + 4] = s2[a[r]];
+                    }
+                }
+            }
+            wave_sync();
+        } else {
         for (int t = lane; t < e * W; t += 64) {
             const int r = t / W, c = t - r * W;
             const int R = L.sel[k - e + r];
@@ -226,8 +298,28 @@ __global__ __launch_bounds__(256, DEC_OCC) void k_decode_fused(UniformArgs a, co
             dst[4] = s2[c];
         }
         wave_sync();
+        }
 
         // ---- 4. stream the survivors: passes over (tile, block of kPass rows) --
+        // the 3-bit split selectors of a survivor's 5 dwords
+        auto split = [](const u32x4 &v, uint32_t d, uint32_t (&s0)[5], uint32_t (&s1)[5],
+                        uint32_t (&s2)[5]) {
+            const uint32_t x[5] = {v.x, v.y, v.z, v.w, d};
+#pragma unroll
+            for (int w = 0; w < 5; ++w) {
+                s0[w] = x[w] & 0x07070707u;
+                s1[w] = (x[w] >> 3) & 0x07070707u;
+                s2[w] = (x[w] >> 6) & 0x03030303u;
+            }
+        };
+        // ring slot q took survivor j: load survivor j + kRing into it
+        auto refill = [&](int q, int j) {
+            if (j + kRing < k) {
+                const uint32_t so = __builtin_amdgcn_readlane(so_lane, j + kRing);
+                rq[q] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, v16, so, DEC_LD_AUX);
+                rd[q] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, v4, so, DEC_LD_AUX);
+            }
+        };
         for (int toff = 0; toff < a.len; toff += kTile) {
             for (int rb = 0; rb < e; rb += kPass) {
                 if (toff || rb) start_tile(toff);  // pass 0's loads are already in flight
@@ -236,37 +328,53 @@ __global__ __launch_bounds__(256, DEC_OCC) void k_decode_fused(UniformArgs a, co
                 for (int r = 0; r < kPass; ++r)
 #pragma unroll
                     for (int w = 0; w < 5; ++w) acc[r][w] = 0;
+                // with DEC_PAIR, survivors go in pairs: the six split products of
+                // two survivors fold into a row with three 3-input XORs
                 for (int jb = 0; jb < k; jb += kRing) {
 #pragma unroll
-                    for (int q = 0; q < kRing; ++q) {
+                    for (int q = 0; q < kRing; q += DEC_PAIR ? 2 : 1) {
                         const int j = jb + q;
-                        if (j < k) {
-                            const uint32_t x[5] = {rq[q].x, rq[q].y, rq[q].z, rq[q].w, rd[q]};
-                            uint32_t q0[5], q1[5], q2[5];
-#pragma unroll
-                            for (int w = 0; w < 5; ++w) {
-                                q0[w] = x[w] & 0x07070707u;
-                                q1[w] = (x[w] >> 3) & 0x07070707u;
-                                q2[w] = (x[w] >> 6) & 0x03030303u;
-                            }
-                            if (j + kRing < k) {
-                                const uint32_t so = __builtin_amdgcn_readlane(so_lane, j + kRing);
-                                rq[q] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, v16, so, DEC_LD_AUX);
-                                rd[q] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, v4, so, DEC_LD_AUX);
-                            }
-                            const uint32_t *tj = L.tab + (j * kRows + rb) * 8;
+                        if (DEC_PAIR && j + 1 < k) {
+                            uint32_t a0[5], a1[5], a2[5], b0[5], b1[5], b2[5];
+                            split(rq[q], rd[q], a0, a1, a2);
+                            split(rq[q + 1], rd[q + 1], b0, b1, b2);
+                            refill(q, j);
+                            refill(q + 1, j + 1);
+                            const uint32_t *ta = L.tab + (j * kRows + rb) * 8;
+                            const uint32_t *tb = ta + kRows * 8;
 #pragma unroll
                             for (int r = 0; r < kPass; ++r) {
                                 if (rb + r < e) {
-                                    const uint4 t = reinterpret_cast<const uint4 *>(tj + r * 8)[0];
-                                    const uint32_t t2 = tj[r * 8 + 4];
+                                    const uint4 t = reinterpret_cast<const uint4 *>(ta + r * 8)[0];
+                                    const uint32_t t2 = ta[r * 8 + 4];
+                                    const uint4 u = reinterpret_cast<const uint4 *>(tb + r * 8)[0];
+                                    const uint32_t u2 = tb[r * 8 + 4];
 #pragma unroll
                                     for (int w = 0; w < 5; ++w) {
-                                        const uint32_t p0 = __builtin_amdgcn_perm(t.y, t.x, q0[w]);
-                                        const uint32_t p1 = __builtin_amdgcn_perm(t.w, t.z, q1[w]);
-                                        const uint32_t p2 = __builtin_amdgcn_perm(t2, t2, q2[w]);
-                                        acc[r][w] = acc[r][w] ^ xor3(p0, p1, p2);
+                                        uint32_t x = xor3(acc[r][w], __builtin_amdgcn_perm(t.y, t.x, a0[w]),
+                                                          __builtin_amdgcn_perm(t.w, t.z, a1[w]));
+                                        x = xor3(x, __builtin_amdgcn_perm(t2, t2, a2[w]),
+                                                 __builtin_amdgcn_perm(u.y, u.x, b0[w]));
+                                        acc[r][w] = xor3(x, __builtin_amdgcn_perm(u.w, u.z, b1[w]),
+                                                         __builtin_amdgcn_perm(u2, u2, b2[w]));
                                     }
+                                }
+                            }
+                        } else if (j < k) {
+                            uint32_t a0[5], a1[5], a2[5];
+                            split(rq[q], rd[q], a0, a1, a2);
+                            refill(q, j);
+                            const uint32_t *ta = L.tab + (j * kRows + rb) * 8;
+#pragma unroll
+                            for (int r = 0; r < kPass; ++r) {
+                                if (rb + r < e) {
+                                    const uint4 t = reinterpret_cast<const uint4 *>(ta + r * 8)[0];
+                                    const uint32_t t2 = ta[r * 8 + 4];
+#pragma unroll
+                                    for (int w = 0; w < 5; ++w)
+                                        acc[r][w] ^= xor3(__builtin_amdgcn_perm(t.y, t.x, a0[w]),
+                                                          __builtin_amdgcn_perm(t.w, t.z, a1[w]),
+                                                          __builtin_amdgcn_perm(t2, t2, a2[w]));
                                 }
                             }
                         }
@@ -294,14 +402,14 @@ bool decode_fused_ok(int k, int n, int64_t group_stride, int64_t shard_stride, i
     const int m = n - k;
     const int emax = k < m ? k : m;
     return emax <= kRows && k <= 64 && n * shard_stride < (int64_t(1) << 31) && len > 0 &&
-           5888 + ((m * k + 15) & ~15) + kWaves * wave_lds_bytes(k) <= 64 * 1024 &&
+           kRowsAt + ((m * k + 15) & ~15) + kWaves * wave_lds_bytes(k) <= 64 * 1024 &&
            group_stride >= n * shard_stride;
 }
 
 hipError_t launch_decode_fused(const UniformArgs &a, const uint8_t *present,
                                const uint8_t *parity_rows, int32_t *status,
                                const uint32_t *ptab, const uint8_t *gftab, hipStream_t s) {
-    const size_t lds = 5888 + (size_t)(((a.n - a.k) * a.k + 15) & ~15) +
+    const size_t lds = kRowsAt + (size_t)(((a.n - a.k) * a.k + 15) & ~15) +
                        (size_t)kWaves * wave_lds_bytes(a.k);
     int64_t blocks = (a.ngroups + kWaves - 1) / kWaves;
     const int64_t cap = 256 * 8;
