@@ -1,7 +1,7 @@
 // cook.hip -- batched packet cook / de_cook for gfx950.
 //
 // Semantics: packet.cpp do_cook (:303-308) and de_cook (:310-326), see
-// include/rsmi_cook.h.  kLpp lanes (16 by default, a quarter wave) own one
+// include/rsmi_cook.h.  kLpp lanes (8 by default, an eighth of a wave) own one
 // packet, so a wave works on 64/kLpp packets at once.  A packet is walked in
 // rounds of 96 16-byte pieces (1536 B); in a round lane l owns pieces l,
 // l+kLpp, l+2kLpp, ..., so every load and store instruction covers 16*kLpp
@@ -40,12 +40,12 @@ constexpr int kLpp = kCookLpp;          // lanes per packet
 constexpr int kPpw = 64 / kLpp;         // packets per wave
 constexpr int kPpl = 96 / kLpp;         // pieces per lane per round
 #ifndef COOK_OCC
-#define COOK_OCC (kLpp == 16 ? 5 : 6)   // waves per SIMD the register budget is cut for
+#define COOK_OCC (kLpp == 8 ? 4 : kLpp == 16 ? 5 : 6)  // waves per SIMD the register budget is cut for
 #endif
 #ifndef COOK_SB
 #define COOK_SB 1  // scheduling fence every COOK_SB pieces (0: none), bounds registers
 #endif
-constexpr int kThreads = kLpp == 16 ? 256 : 512;  // LDS (tables per block) bounds residency
+constexpr int kThreads = kLpp == 32 ? 512 : 256;  // LDS (tables per block) bounds residency
 constexpr int kRound = 1536;            // 96 pieces per packet per round
 constexpr int kScrCook = 144;           // per-packet LDS: iv2[64] | overlay[64] | misc[16]
 constexpr int kScrDecook = 304;         // iv2[288] (iv_len up to 255) | misc[16]
@@ -93,7 +93,7 @@ __device__ __forceinline__ uint32_t group_xor(uint32_t c) {
     c ^= (uint32_t)__builtin_amdgcn_ds_swizzle((int)c, 0x041F);
     c ^= (uint32_t)__builtin_amdgcn_ds_swizzle((int)c, 0x081F);
     c ^= (uint32_t)__builtin_amdgcn_ds_swizzle((int)c, 0x101F);
-    c ^= (uint32_t)__builtin_amdgcn_ds_swizzle((int)c, 0x201F);
+    if (kLpp >= 16) c ^= (uint32_t)__builtin_amdgcn_ds_swizzle((int)c, 0x201F);
     if (kLpp == 32) c ^= (uint32_t)__builtin_amdgcn_ds_swizzle((int)c, 0x401F);
     return c;
 }
@@ -302,15 +302,20 @@ __global__ __launch_bounds__(kThreads, COOK_OCC) void k_cook(CookArgs a) {
         const bool ok = have && L >= 0 && L <= RSMI_COOK_MAX_LEN && ivl <= RSMI_COOK_IV_MAX &&
                         round16(out) <= a.cap && ((uintptr_t)pkt & 3) == 0;
         const int ext = ok ? round16(out) : 0;
+        const uint32_t magic = ivl ? 0xFFFFFFFFu / (uint32_t)ivl : 0u;
+        if (ok && ivl && !a.iv && 8 * hl < ivl) {  // device-drawn IV: 8 bytes per draw, one per lane
+            const uint64_t z = splitmix(a.seed, (uint64_t)pk, 1 + (uint64_t)hl);
+            reinterpret_cast<uint32_t *>(ovl)[2 * hl] = (uint32_t)z;
+            reinterpret_cast<uint32_t *>(ovl)[2 * hl + 1] = (uint32_t)(z >> 32);
+        }
+        wave_sync();
         if (ok && ivl) {  // iv repeated: iv2[t] = iv[t % ivl], t < ivl + 20 (<= 52)
             for (int t = hl; t < ivl + 20; t += kLpp) {
-                const int j = t % ivl;
-                scr[t] = a.iv ? a.iv[pk * RSMI_COOK_IV_MAX + j]
-                              : (uint8_t)(splitmix(a.seed, (uint64_t)pk, 1 + (j >> 3)) >> (8 * (j & 7)));
+                const uint32_t j = mod_ivl((uint32_t)t, (uint32_t)ivl, magic);
+                scr[t] = a.iv ? a.iv[pk * RSMI_COOK_IV_MAX + j] : ovl[j];
             }
         }
         wave_sync();
-        const uint32_t magic = ivl ? 0xFFFFFFFFu / (uint32_t)ivl : 0u;
         const uint32_t sstep = ivl ? mod_ivl(16u * kLpp, (uint32_t)ivl, magic) : 0u;
         const int Q = (L + 15) >> 4;            // pieces holding payload (crc input)
         const int P0 = L & ~15;                 // first piece that holds tail bytes
@@ -423,7 +428,7 @@ __global__ __launch_bounds__(kThreads, COOK_OCC) void k_decook(CookArgs a) {
         const uint32_t sstep = ivl ? mod_ivl(16u * kLpp, (uint32_t)ivl, magic) : 0u;
         if (ok && ivl) {
             for (int t = hl; t < ivl + 20; t += kLpp) {
-                const int pos = L1 + t % ivl;
+                const int pos = L1 + (int)mod_ivl((uint32_t)t, (uint32_t)ivl, magic);
                 scr[t] = pkt[pos] ^ (a.ks ? a.ks[pos] : 0);
             }
         }

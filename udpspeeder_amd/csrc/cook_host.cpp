@@ -94,6 +94,7 @@ struct CrcTables {
             }
         for (int c = 1; c < 4; ++c) put_map(&blob[rsmi::kCookUns + 128 * (c - 1)], -c);
         for (int c = 1; c < 4; ++c) put_map(&blob[rsmi::kCookUns + 128 * (2 + c)], -4 * c);
+        if (!COOK_NIB) return;
         // nibble i of a piece is the low (i even) or high nibble of byte i / 2
         for (int i = 0; i < 32; ++i)
             for (uint32_t v = 0; v < 16; ++v) {

@@ -70,10 +70,10 @@ hipError_t launch_encode_bitslice_ragged(const rsmi_group *groups, const uint32_
 constexpr int kPtabDwords = 8;  // per coefficient: T0lo T0hi T1lo T1hi | T2 pad pad pad
 
 // ---- packet cook / de_cook (cook.hip, cook_host.cpp) -------------------------------
-// A packet is walked by kCookLpp lanes of a wave (16: four packets per wave,
-// or 32: two), each holding every kCookLpp-th 16-byte piece.
+// A packet is walked by kCookLpp lanes of a wave (8: eight packets per wave;
+// 16: four; 32: two), each holding every kCookLpp-th 16-byte piece.
 #ifndef COOK_LPP
-#define COOK_LPP 16
+#define COOK_LPP 8
 #endif
 constexpr int kCookLpp = COOK_LPP;
 // CRC table blob (u32 words), built on the host by cook_host.cpp:
@@ -93,7 +93,7 @@ constexpr int kCookZH = kCookLane + kCookLpp * 128;
 constexpr int kCookUns = kCookZH + 1024;
 constexpr int kCookNib = kCookUns + 6 * 128;
 constexpr int kCookZN = kCookNib + 512;
-constexpr int kCookTabWords = kCookZN + 128;
+constexpr int kCookTabWords = COOK_NIB ? kCookZN + 128 : kCookNib;
 constexpr int kCookKsBytes = 65536 + 128;  // key stream covers every byte position used
 
 struct CookArgs {
