@@ -438,7 +438,10 @@ class DecodeManager:
             data = [bufs[out[i]] for i in range(k)]
             lens_i = [int.from_bytes(d[:2], "big") for d in data]
             if all(l <= MAX_DATA_LEN for l in lens_i):
-                self.ready = [data[i][2:2 + lens_i[i]] for i in missed]
+                # a malformed row can claim more bytes than it holds: the reference
+                # then reads past the row into stale ring-buffer memory
+                # (fec_manager.cpp:715-717); here those bytes are zero (documented)
+                self.ready = [data[i][2:2 + lens_i[i]].ljust(lens_i[i], b"\0") for i in missed]
             self.ar.set_invalid(seq, self.now)
 
     def output(self) -> List[bytes]:

@@ -192,6 +192,23 @@ def test_gpu_decoder_matches_oracle_long(gpu, mode, rs):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("threads", [1, 7])
+@pytest.mark.parametrize("mode", [0, 1])
+def test_gpu_decoder_threaded_outputs(gpu, monkeypatch, mode, threads):
+    """Output resolution split over 7 threads (every batch, however small) keeps
+    the reference's output order and bytes."""
+    import torch
+    monkeypatch.setenv("RSMI_FDEC_PAR_MIN", "1")
+    monkeypatch.setenv("RSMI_HOST_THREADS", str(threads))
+    chan = _long_run(mode, "1:3,2:4,10:6,20:10", 91 + mode)
+    ret, out, ev = _oracle_run(chan)
+    g_ret, g_out = _gpu_run(chan, _cuts(len(chan), 5, 4), torch)
+    assert g_ret == ret
+    assert [e for _, e in g_out] == ev
+    assert [b for b, _ in g_out] == out
+
+
+@pytest.mark.gpu
 def test_gpu_per_call_interface(gpu):
     """input()/output() one packet at a time (misc.cpp:409-425's loop)."""
     from udpspeeder_amd.fec import FecDecoder

@@ -20,6 +20,7 @@
 #include <new>
 #include <string>
 #include <unordered_map>
+#include <thread>
 #include <vector>
 
 #include "rsmi_internal.hpp"
@@ -147,6 +148,26 @@ int host_grow(uint8_t **p, size_t *cap, size_t need) {
 
 }  // namespace
 
+struct Spill {
+    std::vector<std::pair<std::unique_ptr<uint8_t[]>, size_t>> chunks;
+    size_t chunk = 0, used = 0;
+    void reset() { chunk = used = 0; }
+    uint8_t *alloc(size_t n) {
+        while (chunk < chunks.size() && used + n > chunks[chunk].second) {
+            ++chunk;
+            used = 0;
+        }
+        if (chunk == chunks.size()) {
+            const size_t c = std::max<size_t>(n, size_t(16) << 20);
+            chunks.emplace_back(std::unique_ptr<uint8_t[]>(new uint8_t[c]), c);
+            used = 0;
+        }
+        uint8_t *p = chunks[chunk].first.get() + used;
+        used += n;
+        return p;
+    }
+};
+
 struct rsmi_fdec {
     int buff_num = 2000;
     AntiReplay ar;
@@ -164,24 +185,10 @@ struct rsmi_fdec {
     std::vector<uint8_t> present;  // all buckets' present flags
     std::vector<RowRef> rows;      // k per job
     std::vector<std::pair<int64_t, int>> d2h_rows;  // (job, row) copied back, in d2h order
-    // outputs that straddle two rows, copied into bump-allocated chunks that are
-    // kept from batch to batch (fresh pages would cost a fault per 4 KiB)
-    std::vector<std::pair<std::unique_ptr<uint8_t[]>, size_t>> spill;
-    size_t spill_chunk = 0, spill_used = 0;
-    uint8_t *spill_alloc(size_t n) {
-        while (spill_chunk < spill.size() && spill_used + n > spill[spill_chunk].second) {
-            ++spill_chunk;
-            spill_used = 0;
-        }
-        if (spill_chunk == spill.size()) {
-            const size_t c = std::max<size_t>(n, size_t(64) << 20);
-            spill.emplace_back(std::unique_ptr<uint8_t[]>(new uint8_t[c]), c);
-            spill_used = 0;
-        }
-        uint8_t *p = spill[spill_chunk].first.get() + spill_used;
-        spill_used += n;
-        return p;
-    }
+    // outputs that straddle two rows are copied into bump-allocated chunks, one
+    // arena per resolver thread, kept from batch to batch (fresh pages would cost
+    // a fault per 4 KiB)
+    std::vector<Spill> spills = std::vector<Spill>(1);
     int64_t staging_bytes = 0, d2h_bytes = 0;
     const uint8_t *host_base = nullptr;
     bool planned = false, ran = false, resolved = false, plan_only = false;
@@ -371,6 +378,89 @@ int input_packet(rsmi_fdec *D, const uint8_t *s, int len, uint64_t dsrc, int32_t
     return 0;
 }
 
+// Output records of outs[b, e) (fec_manager.cpp:97-129 and :713-755), read from
+// the rows the host holds and the rows copied back; records that straddle two
+// rows are copied into sp.
+void resolve_outputs(const rsmi_fdec *D, size_t b, size_t e, Spill &sp, std::vector<Out> &res) {
+    for (size_t oi = b; oi < e; ++oi) {
+        const Out &o = D->outs[oi];
+        if (o.job < 0) {
+            res.push_back(o);
+            continue;
+        }
+        const Job &J = D->jobs[(size_t)o.job];
+        const RowRef *rr = D->rows.data() + J.rows0;
+        auto row = [&](int i) -> const uint8_t * {
+            return rr[i].host ? rr[i].host : D->hblob + rr[i].d2h;
+        };
+        const int64_t L = J.len;
+        const int64_t cur = (int64_t)J.k * L;  // the blob: the k data rows back to back
+        // n bytes of the blob at pos: a pointer into one row, or a spilled copy
+        auto span = [&](int64_t pos, int64_t n) -> const uint8_t * {
+            const int64_t r = pos / L, o0 = pos - r * L;
+            if (o0 + n <= L) return row((int)r) + o0;
+            uint8_t *buf = sp.alloc((size_t)n);
+            for (int64_t c = 0; c < n;) {
+                const int64_t rr2 = (pos + c) / L, oo = pos + c - rr2 * L;
+                const int64_t t = std::min(n - c, L - oo);
+                std::memcpy(buf + c, row((int)rr2) + oo, (size_t)t);
+                c += t;
+            }
+            return buf;
+        };
+        if (J.type == 0) {  // blob_decode_t::output (fec_manager.cpp:97-129)
+            if (cur < 4) continue;
+            const uint32_t cnt = rd_u32(span(0, 4));
+            if (cnt > (uint32_t)kMaxBlobPackets) continue;
+            int64_t pos = 4;
+            const size_t mark = res.size();
+            bool ok = true;
+            for (uint32_t i = 0; i < cnt; ++i) {
+                if (pos + 2 > cur) { ok = false; break; }
+                const int l = (int)rd_u16(span(pos, 2));
+                pos += 2;
+                if (pos + l > cur) { ok = false; break; }
+                res.push_back(Out{o.event, o.job, l ? span(pos, l) : row(0), l});
+                pos += l;
+            }
+            if (!ok) res.resize(mark);
+        } else {  // mode 1 (:713-755): every data row's u16 <= max_data_len, then the missed rows
+            bool ok = true;
+            for (int i = 0; i < J.k; ++i)
+                if ((int)rd_u16(row(i)) > kMaxDataLen) ok = false;
+            if (!ok) continue;
+            // missed = rows not received + the packet that completed the group
+            const Bucket &B = D->buckets[(size_t)J.bucket];
+            const uint8_t *pres = D->present.data() + B.present_off + J.row * B.n;
+            for (int i = 0; i < J.k; ++i) {
+                if (pres[i] && i != J.inner) continue;
+                const int64_t l = rd_u16(row(i));
+                if (l + 2 <= L) {
+                    res.push_back(Out{o.event, o.job, row(i) + 2, (int32_t)l});
+                } else {  // a malformed row claims more than it holds: the reference reads
+                          // stale ring-buffer bytes past it (:715-717); zeros here
+                    uint8_t *buf = sp.alloc((size_t)l);
+                    std::memcpy(buf, row(i) + 2, (size_t)(L - 2));
+                    std::memset(buf + (L - 2), 0, (size_t)(l - (L - 2)));
+                    res.push_back(Out{o.event, o.job, buf, (int32_t)l});
+                }
+            }
+        }
+    }
+}
+
+int env_int(const char *name, int dflt) {
+    const char *v = std::getenv(name);
+    return v && *v ? std::atoi(v) : dflt;
+}
+
+// resolver threads: RSMI_HOST_THREADS, else the hardware's, at most 16
+int host_threads() {
+    int t = env_int("RSMI_HOST_THREADS", 0);
+    if (t <= 0) t = std::min<int>(16, (int)std::max(1u, std::thread::hardware_concurrency()));
+    return t;
+}
+
 }  // namespace
 
 extern "C" {
@@ -417,7 +507,7 @@ int rsmi_fdec_plan(rsmi_fdec *D, int64_t n, const int32_t *len, const uint64_t *
     D->present.clear();
     D->rows.clear();
     D->d2h_rows.clear();
-    D->spill_chunk = D->spill_used = 0;  // the chunks are reused
+    for (Spill &sp : D->spills) sp.reset();  // the chunks are reused
     D->staging_bytes = D->d2h_bytes = 0;
     D->host_base = host_base;
     for (int64_t i = 0; i < n; ++i) {
@@ -552,62 +642,27 @@ int rsmi_fdec_outputs(rsmi_fdec *D, int64_t *n_out) {
         if (any_job && !D->ran) return fail(RSMI_ERR_INVALID, "rsmi_fdec_outputs before rsmi_fdec_run_dev");
         int rc = wait_idle(D);
         if (rc) return rc;
+        const size_t N = D->outs.size();
+        int T = N >= (size_t)env_int("RSMI_FDEC_PAR_MIN", 4096) ? host_threads() : 1;
+        if (T > (int)N) T = N ? (int)N : 1;
+        if ((int)D->spills.size() < T) D->spills.resize((size_t)T);
         std::vector<Out> res;
-        res.reserve(D->outs.size() * 2);
-        for (const Out &o : D->outs) {
-            if (o.job < 0) {
-                res.push_back(o);
-                continue;
-            }
-            const Job &J = D->jobs[(size_t)o.job];
-            const RowRef *rr = D->rows.data() + J.rows0;
-            auto row = [&](int i) -> const uint8_t * {
-                return rr[i].host ? rr[i].host : D->hblob + rr[i].d2h;
-            };
-            const int64_t L = J.len;
-            const int64_t cur = (int64_t)J.k * L;  // the blob: the k data rows back to back
-            // n bytes of the blob at pos: a pointer into one row, or a spilled copy
-            auto span = [&](int64_t pos, int64_t n) -> const uint8_t * {
-                const int64_t r = pos / L, o0 = pos - r * L;
-                if (o0 + n <= L) return row((int)r) + o0;
-                uint8_t *buf = D->spill_alloc((size_t)n);
-                for (int64_t c = 0; c < n;) {
-                    const int64_t rr2 = (pos + c) / L, oo = pos + c - rr2 * L;
-                    const int64_t t = std::min(n - c, L - oo);
-                    std::memcpy(buf + c, row((int)rr2) + oo, (size_t)t);
-                    c += t;
-                }
-                return buf;
-            };
-            if (J.type == 0) {  // blob_decode_t::output (fec_manager.cpp:97-129)
-                if (cur < 4) continue;
-                const uint32_t cnt = rd_u32(span(0, 4));
-                if (cnt > (uint32_t)kMaxBlobPackets) continue;
-                int64_t pos = 4;
-                const size_t mark = res.size();
-                bool ok = true;
-                for (uint32_t i = 0; i < cnt; ++i) {
-                    if (pos + 2 > cur) { ok = false; break; }
-                    const int l = (int)rd_u16(span(pos, 2));
-                    pos += 2;
-                    if (pos + l > cur) { ok = false; break; }
-                    res.push_back(Out{o.event, o.job, l ? span(pos, l) : row(0), l});
-                    pos += l;
-                }
-                if (!ok) res.resize(mark);
-            } else {  // mode 1 (:713-755): every data row's u16 <= max_data_len, then the missed rows
-                bool ok = true;
-                for (int i = 0; i < J.k; ++i)
-                    if ((int)rd_u16(row(i)) > kMaxDataLen) ok = false;
-                if (!ok) continue;
-                // missed = rows not received + the packet that completed the group
-                const Bucket &B = D->buckets[(size_t)J.bucket];
-                const uint8_t *pres = D->present.data() + B.present_off + J.row * B.n;
-                for (int i = 0; i < J.k; ++i) {
-                    if (pres[i] && i != J.inner) continue;
-                    res.push_back(Out{o.event, o.job, row(i) + 2, (int32_t)rd_u16(row(i))});
-                }
-            }
+        if (T == 1) {
+            res.reserve(N * 2);
+            resolve_outputs(D, 0, N, D->spills[0], res);
+        } else {  // groups resolve independently: T contiguous ranges, joined in order
+            std::vector<std::vector<Out>> part((size_t)T);
+            std::vector<std::thread> th;
+            for (int t = 1; t < T; ++t)
+                th.emplace_back([D, N, T, t, &part] {
+                    resolve_outputs(D, N * t / T, N * (t + 1) / T, D->spills[(size_t)t], part[(size_t)t]);
+                });
+            resolve_outputs(D, 0, N / T, D->spills[0], part[0]);
+            for (std::thread &x : th) x.join();
+            size_t tot = 0;
+            for (auto &v : part) tot += v.size();
+            res.reserve(tot);
+            for (auto &v : part) res.insert(res.end(), v.begin(), v.end());
         }
         D->outs.swap(res);
         D->resolved = true;
