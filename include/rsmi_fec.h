@@ -142,7 +142,10 @@ int rsmi_fenc_run_dev(rsmi_fenc *enc, uint8_t *slots_base, int64_t slot_stride, 
  * Differences from the reference: a group whose shard indices include one
  * >= k + m makes the reference abort (assert on rs_decode2, :632 and :710);
  * here that group is dropped like a failed decode (no output, anti-replay
- * marked).  Nothing else differs. */
+ * marked).  A malformed mode-1 row whose u16 length exceeds the row makes the
+ * reference return bytes past the row from its ring buffer's stale contents
+ * (:715-717); the output has the same length here with those bytes zero.
+ * Nothing else differs. */
 typedef struct rsmi_fdec rsmi_fdec;
 
 /* buff_num: fec_buff_num (fec_manager.cpp:33), 0 for the default 2000. */
