@@ -7,6 +7,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -67,6 +68,11 @@ struct Device {
     size_t hdev_bytes = 0;
     int32_t *hstatus_dev = nullptr;
     size_t hstatus_cap = 0;
+    // cross-stream ordering of the codec's kernels (StreamOrder below)
+    std::mutex omu;
+    hipEvent_t oev = nullptr;
+    hipStream_t olast = nullptr;
+    bool oany = false;
 };
 
 std::mutex g_devs_mu;
@@ -138,6 +144,45 @@ int ensure_code(Device &D, int k, int n, const Code **out) {
     *out = &it->second;
     return RSMI_OK;
 }
+
+// The codec's launches on different streams run one after another: a launch
+// on stream s waits for the previous codec launch when that was on another
+// stream.  Each kernel fills the chip and is HBM-bound, so running two at once
+// gains nothing ("Two streams").  RSMI_STREAM_ORDER=0 turns this
+// off; streams being captured are left alone (graph edges order them).
+struct StreamOrder {
+    Device *D;
+    hipStream_t s;
+    bool on;
+    StreamOrder(Device *d, hipStream_t st) : D(d), s(st), on(enabled()) {
+        if (!on) return;
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) {
+            on = false;
+            return;
+        }
+        D->omu.lock();
+        if (D->oany && D->olast != s) (void)hipStreamWaitEvent(s, D->oev, 0);
+    }
+    ~StreamOrder() {
+        if (!on) return;
+        if (!D->oev) (void)hipEventCreateWithFlags(&D->oev, hipEventDisableTiming);
+        if (D->oev && hipEventRecord(D->oev, s) == hipSuccess) {
+            D->olast = s;
+            D->oany = true;
+        }
+        D->omu.unlock();
+    }
+    StreamOrder(const StreamOrder &) = delete;
+    StreamOrder &operator=(const StreamOrder &) = delete;
+    static bool enabled() {
+        static const bool e = [] {
+            const char *v = std::getenv("RSMI_STREAM_ORDER");
+            return !(v && v[0] == '0');
+        }();
+        return e;
+    }
+};
 
 // caller holds D.mu
 int ensure_ws(Device &D, hipStream_t s, size_t bytes, uint8_t **out) {
@@ -214,6 +259,7 @@ int encode_dev(int k, int n, uint8_t *base, int64_t gs, int64_t ss, int len, int
     if (n == k || len == 0 || ngroups == 0) return RSMI_OK;
     int W;
     UniformArgs a = make_args(k, n, base, gs, ss, len, ngroups, &W);
+    StreamOrder order(D, s);
     hipError_t e = hipErrorNotSupported;
     if (g_opt_bitslice.load() && has_bitslice(k, n)) e = launch_encode_bitslice(a, s);
     if (e == hipErrorNotSupported) e = launch_encode_generic(a, W, C->dev_rows, D->ptab, s);
@@ -243,6 +289,7 @@ int decode_dev(int k, int n, uint8_t *base, int64_t gs, int64_t ss, int len, int
     if (ngroups == 0) return RSMI_OK;
     int W;
     UniformArgs a = make_args(k, n, base, gs, ss, len, ngroups, &W);
+    StreamOrder order(D, s);
     if (fused) {
         hipError_t e = launch_decode_fused(a, present, C->dev_rows, status, D->ptab, D->gftab, s);
         if (e != hipSuccess) return hip_fail(e, "fused decode launch");
@@ -287,6 +334,7 @@ int encode_ragged_dev(const rsmi_group *dg, int64_t ngroups, uint8_t *base, hipS
     int rc;
     Device *D = current(&rc);
     if (!D) return rc;
+    StreamOrder order(D, s);
     hipError_t e = launch_encode_ragged(dg, ngroups, base, D->code_dir, D->ptab, s);
     if (e != hipSuccess) return hip_fail(e, "ragged encode launch");
     return RSMI_OK;

@@ -25,6 +25,9 @@
 #ifndef BS_PERSIST
 #define BS_PERSIST 0  // 1: balanced persistent grid (measured 5 % slower than one wave per chunk)
 #endif
+#ifndef BS_FENCE
+#define BS_FENCE 0  // agent-scope release at the end of every wave
+#endif
 #ifndef BS_LD_AUX
 #define BS_LD_AUX 2  // cache-policy bits of the streaming loads (2 = nt: read once)
 #endif
@@ -101,6 +104,7 @@ __device__ __forceinline__ DevIO make_io(const UniformArgs &a, uint32_t cols, ui
             DevIO io = make_io(a, cols, P, wave);                                         \
             bs_code_##K##_##N(io);                                                        \
         }                                                                                 \
+        if (BS_FENCE) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");                  \
     }
 BS_FOR_EACH_CODE(BS_KERNEL)
 #undef BS_KERNEL

@@ -48,6 +48,9 @@ constexpr int kTile = 1280;    // bytes per lane-tile pass (64 x 16 + 64 x 4)
 #ifndef DEC_PAIR
 #define DEC_PAIR 0             // fold survivors in pairs (fewer XORs, more VGPRs)
 #endif
+#ifndef DEC_FENCE
+#define DEC_FENCE 0            // agent-scope release at the end of every wave
+#endif
 #ifndef DEC_OCC
 #define DEC_OCC 4              // waves per SIMD the register budget is cut for
 #endif
@@ -395,6 +398,9 @@ __global__ __launch_bounds__(256, DEC_OCC) void k_decode_fused(UniformArgs a, co
         if (lane == 0 && status_out) status_out[g] = RSMI_DEC_OK;
         wave_sync();  // the LDS slice is rewritten by the next group
     }
+#if DEC_FENCE
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+#endif
 }
 
 }  // namespace
