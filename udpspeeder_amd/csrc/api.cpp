@@ -591,6 +591,16 @@ int decode_pinned(int k, int n, uint8_t *hs, int64_t hgs, int64_t ss, int len, i
 
 const char *last_error() { return g_err.c_str(); }
 std::atomic<int> &opt_bitslice() { return g_opt_bitslice; }
+
+// StreamOrder for launches outside this file (cook): run f between the wait
+// and the record.
+hipError_t ordered_launch(hipStream_t s, hipError_t (*f)(void *), void *arg) {
+    int rc;
+    Device *D = current(&rc);
+    if (!D) return f(arg);
+    StreamOrder order(D, s);
+    return f(arg);
+}
 void set_error(const std::string &m) { g_err = m; }
 
 }  // namespace rsmi
