@@ -34,7 +34,8 @@ constexpr int kWaves = 4;      // waves per block (one group each)
 #define DEC_RING 4
 #endif
 #ifndef DEC_LD_AUX
-#define DEC_LD_AUX 2           // cache policy of the survivor loads (2 = nt: 9 % faster)
+#define DEC_LD_AUX 0           // cache policy of the survivor loads (2 = nt: 9 % faster alone,
+                               // but the next encode is 1.5 % slower: no gain in bench.py)
 #endif
 #ifndef DEC_ST_AUX
 #define DEC_ST_AUX 0           // cache policy of the rebuilt-row stores
