@@ -68,11 +68,6 @@ struct Device {
     size_t hdev_bytes = 0;
     int32_t *hstatus_dev = nullptr;
     size_t hstatus_cap = 0;
-    // cross-stream ordering of the codec's kernels (StreamOrder below)
-    std::mutex omu;
-    hipEvent_t oev = nullptr;
-    hipStream_t olast = nullptr;
-    bool oany = false;
 };
 
 std::mutex g_devs_mu;
@@ -144,45 +139,6 @@ int ensure_code(Device &D, int k, int n, const Code **out) {
     *out = &it->second;
     return RSMI_OK;
 }
-
-// The codec's launches on different streams run one after another: a launch
-// on stream s waits for the previous codec launch when that was on another
-// stream.  Each kernel fills the chip and is HBM-bound, so running two at once
-// gains nothing ("Two streams").  RSMI_STREAM_ORDER=0 turns this
-// off; streams being captured are left alone (graph edges order them).
-struct StreamOrder {
-    Device *D;
-    hipStream_t s;
-    bool on;
-    StreamOrder(Device *d, hipStream_t st) : D(d), s(st), on(enabled()) {
-        if (!on) return;
-        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-        if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) {
-            on = false;
-            return;
-        }
-        D->omu.lock();
-        if (D->oany && D->olast != s) (void)hipStreamWaitEvent(s, D->oev, 0);
-    }
-    ~StreamOrder() {
-        if (!on) return;
-        if (!D->oev) (void)hipEventCreateWithFlags(&D->oev, hipEventDisableTiming);
-        if (D->oev && hipEventRecord(D->oev, s) == hipSuccess) {
-            D->olast = s;
-            D->oany = true;
-        }
-        D->omu.unlock();
-    }
-    StreamOrder(const StreamOrder &) = delete;
-    StreamOrder &operator=(const StreamOrder &) = delete;
-    static bool enabled() {
-        static const bool e = [] {
-            const char *v = std::getenv("RSMI_STREAM_ORDER");
-            return !(v && v[0] == '0');
-        }();
-        return e;
-    }
-};
 
 // caller holds D.mu
 int ensure_ws(Device &D, hipStream_t s, size_t bytes, uint8_t **out) {
@@ -259,7 +215,6 @@ int encode_dev(int k, int n, uint8_t *base, int64_t gs, int64_t ss, int len, int
     if (n == k || len == 0 || ngroups == 0) return RSMI_OK;
     int W;
     UniformArgs a = make_args(k, n, base, gs, ss, len, ngroups, &W);
-    StreamOrder order(D, s);
     hipError_t e = hipErrorNotSupported;
     if (g_opt_bitslice.load() && has_bitslice(k, n)) e = launch_encode_bitslice(a, s);
     if (e == hipErrorNotSupported) e = launch_encode_generic(a, W, C->dev_rows, D->ptab, s);
@@ -289,7 +244,6 @@ int decode_dev(int k, int n, uint8_t *base, int64_t gs, int64_t ss, int len, int
     if (ngroups == 0) return RSMI_OK;
     int W;
     UniformArgs a = make_args(k, n, base, gs, ss, len, ngroups, &W);
-    StreamOrder order(D, s);
     if (fused) {
         hipError_t e = launch_decode_fused(a, present, C->dev_rows, status, D->ptab, D->gftab, s);
         if (e != hipSuccess) return hip_fail(e, "fused decode launch");
@@ -334,7 +288,6 @@ int encode_ragged_dev(const rsmi_group *dg, int64_t ngroups, uint8_t *base, hipS
     int rc;
     Device *D = current(&rc);
     if (!D) return rc;
-    StreamOrder order(D, s);
     hipError_t e = launch_encode_ragged(dg, ngroups, base, D->code_dir, D->ptab, s);
     if (e != hipSuccess) return hip_fail(e, "ragged encode launch");
     return RSMI_OK;
@@ -592,15 +545,6 @@ int decode_pinned(int k, int n, uint8_t *hs, int64_t hgs, int64_t ss, int len, i
 const char *last_error() { return g_err.c_str(); }
 std::atomic<int> &opt_bitslice() { return g_opt_bitslice; }
 
-// StreamOrder for launches outside this file (cook): run f between the wait
-// and the record.
-hipError_t ordered_launch(hipStream_t s, hipError_t (*f)(void *), void *arg) {
-    int rc;
-    Device *D = current(&rc);
-    if (!D) return f(arg);
-    StreamOrder order(D, s);
-    return f(arg);
-}
 void set_error(const std::string &m) { g_err = m; }
 
 }  // namespace rsmi

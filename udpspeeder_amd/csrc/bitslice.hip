@@ -34,6 +34,10 @@
 #ifndef BS_ST_AUX
 #define BS_ST_AUX 2  // cache-policy bits of the parity stores (2 = nt)
 #endif
+#ifndef BS_ST_SGPR
+#define BS_ST_SGPR 0  // 1: shard offset of the parity stores in soffset (the round-1 form: wrong
+                      // parity dwords under co-resident load, see DevIO::store)
+#endif
 #define BS_ACC3(acc, a, b) ((acc) = __builtin_amdgcn_bitop3_b32((acc), (a), (b), 0x96))
 #define BS_ACC2(acc, a) ((acc) ^= (a))
 // keep the generated shard blocks in order so the raw-load ring bounds the
@@ -64,12 +68,25 @@ struct DevIO {
         p[0] = x.x; p[1] = x.y; p[2] = x.z; p[3] = x.w;
         p[4] = y.x; p[5] = y.y; p[6] = y.z; p[7] = y.w;
     }
+    // Stores keep the whole offset in the VGPR (soffset 0).  LLVM's hazard
+    // recognizer (GCNHazardRecognizer::createsVALUHazard) exempts MUBUF stores
+    // with a register soffset from the "store of > 64 bits, then a VALU write
+    // of its data VGPRs" wait state, and the register allocator reuses the
+    // first data VGPR of the second store in the very next VALU instruction.
+    // On gfx950 the store then sometimes sent the NEW value of that VGPR for
+    // lanes 12-15 of each 16 (wrong first dwords of 16-B pieces at 192..255
+    // mod 256) once another kernel's waves shared the CU: DESIGN.md §4.
     __device__ __forceinline__ void store(int j, const uint32_t (&q)[8]) const {
         typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
         const u32x4 x = {q[0], q[1], q[2], q[3]};
         const u32x4 y = {q[4], q[5], q[6], q[7]};
+#if BS_ST_SGPR
         __builtin_amdgcn_raw_buffer_store_b128(x, rsrc, v0, j * ss, BS_ST_AUX);
         __builtin_amdgcn_raw_buffer_store_b128(y, rsrc, v1, j * ss, BS_ST_AUX);
+#else
+        __builtin_amdgcn_raw_buffer_store_b128(x, rsrc, v0 + j * ss, 0, BS_ST_AUX);
+        __builtin_amdgcn_raw_buffer_store_b128(y, rsrc, v1 + j * ss, 0, BS_ST_AUX);
+#endif
     }
 };
 

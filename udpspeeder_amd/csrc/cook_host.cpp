@@ -136,18 +136,7 @@ rsmi::CookArgs make_args(const rsmi_cook_ctx *c, const rsmi_packet_batch *b) {
 }
 
 int launch(const rsmi::CookArgs &a, const rsmi_cook_ctx *c, bool decook, hipStream_t s) {
-    struct L {
-        const rsmi::CookArgs *a;
-        bool decook;
-        int max_blocks;
-        hipStream_t s;
-    } l{&a, decook, c->max_blocks, s};
-    const hipError_t e = rsmi::ordered_launch(
-        s, [](void *p) {
-            const L *q = static_cast<const L *>(p);
-            return rsmi::launch_cook(*q->a, q->decook, q->max_blocks, q->s);
-        },
-        &l);
+    const hipError_t e = rsmi::launch_cook(a, decook, c->max_blocks, s);
     if (e != hipSuccess)
         return fail(RSMI_ERR_HIP, std::string(decook ? "decook" : "cook") + " launch: " +
                                       hipGetErrorString(e));

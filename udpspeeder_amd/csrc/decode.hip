@@ -45,6 +45,10 @@ static_assert(kRing % 2 == 0, "ring slots are consumed in pairs under DEC_PAIR")
 constexpr int kRows = 10;      // max e handled by the fused kernel (emax <= kRows)
 constexpr int kPass = 5;       // rows accumulated per pass over the survivors
 constexpr int kTile = 1280;    // bytes per lane-tile pass (64 x 16 + 64 x 4)
+#ifndef DEC_ST_SGPR
+#define DEC_ST_SGPR 0          // 1: row offset of the rebuilt-row stores in soffset (see bitslice.hip
+                               // DevIO::store: no hazard wait state is inserted for that form)
+#endif
 #ifndef DEC_PAIR
 #define DEC_PAIR 0             // fold survivors in pairs (fewer XORs, more VGPRs)
 #endif
@@ -389,8 +393,13 @@ __global__ __launch_bounds__(256, DEC_OCC) void k_decode_fused(UniformArgs a, co
                     if (rb + r < e) {
                         const uint32_t so = __builtin_amdgcn_readlane(mo_lane, rb + r);
                         const u32x4 v = {acc[r][0], acc[r][1], acc[r][2], acc[r][3]};
+#if DEC_ST_SGPR
                         __builtin_amdgcn_raw_buffer_store_b128(v, rsrc, v16, so, DEC_ST_AUX);
                         __builtin_amdgcn_raw_buffer_store_b32(acc[r][4], rsrc, v4, so, DEC_ST_AUX);
+#else
+                        __builtin_amdgcn_raw_buffer_store_b128(v, rsrc, v16 + so, 0, DEC_ST_AUX);
+                        __builtin_amdgcn_raw_buffer_store_b32(acc[r][4], rsrc, v4 + so, 0, DEC_ST_AUX);
+#endif
                     }
                 }
             }

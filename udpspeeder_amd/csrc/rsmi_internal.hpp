@@ -110,8 +110,6 @@ struct CookArgs {
 };
 size_t cook_lds_bytes(bool decook);
 hipError_t launch_cook(const CookArgs &a, bool decook, int max_blocks, hipStream_t s);
-// f(arg) ordered after the codec's previous launch on another stream (api.cpp)
-hipError_t ordered_launch(hipStream_t s, hipError_t (*f)(void *), void *arg);
 
 
 
