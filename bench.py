@@ -1,18 +1,26 @@
 """bench.py -- device-resident RS(20,10) encode + decode throughput on MI355X.
 
-One step = one pass of the hot path over one batch per GPU (BASELINE.json
-configs[1] + configs[2]): rs_encode2 of G groups (RS(20,10), 1250-B shards)
-followed by rs_decode2 of the same G groups with 5 random erasures each
-(decode plans built on the GPU inside the step).  Inputs are resident in HBM
-before the timed region.  Groups are sharded across ranks with no data-path
-collective (weak scaling by default: G groups per GPU; --scaling strong
-splits --total-groups, C4's 2^20, across the ranks).
+One step = one pass of the hot path over one batch per GPU: rs_encode2 of the
+rank's groups (RS(20,10), 1250-B shards) followed by rs_decode2 of the same
+groups with 5 random erasures each (decode plans built on the GPU inside the
+step).  Inputs are resident in HBM before the timed region.
 
-Prints ONE JSON line (rank 0).  value = payload GiB/s over all GPUs, payload
-= k*len bytes per group per operation (encode + decode).  roofline is for the
-dominant kernel (encode), measured with HIP events on the launch stream;
-cpu_baseline times the reference codec (oracle/_ref) -- or the C restatement
-if the reference build is absent -- on this host's cores.
+* N = 1 (default): BASELINE configs[1] + configs[2], 65,536 groups.
+* N > 1: configs[4] (C4), 2^20 groups split into contiguous ranges over the
+  ranks (strong scaling), one process per GPU, no data-path collective: FEC
+  groups are independent.  ``--scaling weak`` keeps
+  ``--groups`` per GPU instead.
+
+``python bench.py --gpus N`` without a torch.distributed launcher starts the N
+ranks itself (``torch.distributed.run`` on 127.0.0.1) before touching the
+GPU; a WORLD_SIZE that disagrees with --gpus is an error.
+
+Prints ONE JSON line (rank 0).  value = payload GiB/s over all GPUs (k*len
+bytes per group per operation, encode + decode), timed between barriers and
+taken as the max over ranks.  ``roofline`` is for whichever kernel takes
+longer per step, measured with HIP events on the launch stream;
+``cpu_baseline`` times the reference codec (oracle/_ref) on this host, 1
+thread and the CPU share (16 threads).
 """
 from __future__ import annotations
 
@@ -20,6 +28,7 @@ import argparse
 import json
 import os
 import statistics
+import subprocess
 import sys
 import time
 
@@ -29,29 +38,58 @@ sys.path.insert(0, ROOT)
 METRIC = "device-resident RS encode+decode GiB/s (payload bytes) & FEC-groups/s, 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 K, M, LEN, STRIDE, ERASURES = 20, 10, 1250, 1280, 5
+C4_GROUPS = 1 << 20
+TRAFFIC = {"encode": os.path.join(ROOT, "profiles", "traffic.json"),
+           "decode": os.path.join(ROOT, "profiles", "traffic_decode.json")}
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--groups", type=int, default=65536, help="groups per GPU (weak scaling)")
-    p.add_argument("--scaling", choices=["weak", "strong"], default="weak")
-    p.add_argument("--total-groups", type=int, default=1 << 20, help="strong scaling total (C4)")
-    p.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cores)")
+    p.add_argument("--scaling", choices=["weak", "strong"], default=None,
+                   help="default: weak at N=1 (C1+C2), strong over --total-groups at N>1 (C4)")
+    p.add_argument("--total-groups", type=int, default=C4_GROUPS, help="strong scaling total")
+    p.add_argument("--cpu-threads", type=int, default=16, help="threads of the all-cores CPU leg")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--no-extras", action="store_true", help="skip the C2-worst / C3 lines")
+    p.add_argument("--no-extras", action="store_true", help="skip the other_configs lines")
     p.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL)")
     p.add_argument("--share-device", action="store_true",
                    help="map every rank to cuda:0 (rehearsing N>1 on a 1-GPU box, gloo only)")
-    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
-                   help="per-launch HBM bytes from a rocprofv3 --pmc pass (optional)")
-    return p.parse_args()
+    p.add_argument("--rehearse", action="store_true",
+                   help="CPU only: run the launcher / barrier / max-over-ranks / JSON path with a "
+                        "numpy stand-in step (tests; never a measurement)")
+    return p.parse_args(argv)
+
+
+def launch_ranks(args) -> int:
+    """Start args.gpus ranks through torch.distributed.run and return its exit
+    code.  Runs before this process touches the GPU."""
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr=127.0.0.1", f"--master-port={port}",
+           os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
 
 
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        sys.exit(f"bench.py: WORLD_SIZE={world} but --gpus={args.gpus}")
+    scaling = args.scaling or ("weak" if world == 1 else "strong")
+    if args.rehearse:
+        return rehearse(args, world, rank, scaling)
+
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -59,11 +97,6 @@ def main():
     import udpspeeder_amd as u
     from udpspeeder_amd import shard, synth
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and rank == 0:
-        print(f"warning: WORLD_SIZE={world} but --gpus={args.gpus}", file=sys.stderr)
     if args.share_device:
         local = 0
     torch.cuda.set_device(local)
@@ -74,10 +107,12 @@ def main():
         else:
             dist.init_process_group(args.backend, rank=rank, world_size=world)
 
-    if args.scaling == "weak":
+    if scaling == "weak":
         g0, g1 = shard.weak_range(rank, args.groups)
+        total_groups = args.groups * world
     else:
         g0, g1 = shard.strong_range(rank, world, args.total_groups)
+        total_groups = args.total_groups
     G = g1 - g0
     n = K + M
 
@@ -89,8 +124,7 @@ def main():
     stream = torch.cuda.current_stream()
     u.reserve(K, n, G, stream)
 
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
-           torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
 
     def step(i=None):
         if i is not None:
@@ -115,70 +149,64 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    if world > 1:
-        # max over ranks: the job is as slow as its slowest GPU
-        t = torch.tensor([elapsed], dtype=torch.float64,
-                         device=dev if args.backend == "nccl" else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    bad = int((status != 0).sum().item())
     enc_ms = statistics.mean(a.elapsed_time(b) for a, b, _ in ev)
     dec_ms = statistics.mean(b.elapsed_time(c) for _, b, c in ev)
+    bad = int((status != 0).sum().item())
+    if world > 1:
+        # max over ranks: the job is as slow as its slowest GPU
+        t = torch.tensor([elapsed, enc_ms, dec_ms, float(bad)], dtype=torch.float64,
+                         device=dev if args.backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, enc_ms, dec_ms, bad = float(t[0]), float(t[1]), float(t[2]), int(t[3])
 
-    total_groups = G * world if args.scaling == "weak" else args.total_groups
-    payload = 2.0 * total_groups * K * LEN * args.steps  # encode + decode
-    value = payload / elapsed / 2**30
+    payload_op = float(total_groups) * K * LEN  # one operation over the whole job
+    value = 2.0 * payload_op * args.steps / elapsed / 2**30
     groups_per_s = total_groups * args.steps / elapsed
 
-    # ---- roofline for the dominant kernel (encode): algorithmic bytes / launch
-    alg_bytes = G * (K + M) * LEN  # read k*len + write m*len per group
-    achieved = alg_bytes / (enc_ms * 1e-3) / 1e9
-    traffic = None
-    if os.path.exists(args.traffic_json):
-        try:
-            tj = json.load(open(args.traffic_json))
-            if tj.get("groups") == G and tj.get("kernel"):
-                traffic = tj.get("hbm_bytes_per_launch")
-        except (OSError, ValueError):
-            traffic = None
-    roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "kernel": "encode RS(20,10)", "alg_bytes_per_launch": alg_bytes,
-                "avg_launch_ms": round(enc_ms, 4)}
-    # decode roofline: k*len read + e*len written for every group with e > 0
+    # ---- rooflines: algorithmic bytes per launch / average launch time
+    enc_alg = G * (K + M) * LEN  # read k*len + write m*len per group
     pres_np = present.cpu().numpy()
     e_rows = (pres_np[:, :K] == 0).sum(1)
-    dec_alg = int(((e_rows > 0) * K * LEN).sum() + (e_rows * LEN).sum())
-    dec_achieved = dec_alg / (dec_ms * 1e-3) / 1e9
-    roofline_decode = {"bound": "hbm", "achieved": round(dec_achieved, 1), "peak": HBM_PEAK_GBS,
-                       "unit": "GB/s", "frac": round(dec_achieved / HBM_PEAK_GBS, 4),
-                       "kernel": "fused decode RS(20,10), 5 random erasures",
-                       "alg_bytes_per_launch": dec_alg, "avg_launch_ms": round(dec_ms, 4)}
+    dec_alg = int(((e_rows > 0) * K * LEN).sum() + (e_rows * LEN).sum())  # k*len read + e*len written
+    roof = {
+        "encode": roofline("encode", "k_bs_20_30: bit-sliced RS(20,10) encode", enc_alg, enc_ms, G),
+        "decode": roofline("decode", "k_decode_fused: RS(20,10) decode, 5 random erasures",
+                           dec_alg, dec_ms, G),
+    }
+    dominant = "decode" if dec_ms >= enc_ms else "encode"
+    other = "encode" if dominant == "decode" else "decode"
+
     extras = None
     if rank == 0 and world == 1 and not args.no_extras:
         extras = extra_configs(u, synth, torch, dev, buf, G)
-
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(buf, present, G, args.cpu_threads)
 
     if rank == 0:
+        if scaling == "weak":
+            workload = ("C1+C2: RS(20,10) encode + decode (5 random erasures), 1250-B shards, "
+                        "device-resident" if world == 1 else
+                        f"weak scaling: {G} groups per GPU, RS(20,10) encode + decode")
+        else:
+            workload = (f"C4: RS(20,10) encode + decode (5 random erasures), 1250-B shards, "
+                        f"{total_groups} groups split over {world} GPU(s), device-resident")
         line = {
             "metric": METRIC, "value": round(value, 2), "unit": "GiB/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
-            "scaling": args.scaling, "vs_baseline": None, "dtype": "u8",
+            "scaling": scaling, "vs_baseline": None, "dtype": "u8",
             "data": "synthetic: SplitMix64 payload bytes, seeded 5-of-30 erasures per group",
-            "config": {"workload": "C1+C2: RS(20,10) encode + decode (5 random erasures), "
-                                   "1250-B shards, device-resident",
-                       "k": K, "m": M, "len": LEN, "shard_stride": STRIDE,
+            "config": {"workload": workload, "k": K, "m": M, "len": LEN, "shard_stride": STRIDE,
                        "groups_per_gpu": G, "global_groups": total_groups,
                        "parallelism": f"groups sharded over {world} GPU(s), no collective"},
             "groups_per_s": round(groups_per_s, 1),
             "encode_ms": round(enc_ms, 4), "decode_ms": round(dec_ms, 4),
+            "encode_GiBps": round(payload_op / (enc_ms * 1e-3) / 2**30, 2),
+            "decode_GiBps": round(payload_op / (dec_ms * 1e-3) / 2**30, 2),
             "decode_failures": bad,
-            "roofline": roofline,
-            "roofline_decode": roofline_decode,
+            "roofline": roof[dominant],
+            f"roofline_{other}": roof[other],
             "cpu_baseline": cpu,
             "other_configs": extras,
         }
@@ -187,8 +215,63 @@ def main():
         dist.destroy_process_group()
 
 
+def roofline(which, kernel, alg_bytes, ms, G):
+    achieved = alg_bytes / (ms * 1e-3) / 1e9
+    traffic = None
+    path = TRAFFIC[which]
+    if os.path.exists(path):
+        try:
+            tj = json.load(open(path))
+            if tj.get("groups") == G:
+                traffic = tj.get("hbm_bytes_per_launch")
+        except (OSError, ValueError):
+            traffic = None
+    return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": kernel,
+            "alg_bytes_per_launch": int(alg_bytes), "avg_launch_ms": round(ms, 4)}
+
+
+def rehearse(args, world, rank, scaling):
+    """The multi-rank harness without a GPU (tests only): gloo, a numpy XOR
+    stand-in for the step, the same barriers, max-over-ranks and JSON line."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    from udpspeeder_amd import shard
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    total = args.total_groups if scaling == "strong" else args.groups * world
+    g0, g1 = (shard.strong_range(rank, world, total) if scaling == "strong"
+              else shard.weak_range(rank, args.groups))
+    a = np.random.default_rng(rank).integers(0, 256, (g1 - g0, 64), dtype=np.uint8)
+    for _ in range(args.warmup):
+        a ^= a[::-1]
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        a ^= a[::-1]
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    owned = torch.tensor([float(g1 - g0)], dtype=torch.float64)
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        dist.all_reduce(owned)
+    if rank == 0:
+        print(json.dumps({"metric": "rehearsal (no GPU): harness only", "rehearsal": True,
+                          "value": round(float(owned.item()) * args.steps / elapsed, 1),
+                          "unit": "groups/s", "n_gpus": world, "steps": args.steps,
+                          "warmup": args.warmup, "scaling": scaling,
+                          "groups_covered": int(owned.item()), "global_groups": total}),
+              flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def _time_ms(torch, fn, reps=10, warm=2):
-    import statistics as st
     ts = []
     for i in range(reps + warm):
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -198,12 +281,14 @@ def _time_ms(torch, fn, reps=10, warm=2):
         torch.cuda.synchronize()
         if i >= warm:
             ts.append(a.elapsed_time(b))
-    return st.median(ts)
+    return statistics.median(ts)
 
 
 def extra_configs(u, synth, torch, dev, buf, G):
     """BASELINE configs beside the headline step (device-resident, N=1):
-    C2 worst case (5 data erasures) and C3 (ragged mode-0 mix)."""
+    C2 worst case (5 data erasures), C3 (ragged mode-0 mix), C4's 2^20 groups
+    on this one GPU (the strong-scaling base), the f2 cook/de_cook row and the
+    per-call latency of the level-1 drop-in (rs_encode2 / rs_decode2)."""
     n = K + M
     out = {}
     # C2 worst case: every group loses 5 data shards
@@ -215,8 +300,22 @@ def extra_configs(u, synth, torch, dev, buf, G):
     out["c2_worst_5_data_erasures"] = {
         "decode_ms": round(ms, 4), "groups": G,
         "payload_GiBps": round(G * K * LEN / (ms * 1e-3) / 2**30, 1),
-        "alg_GBps": round(alg / (ms * 1e-3) / 1e9, 1), "failures": int((st != 0).sum().item())}
-    # C3: ragged mix from -f 1:3,2:4,10:6,20:10, len 64..1250, one bucketed launch
+        "alg_GBps": round(alg / (ms * 1e-3) / 1e9, 1),
+        "roofline_frac": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+        "failures": int((st != 0).sum().item())}
+    out.update(c3_configs(u, synth, torch, dev, G))
+    out["c4_one_gpu"] = c4_one_gpu(u, synth, torch, dev)
+    out["f2_cook_decook"] = cook_config(torch, dev, buf, G)
+    out["dropin_latency_us"] = dropin_latency(u)
+    return out
+
+
+def c3_configs(u, synth, torch, dev, G):
+    """C3: ragged mix from -f 1:3,2:4,10:6,20:10, len 64..1250: one bucketed
+    encode launch, then (if built) one ragged decode launch with 5 random
+    erasures per group (erasures limited to the group's n)."""
+    import numpy as np
+    out = {}
     table = u.rs_from_str(synth.C3_FEC)
     ks, ms_, ls = synth.ragged_mix(synth.RAGGED_SEED, 0, G, [y for _, y in table])
     groups, total = u.make_groups(ks, ks + ms_, ls)
@@ -232,14 +331,53 @@ def extra_configs(u, synth, torch, dev, buf, G):
         "alg_GBps": round(alg / (t * 1e-3) / 1e9, 1), "alg_bytes": alg,
         "roofline_frac": round(alg / (t * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
     plan.close()
+    if hasattr(u.rs, "decode_ragged"):
+        pres_np = synth.ragged_present(synth.ERASE_SEED, 0, ks, ks + ms_, ERASURES)
+        pres = torch.from_numpy(pres_np).to(dev)
+        st = torch.empty(G, dtype=torch.int32, device=dev)
+        t = _time_ms(torch, lambda: u.rs.decode_ragged(base, dg, G, pres, status=st))
+        e = np.minimum(synth.ragged_missing_data(pres_np, ks, ks + ms_), ks)
+        alg = int((((e > 0) * ks + e) * ls).sum())
+        out["c3_ragged_decode"] = {
+            "decode_ms": round(t, 4), "groups": G,
+            "payload_GiBps": round(float((ks * ls).sum()) / (t * 1e-3) / 2**30, 1),
+            "alg_GBps": round(alg / (t * 1e-3) / 1e9, 1), "alg_bytes": alg,
+            "roofline_frac": round(alg / (t * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "failures": int((st != 0).sum().item())}
     del base
-    # f2: cook + de_cook of every packet C1 emits (8-B header + 1250-B shard)
+    return out
+
+
+def c4_one_gpu(u, synth, torch, dev, steps=5):
+    """C4's 2^20 RS(20,10) groups on one GPU: the base of the strong-scaling
+    curve that bench.py --gpus N (N > 1) measures."""
+    n = K + M
+    Gc = C4_GROUPS
+    b = torch.empty((Gc, n, STRIDE), dtype=torch.uint8, device=dev)
+    u.fill_data(b, K, LEN, synth.DATA_SEED)
+    p = torch.from_numpy(synth.erasure_present(synth.ERASE_SEED, 0, Gc, n, ERASURES)).to(dev)
+    st = torch.empty(Gc, dtype=torch.int32, device=dev)
+    u.reserve(K, n, Gc)
+
+    def step():
+        u.encode(b, K, n, LEN)
+        u.decode(b, p, K, n, LEN, status=st)
+    ms = _time_ms(torch, step, reps=steps, warm=1)
+    r = {"groups": Gc, "ms_per_step": round(ms, 3),
+         "GiBps": round(2.0 * Gc * K * LEN / (ms * 1e-3) / 2**30, 1),
+         "failures": int((st != 0).sum().item())}
+    del b
+    return r
+
+
+def cook_config(torch, dev, buf, G):
+    """f2: cook + de_cook of every packet C1 emits (8-B header + 1250-B shard)."""
     from udpspeeder_amd.cook import CookContext
+    n = K + M
     plen, pstride = 8 + LEN, 1312
     npk = G * n
     pk = torch.empty((npk, pstride), dtype=torch.uint8, device=dev)
     pk[:, :8] = 0x5A
-    pk.view(G, n, pstride)[:, :, 8:8 + LEN] = buf[:, :, :LEN]
     lens = torch.full((npk,), plen, dtype=torch.int32, device=dev)
     olen = torch.empty_like(lens)
     back = torch.empty_like(lens)
@@ -261,70 +399,115 @@ def extra_configs(u, synth, torch, dev, buf, G):
     ok = bool((back == plen).all()) and torch.equal(
         pk.view(G, n, pstride)[:, :, 8:8 + LEN], buf[:, :, :LEN])
     cooked = float(olen.float().mean())
-    alg = npk * (plen + cooked)
-    out["f2_cook_decook"] = {
-        "packets": npk, "len": plen, "key": True, "cook_ms": round(tc, 4),
-        "decook_ms": round(td, 4), "cook_Mpps": round(npk / tc / 1e3, 1),
-        "decook_Mpps": round(npk / td / 1e3, 1),
-        "cook_frac": round(alg / (tc * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-        "decook_frac": round(alg / (td * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "roundtrip_ok": ok}
+    alg = npk * (plen + cooked)  # read the plain packet, write the cooked one
     ctx.close()
     del pk
-    return out
+    return {"packets": npk, "len": plen, "key": True, "cook_ms": round(tc, 4),
+            "decook_ms": round(td, 4), "cook_Mpps": round(npk / tc / 1e3, 1),
+            "decook_Mpps": round(npk / td / 1e3, 1), "alg_bytes": int(alg),
+            "cook_frac": round(alg / (tc * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "decook_frac": round(alg / (td * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "roundtrip_ok": ok}
+
+
+def dropin_latency(u, calls=300):
+    """Wall time of one level-1 drop-in call (the reference-mangled
+    rs_encode2 / rs_decode2 on host buffers, lib/rs.cpp:56-64): RS(20,10),
+    1250 B, 5 erasures; median over ``calls`` calls, microseconds."""
+    import ctypes as C
+    import numpy as np
+    n = K + M
+    rows = np.random.default_rng(3).integers(0, 256, (n, LEN), dtype=np.uint8)
+    arr = (C.c_void_p * n)(*[rows[j].ctypes.data for j in range(n)])
+    enc = u.lib().compat["rs_encode2"]
+    dec = u.lib().compat["rs_decode2"]
+    te = []
+    for i in range(calls + 20):
+        t0 = time.perf_counter()
+        enc(K, n, arr, LEN)
+        te.append(time.perf_counter() - t0)
+    td = []
+    erased = [1, 4, 9, 22, 27]
+    for i in range(calls + 20):
+        ptrs = (C.c_void_p * n)(*[None if j in erased else rows[j].ctypes.data
+                                  for j in range(n)])
+        t0 = time.perf_counter()
+        rc = dec(K, n, ptrs, LEN)
+        td.append(time.perf_counter() - t0)
+        if rc:
+            raise SystemExit("dropin_latency: rs_decode2 failed")
+    return {"rs_encode2": round(statistics.median(te[20:]) * 1e6, 1),
+            "rs_decode2": round(statistics.median(td[20:]) * 1e6, 1),
+            "calls": calls, "what": "one RS(20,10) 1250-B group per call, host buffers, "
+                                    "synchronous (pinned staging, H2D, kernel, D2H)"}
 
 
 def cpu_baseline(buf, present, G, threads):
-    """Time the reference codec (oracle/_ref/libref_rs.so: lib/fec.cpp + lib/rs.cpp
-    unmodified) on this host -- or the C restatement if the reference build is
-    absent -- on the same C1+C2 groups; median of 3 reps; checked against the
-    GPU's parity."""
+    """Time the reference codec (oracle/_ref/libref_rs.so: lib/fec.cpp +
+    lib/rs.cpp unmodified) on this host -- or the C restatement if the
+    reference build is absent -- on the same C1+C2 groups: 1 thread on a
+    4,096-group sample and ``threads`` threads on a 65,536-group sample,
+    median of 5 reps each, checked against the GPU's parity.  ``value`` is the
+    multi-threaded rate; the 1-thread run also gives the reference's per-call
+    latency (one rs_encode2 / rs_decode2 per group, lib/rs.cpp:56-64)."""
     import numpy as np
     import platform
     from oracle.cpu import Oracle, Reference
 
-    nthreads = threads or min(16, os.cpu_count() or 1)
     n = K + M
-    host = buf.cpu().numpy()  # data + GPU parity (+ decoded rows == data)
-    pres = present.cpu().numpy()
-    sample = min(G, 65536)
-    gpu_par = host[:sample, K:, :LEN].copy()
-    if Reference.available():
-        lib, kind = Reference(), "reference"
-        enc = lambda b: lib.encode_batch(K, n, b.reshape(-1), n * STRIDE, STRIDE, LEN, sample,
-                                         nthreads)
-        dec = lambda b: lib.decode_batch(K, n, b.reshape(-1), n * STRIDE, STRIDE, LEN, sample,
-                                         pres[:sample], False, nthreads)
-    else:
-        lib, kind = Oracle(), "port"
-        nthreads = 1
-        enc = lambda b: lib.encode_batch(K, n, b.reshape(-1), n * STRIDE, STRIDE, LEN, sample)
-        dec = lambda b: lib.decode_batch(K, n, b.reshape(-1), n * STRIDE, STRIDE, LEN, sample,
-                                         pres[:sample])
-    pristine = np.ascontiguousarray(host[:sample])
-    times = []
-    for _ in range(3):
-        b = pristine.copy()
-        b[:, K:] = 0
-        t0 = time.perf_counter()
-        enc(b)
-        t1 = time.perf_counter()
-        if _ == 0 and not (b[:, K:, :LEN] == gpu_par).all():
-            raise SystemExit("cpu_baseline: CPU parity differs from GPU parity")
-        t2 = time.perf_counter()
-        dec(b)
-        t3 = time.perf_counter()
-        times.append((t1 - t0) + (t3 - t2))
-    med = statistics.median(times)
-    gib = 2.0 * sample * K * LEN / med / 2**30
+    host = buf[:min(G, 65536)].cpu().numpy()  # data + GPU parity (+ decoded rows == data)
+    pres = present[:min(G, 65536)].cpu().numpy()
+    ref = Reference.available()
+    lib = Reference() if ref else Oracle()
+    kind = "reference" if ref else "port"
+
+    def run(sample, nthreads, reps=5):
+        pristine = np.ascontiguousarray(host[:sample])
+        gpu_par = pristine[:, K:, :LEN].copy()
+        te, td = [], []
+        for r in range(reps):
+            b = pristine.copy()
+            b[:, K:] = 0
+            t0 = time.perf_counter()
+            if ref:
+                lib.encode_batch(K, n, b.reshape(-1), n * STRIDE, STRIDE, LEN, sample, nthreads)
+            else:
+                lib.encode_batch(K, n, b.reshape(-1), n * STRIDE, STRIDE, LEN, sample)
+            t1 = time.perf_counter()
+            if r == 0 and not (b[:, K:, :LEN] == gpu_par).all():
+                raise SystemExit("cpu_baseline: CPU parity differs from GPU parity")
+            t2 = time.perf_counter()
+            if ref:
+                lib.decode_batch(K, n, b.reshape(-1), n * STRIDE, STRIDE, LEN, sample,
+                                 pres[:sample], False, nthreads)
+            else:
+                lib.decode_batch(K, n, b.reshape(-1), n * STRIDE, STRIDE, LEN, sample,
+                                 pres[:sample])
+            t3 = time.perf_counter()
+            te.append(t1 - t0)
+            td.append(t3 - t2)
+        tot = [a + b for a, b in zip(te, td)]
+        return (2.0 * sample * K * LEN / statistics.median(tot) / 2**30,
+                statistics.median(te) / sample, statistics.median(td) / sample)
+
+    one_sample = min(4096, host.shape[0])
+    gib1, enc1, dec1 = run(one_sample, 1)
+    nthreads = threads if ref else 1
+    many_sample = host.shape[0]
+    gibn, _, _ = run(many_sample, nthreads) if nthreads > 1 else (gib1, enc1, dec1)
     try:
         model = [l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo")
                  if l.startswith("model name")][0]
     except (OSError, IndexError):
         model = platform.processor()
-    return {"value": round(gib, 3), "unit": "GiB/s", "cores": nthreads, "kind": kind,
-            "sample": f"{sample} groups RS(20,10)x1250B encode + decode(5 erasures), "
-                      f"median of 3 reps, {nthreads} threads on {model}",
-            "groups_per_s": round(sample / med, 1)}
+    return {"value": round(gibn, 3), "unit": "GiB/s", "cores": nthreads, "kind": kind,
+            "sample": f"{many_sample} groups RS(20,10)x1250B encode + decode (5 erasures), "
+                      f"median of 5 reps, {nthreads} threads on {model} "
+                      f"(the GPU box's CPU share; os.cpu_count()={os.cpu_count()})",
+            "single_thread": {"value": round(gib1, 3), "unit": "GiB/s", "cores": 1,
+                              "sample": f"{one_sample} groups, median of 5 reps",
+                              "rs_encode2_us_per_call": round(enc1 * 1e6, 1),
+                              "rs_decode2_us_per_call": round(dec1 * 1e6, 1)}}
 
 
 if __name__ == "__main__":
