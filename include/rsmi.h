@@ -48,6 +48,8 @@ extern "C" {
 #define RSMI_DEC_OK 0
 #define RSMI_DEC_TOO_FEW (-1) /* fewer than k shards present        */
 #define RSMI_DEC_SINGULAR 1   /* decode matrix singular (never for valid codes) */
+#define RSMI_DEC_UNSUPPORTED 2 /* ragged decode only: invalid descriptor, or its (k,n)
+                                  code is not resident (rsmi_prepare_code)        */
 
 /* Library version, e.g. 0x000100 = 0.1.0. */
 int rsmi_version(void);
@@ -140,6 +142,29 @@ int rsmi_ragged_plan_create(const rsmi_group *groups, int64_t ngroups,
                             rsmi_ragged_plan **plan);
 int rsmi_encode_ragged_plan(const rsmi_ragged_plan *plan, uint8_t *base, void *stream);
 int rsmi_ragged_plan_uses_bitslice(const rsmi_ragged_plan *plan);
+
+/* Ragged decode: rs_decode2(k, n, data, len) on every group of a ragged
+ * batch (fec_manager.cpp:632 once per mode-0 group, each with its own k, n
+ * and length).  present_bits (DEVICE uint32[ngroups * 8]): bit (j % 32) of
+ * word g*8 + j/32 set = shard j of group g received (bits >= n ignored).
+ * Missing data shards are rebuilt in their own slots from the first k
+ * present shards in ascending order, as rsmi_decode_dev does; the slot
+ * padding rule above applies.  status (DEVICE int32[ngroups], required)
+ * receives RSMI_DEC_*.  One launch for groups with min(k, n-k) <= 10 and
+ * k <= 64 (all of -f's default and C3 tables), a second, workgroup-per-group
+ * launch for the rest.  Codes must be resident; a plan makes them so. */
+int rsmi_decode_ragged_plan(const rsmi_ragged_plan *plan, uint8_t *base,
+                            const uint32_t *present_bits, int32_t *status, void *stream);
+/* Same with a DEVICE descriptor array (graph-capturable): kmax = the largest k
+ * in the batch (sizes the one-wave kernel's LDS); groups whose code is not
+ * resident get RSMI_DEC_UNSUPPORTED. */
+int rsmi_decode_ragged_dev(const rsmi_group *dev_groups, int64_t ngroups, uint8_t *base,
+                           const uint32_t *present_bits, int32_t *status, int kmax,
+                           void *stream);
+/* Same with a HOST descriptor array: builds a plan, launches it on `stream`
+ * and returns once it has completed. */
+int rsmi_decode_ragged(const rsmi_group *groups, int64_t ngroups, uint8_t *base,
+                       const uint32_t *present_bits, int32_t *status, void *stream);
 void rsmi_ragged_plan_destroy(rsmi_ragged_plan *plan);
 
 /* ---- host-memory convenience (pinned staging + H2D/D2H on an internal

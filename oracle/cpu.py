@@ -71,6 +71,26 @@ def erasures(seed: int, g0: int, ng: int, n: int, e: int, limit: int | None = No
     return perm[:, :e]
 
 
+def ragged_erasures(seed: int, g0: int, ns: np.ndarray, ms: np.ndarray, emax: int = 5) -> np.ndarray:
+    """C3 decode erasures: [ng, 256] present flags; group g0+i loses min(emax,
+    m_i) distinct shards, a partial Fisher-Yates over range(n_i) driven by
+    words mix((seed^g)+(i+1)*GAMMA); flags at and beyond n_i are 0."""
+    ns = np.asarray(ns, np.int64)
+    ms = np.asarray(ms, np.int64)
+    ng = len(ns)
+    out = np.zeros((ng, 256), np.uint8)
+    r = splitmix_words(seed, np.arange(g0, g0 + ng, dtype=np.uint64), emax) if emax else None
+    for g in range(ng):
+        n, e = int(ns[g]), int(min(emax, ms[g]))
+        perm = list(range(n))
+        for i in range(e):
+            pick = i + int(r[g, i] % np.uint64(n - i))
+            perm[i], perm[pick] = perm[pick], perm[i]
+        out[g, :n] = 1
+        out[g, perm[:e]] = 0
+    return out
+
+
 def present_from_erasures(er: np.ndarray, n: int) -> np.ndarray:
     p = np.ones((er.shape[0], n), dtype=np.uint8)
     p[np.arange(er.shape[0])[:, None], er] = 0

@@ -24,11 +24,13 @@ from __future__ import annotations
 import hashlib
 import json
 import os
+import sys
 
 import numpy as np
 
 from oracle.cpu import (DATA_SEED, ERASE_SEED, RAGGED_SEED, Oracle, Reference, erasures,
-                        group_data, present_from_erasures, ragged_draw)
+                        group_data, present_from_erasures, ragged_draw,
+                        ragged_erasures)
 
 OUT = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "golden")
 
@@ -199,13 +201,51 @@ def full_hashes(ref: Reference, ora: Oracle, nthreads: int):
                                "sum_payload": int((kk * ll).sum()),
                                "sum_parity": int((mm * ll).sum()),
                                "parity_sha256": hr.hexdigest()}
+    res["c3_ragged_decode"] = c3_ragged_decode(ref, ora)
     return res
+
+
+def c3_ragged_decode(ref: Reference, ora: Oracle):
+    """C3 ragged decode, non-codeword: group g's data rows are the DATA_SEED
+    stream, its parity rows the DATA_SEED ^ 0xFFFF stream (not a codeword, so
+    the output pins which survivors rs_decode uses), it loses min(5, m) of its
+    n shards (ragged_erasures), the reference rs_decode2 rebuilds it; the
+    digest covers every group's k data rows (len bytes each) in order."""
+    tab = ora.rs_from_str(C3_STR)
+    ty = np.array([y for (_, y) in tab], np.int64)
+    G = 65536
+    kk, mm, ll = ragged_draw(RAGGED_SEED, 0, G, ty)
+    pres = ragged_erasures(ERASE_SEED, 0, kk + mm, mm, 5)
+    h = hashlib.sha256()
+    rebuilt = 0
+    for g in range(G):
+        k_, m_, l_ = int(kk[g]), int(mm[g]), int(ll[g])
+        n_ = k_ + m_
+        buf = np.zeros((n_, l_), np.uint8)
+        buf[:k_] = group_data(DATA_SEED, g, 1, k_, l_)[0]
+        buf[k_:] = group_data(DATA_SEED ^ 0xFFFF, g, 1, m_, l_)[0]
+        p = pres[g:g + 1, :n_]
+        st = ref.decode_batch(k_, n_, buf.reshape(-1), 0, l_, l_, 1, p, True, 1)
+        assert st[0] == 0
+        rebuilt += int((p[0, :k_] == 0).sum())
+        h.update(buf[:k_].tobytes())
+    return {"fec": C3_STR, "groups": G, "ragged_seed": RAGGED_SEED, "erase_seed": ERASE_SEED,
+            "erasures": 5, "parity_seed": DATA_SEED ^ 0xFFFF, "rebuilt_rows": rebuilt,
+            "data_out_sha256": h.hexdigest()}
 
 
 def main():
     os.makedirs(OUT, exist_ok=True)
     ref = Reference()
     ora = Oracle()
+    if sys.argv[1:] == ["--c3-decode"]:  # add/refresh only the C3 decode digest
+        path = os.path.join(OUT, "full_hashes.json")
+        full = json.load(open(path))
+        full["c3_ragged_decode"] = c3_ragged_decode(ref, ora)
+        with open(path, "w") as f:
+            json.dump(full, f, indent=1)
+        print("c3_ragged_decode written to", path)
+        return
     with open(os.path.join(OUT, "kat_rs3_6.json"), "w") as f:
         json.dump(kat(ref), f, indent=1)
     mats = {f"{k}_{n}": ref.enc_matrix(k, n)[k:] for (k, n) in MATRIX_SET}

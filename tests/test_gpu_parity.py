@@ -357,6 +357,131 @@ def test_ragged_bitslice_plan_vs_oracle(gpu, oracle):
                 .reshape(d.n, d.shard_stride)[:, pad:]).all(), i
 
 
+def _ragged_noncodeword(gpu, ks, ms, ls, parity_seed):
+    """Ragged batch on the GPU: data rows = DATA_SEED stream, parity rows =
+    parity_seed stream (fill_ragged on descriptors that start at row k)."""
+    import torch
+    import udpspeeder_amd as u
+    groups, total = u.make_groups(ks, ks + ms, ls)
+    base = torch.zeros(total, dtype=torch.uint8, device=gpu)
+    u.rs.fill_ragged(base, u.rs.groups_to_device(groups, gpu), len(groups), DATA_SEED)
+    par, _ = u.make_groups(np.maximum(ms, 1), np.maximum(ms, 1), ls)
+    for i in range(len(groups)):
+        par[i].offset = groups[i].offset + groups[i].k * groups[i].shard_stride
+        par[i].shard_stride = groups[i].shard_stride
+    u.rs.fill_ragged(base, u.rs.groups_to_device(par, gpu), len(groups), parity_seed)
+    return groups, base
+
+
+def test_ragged_decode_c3_full_sha(gpu, golden):
+    """C3 decode: the reference's full-size ragged non-codeword digest through
+    one ragged plan (k_decode_ragged)."""
+    import torch
+    import udpspeeder_amd as u
+    from udpspeeder_amd import synth
+    F = golden.full["c3_ragged_decode"]
+    table = u.rs_from_str(F["fec"])
+    ks, ms, ls = synth.ragged_mix(F["ragged_seed"], 0, F["groups"], [y for _, y in table])
+    groups, base = _ragged_noncodeword(gpu, ks, ms, ls, F["parity_seed"])
+    flags = synth.ragged_erasures(F["erase_seed"], 0, ks + ms, ms, F["erasures"])
+    bits = torch.from_numpy(synth.present_bits(flags).view(np.int32)).to(gpu)
+    host = base.cpu().numpy()
+    for i in range(len(groups)):  # erased slots hold junk: the decode must not read them
+        d = groups[i]
+        for j in np.nonzero(flags[i, :d.n] == 0)[0]:
+            host[d.offset + j * d.shard_stride:d.offset + j * d.shard_stride + d.len] = 0x77
+    base.copy_(torch.from_numpy(host))
+    plan = u.rs.RaggedPlan(groups)
+    st = plan.decode(base, bits)
+    torch.cuda.synchronize()
+    plan.close()
+    assert int((st != 0).sum()) == 0
+    out = base.cpu().numpy()
+    h = hashlib.sha256()
+    for i in range(len(groups)):
+        d = groups[i]
+        h.update(out[d.offset:d.offset + d.k * d.shard_stride].reshape(d.k, d.shard_stride)
+                 [:, :d.len].tobytes())
+    assert h.hexdigest() == F["data_out_sha256"]
+
+
+def test_ragged_decode_vs_oracle_mixed(gpu, oracle):
+    """Random codes (small and big: e > 10 and k > 64 go to the workgroup
+    kernel), random lengths incl. 0/1/17/3000, random erasure counts incl.
+    too few; every group against the C oracle, padding rule checked."""
+    import torch
+    import udpspeeder_amd as u
+    from udpspeeder_amd import synth
+    rng = np.random.default_rng(21)
+    G = 600
+    ks = rng.integers(1, 40, G)
+    ms = rng.integers(0, 30, G)
+    ks[:40] = rng.integers(60, 200, 40)
+    ms[:40] = rng.integers(1, 56, 40)
+    ls = rng.integers(0, 3000, G)
+    ls[40:46] = [0, 1, 17, 1280, 1281, 3000]
+    groups, total = u.make_groups(ks, ks + ms, ls)
+    host = rng.integers(0, 256, total, dtype=np.uint8)
+    flags = np.zeros((G, 256), np.uint8)
+    for i in range(G):
+        n = int(ks[i] + ms[i])
+        flags[i, :n] = 1
+        ne = int(rng.integers(0, ms[i] + 2))  # sometimes one too many
+        flags[i, rng.choice(n, min(ne, n), replace=False)] = 0
+    base = upload(host, gpu)
+    bits = torch.from_numpy(synth.present_bits(flags).view(np.int32)).to(gpu)
+    st = u.rs.decode_ragged(base, groups, bits).cpu().numpy()
+    out = base.cpu().numpy()
+    for i in range(G):
+        d = groups[i]
+        n, k = d.n, d.k
+        seg = host[d.offset:d.offset + n * d.shard_stride].copy()
+        ost = oracle.decode_batch(k, n, seg, 0, d.shard_stride, d.len, 1, flags[i:i + 1, :n])
+        assert st[i] == ost[0], (i, k, n, st[i], ost[0])
+        got = out[d.offset:d.offset + n * d.shard_stride].reshape(n, d.shard_stride)
+        exp = seg.reshape(n, d.shard_stride)
+        org = host[d.offset:d.offset + n * d.shard_stride].reshape(n, d.shard_stride)
+        if st[i] == 0:
+            assert (got[:k, :d.len] == exp[:k, :d.len]).all(), (i, k, n, d.len)
+        pad = pad_end(d.len, d.shard_stride)
+        assert (got[:, pad:] == org[:, pad:]).all(), i
+        assert (got[k:] == org[k:]).all(), i  # parity slots untouched
+
+
+def test_ragged_decode_dev_unresident_code(gpu, oracle):
+    """The device-descriptor form: resident codes decode, a code that was
+    never made resident reports RSMI_DEC_UNSUPPORTED and is left alone."""
+    import torch
+    import udpspeeder_amd as u
+    from udpspeeder_amd import synth
+    from udpspeeder_amd._lib import RSMI_DEC_UNSUPPORTED
+    ks = np.array([20, 13, 251]); ms = np.array([10, 7, 3]); ls = np.array([1250, 700, 100])
+    u.prepare_code(20, 30)
+    u.prepare_code(13, 20)
+    groups, total = u.make_groups(ks, ks + ms, ls)
+    rng = np.random.default_rng(2)
+    host = rng.integers(0, 256, total, dtype=np.uint8)
+    flags = np.zeros((3, 256), np.uint8)
+    for i in range(3):
+        flags[i, :ks[i] + ms[i]] = 1
+        flags[i, [0, 2]] = 0
+    base = upload(host, gpu)
+    bits = torch.from_numpy(synth.present_bits(flags).view(np.int32)).to(gpu)
+    st = u.rs.decode_ragged_dev(base, u.rs.groups_to_device(groups, gpu), 3, bits, kmax=20)
+    st = st.cpu().numpy()
+    out = base.cpu().numpy()
+    assert st.tolist() == [0, 0, RSMI_DEC_UNSUPPORTED]
+    d = groups[2]
+    assert (out[d.offset:d.offset + d.n * d.shard_stride] ==
+            host[d.offset:d.offset + d.n * d.shard_stride]).all()
+    for i in range(2):
+        d = groups[i]
+        seg = host[d.offset:d.offset + d.n * d.shard_stride].copy()
+        oracle.decode_batch(d.k, d.n, seg, 0, d.shard_stride, d.len, 1, flags[i:i + 1, :d.n])
+        got = out[d.offset:d.offset + d.n * d.shard_stride].reshape(d.n, d.shard_stride)
+        assert (got[:d.k, :d.len] == seg.reshape(d.n, d.shard_stride)[:d.k, :d.len]).all()
+
+
 # ---------------------------------------------------------------- drop-in shim
 def test_compat_kat_misc_unit_test(gpu, golden):
     """misc.cpp:335-361 through the reference-mangled rs_encode2/rs_decode2."""

@@ -144,3 +144,28 @@ def test_prng_pins(golden):
 def oracle_table():
     from oracle.cpu import Oracle
     return Oracle().rs_from_str(C3_STR)
+
+
+def test_c3_ragged_decode_digest(oracle, golden):
+    """The C restatement reproduces the reference's full-size C3 ragged
+    non-codeword decode digest (tests/golden/full_hashes.json)."""
+    from oracle.cpu import ragged_erasures
+    F = golden.full["c3_ragged_decode"]
+    ty = np.array([y for _, y in oracle.rs_from_str(F["fec"])], np.int64)
+    kk, mm, ll = ragged_draw(F["ragged_seed"], 0, F["groups"], ty)
+    pres = ragged_erasures(F["erase_seed"], 0, kk + mm, mm, F["erasures"])
+    h = hashlib.sha256()
+    rebuilt = 0
+    for g in range(F["groups"]):
+        k, m, ln = int(kk[g]), int(mm[g]), int(ll[g])
+        n = k + m
+        buf = np.zeros((n, ln), np.uint8)
+        buf[:k] = group_data(DATA_SEED, g, 1, k, ln)[0]
+        buf[k:] = group_data(F["parity_seed"], g, 1, m, ln)[0]
+        p = pres[g:g + 1, :n]
+        st = oracle.decode_batch(k, n, buf.reshape(-1), 0, ln, ln, 1, p)
+        assert st[0] == 0
+        rebuilt += int((p[0, :k] == 0).sum())
+        h.update(buf[:k].tobytes())
+    assert rebuilt == F["rebuilt_rows"]
+    assert h.hexdigest() == F["data_out_sha256"]

@@ -67,3 +67,18 @@ def test_gloo_world2_partition():
     assert all(p.exitcode == 0 for p in ps)
     lo, hi, tmax = q.get(timeout=5)
     assert lo == 1 and hi == 1 and tmax == 2.0
+
+
+def test_ragged_erasures_match_oracle():
+    rng = np.random.default_rng(4)
+    ks = rng.integers(1, 60, 3000)
+    ms = rng.integers(0, 40, 3000)
+    ms[:5] = [0, 1, 2, 3, 4]
+    a = synth.ragged_erasures(synth.ERASE_SEED, 7, ks + ms, ms, 5)
+    b = cpu.ragged_erasures(cpu.ERASE_SEED, 7, ks + ms, ms, 5)
+    assert (a == b).all()
+    assert ((a.sum(1)) == ks + ms - np.minimum(ms, 5)).all()
+    bits = synth.present_bits(a)
+    assert bits.dtype == np.uint32 and bits.shape == (3000, 8)
+    back = np.unpackbits(bits.view(np.uint8), axis=1, bitorder="little")
+    assert (back == a).all()

@@ -22,6 +22,7 @@ RSMI_OPT_FUSED_DECODE = 2
 RSMI_DEC_OK = 0
 RSMI_DEC_TOO_FEW = -1
 RSMI_DEC_SINGULAR = 1
+RSMI_DEC_UNSUPPORTED = 2
 
 # Mangled C++ names of the drop-in surface (include/rs_compat.h); these are the
 # exact symbols the reference's objects link against (lib/rs.h, lib/fec.h).
@@ -97,6 +98,9 @@ def _bind(lib: C.CDLL) -> C.CDLL:
         "rsmi_encode_ragged_plan": ([vp, vp, vp], i32),
         "rsmi_ragged_plan_uses_bitslice": ([vp], i32),
         "rsmi_ragged_plan_destroy": ([vp], None),
+        "rsmi_decode_ragged_plan": ([vp, vp, vp, vp, vp], i32),
+        "rsmi_decode_ragged_dev": ([vp, i64, vp, vp, vp, i32, vp], i32),
+        "rsmi_decode_ragged": ([vp, i64, vp, vp, vp, vp], i32),
         "rsmi_encode_pinned": ([i32, i32, vp, i64, vp, i64, i64, i32, i64, i64], i32),
         "rsmi_decode_pinned": ([i32, i32, vp, i64, i64, i32, i64, vp, vp, i64], i32),
         "rsmi_cook_ctx_create": ([C.c_char_p, i32, vp], i32),

@@ -293,6 +293,22 @@ int encode_ragged_dev(const rsmi_group *dg, int64_t ngroups, uint8_t *base, hipS
     return RSMI_OK;
 }
 
+int decode_ragged_dev(const rsmi_group *dg, int64_t ngroups, uint8_t *base,
+                      const uint32_t *present_bits, int32_t *status, int kmax, hipStream_t s) {
+    if (ngroups < 0) return fail(RSMI_ERR_INVALID, "negative ngroups");
+    if (ngroups == 0) return RSMI_OK;
+    if (!dg || !base || !present_bits || !status)
+        return fail(RSMI_ERR_INVALID, "null descriptors/base/present_bits/status");
+    if (((uintptr_t)base) % 16) return fail(RSMI_ERR_INVALID, "base must be 16-aligned");
+    int rc;
+    Device *D = current(&rc);
+    if (!D) return rc;
+    hipError_t e = launch_decode_ragged(dg, ngroups, base, present_bits, status, kmax,
+                                        D->code_dir, D->ptab, D->gftab, s);
+    if (e != hipSuccess) return hip_fail(e, "ragged decode launch");
+    return RSMI_OK;
+}
+
 uint64_t *device_code_dir(int *rc) {
     Device *D = current(rc);
     return D ? D->code_dir : nullptr;
@@ -625,6 +641,29 @@ int rsmi_encode_ragged(const rsmi_group *groups, int64_t ngroups, uint8_t *base,
     if (rc) return rc;
     if (e != hipSuccess) {
         rsmi::set_error(std::string("ragged encode: ") + hipGetErrorString(e));
+        return RSMI_ERR_HIP;
+    }
+    return RSMI_OK;
+}
+
+int rsmi_decode_ragged_dev(const rsmi_group *groups, int64_t ngroups, uint8_t *base,
+                           const uint32_t *present_bits, int32_t *status, int kmax, void *stream) {
+    return rsmi::decode_ragged_dev(groups, ngroups, base, present_bits, status, kmax,
+                                   (hipStream_t)stream);
+}
+
+int rsmi_decode_ragged(const rsmi_group *groups, int64_t ngroups, uint8_t *base,
+                       const uint32_t *present_bits, int32_t *status, void *stream) {
+    if (ngroups == 0) return RSMI_OK;
+    rsmi_ragged_plan *plan = nullptr;
+    int rc = rsmi_ragged_plan_create(groups, ngroups, &plan);
+    if (rc) return rc;
+    rc = rsmi_decode_ragged_plan(plan, base, present_bits, status, stream);
+    const hipError_t e = hipStreamSynchronize((hipStream_t)stream);
+    rsmi_ragged_plan_destroy(plan);
+    if (rc) return rc;
+    if (e != hipSuccess) {
+        rsmi::set_error(std::string("ragged decode: ") + hipGetErrorString(e));
         return RSMI_ERR_HIP;
     }
     return RSMI_OK;

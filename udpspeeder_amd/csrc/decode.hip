@@ -1,5 +1,5 @@
-// decode.hip -- fused batched RS decode for gfx950: one wavefront per group
-// builds that group's decode matrix in LDS and streams the reconstruction.
+// decode.hip -- batched RS decode for gfx950: one wavefront per group builds
+// that group's decode matrix and streams the reconstruction.
 //
 // Semantics are rs_decode2's (lib/rs.cpp:21-40 -> lib/fec.cpp:838-882): the k
 // survivors used are the first k present shards in ascending index order; a
@@ -8,10 +8,12 @@
 //     d_E = A^-1 (p_R + B d_P),   A = enc[R][E],  B = enc[R][P]
 // Gauss-Jordan on [A | M] (M's column per survivor: a unit vector for a parity
 // survivor, enc[R][s] for a data survivor) leaves [I | coef]; the inverse is
-// unique, so coef equals the rows fec_decode derives.  Rebuilt rows are
-// written into their own (data) slots.
+// unique, so coef equals the rows fec_decode derives.  No pivot search is
+// needed: every leading minor of A is a square submatrix of the code's parity
+// rows, invertible because the code is MDS.  Rebuilt rows are written into
+// their own (data) slots.
 //
-// Per wave:
+// Per wave and group:
 //   1. ballot the group's present flags -> sel[k], miss[e], status;
 //   2. issue the first RING survivor loads (they fly during step 3);
 //   3. Gauss-Jordan with column c of [A | M] in lane c (e bytes in registers,
@@ -21,9 +23,15 @@
 //      kernels.hip) in LDS;
 //   4. stream: per survivor, 5 dwords per lane (one 1-KiB dwordx4 wave-load +
 //      one 256-B dword wave-load cover a 1280-B tile), GF multiply-accumulate
-//      into e row accumulators, prefetch survivor j+RING; store e rows.
+//      into the row accumulators, prefetch survivor j+RING; store the rows.
 // Buffer descriptors with out-of-range offsets handle ragged tails: those
 // loads read 0 and those stores are dropped.
+//
+// Kernels: k_decode_fused (uniform batch: one code, the code's parity rows in
+// LDS), k_decode_ragged (every group its own k, n, len, stride; parity rows
+// read through the device code directory) and k_decode_ragged_big (one
+// workgroup per group for the groups the one-wave form defers: e > 10, k > 32
+// or a slot extent >= 2 GiB).
 #include "rsmi_internal.hpp"
 
 namespace rsmi {
@@ -34,30 +42,23 @@ constexpr int kWaves = 4;      // waves per block (one group each)
 #define DEC_RING 4
 #endif
 #ifndef DEC_LD_AUX
-#define DEC_LD_AUX 0           // cache policy of the survivor loads (2 = nt: 9 % faster alone,
-                               // but the next encode is 1.5 % slower: no gain in bench.py)
+#define DEC_LD_AUX 0           // cache policy of the survivor loads (2 = nt)
 #endif
 #ifndef DEC_ST_AUX
 #define DEC_ST_AUX 0           // cache policy of the rebuilt-row stores
 #endif
 constexpr int kRing = DEC_RING;  // survivors in flight per wave
-static_assert(kRing % 2 == 0, "ring slots are consumed in pairs under DEC_PAIR");
-constexpr int kRows = 10;      // max e handled by the fused kernel (emax <= kRows)
+constexpr int kRows = 10;      // max e handled by the one-wave kernels
 constexpr int kPass = 5;       // rows accumulated per pass over the survivors
 constexpr int kTile = 1280;    // bytes per lane-tile pass (64 x 16 + 64 x 4)
 #ifndef DEC_ST_SGPR
 #define DEC_ST_SGPR 0          // 1: row offset of the rebuilt-row stores in soffset (see bitslice.hip
                                // DevIO::store: no hazard wait state is inserted for that form)
 #endif
-#ifndef DEC_PAIR
-#define DEC_PAIR 0             // fold survivors in pairs (fewer XORs, more VGPRs)
-#endif
-#ifndef DEC_FENCE
-#define DEC_FENCE 0            // agent-scope release at the end of every wave
-#endif
 #ifndef DEC_OCC
 #define DEC_OCC 4              // waves per SIMD the register budget is cut for
 #endif
+constexpr int kDefer = 0x100;  // internal status: left for k_decode_ragged_big
 
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
     return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
@@ -69,7 +70,34 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-constexpr int kRowsAt = 6144;  // smem: s01 | s2 | exp | log | inv | parity rows | wave slices
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kTabBytes = 6144;  // smem: s01 | s2 | exp | log | inv, then per-kernel regions
+
+// The block-shared tables: v_perm split tables of all 256 coefficients, GF
+// exp/log and inverses.
+struct Tables {
+    const uint4 *s01;
+    const uint32_t *s2;
+    const uint8_t *lexp, *llog, *linv;
+};
+
+__device__ __forceinline__ Tables load_tables(uint8_t *smem, const uint32_t *ptab,
+                                              const uint8_t *gftab) {
+    uint4 *s01 = reinterpret_cast<uint4 *>(smem);              // 256 x 16 B
+    uint32_t *s2 = reinterpret_cast<uint32_t *>(smem + 4096);  // 256 x 4 B
+    uint8_t *lexp = smem + 5120;                               // 512
+    uint8_t *llog = smem + 5632;                               // 256
+    uint8_t *linv = smem + 5888;                               // 256: x^-1
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) {
+        s01[i] = reinterpret_cast<const uint4 *>(ptab + i * kPtabDwords)[0];
+        s2[i] = ptab[i * kPtabDwords + 4];
+    }
+    for (int i = threadIdx.x; i < 768; i += blockDim.x) smem[5120 + i] = gftab[i];
+    for (int i = threadIdx.x; i < 256; i += blockDim.x)
+        linv[i] = i ? gftab[255 - gftab[512 + i]] : 0;  // exp[255 - log x]
+    return Tables{s01, s2, lexp, llog, linv};
+}
 
 // c * x for a byte x (upper bits zero), c given by its split table (t, t2)
 __device__ __forceinline__ uint32_t gmul_t(uint4 t, uint32_t t2, uint32_t x) {
@@ -87,12 +115,261 @@ struct WaveLds {  // per-wave LDS slice
     uint32_t *tab;  // [k][kRows] entries of 8 dwords (T0lo T0hi T1lo T1hi T2 - - -)
 };
 
+__host__ __device__ inline int aug_bytes(int k) { return (kRows * (kRows + k) + 15) & ~15; }
+
 __host__ __device__ inline int wave_lds_bytes(int k) {
     // sel[256] miss[256] aug[kRows*(kRows+k)] tab[k*kRows*32]
-    const int aug = (kRows * (kRows + k) + 15) & ~15;
-    return 512 + aug + k * kRows * 32;
+    return 512 + aug_bytes(k) + k * kRows * 32;
 }
 
+__device__ __forceinline__ WaveLds wave_slice(uint8_t *wl, int k) {
+    return WaveLds{wl, wl + 256, wl + 512, reinterpret_cast<uint32_t *>(wl + 512 + aug_bytes(k))};
+}
+
+// ---- 1. survivor selection (rs.cpp:24-39) ------------------------------------
+// flag(b, idx) is the present flag of shard idx (b = idx rounded down to 64);
+// writes sel[0..k) (the first k present, ascending) and miss[0..e) (missing
+// data rows, ascending).  Returns the present count, e in e_out.
+template <class Flag>
+__device__ __forceinline__ int select_survivors(int k, int n, Flag flag, const WaveLds &L, int lane,
+                                                int &e_out) {
+    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+    int cnt = 0, e = 0;
+    for (int b = 0; b < n && cnt < k; b += 64) {
+        const int idx = b + lane;
+        const bool f = idx < n && flag(b, idx);
+        const uint64_t mk = __ballot(f);
+        const int rank = cnt + __popcll(mk & lt);
+        if (f && rank < k) L.sel[rank] = (uint8_t)idx;
+        cnt += __popcll(mk);
+    }
+    if (cnt >= k) {
+        for (int b = 0; b < k; b += 64) {
+            const int idx = b + lane;
+            const bool ms = idx < k && !flag(b, idx);
+            const uint64_t mk = __ballot(ms);
+            if (ms) L.miss[e + __popcll(mk & lt)] = (uint8_t)idx;
+            e += __popcll(mk);
+        }
+    }
+    // values that steer control flow are wave-uniform: say so, or the
+    // compiler wraps every buffer op below in a waterfall loop
+    e_out = __builtin_amdgcn_readfirstlane(e);
+    return __builtin_amdgcn_readfirstlane(cnt);
+}
+
+// ---- 3. Gauss-Jordan ------------------------------------------------------------
+// prow(R) points at the code's parity row R (R >= k: row R - k of the parity
+// rows).  Register form: lane c holds column c of [A | M], W = e + k <= 64.
+// Leaves coef[r][j] expanded into its split table at tab[j][r].
+template <class Row>
+__device__ __forceinline__ int gauss_jordan_regs(int k, int e, uint32_t sel_lane, const WaveLds &L,
+                                                 const Tables &T, Row prow, int lane) {
+    int st = RSMI_DEC_OK;
+    const int W = e + k;
+    // lane c holds column c: a missing data index (c < e) or survivor c - e
+    const uint32_t col = lane < e ? (uint32_t)L.miss[lane]
+                                  : (lane < W ? (uint32_t)L.sel[lane - e] : 0u);
+    uint32_t a[kRows];
+#pragma unroll
+    for (int r = 0; r < kRows; ++r) {
+        a[r] = 0;
+        if (r < e) {
+            const uint32_t R = __builtin_amdgcn_readlane(sel_lane, k - e + r);
+            const uint32_t v = prow(R)[col < (uint32_t)k ? col : 0u];
+            a[r] = (lane >= e && col >= (uint32_t)k) ? (uint32_t)(col == R) : v;
+        }
+    }
+#pragma unroll
+    for (int p = 0; p < kRows; ++p) {
+        if (p < e) {
+            const uint32_t piv = __builtin_amdgcn_readlane(a[p], p);
+            if (piv == 0) {
+                st = RSMI_DEC_SINGULAR;
+                break;
+            }
+            const uint32_t ip = __builtin_amdgcn_readfirstlane(T.linv[piv]);
+            a[p] = gmul_t(T.s01[ip], T.s2[ip], a[p]);
+#pragma unroll
+            for (int r = 0; r < kRows; ++r) {
+                if (r < e && r != p) {
+                    const uint32_t f = __builtin_amdgcn_readlane(a[r], p);
+                    a[r] ^= gmul_t(T.s01[f], T.s2[f], a[p]);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+    }
+    st = __builtin_amdgcn_readfirstlane(st);
+    if (st != RSMI_DEC_OK) return st;
+    // coef[r][j] sits in lane e + j: expand into split tables tab[j][r]
+    if (lane >= e && lane < W) {
+        uint32_t *dst = L.tab + (lane - e) * kRows * 8;
+#pragma unroll
+        for (int r = 0; r < kRows; ++r) {
+            if (r < e) {
+                reinterpret_cast<uint4 *>(dst + r * 8)[0] = T.s01[a[r]];
+                dst[r * 8 + 4] = T.s2[a[r]];
+            }
+        }
+    }
+    wave_sync();
+    return RSMI_DEC_OK;
+}
+
+// LDS form for W > 64 (k <= 64, e <= kRows): [A | M] in the wave's aug slice.
+template <class Row>
+__device__ __forceinline__ int gauss_jordan_lds(int k, int e, const WaveLds &L, const Tables &T,
+                                                Row prow, int lane) {
+    int st = RSMI_DEC_OK;
+    const int W = e + k;
+    for (int t = lane; t < e * W; t += 64) {
+        const int r = t / W, c = t - r * W;
+        const int R = L.sel[k - e + r];
+        const uint8_t *pr = prow(R);
+        uint8_t v;
+        if (c < e) {
+            v = pr[L.miss[c]];
+        } else {
+            const int s = L.sel[c - e];
+            v = (s >= k) ? (uint8_t)(s == R) : pr[s];
+        }
+        L.aug[t] = v;
+    }
+    wave_sync();
+    for (int p = 0; p < e && st == RSMI_DEC_OK; ++p) {
+        const uint32_t piv = __builtin_amdgcn_readfirstlane(L.aug[p * W + p]);
+        if (piv == 0) {
+            st = RSMI_DEC_SINGULAR;
+            break;
+        }
+        const uint32_t ipiv = __builtin_amdgcn_readfirstlane(T.lexp[255 - T.llog[piv]]);
+        for (int c = p + 1 + lane; c < W; c += 64)
+            L.aug[p * W + c] = (uint8_t)gmul(T.lexp, T.llog, ipiv, L.aug[p * W + c]);
+        wave_sync();
+        const int cols = W - p - 1;
+        for (int t = lane; t < e * cols; t += 64) {
+            const int r = t / cols;
+            if (r == p) continue;
+            const int c = p + 1 + (t - r * cols);
+            const uint32_t f = L.aug[r * W + p];
+            if (f) L.aug[r * W + c] ^= (uint8_t)gmul(T.lexp, T.llog, f, L.aug[p * W + c]);
+        }
+        wave_sync();
+    }
+    st = __builtin_amdgcn_readfirstlane(st);
+    if (st != RSMI_DEC_OK) return st;
+    // expand coef[r][j] = aug[r][e + j] into split tables tab[j][r]
+    for (int t = lane; t < e * k; t += 64) {
+        const int r = t / k, j = t - r * k;
+        const uint32_t c = L.aug[r * W + e + j];
+        uint32_t *dst = L.tab + (j * kRows + r) * 8;
+        reinterpret_cast<uint4 *>(dst)[0] = T.s01[c];
+        dst[4] = T.s2[c];
+    }
+    wave_sync();
+    return RSMI_DEC_OK;
+}
+
+// ---- 2 + 4. survivor streaming ---------------------------------------------------
+// One group's reconstruction: the wave-uniform descriptor covers the group's
+// n slots; survivor j's slot offset sits in lane j of so_lane, missing row
+// r's in lane r of mo_lane.
+struct Rebuild {
+    __amdgpu_buffer_rsrc_t rsrc;
+    uint32_t so_lane, mo_lane;
+    int k, e, len, lpad;
+    uint32_t v16, v4;
+    u32x4 rq[kRing];
+    uint32_t rd[kRing];
+
+    __device__ __forceinline__ void load(int q, int j) {
+        const uint32_t so = __builtin_amdgcn_readlane(so_lane, j);
+        rq[q] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, v16, so, DEC_LD_AUX);
+        rd[q] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, v4, so, DEC_LD_AUX);
+    }
+    // whole cache lines where the slot has room (rsmi.h padding rule)
+    __device__ __forceinline__ void start_tile(int toff, int lane) {
+        const int tlen = lpad - toff;
+        v16 = (16 * lane < tlen) ? (uint32_t)(toff + 16 * lane) : 0x80000000u;
+        v4 = (1024 + 4 * lane < tlen) ? (uint32_t)(toff + 1024 + 4 * lane) : 0x80000000u;
+#pragma unroll
+        for (int q = 0; q < kRing; ++q)
+            if (q < k) load(q, q);
+    }
+    // passes over (tile, block of kPass rows); tile 0's first loads were
+    // issued by start_tile(0) before the Gauss-Jordan
+    __device__ __forceinline__ void run(const uint32_t *tab, int lane) {
+        for (int toff = 0; toff < len; toff += kTile) {
+            for (int rb = 0; rb < e; rb += kPass) {
+                if (toff || rb) start_tile(toff, lane);
+                uint32_t acc[kPass][5];
+#pragma unroll
+                for (int r = 0; r < kPass; ++r)
+#pragma unroll
+                    for (int w = 0; w < 5; ++w) acc[r][w] = 0;
+                for (int jb = 0; jb < k; jb += kRing) {
+#pragma unroll
+                    for (int q = 0; q < kRing; ++q) {
+                        const int j = jb + q;
+                        if (j < k) {
+                            // the 3-bit split selectors of the survivor's 5 dwords
+                            const uint32_t x[5] = {rq[q].x, rq[q].y, rq[q].z, rq[q].w, rd[q]};
+                            uint32_t a0[5], a1[5], a2[5];
+#pragma unroll
+                            for (int w = 0; w < 5; ++w) {
+                                a0[w] = x[w] & 0x07070707u;
+                                a1[w] = (x[w] >> 3) & 0x07070707u;
+                                a2[w] = (x[w] >> 6) & 0x03030303u;
+                            }
+                            // ring slot q took survivor j: load survivor j + kRing into it
+                            if (j + kRing < k) load(q, j + kRing);
+                            const uint32_t *ta = tab + (j * kRows + rb) * 8;
+#pragma unroll
+                            for (int r = 0; r < kPass; ++r) {
+                                if (rb + r < e) {
+                                    const uint4 t = reinterpret_cast<const uint4 *>(ta + r * 8)[0];
+                                    const uint32_t t2 = ta[r * 8 + 4];
+#pragma unroll
+                                    for (int w = 0; w < 5; ++w)
+                                        acc[r][w] ^= xor3(__builtin_amdgcn_perm(t.y, t.x, a0[w]),
+                                                          __builtin_amdgcn_perm(t.w, t.z, a1[w]),
+                                                          __builtin_amdgcn_perm(t2, t2, a2[w]));
+                                }
+                            }
+                        }
+                    }
+                }
+#pragma unroll
+                for (int r = 0; r < kPass; ++r) {
+                    if (rb + r < e) {
+                        const uint32_t so = __builtin_amdgcn_readlane(mo_lane, rb + r);
+                        const u32x4 v = {acc[r][0], acc[r][1], acc[r][2], acc[r][3]};
+#if DEC_ST_SGPR
+                        __builtin_amdgcn_raw_buffer_store_b128(v, rsrc, v16, so, DEC_ST_AUX);
+                        __builtin_amdgcn_raw_buffer_store_b32(acc[r][4], rsrc, v4, so, DEC_ST_AUX);
+#else
+                        __builtin_amdgcn_raw_buffer_store_b128(v, rsrc, v16 + so, 0, DEC_ST_AUX);
+                        __builtin_amdgcn_raw_buffer_store_b32(acc[r][4], rsrc, v4 + so, 0, DEC_ST_AUX);
+#endif
+                    }
+                }
+            }
+        }
+    }
+};
+
+// descriptor base through readfirstlane (cdna_hip_programming.md T20)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t group_rsrc(const uint8_t *gbase, uint32_t bytes) {
+    const uint64_t gb = (uint64_t)(uintptr_t)gbase;
+    const uint64_t gbu = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(gb >> 32)) << 32) |
+                         (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)gb);
+    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<uint8_t *>(gbu), 0, (int)bytes,
+                                             0x00020000);
+}
+
+// The uniform kernel keeps its own straight-line form (not Rebuild / the
+// helper functions): written that way it fits 4 waves/SIMD without spills.
 __global__ __launch_bounds__(256, DEC_OCC) void k_decode_fused(UniformArgs a, const uint8_t *present,
                                                       const uint8_t *prows, int32_t *status_out,
                                                       const uint32_t *ptab, const uint8_t *gftab) {
@@ -107,8 +384,8 @@ __global__ __launch_bounds__(256, DEC_OCC) void k_decode_fused(UniformArgs a, co
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     const int rows_bytes = ((n - k) * k + 15) & ~15;
-    uint8_t *lrows = smem + kRowsAt;  // the code's parity rows, (n-k) x k
-    uint8_t *wl = smem + kRowsAt + rows_bytes + wid * wbytes;
+    uint8_t *lrows = smem + kTabBytes;  // the code's parity rows, (n-k) x k
+    uint8_t *wl = smem + kTabBytes + rows_bytes + wid * wbytes;
     WaveLds L{wl, wl + 256, wl + 512,
               reinterpret_cast<uint32_t *>(wl + 512 + ((kRows * (kRows + k) + 15) & ~15))};
 
@@ -336,39 +613,11 @@ __global__ __launch_bounds__(256, DEC_OCC) void k_decode_fused(UniformArgs a, co
                 for (int r = 0; r < kPass; ++r)
 #pragma unroll
                     for (int w = 0; w < 5; ++w) acc[r][w] = 0;
-                // with DEC_PAIR, survivors go in pairs: the six split products of
-                // two survivors fold into a row with three 3-input XORs
                 for (int jb = 0; jb < k; jb += kRing) {
 #pragma unroll
-                    for (int q = 0; q < kRing; q += DEC_PAIR ? 2 : 1) {
+                    for (int q = 0; q < kRing; ++q) {
                         const int j = jb + q;
-                        if (DEC_PAIR && j + 1 < k) {
-                            uint32_t a0[5], a1[5], a2[5], b0[5], b1[5], b2[5];
-                            split(rq[q], rd[q], a0, a1, a2);
-                            split(rq[q + 1], rd[q + 1], b0, b1, b2);
-                            refill(q, j);
-                            refill(q + 1, j + 1);
-                            const uint32_t *ta = L.tab + (j * kRows + rb) * 8;
-                            const uint32_t *tb = ta + kRows * 8;
-#pragma unroll
-                            for (int r = 0; r < kPass; ++r) {
-                                if (rb + r < e) {
-                                    const uint4 t = reinterpret_cast<const uint4 *>(ta + r * 8)[0];
-                                    const uint32_t t2 = ta[r * 8 + 4];
-                                    const uint4 u = reinterpret_cast<const uint4 *>(tb + r * 8)[0];
-                                    const uint32_t u2 = tb[r * 8 + 4];
-#pragma unroll
-                                    for (int w = 0; w < 5; ++w) {
-                                        uint32_t x = xor3(acc[r][w], __builtin_amdgcn_perm(t.y, t.x, a0[w]),
-                                                          __builtin_amdgcn_perm(t.w, t.z, a1[w]));
-                                        x = xor3(x, __builtin_amdgcn_perm(t2, t2, a2[w]),
-                                                 __builtin_amdgcn_perm(u.y, u.x, b0[w]));
-                                        acc[r][w] = xor3(x, __builtin_amdgcn_perm(u.w, u.z, b1[w]),
-                                                         __builtin_amdgcn_perm(u2, u2, b2[w]));
-                                    }
-                                }
-                            }
-                        } else if (j < k) {
+                        if (j < k) {
                             uint32_t a0[5], a1[5], a2[5];
                             split(rq[q], rd[q], a0, a1, a2);
                             refill(q, j);
@@ -407,9 +656,200 @@ __global__ __launch_bounds__(256, DEC_OCC) void k_decode_fused(UniformArgs a, co
         if (lane == 0 && status_out) status_out[g] = RSMI_DEC_OK;
         wave_sync();  // the LDS slice is rewritten by the next group
     }
-#if DEC_FENCE
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-#endif
+}
+
+// ---- ragged batches ---------------------------------------------------------------
+// One wave per group; each group its own (k, n, len, shard_stride, offset) from
+// its rsmi_group descriptor, present flags as a 256-bit mask per group (8
+// words: bit j of word j/32 = shard j received), parity rows through the
+// device code directory.  Groups this form cannot take (e > kRows, k > kmax,
+// or n slots spanning >= 2 GiB) get kDefer for k_decode_ragged_big.
+__global__ __launch_bounds__(256, DEC_OCC) void k_decode_ragged(
+    const rsmi_group *groups, int64_t ngroups, uint8_t *base, const uint32_t *present,
+    int32_t *status_out, const uint64_t *code_dir, const uint32_t *ptab, const uint8_t *gftab,
+    int kmax) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const Tables T = load_tables(smem, ptab, gftab);
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const WaveLds L = wave_slice(smem + kTabBytes + wid * wave_lds_bytes(kmax), kmax);
+    __syncthreads();
+
+    const int64_t nwaves = (int64_t)gridDim.x * kWaves;
+    for (int64_t g = (int64_t)blockIdx.x * kWaves + wid; g < ngroups; g += nwaves) {
+        const rsmi_group d = groups[g];
+        const int k = __builtin_amdgcn_readfirstlane(d.k);
+        const int n = __builtin_amdgcn_readfirstlane(d.n);
+        const int len = __builtin_amdgcn_readfirstlane(d.len);
+        const uint32_t ss = __builtin_amdgcn_readfirstlane(d.shard_stride);
+        const uint64_t off = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(d.offset >> 32)) << 32) |
+                             (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)d.offset);
+        const uint8_t *rows = (k >= 1 && n > k && n <= 256)
+                                  ? reinterpret_cast<const uint8_t *>(code_dir[k * 257 + n])
+                                  : nullptr;
+        if (k < 1 || n < k || n > 256 || (n > k && !rows)) {
+            if (lane == 0) status_out[g] = RSMI_DEC_UNSUPPORTED;
+            continue;
+        }
+        const uint32_t w8 = present[g * 8 + (lane & 7)];  // lane i (< 8) holds word i of the mask
+        int e;
+        const int cnt = select_survivors(
+            k, n,
+            [&](int b, int idx) {
+                // words b/32 and b/32 + 1 cover shards b..b+63 (readlane ignores exec)
+                const uint32_t lo = __builtin_amdgcn_readlane(w8, (b >> 5) & 7);
+                const uint32_t hi = __builtin_amdgcn_readlane(w8, ((b >> 5) + 1) & 7);
+                return ((((idx & 32) ? hi : lo) >> (idx & 31)) & 1u) != 0;
+            },
+            L, lane, e);
+        wave_sync();
+        if (cnt < k || e == 0) {
+            if (lane == 0) status_out[g] = cnt < k ? RSMI_DEC_TOO_FEW : RSMI_DEC_OK;
+            continue;
+        }
+        if (e > kRows || k > kmax || k > 64 || (uint64_t)n * ss >= 0x80000000ull) {
+            if (lane == 0) status_out[g] = kDefer;
+            continue;
+        }
+        auto prow = [&](uint32_t R) { return rows + (R - k) * k; };
+        Rebuild B;
+        B.rsrc = group_rsrc(base + off, (uint32_t)(n * ss));
+        B.k = k;
+        B.e = e;
+        B.len = len;
+        B.lpad = (int)(((uint32_t)len + 127) / 128 * 128 < ss ? ((uint32_t)len + 127) / 128 * 128 : ss);
+        const uint32_t sel_lane = lane < k ? (uint32_t)L.sel[lane] : 0u;
+        B.so_lane = sel_lane * ss;
+        B.mo_lane = (lane < e ? (uint32_t)L.miss[lane] : 0u) * ss;
+        if (len > 0) B.start_tile(0, lane);
+        const int st = (e + k <= 64) ? gauss_jordan_regs(k, e, sel_lane, L, T, prow, lane)
+                                     : gauss_jordan_lds(k, e, L, T, prow, lane);
+        if (st != RSMI_DEC_OK) {
+            if (lane == 0) status_out[g] = st;
+            continue;
+        }
+        if (len > 0) B.run(L.tab, lane);
+        if (lane == 0) status_out[g] = RSMI_DEC_OK;
+        wave_sync();  // the LDS slice is rewritten by the next group
+    }
+}
+
+// The deferred groups: one 256-thread workgroup per group.  Gauss-Jordan on
+// [A | M] in LDS (e x (e + k) <= 128 x 256 bytes for n <= 256), coefficients
+// left in place, then each thread rebuilds dwords of up to 8 rows at a time
+// with the v_perm split tables.  Not a hot path: big codes only.
+constexpr int kBigAug = 128 * 256;
+constexpr int kBigRows = 8;
+
+__global__ __launch_bounds__(256) void k_decode_ragged_big(
+    const rsmi_group *groups, int64_t ngroups, uint8_t *base, const uint32_t *present,
+    int32_t *status_out, const uint64_t *code_dir, const uint32_t *ptab, const uint8_t *gftab) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const Tables T = load_tables(smem, ptab, gftab);
+    uint8_t *sel = smem + kTabBytes, *miss = sel + 256, *aug = miss + 256;
+    __shared__ int s_e;
+    const int tid = threadIdx.x, lane = tid & 63;
+    __syncthreads();
+    for (int64_t g = blockIdx.x; g < ngroups; g += gridDim.x) {
+        if (status_out[g] != kDefer) continue;  // uniform per block
+        const rsmi_group d = groups[g];
+        const int k = d.k, n = d.n, len = (int)d.len;
+        const uint64_t ss = d.shard_stride;
+        uint8_t *gb = base + d.offset;
+        const uint8_t *rows = reinterpret_cast<const uint8_t *>(code_dir[k * 257 + n]);
+        const uint32_t *pw = present + g * 8;
+        if (tid < 64) {  // wave 0 selects (the one-wave kernel found >= k present)
+            const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+            int cnt = 0, e = 0;
+            for (int b = 0; b < n && cnt < k; b += 64) {
+                const int idx = b + lane;
+                const bool f = idx < n && ((pw[idx >> 5] >> (idx & 31)) & 1u);
+                const uint64_t mk = __ballot(f);
+                const int rank = cnt + __popcll(mk & lt);
+                if (f && rank < k) sel[rank] = (uint8_t)idx;
+                cnt += __popcll(mk);
+            }
+            for (int b = 0; b < k; b += 64) {
+                const int idx = b + lane;
+                const bool ms = idx < k && !((pw[idx >> 5] >> (idx & 31)) & 1u);
+                const uint64_t mk = __ballot(ms);
+                if (ms) miss[e + __popcll(mk & lt)] = (uint8_t)idx;
+                e += __popcll(mk);
+            }
+            if (lane == 0) s_e = e;
+        }
+        __syncthreads();
+        const int e = s_e, W = e + k;
+        for (int t = tid; t < e * W; t += 256) {
+            const int r = t / W, c = t - r * W;
+            const int R = sel[k - e + r];
+            const uint8_t *pr = rows + (R - k) * k;
+            uint8_t v;
+            if (c < e) {
+                v = pr[miss[c]];
+            } else {
+                const int s = sel[c - e];
+                v = (s >= k) ? (uint8_t)(s == R) : pr[s];
+            }
+            aug[t] = v;
+        }
+        __syncthreads();
+        int st = RSMI_DEC_OK;
+        for (int p = 0; p < e; ++p) {
+            const uint32_t piv = aug[p * W + p];
+            if (piv == 0) {
+                st = RSMI_DEC_SINGULAR;
+                break;
+            }
+            const uint32_t ipiv = T.lexp[255 - T.llog[piv]];
+            for (int c = p + 1 + tid; c < W; c += 256)
+                aug[p * W + c] = (uint8_t)gmul(T.lexp, T.llog, ipiv, aug[p * W + c]);
+            __syncthreads();
+            const int cols = W - p - 1;
+            for (int t = tid; t < e * cols; t += 256) {
+                const int r = t / cols;
+                if (r == p) continue;
+                const int c = p + 1 + (t - r * cols);
+                const uint32_t f = aug[r * W + p];
+                if (f) aug[r * W + c] ^= (uint8_t)gmul(T.lexp, T.llog, f, aug[p * W + c]);
+            }
+            __syncthreads();
+        }
+        if (st == RSMI_DEC_OK) {
+            // coef[r][j] = aug[r][e + j]; rows in blocks of kBigRows, dwords per thread
+            const int words = (len + 3) >> 2;
+            for (int rb = 0; rb < e; rb += kBigRows) {
+                for (int w = tid; w < words; w += 256) {
+                    uint32_t acc[kBigRows];
+#pragma unroll
+                    for (int r = 0; r < kBigRows; ++r) acc[r] = 0;
+                    for (int j = 0; j < k; ++j) {
+                        const uint32_t x =
+                            *reinterpret_cast<const uint32_t *>(gb + sel[j] * ss + 4 * w);
+                        const uint32_t a0 = x & 0x07070707u, a1 = (x >> 3) & 0x07070707u,
+                                       a2 = (x >> 6) & 0x03030303u;
+#pragma unroll
+                        for (int r = 0; r < kBigRows; ++r) {
+                            if (rb + r < e) {
+                                const uint32_t c = aug[(rb + r) * W + e + j];
+                                const uint4 t = T.s01[c];
+                                const uint32_t t2 = T.s2[c];
+                                acc[r] ^= xor3(__builtin_amdgcn_perm(t.y, t.x, a0),
+                                               __builtin_amdgcn_perm(t.w, t.z, a1),
+                                               __builtin_amdgcn_perm(t2, t2, a2));
+                            }
+                        }
+                    }
+#pragma unroll
+                    for (int r = 0; r < kBigRows; ++r)
+                        if (rb + r < e)
+                            *reinterpret_cast<uint32_t *>(gb + miss[rb + r] * ss + 4 * w) = acc[r];
+                }
+            }
+        }
+        if (tid == 0) status_out[g] = st;
+        __syncthreads();  // sel / miss / aug are rewritten by the next group
+    }
 }
 
 }  // namespace
@@ -418,14 +858,14 @@ bool decode_fused_ok(int k, int n, int64_t group_stride, int64_t shard_stride, i
     const int m = n - k;
     const int emax = k < m ? k : m;
     return emax <= kRows && k <= 64 && n * shard_stride < (int64_t(1) << 31) && len > 0 &&
-           kRowsAt + ((m * k + 15) & ~15) + kWaves * wave_lds_bytes(k) <= 64 * 1024 &&
+           kTabBytes + ((m * k + 15) & ~15) + kWaves * wave_lds_bytes(k) <= 64 * 1024 &&
            group_stride >= n * shard_stride;
 }
 
 hipError_t launch_decode_fused(const UniformArgs &a, const uint8_t *present,
                                const uint8_t *parity_rows, int32_t *status,
                                const uint32_t *ptab, const uint8_t *gftab, hipStream_t s) {
-    const size_t lds = kRowsAt + (size_t)(((a.n - a.k) * a.k + 15) & ~15) +
+    const size_t lds = kTabBytes + (size_t)(((a.n - a.k) * a.k + 15) & ~15) +
                        (size_t)kWaves * wave_lds_bytes(a.k);
     int64_t blocks = (a.ngroups + kWaves - 1) / kWaves;
     const int64_t cap = 256 * 8;
@@ -433,6 +873,25 @@ hipError_t launch_decode_fused(const UniformArgs &a, const uint8_t *present,
     if (blocks < 1) blocks = 1;
     k_decode_fused<<<(unsigned)blocks, 64 * kWaves, lds, s>>>(a, present, parity_rows, status,
                                                              ptab, gftab);
+    return hipGetLastError();
+}
+
+hipError_t launch_decode_ragged(const rsmi_group *groups, int64_t ngroups, uint8_t *base,
+                                const uint32_t *present_bits, int32_t *status, int kmax,
+                                const uint64_t *code_dir, const uint32_t *ptab,
+                                const uint8_t *gftab, hipStream_t s) {
+    if (ngroups <= 0) return hipSuccess;
+    kmax = kmax < 1 ? 1 : (kmax > 32 ? 32 : kmax);  // larger k: the workgroup kernel
+    const size_t lds = kTabBytes + (size_t)kWaves * wave_lds_bytes(kmax);
+    int64_t blocks = (ngroups + kWaves - 1) / kWaves;
+    if (blocks > 256 * 8) blocks = 256 * 8;
+    k_decode_ragged<<<(unsigned)blocks, 64 * kWaves, lds, s>>>(groups, ngroups, base, present_bits,
+                                                              status, code_dir, ptab, gftab, kmax);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    const int64_t bb = ngroups < 256 * 4 ? ngroups : 256 * 4;
+    k_decode_ragged_big<<<(unsigned)bb, 256, kTabBytes + 512 + kBigAug, s>>>(
+        groups, ngroups, base, present_bits, status, code_dir, ptab, gftab);
     return hipGetLastError();
 }
 

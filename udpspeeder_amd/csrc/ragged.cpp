@@ -19,12 +19,15 @@ namespace rsmi {
 int prepare_code(int k, int n);
 void set_error(const std::string &m);
 uint64_t *device_code_dir(int *rc);
+int decode_ragged_dev(const rsmi_group *dg, int64_t ngroups, uint8_t *base,
+                      const uint32_t *present_bits, int32_t *status, int kmax, hipStream_t s);
 const uint32_t *device_ptab(int *rc);
 }  // namespace rsmi
 
 struct rsmi_ragged_plan {
     int device = -1;
     int64_t ngroups = 0;
+    int kmax = 1;             // largest k in the batch (sizes the decode kernel's LDS)
     bool bitslice = false;
     uint32_t bytes = 0;       // extent of the batch from base (bitslice path)
     uint32_t nwaves = 0;
@@ -49,6 +52,7 @@ extern "C" int rsmi_ragged_plan_create(const rsmi_group *g, int64_t ngroups,
         return fail(RSMI_ERR_INVALID, "invalid ragged plan arguments");
     *out = nullptr;
     uint64_t extent = 0;
+    int kmax = 1;
     bool bs = ngroups < (int64_t(1) << 20);
     std::vector<int> code_of((size_t)ngroups, -1);
     std::vector<uint8_t> seen(257 * 257, 0);
@@ -57,6 +61,7 @@ extern "C" int rsmi_ragged_plan_create(const rsmi_group *g, int64_t ngroups,
         if (d.k < 1 || d.n < d.k || d.n > 256 || d.reserved != 0 || d.offset % 16 ||
             d.shard_stride % 16 || d.shard_stride < d.len)
             return fail(RSMI_ERR_INVALID, "bad rsmi_group at index " + std::to_string(i));
+        kmax = std::max(kmax, (int)d.k);
         const int key = d.k * 257 + d.n;
         if (!seen[key]) {
             seen[key] = 1;
@@ -79,6 +84,7 @@ extern "C" int rsmi_ragged_plan_create(const rsmi_group *g, int64_t ngroups,
         return fail(RSMI_ERR_HIP, "hipGetDevice (no usable GPU?)");
     }
     P->ngroups = ngroups;
+    P->kmax = kmax;
     P->bitslice = bs;
     P->bytes = (uint32_t)std::min<uint64_t>(extent, 0x7FFFFFFFull);
     std::vector<uint32_t> colmap, waves;
@@ -161,6 +167,14 @@ extern "C" int rsmi_encode_ragged_plan(const rsmi_ragged_plan *P, uint8_t *base,
     }
     if (e != hipSuccess) return fail(RSMI_ERR_HIP, std::string("ragged launch: ") + hipGetErrorString(e));
     return RSMI_OK;
+}
+
+extern "C" int rsmi_decode_ragged_plan(const rsmi_ragged_plan *P, uint8_t *base,
+                                       const uint32_t *present_bits, int32_t *status,
+                                       void *stream) {
+    if (!P) return fail(RSMI_ERR_INVALID, "null plan");
+    return rsmi::decode_ragged_dev(P->d_groups, P->ngroups, base, present_bits, status, P->kmax,
+                                   (hipStream_t)stream);
 }
 
 extern "C" int rsmi_ragged_plan_uses_bitslice(const rsmi_ragged_plan *P) {

@@ -55,6 +55,13 @@ hipError_t launch_decode_fused(const UniformArgs &a, const uint8_t *present,
                                const uint8_t *parity_rows, int32_t *status,
                                const uint32_t *ptab, const uint8_t *gftab, hipStream_t s);
 
+// Ragged decode (decode.hip): one-wave-per-group kernel, then the
+// workgroup-per-group kernel for the groups it defers.
+hipError_t launch_decode_ragged(const rsmi_group *groups, int64_t ngroups, uint8_t *base,
+                                const uint32_t *present_bits, int32_t *status, int kmax,
+                                const uint64_t *code_dir, const uint32_t *ptab,
+                                const uint8_t *gftab, hipStream_t s);
+
 // Bit-sliced encode kernels specialised at build time for hot (k,n) codes
 // (gen_bitslice.py -> gen/bitslice_codes.inc).  Returns hipErrorNotSupported
 // when (k,n) has no specialised kernel.

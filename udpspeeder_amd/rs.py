@@ -275,6 +275,22 @@ class RaggedPlan:
         check(lib().rsmi_encode_ragged_plan(self._h, base.data_ptr(), _stream_handle(stream)),
               "rsmi_encode_ragged_plan")
 
+    def decode(self, base, present_bits, status=None, stream=None):
+        """rs_decode2 on every group of the plan's layout; ``present_bits`` an
+        int32 [G, 8] CUDA tensor of 256-bit masks (synth.present_bits).
+        Returns the int32 [G] status tensor."""
+        import torch
+        _check_dev(base, "base")
+        _check_dev(present_bits, "present_bits", torch.int32)
+        if tuple(present_bits.shape) != (self.ngroups, 8) or not present_bits.is_contiguous():
+            raise ValueError("present_bits must be a contiguous [G, 8] int32 tensor")
+        if status is None:
+            status = torch.empty(self.ngroups, dtype=torch.int32, device=base.device)
+        check(lib().rsmi_decode_ragged_plan(self._h, base.data_ptr(), present_bits.data_ptr(),
+                                            status.data_ptr(), _stream_handle(stream)),
+              "rsmi_decode_ragged_plan")
+        return status
+
     def close(self) -> None:
         if self._h:
             import torch
@@ -295,6 +311,33 @@ def encode_ragged_dev(base, dev_groups, ngroups: int, stream=None) -> None:
     24 bytes per group); codes must be resident (prepare_code)."""
     check(lib().rsmi_encode_ragged_dev(dev_groups.data_ptr(), ngroups, base.data_ptr(),
                                        _stream_handle(stream)), "rsmi_encode_ragged_dev")
+
+
+def decode_ragged_dev(base, dev_groups, ngroups: int, present_bits, status=None, kmax: int = 64,
+                      stream=None):
+    """Graph-capturable ragged decode with a device descriptor tensor (24
+    bytes per group); codes must be resident (prepare_code).  Returns status."""
+    import torch
+    _check_dev(present_bits, "present_bits", torch.int32)
+    if status is None:
+        status = torch.empty(ngroups, dtype=torch.int32, device=base.device)
+    check(lib().rsmi_decode_ragged_dev(dev_groups.data_ptr(), ngroups, base.data_ptr(),
+                                       present_bits.data_ptr(), status.data_ptr(), kmax,
+                                       _stream_handle(stream)), "rsmi_decode_ragged_dev")
+    return status
+
+
+def decode_ragged(base, groups, present_bits, status=None, stream=None):
+    """rs_decode2 on every group of a ragged batch described by a host ctypes
+    rsmi_group array (make_groups); synchronous.  Returns status."""
+    import torch
+    _check_dev(present_bits, "present_bits", torch.int32)
+    if status is None:
+        status = torch.empty(len(groups), dtype=torch.int32, device=base.device)
+    check(lib().rsmi_decode_ragged(C.cast(groups, C.c_void_p), len(groups), base.data_ptr(),
+                                   present_bits.data_ptr(), status.data_ptr(),
+                                   _stream_handle(stream)), "rsmi_decode_ragged")
+    return status
 
 
 def prepare_code(k: int, n: int) -> None:

@@ -48,6 +48,41 @@ def erasure_present(seed: int, g0: int, ng: int, n: int, e: int, limit: int = 0)
     return pres
 
 
+def ragged_erasures(seed: int, g0: int, ns, ms, emax: int = 5) -> np.ndarray:
+    """[ng, 256] uint8 present flags for a ragged batch: group i (id g0 + i)
+    loses min(emax, m_i) distinct shards drawn from range(n_i) by a partial
+    Fisher-Yates on its stream (as erasure_present, with per-group n); flags
+    at and beyond n_i are 0."""
+    ns = np.asarray(ns, np.int64)
+    ms = np.asarray(ms, np.int64)
+    ng = len(ns)
+    e = np.minimum(emax, ms)
+    r = stream_words(seed, g0, ng, emax)
+    perm = np.tile(np.arange(256, dtype=np.int64), (ng, 1))
+    rows = np.arange(ng)
+    for i in range(emax):
+        act = i < e
+        span = np.maximum(ns - i, 1).astype(np.uint64)
+        pick = np.where(act, i + (r[:, i] % span).astype(np.int64), i)
+        a = perm[rows, i].copy()
+        perm[rows, i] = perm[rows, pick]
+        perm[rows, pick] = a
+    pres = (np.arange(256)[None, :] < ns[:, None]).astype(np.uint8)
+    for i in range(emax):
+        act = i < e
+        pres[rows[act], perm[act, i]] = 0
+    return pres
+
+
+def present_bits(flags) -> np.ndarray:
+    """[ng, <=256] present flags -> the ragged decode's [ng, 8] uint32 masks
+    (bit j % 32 of word j / 32 = shard j received)."""
+    f = np.zeros((len(flags), 256), np.uint8)
+    fl = np.asarray(flags, np.uint8)
+    f[:, :fl.shape[1]] = fl != 0
+    return np.packbits(f, axis=1, bitorder="little").view("<u4").reshape(-1, 8).copy()
+
+
 def ragged_mix(seed: int, g0: int, ng: int, table_y, kmax: int = 20, lmin: int = 64,
                lmax: int = 1250):
     """(k, m, len) int64 arrays for the C3 ragged batch."""
