@@ -42,7 +42,8 @@ constexpr int kWaves = 4;      // waves per block (one group each)
 #define DEC_RING 4
 #endif
 #ifndef DEC_LD_AUX
-#define DEC_LD_AUX 0           // cache policy of the survivor loads (2 = nt)
+#define DEC_LD_AUX 2           // cache policy of the survivor loads: nt (bench step: decode
+                               // 0.466 vs 0.475 ms with default-policy loads, encode unchanged)
 #endif
 #ifndef DEC_ST_AUX
 #define DEC_ST_AUX 0           // cache policy of the rebuilt-row stores
@@ -57,6 +58,15 @@ constexpr int kTile = 1280;    // bytes per lane-tile pass (64 x 16 + 64 x 4)
 #endif
 #ifndef DEC_OCC
 #define DEC_OCC 4              // waves per SIMD the register budget is cut for
+#endif
+#ifndef DEC_FAKE
+#define DEC_FAKE 0             // measurement only: rows computed per survivor (0 = e, the real decode)
+#endif
+#ifndef DEC_NOMEM
+#define DEC_NOMEM 0            // measurement only: survivor loads all hit one cached slot
+#endif
+#ifndef DEC_PAIR
+#define DEC_PAIR 0             // uniform kernel: fold survivors in pairs (fewer XORs, more VGPRs)
 #endif
 constexpr int kDefer = 0x100;  // internal status: left for k_decode_ragged_big
 
@@ -400,6 +410,8 @@ __global__ __launch_bounds__(256, DEC_OCC) void k_decode_fused(UniformArgs a, co
     __syncthreads();
 
     const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+    // DEC_NOMEM (measurement only): every survivor load reads group 0's slot 0
+    const __amdgpu_buffer_rsrc_t rsrc0 = __builtin_amdgcn_make_buffer_rsrc(a.base, 0, 4096, 0x00020000);
     const int64_t nwaves = (int64_t)gridDim.x * kWaves;
     const int64_t g0 = (int64_t)blockIdx.x * kWaves + wid;
     // present flags of the first 64 shards, prefetched one group ahead
@@ -472,8 +484,8 @@ __global__ __launch_bounds__(256, DEC_OCC) void k_decode_fused(UniformArgs a, co
             for (int q = 0; q < kRing; ++q) {
                 if (q < k) {
                     const uint32_t so = __builtin_amdgcn_readlane(so_lane, q);
-                    rq[q] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, v16, so, DEC_LD_AUX);
-                    rd[q] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, v4, so, DEC_LD_AUX);
+                    rq[q] = __builtin_amdgcn_raw_buffer_load_b128(DEC_NOMEM ? rsrc0 : rsrc, v16, DEC_NOMEM ? 0u : so, DEC_LD_AUX);
+                    rd[q] = __builtin_amdgcn_raw_buffer_load_b32(DEC_NOMEM ? rsrc0 : rsrc, v4, DEC_NOMEM ? 0u : so, DEC_LD_AUX);
                 }
             }
         };
@@ -601,8 +613,8 @@ __global__ __launch_bounds__(256, DEC_OCC) void k_decode_fused(UniformArgs a, co
         auto refill = [&](int q, int j) {
             if (j + kRing < k) {
                 const uint32_t so = __builtin_amdgcn_readlane(so_lane, j + kRing);
-                rq[q] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, v16, so, DEC_LD_AUX);
-                rd[q] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, v4, so, DEC_LD_AUX);
+                rq[q] = __builtin_amdgcn_raw_buffer_load_b128(DEC_NOMEM ? rsrc0 : rsrc, v16, DEC_NOMEM ? 0u : so, DEC_LD_AUX);
+                rd[q] = __builtin_amdgcn_raw_buffer_load_b32(DEC_NOMEM ? rsrc0 : rsrc, v4, DEC_NOMEM ? 0u : so, DEC_LD_AUX);
             }
         };
         for (int toff = 0; toff < a.len; toff += kTile) {
@@ -615,16 +627,44 @@ __global__ __launch_bounds__(256, DEC_OCC) void k_decode_fused(UniformArgs a, co
                     for (int w = 0; w < 5; ++w) acc[r][w] = 0;
                 for (int jb = 0; jb < k; jb += kRing) {
 #pragma unroll
-                    for (int q = 0; q < kRing; ++q) {
+                    for (int q = 0; q < kRing; q += DEC_PAIR ? 2 : 1) {
                         const int j = jb + q;
-                        if (j < k) {
+                        if (DEC_PAIR && j + 1 < k) {
+                            // two survivors per step: their six split products
+                            // fold into a row with three 3-input XORs
+                            uint32_t a0[5], a1[5], a2[5], b0[5], b1[5], b2[5];
+                            split(rq[q], rd[q], a0, a1, a2);
+                            split(rq[q + 1], rd[q + 1], b0, b1, b2);
+                            refill(q, j);
+                            refill(q + 1, j + 1);
+                            const uint32_t *ta = L.tab + (j * kRows + rb) * 8;
+                            const uint32_t *tb = ta + kRows * 8;
+#pragma unroll
+                            for (int r = 0; r < kPass; ++r) {
+                                if (rb + r < e) {
+                                    const uint4 t = reinterpret_cast<const uint4 *>(ta + r * 8)[0];
+                                    const uint32_t t2 = ta[r * 8 + 4];
+                                    const uint4 u = reinterpret_cast<const uint4 *>(tb + r * 8)[0];
+                                    const uint32_t u2 = tb[r * 8 + 4];
+#pragma unroll
+                                    for (int w = 0; w < 5; ++w) {
+                                        uint32_t x = xor3(acc[r][w], __builtin_amdgcn_perm(t.y, t.x, a0[w]),
+                                                          __builtin_amdgcn_perm(t.w, t.z, a1[w]));
+                                        x = xor3(x, __builtin_amdgcn_perm(t2, t2, a2[w]),
+                                                 __builtin_amdgcn_perm(u.y, u.x, b0[w]));
+                                        acc[r][w] = xor3(x, __builtin_amdgcn_perm(u.w, u.z, b1[w]),
+                                                         __builtin_amdgcn_perm(u2, u2, b2[w]));
+                                    }
+                                }
+                            }
+                        } else if (j < k) {
                             uint32_t a0[5], a1[5], a2[5];
                             split(rq[q], rd[q], a0, a1, a2);
                             refill(q, j);
                             const uint32_t *ta = L.tab + (j * kRows + rb) * 8;
 #pragma unroll
                             for (int r = 0; r < kPass; ++r) {
-                                if (rb + r < e) {
+                                if (DEC_FAKE ? r < DEC_FAKE : rb + r < e) {  // DEC_FAKE: measurement only
                                     const uint4 t = reinterpret_cast<const uint4 *>(ta + r * 8)[0];
                                     const uint32_t t2 = ta[r * 8 + 4];
 #pragma unroll
