@@ -11,9 +11,8 @@ shipped or called by the product path.
 * :class:`FecReference` drives the REAL reference managers
   (oracle/_ref/libref_fec.so, fec_manager.cpp compiled unmodified), for the
   golden generator and for pinning this restatement.
-* :func:`zero_stale_tail` rewrites a reference mode-0 group the way the
-  restatement frames it (stale bytes zeroed, parity recomputed by the
-  reference codec), which is what tests/golden/fec_encode.npz stores.
+* :func:`stale_bytes` counts the stale blob-buffer bytes a mode-0 group
+  carries past its blob (reproduced by the restatement and the GPU path).
 """
 from __future__ import annotations
 
@@ -60,6 +59,10 @@ class EncodeManager:
         self.seq = seq0 & 0xFFFFFFFF
         self.pend: List[bytes] = []
         self.blob_len = 4
+        # blob_encode_t::input_buf (fec_manager.h:257): never cleared, so the
+        # bytes past a blob's end are what earlier, longer blobs left there
+        # (blob_encode_t::output, fec_manager.cpp:67-75); zero at first
+        self.blob_buf = bytearray()
         self.ready: List[bytes] = []
         self.oracle = oracle or Oracle()
 
@@ -125,7 +128,12 @@ class EncodeManager:
                 blob = bytearray(len(self.pend).to_bytes(4, "big"))
                 for p in self.pend:
                     blob += len(p).to_bytes(2, "big") + p
-                blob += bytes(k * fec_len - len(blob))  # zero tail (the reference: stale)
+                cl = len(blob)
+                tail = bytes(self.blob_buf[cl:k * fec_len])
+                blob += tail + bytes(k * fec_len - cl - len(tail))  # stale bytes, as sent
+                if len(self.blob_buf) < cl:
+                    self.blob_buf += bytes(cl - len(self.blob_buf))
+                self.blob_buf[:cl] = blob[:cl]
                 data = [bytes(blob[i * fec_len:(i + 1) * fec_len]) for i in range(k)]
                 par = self._parity(data, k, k + m, fec_len)
                 for i in range(k + m):
@@ -156,28 +164,16 @@ class EncodeManager:
         return r
 
 
-def zero_stale_tail(packets: List[bytes], ref_rs) -> Tuple[List[bytes], int]:
-    """A reference mode-0 group (all k+m packets) with the stale bytes past the
-    blob's end zeroed and the parity recomputed by the reference codec
-    (oracle/_ref/libref_rs.so).  Returns (packets, number of nonzero stale
-    bytes replaced)."""
-    k, m = packets[0][5], packets[0][6]
-    n = k + m
-    fec_len = len(packets[0]) - HEADER
+def stale_bytes(packets: List[bytes]) -> int:
+    """Nonzero bytes past the blob's end in a mode-0 group (all k+m packets):
+    the stale content of blob_encode_t's buffer the reference sends."""
+    k = packets[0][5]
     blob = b"".join(p[HEADER:] for p in packets[:k])
     cnt = int.from_bytes(blob[:4], "big")
     pos = 4
     for _ in range(cnt):
         pos += 2 + int.from_bytes(blob[pos:pos + 2], "big")
-    stale = sum(1 for b in blob[pos:] if b)
-    blob = blob[:pos] + bytes(len(blob) - pos)
-    stride = max(16, (fec_len + 15) // 16 * 16)
-    buf = np.zeros(n * stride, np.uint8)
-    for i in range(k):
-        buf[i * stride:i * stride + fec_len] = np.frombuffer(blob[i * fec_len:(i + 1) * fec_len], np.uint8)
-    ref_rs.encode_batch(k, n, buf, n * stride, stride, fec_len, 1)
-    out = [packets[i][:HEADER] + buf[i * stride:i * stride + fec_len].tobytes() for i in range(n)]
-    return out, stale
+    return sum(1 for b in blob[pos:] if b)
 
 
 class FecReference:

@@ -9,11 +9,12 @@ Each case sets g_fec_par (-f string, mode, mtu, queue_len), feeds a fresh
 reference manager a seeded event sequence -- packets of seeded lengths whose
 bytes are the SplitMix64 stream of (seed, event index) (oracle.cpu.cook_payloads),
 and input(0, 0) timer flushes -- and records every input() return value and
-every packet output() returned, with the event it followed.  Mode-0 groups are
-stored as oracle.fec_frame.zero_stale_tail rewrites them: the reference's stale
-bytes past the blob's end zeroed and the parity recomputed by the reference
-codec (the count of nonzero stale bytes replaced is recorded).  The encoder's
-first sequence number (random in the reference) is read from its first header.
+every packet output() returned, with the event it followed, unmodified: mode-0
+groups carry the stale bytes of the reference's blob buffer past the blob's end
+(blob_encode_t::output, fec_manager.cpp:67-75; the count of nonzero ones is
+recorded), the managers being constructed in zeroed memory (ref_fec_driver.cpp).
+The encoder's first sequence number (random in the reference) is read from its
+first header.
 
 Fixtures are data only: lengths, return codes, packet lengths / events, the
 packet bytes themselves for the small cases and a sha256 of all of them.
@@ -26,7 +27,7 @@ import os
 import numpy as np
 
 from oracle.cpu import Reference, cook_payloads, splitmix_words
-from oracle.fec_frame import EncodeManager, FecReference, lossy_channel, zero_stale_tail
+from oracle.fec_frame import EncodeManager, FecReference, lossy_channel, stale_bytes
 
 OUT = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "golden")
 FEC_SEED = 0xFEC0
@@ -100,14 +101,11 @@ def main():
         ret, pk, pev = fr.encode(ev)
         stale = 0
         if mode == 0:
-            fixed, j = [], 0
+            j = 0
             while j < len(pk):
                 k, m = pk[j][5], pk[j][6]
-                g, s = zero_stale_tail(pk[j:j + k + m], rr)
-                fixed += g
-                stale += s
+                stale += stale_bytes(pk[j:j + k + m])
                 j += k + m
-            pk = fixed
         blob = b"".join(pk)
         seq0 = int.from_bytes(pk[0][:4], "big") if pk else 0
         arrays[f"{name}__lens"] = lens
@@ -120,7 +118,7 @@ def main():
         if len(blob) <= FULL_BYTES_MAX:
             arrays[f"{name}__pk_bytes"] = np.frombuffer(blob, np.uint8)
         names.append(name)
-        print(f"{name}: {n} events, {len(pk)} packets, {len(blob)} B, stale bytes zeroed {stale}")
+        print(f"{name}: {n} events, {len(pk)} packets, {len(blob)} B, nonzero stale bytes {stale}")
     arrays["cases"] = np.array(names)
     np.savez_compressed(os.path.join(OUT, "fec_encode.npz"), **arrays)
 

@@ -12,14 +12,39 @@
 // The encoder's first sequence number is drawn by the reference
 // (get_fake_random_number, fec_manager.h:327); callers read it back from the
 // first packet header.
+//
+// Managers are constructed in zeroed memory.  Their constructors leave the
+// big buffers uninitialised (blob_encode_t::input_buf, fec_manager.h:257;
+// the decoder's ring), and the encoder sends bytes of blob_encode_t's buffer
+// past the blob's end (blob_encode_t::output, fec_manager.cpp:67-75): zeroed
+// memory (what a fresh process's mmap-backed allocation of these ~2 MB
+// objects holds) makes those bytes a function of the connection's history
+// alone, so the fixtures are deterministic.
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
+#include <new>
+#include <string>
 
 #include "common.h"
 #include "fec_manager.h"
 #include "log.h"
 
 static void empty_cb(struct ev_loop *, struct ev_timer *, int) {}
+
+template <class T>
+static T *new_zeroed() {
+    void *mem = std::calloc(1, sizeof(T));
+    return mem ? new (mem) T() : nullptr;
+}
+
+template <class T>
+static void free_zeroed(T *p) {
+    if (!p) return;
+    p->~T();
+    std::free(p);
+}
+
 
 extern "C" {
 
@@ -35,13 +60,26 @@ int ref_fec_config(const char *rs_str, int mode, int mtu, int queue_len) {
     return rc;
 }
 
+// fec_parameter_t::rs_from_str (fec_manager.h:40-136) on a fresh table:
+// returns its result (0 or -1), the table size in *cnt and y of x = 1..cnt.
+int ref_rs_table(const char *rs_str, int *cnt, int *ys) {
+    log_level = log_fatal;
+    fec_parameter_t *p = new_zeroed<fec_parameter_t>();
+    std::string tmp(rs_str);
+    int rc = p->rs_from_str((char *)tmp.c_str());
+    *cnt = rc == 0 ? p->rs_cnt : 0;
+    for (int i = 0; i < *cnt; ++i) ys[i] = p->rs_par[i].y;
+    free_zeroed(p);
+    return rc;
+}
+
 void *ref_fenc_new() {
-    fec_encode_manager_t *m = new fec_encode_manager_t();
+    fec_encode_manager_t *m = new_zeroed<fec_encode_manager_t>();
     m->set_loop_and_cb(ev_default_loop(0), empty_cb);  // as misc.cpp:398 (timer never runs)
     return m;
 }
 
-void ref_fenc_free(void *h) { delete (fec_encode_manager_t *)h; }
+void ref_fenc_free(void *h) { free_zeroed((fec_encode_manager_t *)h); }
 
 // Feed events to input(); after each, collect output().  len[i] >= 0: packet
 // at buf + off[i]; len[i] < 0: input(0, 0).  Emitted packets are appended to
@@ -72,9 +110,9 @@ int64_t ref_fenc_run(void *h, int64_t n, const int32_t *len, const uint64_t *off
     return np;
 }
 
-void *ref_fdec_new() { return new fec_decode_manager_t(); }
+void *ref_fdec_new() { return new_zeroed<fec_decode_manager_t>(); }
 
-void ref_fdec_free(void *h) { delete (fec_decode_manager_t *)h; }
+void ref_fdec_free(void *h) { free_zeroed((fec_decode_manager_t *)h); }
 
 // Feed packets to fec_decode_manager_t::input (each copied into a buf_len
 // buffer first, as the receive path's buffers are); after each, collect

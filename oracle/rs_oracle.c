@@ -263,17 +263,27 @@ int orc_decode_batch(int k, int n, uint8_t *buf, int64_t group_stride,
  * Interpolation (fec_manager.h:122): y = pre_y + (now_y-pre_y)*(x-pre_x)/dist
  * + 0.9999 in double, truncated; clamp so x+y <= 255 (fec_manager.h:124-127). */
 int orc_rs_from_str(const char *s, uint8_t *xs, uint8_t *ys /* >= 255 each */) {
+    /* string_to_vec(s, ",") (common.cpp:919-934) is strtok: tokens between
+     * commas, empty ones skipped; each is sscanf'd with "%d:%d" (trailing
+     * characters ignored) */
     int px[256], py[256], cnt = 0;
+    char tok[4096];
     const char *p = s;
     while (*p) {
-        int x, y, used = 0;
-        if (sscanf(p, "%d:%d%n", &x, &y, &used) != 2) return -1;
-        if (x < 1 || y < 0 || x + y > 255) return -1;
-        if (cnt >= 256) return -1;
-        px[cnt] = x; py[cnt] = y; cnt++;
-        p += used;
+        const char *c = strchr(p, ',');
+        size_t n = c ? (size_t)(c - p) : strlen(p);
+        if (n > 0) {
+            int x, y;
+            if (n >= sizeof(tok)) return -1;
+            memcpy(tok, p, n);
+            tok[n] = 0;
+            if (sscanf(tok, "%d:%d", &x, &y) != 2) return -1;
+            if (x < 1 || y < 0 || x + y > 255) return -1;
+            if (cnt >= 256) return -1;
+            px[cnt] = x; py[cnt] = y; cnt++;
+        }
+        p += n;
         if (*p == ',') p++;
-        else if (*p) return -1;
     }
     if (cnt < 1) return -1;
     for (int i = 1; i < cnt; i++)

@@ -132,3 +132,35 @@ def test_fec_param_table(oracle, golden):
     for bad in ["", "0:1", "3:2,2:4", "200:100", "a:b", "1:-1", "10"]:
         assert u.rs_from_str(bad) is None
     assert u.rs_to_str(u.rs_from_str("2:1,4:2")) == "1:1,2:1,3:2,4:2"
+
+
+FEC_GRAMMAR = ["20:10", "20:10,", ",20:10", "1:3,,2:4", ",,5:5,,", "20:10abc", " 20: 10",
+               "+3:2", "1:2:3", "3:2,x", "", ",", "a:b", "0:1", "20 :10", "3:2,2:4",
+               "1:3,2:4,10:6,20:10", "\t4:1,\n9:3", "10:5,40:20,", "254:1", "255:1"]
+
+
+def test_fec_grammar_matches_reference(oracle):
+    """-f parsing: strtok's empty-token skipping and sscanf("%d:%d")'s
+    leniency (fec_manager.h:40-69, common.cpp:919-934), against the reference's
+    own rs_from_str (oracle/_ref/libref_fec.so), for our three parsers."""
+    import ctypes as C
+    from oracle.fec_frame import REF_FEC_SO
+    if not os.path.exists(REF_FEC_SO):
+        pytest.skip("reference FEC build absent")
+    ref = C.CDLL(REF_FEC_SO)
+    ref.ref_rs_table.argtypes = [C.c_char_p, C.c_void_p, C.c_void_p]
+    from udpspeeder_amd._lib import rsmi_fec_config
+    for s in FEC_GRAMMAR:
+        cnt = C.c_int(0)
+        ys = (C.c_int * 256)()
+        rc = ref.ref_rs_table(s.encode(), C.byref(cnt), ys)
+        want = [(x + 1, ys[x]) for x in range(cnt.value)] if rc == 0 else None
+        assert u.rs_from_str(s) == want, s
+        assert oracle.rs_from_str(s) == want, s
+        cfg = rsmi_fec_config()
+        crc = u.lib().rsmi_fec_config_init(C.byref(cfg), s.encode(), 0, 1250, 200)
+        if want is None:
+            assert crc != 0, s
+        else:
+            assert crc == 0 and cfg.rs_cnt == len(want), s
+            assert [cfg.rs_y[i] for i in range(cfg.rs_cnt)] == [y for _, y in want], s

@@ -89,6 +89,13 @@ struct HostArr {
     T &operator[](size_t i) { return p[i]; }
 };
 
+// A mode-0 group of this batch that still holds bytes of the blob buffer:
+// positions [0, cl) were written by it; later, shorter blobs overwrite a prefix.
+struct BlobHolder {
+    int64_t slot0;
+    int fec_len, cl;
+};
+
 // One encode launch over a run of consecutive groups with the same code and
 // shard length.
 struct Run {
@@ -115,6 +122,17 @@ struct rsmi_fenc {
     std::vector<int32_t> g_k, g_m, g_len;
     std::vector<uint32_t> g_seq;
     std::vector<Run> runs;
+    // ---- mode 0's blob buffer (blob_encode_t::input_buf, fec_manager.h:257),
+    // never cleared by the reference: the last data shard carries its bytes
+    // past the blob's end (blob_encode_t::output, fec_manager.cpp:67-75).
+    // Position p holds the byte of the latest blob longer than p.  `stack`
+    // keeps this batch's groups that are such a latest writer for some
+    // position (cl decreasing from the bottom, latest on top); the device copy
+    // dshadow holds the buffer as of the batch start (zero beyond shadow_len).
+    std::vector<BlobHolder> stack;
+    int shadow_len = 0;
+    HostArr<rsmi::ByteRun> stale;       // stale bytes of this batch's groups
+    HostArr<rsmi::ByteRun> shadow_upd;  // the buffer at the batch end -> dshadow
     int64_t n_slots = 0;
     int32_t stride_min = rsmi::kSlotShard;
     bool planned = false;
@@ -124,6 +142,7 @@ struct rsmi_fenc {
     int device = -1;
     uint8_t *dplan = nullptr;
     size_t plan_cap = 0;
+    uint8_t *dshadow = nullptr;  // kBlobBufBytes, zeroed at the first run
     uint8_t *dcarry[2] = {nullptr, nullptr};
     size_t carry_cap[2] = {0, 0};
     int carry_cur = 0;  // pending packets live in dcarry[carry_cur] (or the batch input)
@@ -161,6 +180,70 @@ int grow(uint8_t **p, size_t *cap, size_t need, bool pinned) {
     return RSMI_OK;
 }
 
+// Blob positions [a, b) of holder H -> runs into rows of the group at slot0
+// (fec_len-byte rows), split at both groups' row boundaries.
+void copy_from_holder(rsmi_fenc *E, int64_t slot0, int fec_len, const BlobHolder &H, int a, int b) {
+    while (a < b) {
+        const int doff = a % fec_len, soff = a % H.fec_len;
+        const int n = std::min({b - a, fec_len - doff, H.fec_len - soff});
+        E->stale.push_back(rsmi::ByteRun{(uint64_t)(slot0 + a / fec_len),
+                                         (uint64_t)(H.slot0 + a / H.fec_len), (uint32_t)doff,
+                                         (uint32_t)soff, (uint32_t)n, 0});
+        a += n;
+    }
+}
+
+// Mode 0: the bytes [cl, k*fec_len) of the group's data rows are whatever
+// the blob buffer held there (k_frame wrote zeros; these runs overwrite them
+// before the encode).  Then the group becomes the latest writer of [0, cl).
+void stale_runs(rsmi_fenc *E, int64_t slot0, int k, int fec_len, int cl) {
+    const int end = k * fec_len;
+    std::vector<BlobHolder> &st = E->stack;
+    for (int p = cl; p < end;) {
+        // the latest holder with cl > p: the topmost such (cl decreases upward)
+        int lo = 0, hi = (int)st.size();  // st[0, lo) have cl > p
+        while (lo < hi) {
+            const int mid = (lo + hi) / 2;
+            if (st[mid].cl > p) lo = mid + 1;
+            else hi = mid;
+        }
+        if (lo > 0) {
+            const BlobHolder &H = st[lo - 1];
+            const int q = std::min(end, H.cl);
+            copy_from_holder(E, slot0, fec_len, H, p, q);
+            p = q;
+        } else {  // no writer in this batch: the buffer as of the batch start
+            const int q = std::min(end, E->shadow_len);
+            for (int a = p; a < q;) {
+                const int doff = a % fec_len, n = std::min(q - a, fec_len - doff);
+                E->stale.push_back(rsmi::ByteRun{(uint64_t)(slot0 + a / fec_len), rsmi::kShadowLoc,
+                                                 (uint32_t)doff, (uint32_t)a, (uint32_t)n, 0});
+                a += n;
+            }
+            break;  // beyond shadow_len the buffer is still zero, as k_frame wrote
+        }
+    }
+    while (!st.empty() && st.back().cl <= cl) st.pop_back();
+    st.push_back(BlobHolder{slot0, fec_len, cl});
+}
+
+// The blob buffer at the batch end, written back to the device copy: the top
+// holder owns [0, cl_top), the one below it [cl_top, cl_below), ...
+void shadow_update(rsmi_fenc *E) {
+    int lo = 0;
+    for (size_t i = E->stack.size(); i-- > 0;) {
+        const BlobHolder &H = E->stack[i];
+        for (int a = lo; a < H.cl;) {
+            const int soff = a % H.fec_len, n = std::min(H.cl - a, H.fec_len - soff);
+            E->shadow_upd.push_back(rsmi::ByteRun{rsmi::kShadowLoc, (uint64_t)(H.slot0 + a / H.fec_len),
+                                                  (uint32_t)a, (uint32_t)soff, (uint32_t)n, 0});
+            a += n;
+        }
+        lo = std::max(lo, H.cl);
+    }
+    E->shadow_len = std::max(E->shadow_len, lo);
+}
+
 // Close the open group (the about_to_fec branch, fec_manager.cpp:248-367).
 // Early-sent mode-1 packets of the group are pointed at their group slots.
 void close_group(rsmi_fenc *E, int k, int m, int fec_len) {
@@ -188,6 +271,7 @@ void close_group(rsmi_fenc *E, int k, int m, int fec_len) {
         if (p.emitted >= 0) E->packets[(size_t)p.emitted].slot = slot0 + (int64_t)j;
     }
     E->jobs.push_back(G);
+    if (E->cfg.mode == 0) stale_runs(E, slot0, k, fec_len, E->blob_len);
     E->g_slot0.push_back(slot0);
     E->g_k.push_back(k);
     E->g_m.push_back(m);
@@ -305,21 +389,24 @@ int rsmi_fec_config_init(rsmi_fec_config *cfg, const char *s, int mode, int mtu,
     if (mode != 0 && mode != 1) return fail(RSMI_ERR_INVALID, "mode must be 0 or 1");
     if (mtu < 1 || queue_len < 1) return fail(RSMI_ERR_INVALID, "bad mtu/queue_len");
     // rs_from_str (fec_manager.h:40-136)
+    // string_to_vec(s, ",") (common.cpp:919-934) is strtok: empty tokens vanish
     std::vector<std::pair<int, int>> pv;
     std::string str(s);
     size_t pos = 0;
-    while (true) {
+    while (pos <= str.size()) {
         size_t c = str.find(',', pos);
-        std::string tok = str.substr(pos, c == std::string::npos ? std::string::npos : c - pos);
+        if (c == std::string::npos) c = str.size();
+        std::string tok = str.substr(pos, c - pos);
+        pos = c + 1;
+        if (tok.empty()) continue;
         int x, y;
         if (std::sscanf(tok.c_str(), "%d:%d", &x, &y) != 2)
             return fail(RSMI_ERR_INVALID, "failed to parse [" + tok + "]");
         if (x < 1 || y < 0 || x + y > RSMI_FEC_MAX_PACKETS)
             return fail(RSMI_ERR_INVALID, "invalid x:y in [" + tok + "]");
         pv.emplace_back(x, y);
-        if (c == std::string::npos) break;
-        pos = c + 1;
     }
+    if (pv.empty()) return fail(RSMI_ERR_INVALID, std::string("failed to parse [") + s + "]");
     for (size_t i = 1; i < pv.size(); ++i)
         if (pv[i].first <= pv[i - 1].first)
             return fail(RSMI_ERR_INVALID, "x in x:y should be in ascend order");
@@ -374,6 +461,7 @@ void rsmi_fenc_destroy(rsmi_fenc *E) {
     if (!E) return;
     (void)wait_idle(E);
     if (E->dplan) (void)hipFree(E->dplan);
+    if (E->dshadow) (void)hipFree(E->dshadow);
     for (int i = 0; i < 2; ++i)
         if (E->dcarry[i]) (void)hipFree(E->dcarry[i]);
     if (E->done) (void)hipEventDestroy(E->done);
@@ -405,6 +493,9 @@ int rsmi_fenc_plan(rsmi_fenc *E, int64_t n_events, const int32_t *len, const uin
     E->g_len.clear();
     E->g_seq.clear();
     E->runs.clear();
+    E->stack.clear();
+    E->stale.clear();
+    E->shadow_upd.clear();
     E->n_slots = 0;
     E->stride_min = rsmi::kSlotShard;
     for (Pending &p : E->pend) p.emitted = -1;  // sent in an earlier batch
@@ -435,6 +526,7 @@ int rsmi_fenc_plan(rsmi_fenc *E, int64_t n_events, const int32_t *len, const uin
         E->packets[(size_t)p.emitted].slot = slot;
         E->stride_min = std::max(E->stride_min, (int32_t)((rsmi::kSlotShard + p.len + 2 + 15) & ~15u));
     }
+    shadow_update(E);
     // the open group's payloads move to the other carry buffer
     size_t cbytes = 0;
     for (const Pending &p : E->pend) cbytes += (p.len + 15) & ~15u;
@@ -496,19 +588,35 @@ int rsmi_fenc_run_dev(rsmi_fenc *E, uint8_t *slots, int64_t S, void *stream) {
     int rc0 = grow(&E->dcarry[E->carry_cur], &E->carry_cap[E->carry_cur], E->carry_need, false);
     if (rc0) return rc0;
     const rsmi::CarryBase carry{{E->dcarry[0], E->dcarry[1]}};
+    if (!E->dshadow) {
+        if (hipMalloc(&E->dshadow, rsmi::kBlobBufBytes) != hipSuccess)
+            return fail(RSMI_ERR_NOMEM, "fenc: hipMalloc(blob buffer)");
+        if (hipMemsetAsync(E->dshadow, 0, rsmi::kBlobBufBytes, s) != hipSuccess)
+            return fail(RSMI_ERR_HIP, "fenc: clear blob buffer");
+    }
     const size_t gb = E->jobs.size() * sizeof(FrameGroup), sb = E->srcs.size() * sizeof(FrameSrc),
-                 cb = E->carry.size() * sizeof(CarryCopy);
-    const size_t go = 0, so = (gb + 255) & ~size_t(255), co = (so + sb + 255) & ~size_t(255);
-    const size_t all = co + cb + 16;
+                 cb = E->carry.size() * sizeof(CarryCopy),
+                 rb = E->stale.size() * sizeof(rsmi::ByteRun),
+                 ub = E->shadow_upd.size() * sizeof(rsmi::ByteRun);
+    const size_t go = 0, so = (gb + 255) & ~size_t(255), co = (so + sb + 255) & ~size_t(255),
+                 ro = (co + cb + 255) & ~size_t(255), uo = (ro + rb + 255) & ~size_t(255);
+    const size_t all = uo + ub + 16;
     int rc = grow(&E->dplan, &E->plan_cap, all, false);
     if (rc) return rc;
     hipError_t e = hipSuccess;
     if (gb) e = hipMemcpyAsync(E->dplan + go, E->jobs.p, gb, hipMemcpyHostToDevice, s);
     if (e == hipSuccess && sb) e = hipMemcpyAsync(E->dplan + so, E->srcs.p, sb, hipMemcpyHostToDevice, s);
     if (e == hipSuccess && cb) e = hipMemcpyAsync(E->dplan + co, E->carry.p, cb, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess && rb) e = hipMemcpyAsync(E->dplan + ro, E->stale.p, rb, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess && ub)
+        e = hipMemcpyAsync(E->dplan + uo, E->shadow_upd.p, ub, hipMemcpyHostToDevice, s);
     if (e == hipSuccess)
         e = rsmi::launch_frame(reinterpret_cast<const FrameGroup *>(E->dplan + go), (int64_t)E->jobs.size(),
                                reinterpret_cast<const FrameSrc *>(E->dplan + so), carry, slots, S, s);
+    // stale bytes past each blob, before the parity is computed over them
+    if (e == hipSuccess)
+        e = rsmi::launch_byte_runs(reinterpret_cast<const rsmi::ByteRun *>(E->dplan + ro),
+                                   (int64_t)E->stale.size(), slots, S, E->dshadow, s);
     if (e != hipSuccess) return fail(RSMI_ERR_HIP, std::string("fenc frame: ") + hipGetErrorString(e));
     // parity of every group
     for (const Run &r : E->runs) {
@@ -516,8 +624,12 @@ int rsmi_fenc_run_dev(rsmi_fenc *E, uint8_t *slots, int64_t S, void *stream) {
                              r.len, r.count, stream);
         if (rc) return rc;
     }
-    e = rsmi::launch_carry(reinterpret_cast<const CarryCopy *>(E->dplan + co), (int64_t)E->carry.size(),
-                           carry, s);
+    // the blob buffer as this batch leaves it (read by the next batch's stale runs)
+    e = rsmi::launch_byte_runs(reinterpret_cast<const rsmi::ByteRun *>(E->dplan + uo),
+                               (int64_t)E->shadow_upd.size(), slots, S, E->dshadow, s);
+    if (e == hipSuccess)
+        e = rsmi::launch_carry(reinterpret_cast<const CarryCopy *>(E->dplan + co),
+                               (int64_t)E->carry.size(), carry, s);
     if (e == hipSuccess) e = hipEventRecord(E->done, s);
     if (e != hipSuccess) return fail(RSMI_ERR_HIP, std::string("fenc carry: ") + hipGetErrorString(e));
     E->in_flight = true;

@@ -14,7 +14,9 @@
 // dword, funnel-shifted with v_alignbyte) and one 16-byte store.
 //
 // k_carry copies packets still pending at the end of a batch into the
-// encoder's carry area with the same unaligned-window loads.
+// encoder's carry area with the same unaligned-window loads.  k_byte_runs
+// fills mode 0's stale bytes past the blob's end and keeps the encoder's copy
+// of the blob buffer (fec_enc.cpp).
 #include "rsmi_internal.hpp"
 
 namespace rsmi {
@@ -340,7 +342,35 @@ __global__ __launch_bounds__(kThreads) void k_gather(const GatherCopy *jobs, int
     }
 }
 
+// Byte runs (mode-0 stale bytes, fec_enc.cpp): one wave per run, a byte per
+// lane; runs are short (stale tails) or one shard row (buffer updates).
+__global__ __launch_bounds__(kThreads) void k_byte_runs(const ByteRun *runs, int64_t nruns,
+                                                         uint8_t *slots, int64_t slot_stride,
+                                                         uint8_t *shadow) {
+    const int lane = threadIdx.x & 63;
+    const int64_t w0 = (int64_t)blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
+    auto at = [&](uint64_t loc, uint32_t off) {
+        return (loc & kShadowLoc) ? shadow + off
+                                  : slots + (int64_t)loc * slot_stride + kSlotShard + off;
+    };
+    for (int64_t w = w0; w < nruns; w += (int64_t)gridDim.x * (kThreads / 64)) {
+        const ByteRun R = runs[w];
+        uint8_t *dst = at(R.dst, R.dst_off);
+        const uint8_t *src = at(R.src, R.src_off);
+        for (uint32_t i = lane; i < R.len; i += 64) dst[i] = src[i];
+    }
+}
+
 }  // namespace
+
+hipError_t launch_byte_runs(const ByteRun *runs, int64_t nruns, uint8_t *slots, int64_t slot_stride,
+                            uint8_t *shadow, hipStream_t s) {
+    if (nruns <= 0) return hipSuccess;
+    int64_t blocks = (nruns + kThreads / 64 - 1) / (kThreads / 64);
+    if (blocks > 8192) blocks = 8192;
+    k_byte_runs<<<(unsigned)blocks, kThreads, 0, s>>>(runs, nruns, slots, slot_stride, shadow);
+    return hipGetLastError();
+}
 
 hipError_t launch_gather(const GatherCopy *jobs, int64_t njobs, CarryBase carry, hipStream_t s) {
     if (njobs <= 0) return hipSuccess;

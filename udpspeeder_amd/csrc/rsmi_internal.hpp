@@ -162,6 +162,18 @@ struct GatherCopy {
     uint32_t len, dst_len;
 };
 hipError_t launch_gather(const GatherCopy *jobs, int64_t njobs, CarryBase carry, hipStream_t s);
+// Mode-0 stale bytes (fec_enc.cpp): a byte run between shard rows of the
+// batch's slots and the encoder's device copy of blob_encode_t's buffer.  A
+// location is a slot index (byte slots + slot*stride + kSlotShard + off) or,
+// with kShadowLoc, the buffer itself (byte shadow + off).
+constexpr uint64_t kShadowLoc = 1ull << 63;
+constexpr int kBlobBufBytes = (255 + 5) * 3800;  // blob_encode_t::input_buf, fec_manager.h:257
+struct ByteRun {
+    uint64_t dst, src;
+    uint32_t dst_off, src_off, len, pad;
+};
+hipError_t launch_byte_runs(const ByteRun *runs, int64_t nruns, uint8_t *slots, int64_t slot_stride,
+                            uint8_t *shadow, hipStream_t s);
 hipError_t launch_frame(const FrameGroup *groups, int64_t ngroups, const FrameSrc *srcs,
                         CarryBase carry, uint8_t *slots, int64_t slot_stride, hipStream_t s);
 hipError_t launch_carry(const CarryCopy *jobs, int64_t njobs, CarryBase carry, hipStream_t s);

@@ -11,20 +11,24 @@ for each k.
 """
 from __future__ import annotations
 
+import re
 from typing import List, Optional, Tuple
 
 MAX_FEC_PACKET_NUM = 255  # fec_manager.h:18
+# sscanf(tok, "%d:%d") (fec_manager.h:52): optional leading white space and
+# sign before each number, ':' right after the first; the rest is ignored
+_XY = re.compile(r"[ \t\n\v\f\r]*([+-]?[0-9]+):[ \t\n\v\f\r]*([+-]?[0-9]+)")
 
 
 def rs_from_str(s: str) -> Optional[List[Tuple[int, int]]]:
-    parts = s.split(",")
+    # string_to_vec(s, ",") (common.cpp:919-934) is strtok: empty tokens vanish
+    parts = [p for p in s.split(",") if p]
     pars = []
     for p in parts:
-        try:
-            xs, ys = p.split(":")
-            x, y = int(xs), int(ys)
-        except ValueError:
+        m = _XY.match(p)
+        if not m:
             return None
+        x, y = int(m.group(1)), int(m.group(2))
         if x < 1 or y < 0 or x + y > MAX_FEC_PACKET_NUM:
             return None
         pars.append((x, y))
