@@ -305,6 +305,7 @@ def extra_configs(u, synth, torch, dev, buf, G):
         "failures": int((st != 0).sum().item())}
     out.update(c3_configs(u, synth, torch, dev, G))
     out["c4_one_gpu"] = c4_one_gpu(u, synth, torch, dev)
+    out["rtc_f10_5_encode"] = rtc_config(u, synth, torch, dev)
     out["f2_cook_decook"] = cook_config(torch, dev, buf, G)
     out["dropin_latency_us"] = dropin_latency(u)
     return out
@@ -345,6 +346,35 @@ def c3_configs(u, synth, torch, dev, G):
     plan.close()
     del base
     return out
+
+
+def rtc_config(u, synth, torch, dev, k=10, m=5, groups=131072):
+    """-f 10:5, a code with no build-time network: RS(10,15) over 1250-B shards,
+    131072 groups (C1's data volume), through the network librsmi compiled at
+    run time (hipRTC), and through the generic table kernel for comparison."""
+    from udpspeeder_amd._lib import ENC_BITSLICE_RTC
+    n = k + m
+    t0 = time.time()
+    u.wait_code(k, n)
+    compile_s = time.time() - t0
+    kind = u.code_encoder(k, n)
+    buf = torch.zeros((groups, n, 1280), dtype=torch.uint8, device=dev)
+    u.fill_data(buf, k, LEN, synth.DATA_SEED)
+    ms = _time_ms(torch, lambda: u.encode(buf, k, n, LEN))
+    prev = u.rs.set_bitslice(False)
+    try:
+        ms_generic = _time_ms(torch, lambda: u.encode(buf, k, n, LEN), reps=5)
+    finally:
+        u.rs.set_bitslice(prev)
+    del buf
+    alg = groups * n * LEN
+    return {"code": f"{k}:{m}", "groups": groups, "len": LEN,
+            "encoder": "bitslice_rtc" if kind == ENC_BITSLICE_RTC else f"kind{kind}",
+            "wait_code_s": round(compile_s, 2), "encode_ms": round(ms, 4),
+            "alg_GBps": round(alg / (ms * 1e-3) / 1e9, 1),
+            "roofline_frac": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "generic_encode_ms": round(ms_generic, 4),
+            "generic_roofline_frac": round(alg / (ms_generic * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
 
 
 def c4_one_gpu(u, synth, torch, dev, steps=5):

@@ -89,6 +89,41 @@ int rsmi_decode_matrix(int k, int n, const uint8_t *present, uint8_t *sel,
  * up front to keep later calls free of host<->device traffic. */
 int rsmi_prepare_code(int k, int n);
 
+/* Encoder kinds (rsmi_code_encoder).  Build-time bit-sliced XOR networks
+ * exist for the (x, x+10) codes and the rs_from_str("1:3,2:4,10:6,20:10")
+ * table; every other code that rs_from_str admits (fec_manager.h:40-136) gets
+ * its network compiled at run time with hipRTC, in a background thread started
+ * by rsmi_prepare_code (or the first call that makes the code resident).
+ * Until it is ready that code's encodes run the generic table kernel -- the
+ * output is the same bytes either way.  Knobs: RSMI_RTC=0 disables run-time
+ * compilation; RSMI_RTC_MAX_COEFS (default 2048) caps k*(n-k);
+ * RSMI_RTC_CACHE=<dir>|0 sets or disables the code-object cache
+ * (default $XDG_CACHE_HOME/rsmi, else ~/.cache/rsmi). */
+#define RSMI_ENC_NONE 0          /* n == k: no parity                          */
+#define RSMI_ENC_GENERIC 1       /* v_perm table kernel                        */
+#define RSMI_ENC_BITSLICE 2      /* build-time bit-sliced network              */
+#define RSMI_ENC_BITSLICE_RTC 3  /* run-time compiled bit-sliced network       */
+#define RSMI_ENC_COMPILING 4     /* generic now; network compiling             */
+int rsmi_code_encoder(int k, int n);
+
+/* rsmi_prepare_code, then block until the (k,n) run-time network (if the code
+ * gets one) has compiled or failed, and load it on the current device (do
+ * this before capturing encodes of the code in a graph). */
+int rsmi_wait_code(int k, int n);
+
+/* Compile (or fetch from the disk cache) the run-time network of (k,n)
+ * synchronously, without touching any GPU: warms the code-object cache ahead
+ * of deployment, and makes later rsmi_prepare_code calls instant.  Returns
+ * RSMI_ERR_INVALID when the code gets no run-time network (built-in, n == k,
+ * over RSMI_RTC_MAX_COEFS, RSMI_RTC=0), RSMI_ERR_HIP when hipRTC fails. */
+int rsmi_precompile_code(int k, int n);
+
+/* The bit-sliced XOR network source of (k,n) (n > k) as emitted for hipRTC
+ * (identical to the build-time generator's text).  Copies at most cap-1 bytes
+ * plus a NUL into buf (may be NULL); returns the full length, or
+ * RSMI_ERR_INVALID. */
+int64_t rsmi_bitslice_source(int k, int n, char *buf, int64_t cap);
+
 /* Make (k,n) resident and pre-size the decode workspace that calls on
  * `stream` use, for up to `ngroups` groups (needed before graph capture). */
 int rsmi_reserve(int k, int n, int64_t ngroups, void *stream);

@@ -14,7 +14,11 @@
 #define BS_ACC2(acc, a) ((acc) ^= (a))
 #define BS_SCHED_BARRIER() ((void)0)
 #include "../udpspeeder_amd/csrc/bitslice_core.hpp"
+#ifdef BS_HOST_INC
+#include BS_HOST_INC  // run-time emitted networks (tests/test_bitslice_rtc.py)
+#else
 #include "../udpspeeder_amd/csrc/gen/bitslice_codes.inc"
+#endif
 
 struct HostIO {
     const uint8_t *in;  // k x 32

@@ -66,6 +66,9 @@ class rsmi_fenc_packet(C.Structure):
     _fields_ = [("slot", C.c_int64), ("len", C.c_int32), ("event", C.c_int32)]
 
 
+# encoder kinds (rsmi_code_encoder)
+ENC_NONE, ENC_GENERIC, ENC_BITSLICE, ENC_BITSLICE_RTC, ENC_COMPILING = 0, 1, 2, 3, 4
+
 RSMI_COOK_NO_CHECKSUM, RSMI_COOK_NO_OBSCURE, RSMI_COOK_NO_XOR = 1, 2, 4
 RSMI_COOK_IV_MAX = 32
 RSMI_COOK_MAX_LEN = 65535
@@ -86,6 +89,10 @@ def _bind(lib: C.CDLL) -> C.CDLL:
         "rsmi_decode_matrix": ([i32, i32, vp, vp, vp, vp], i32),
         "rsmi_prepare_code": ([i32, i32], i32),
         "rsmi_reserve": ([i32, i32, i64, vp], i32),
+        "rsmi_code_encoder": ([i32, i32], i32),
+        "rsmi_wait_code": ([i32, i32], i32),
+        "rsmi_precompile_code": ([i32, i32], i32),
+        "rsmi_bitslice_source": ([i32, i32, C.c_char_p, i64], i64),
         "rsmi_encode_dev": ([i32, i32, vp, i64, i64, i32, i64, vp], i32),
         "rsmi_decode_dev": ([i32, i32, vp, i64, i64, i32, i64, vp, vp, vp], i32),
         "rsmi_encode_ragged": ([vp, i64, vp, vp], i32),

@@ -135,6 +135,8 @@ int ensure_code(Device &D, int k, int n, const Code **out) {
                      "code_dir entry");
         }
         it = D.codes.emplace(key, std::move(c)).first;
+        // no build-time network: compile one in the background (bitslice_rtc.cpp)
+        if (n > k && !has_bitslice(k, n)) bitslice_rtc_request({{k, n}});
     }
     *out = &it->second;
     return RSMI_OK;

@@ -580,6 +580,12 @@ int rsmi_fenc_run_dev(rsmi_fenc *E, uint8_t *slots, int64_t S, void *stream) {
         if (hipEventCreateWithFlags(&E->done, hipEventDisableTiming) != hipSuccess)
             return fail(RSMI_ERR_HIP, "fenc: hipEventCreate");
         E->device = cur;
+        // start compiling the run-time networks of the -f table's codes now, so
+        // they are ready by the time those group sizes come (bitslice_rtc.cpp)
+        std::vector<std::pair<int, int>> codes;
+        for (int x = 1; x <= E->cfg.rs_cnt; ++x)
+            if (E->cfg.rs_y[x - 1] > 0) codes.push_back({x, x + E->cfg.rs_y[x - 1]});
+        rsmi::bitslice_rtc_request(codes);
     } else if (cur != E->device) {
         return fail(RSMI_ERR_INVALID, "rsmi_fenc_run_dev on another device than the encoder's");
     }

@@ -93,28 +93,56 @@ def bitmat(c: int):
 RING = int(os.environ.get("BS_RING", "4"))  # raw-load ring: shard j+RING is requested while shard j is computed
 
 
-def emit_code(k: int, n: int) -> str:
+MAX_ROWS = 10  # parity rows per pass: 8 accumulators each (at 12 rows the 168-VGPR budget spills)
+
+
+def row_blocks(m: int):
+    """Passes over the input for m parity rows: ceil(m / MAX_ROWS) blocks of
+    near-equal size.  Every pass reloads the k input shards."""
+    nb = max(1, (m + MAX_ROWS - 1) // MAX_ROWS)
+    bs = (m + nb - 1) // nb
+    return [(b * bs, min(m, (b + 1) * bs)) for b in range(nb) if b * bs < m]
+
+
+def emit_code(k: int, n: int):
     m = n - k
     P = enc_matrix(k, n)
     L = []
-    w = L.append
-    w(f"// RS(k={k}, n={n}): {8 * m} output planes <- {8 * k} input planes")
-    w(f"template <class IO>")
-    w(f"__host__ __device__ __forceinline__ void bs_code_{k}_{n}(IO &io) {{")
-    for i in range(m):
-        w("    uint32_t " + ", ".join(f"o{i}_{u} = 0" for u in range(8)) + ";")
     nxor = 0
+    blocks = row_blocks(m)
+    L.append(f"// RS(k={k}, n={n}): {8 * m} output planes <- {8 * k} input planes")
+    L.append(f"template <class IO>")
+    L.append(f"__host__ __device__ __forceinline__ void bs_code_{k}_{n}(IO &io) {{")
+    for (r0, r1) in blocks:
+        ind = "    " if len(blocks) == 1 else "        "
+        if len(blocks) > 1:
+            L.append(f"    {{  // parity rows {r0}..{r1 - 1}")
+        nxor += emit_block(L.append, ind, k, P, r0, r1)
+        if len(blocks) > 1:
+            L.append(f"    }}")
+            L.append(f"    BS_SCHED_BARRIER();")
+    L.append(f"}}  // {nxor} XOR ops")
+    return "\n".join(L), nxor
+
+
+def emit_block(w0, ind, k, P, r0, r1):
+    """One pass: load every input shard once, accumulate parity rows r0..r1-1."""
+    def w(line):
+        w0(ind + line)
+    nxor = 0
+    for i in range(r0, r1):
+        w("uint32_t " + ", ".join(f"o{i}_{u} = 0" for u in range(8)) + ";")
     R = min(RING, k)
-    w("    uint32_t " + ", ".join(f"rb{r}[8]" for r in range(R)) + ";")
+    w("uint32_t " + ", ".join(f"rb{r}[8]" for r in range(R)) + ";")
     for r in range(R):
-        w(f"    io.load({r}, rb{r});")
+        w(f"io.load({r}, rb{r});")
     for j in range(k):
-        w(f"    {{  // input shard {j}")
-        w(f"        uint32_t (&p)[8] = rb{j % R};")
-        w(f"        bs_transpose8(p);")
+        w(f"{{  // input shard {j}")
+        w(f"    uint32_t (&p)[8] = rb{j % R};")
+        w(f"    bs_transpose8(p);")
         need_lo, need_hi = {}, {}
         terms = {}
-        for i in range(m):
+        for i in range(r0, r1):
             M = bitmat(P[i][j])
             for u in range(8):
                 lo = sum(M[u][t] << t for t in range(4))
@@ -124,57 +152,55 @@ def emit_code(k: int, n: int) -> str:
                     need_lo[lo] = 1
                 if hi:
                     need_hi[hi] = 1
+
         # combination names: single planes are p[t]; multi-plane masks get a temp
         def build(needed, base, tag):
             nonlocal nxor
             names = {}
             for t in range(4):
                 names[1 << t] = f"p[{base + t}]"
-            todo = sorted(needed, key=lambda x: bin(x).count("1"))
-            for mask in todo:
-                if mask in names:
-                    continue
+
+            def get(mm):
                 # split off the highest plane; build the rest recursively
-                def get(mm):
-                    nonlocal nxor
-                    if mm in names:
-                        return names[mm]
-                    hb = mm.bit_length() - 1
-                    rest = mm & ~(1 << hb)
-                    a = get(rest)
-                    nm = f"{tag}{mm}"
-                    w(f"        const uint32_t {nm} = {a} ^ p[{base + hb}];")
-                    nxor += 1
-                    names[mm] = nm
-                    return nm
+                nonlocal nxor
+                if mm in names:
+                    return names[mm]
+                hb = mm.bit_length() - 1
+                rest = mm & ~(1 << hb)
+                a = get(rest)
+                nm = f"{tag}{mm}"
+                w(f"    const uint32_t {nm} = {a} ^ p[{base + hb}];")
+                nxor += 1
+                names[mm] = nm
+                return nm
+            for mask in sorted(needed, key=lambda x: bin(x).count("1")):
                 get(mask)
             return names
         lo_names = build(need_lo, 0, "l")
         hi_names = build(need_hi, 4, "h")
-        for i in range(m):
+        for i in range(r0, r1):
             for u in range(8):
                 lo, hi = terms[(i, u)]
                 a = lo_names[lo] if lo else None
                 b = hi_names[hi] if hi else None
                 acc = f"o{i}_{u}"
                 if a and b:
-                    w(f"        BS_ACC3({acc}, {a}, {b});")
+                    w(f"    BS_ACC3({acc}, {a}, {b});")
                     nxor += 1
                 elif a or b:
-                    w(f"        BS_ACC2({acc}, {a or b});")
+                    w(f"    BS_ACC2({acc}, {a or b});")
                     nxor += 1
         if j + R < k:
-            w(f"        io.load({j + R}, rb{j % R});")
-        w(f"    }}")
-        w(f"    BS_SCHED_BARRIER();")
-    for i in range(m):
-        w(f"    {{")
-        w(f"        uint32_t q[8] = {{" + ", ".join(f"o{i}_{u}" for u in range(8)) + "};")
-        w(f"        bs_transpose8(q);")
-        w(f"        io.store({k + i}, q);")
-        w(f"    }}")
-    w(f"}}  // {nxor} XOR ops")
-    return "\n".join(L), nxor
+            w(f"    io.load({j + R}, rb{j % R});")
+        w(f"}}")
+        w(f"BS_SCHED_BARRIER();")
+    for i in range(r0, r1):
+        w(f"{{")
+        w(f"    uint32_t q[8] = {{" + ", ".join(f"o{i}_{u}" for u in range(8)) + "};")
+        w(f"    bs_transpose8(q);")
+        w(f"    io.store({k + i}, q);")
+        w(f"}}")
+    return nxor
 
 
 def default_codes():
@@ -189,12 +215,32 @@ def default_codes():
     return sorted(codes)
 
 
+def embed(out, specs):
+    here = os.path.dirname(os.path.abspath(__file__))
+    parts = ["// GENERATED by gen_bitslice.py --embed -- do not edit."]
+    for spec in specs:
+        path, name = spec.rsplit(":", 1)
+        txt = open(os.path.join(here, path)).read()
+        txt = "\n".join(l for l in txt.split("\n") if l.strip() != "#pragma once") + "\n"
+        assert ')rsmi"' not in txt
+        parts.append(f'static const char {name}[] = R"rsmi({txt})rsmi";')
+    txt = "\n".join(parts) + "\n"
+    if not (os.path.exists(out) and open(out).read() == txt):
+        with open(out, "w") as f:
+            f.write(txt)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=os.path.join(os.path.dirname(os.path.abspath(__file__)),
                                                   "gen", "bitslice_codes.inc"))
     ap.add_argument("--codes", default="", help="k:n,k:n,... (default: built-in hot set)")
+    ap.add_argument("--embed", nargs="+", metavar="OUT FILE:NAME",
+                    help="write FILEs as C++ string constants NAME into OUT (the device "
+                         "headers bitslice_rtc.cpp hands to hipRTC)")
     args = ap.parse_args()
+    if args.embed:
+        return embed(args.embed[0], args.embed[1:])
     codes = default_codes() if not args.codes else \
         [tuple(int(v) for v in c.split(":")) for c in args.codes.split(",")]
     os.makedirs(os.path.dirname(args.out), exist_ok=True)

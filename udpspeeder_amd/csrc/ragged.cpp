@@ -2,14 +2,18 @@
 //
 // A plan is built once on the host from the rsmi_group descriptors and kept on
 // the device, like an FFT plan: launches over the same batch layout reuse it
-// (and are graph-capturable).  When every group's (k,n) has a specialised
-// bit-sliced network the plan buckets groups by code and maps every 16-byte
-// column to (group, piece) so one launch of k_bs_ragged covers all buckets;
-// otherwise it falls back to the generic one-wave-per-group kernel.
+// (and are graph-capturable).  When every group's (k,n) has a bit-sliced
+// network the plan buckets groups by code and maps every 16-byte column to
+// (group, piece): one launch of k_bs_ragged covers the buckets of build-time
+// codes, and each run-time compiled code (bitslice_rtc.cpp) gets one launch
+// over its own bucket -- if all of those are compiled when the plan is made
+// (plan creation does not wait: rsmi_wait_code).  Otherwise the plan falls
+// back to the generic one-wave-per-group kernel.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <cstring>
+#include <map>
 #include <string>
 #include <vector>
 
@@ -31,6 +35,12 @@ struct rsmi_ragged_plan {
     bool bitslice = false;
     uint32_t bytes = 0;       // extent of the batch from base (bitslice path)
     uint32_t nwaves = 0;
+    uint32_t nwaves_builtin = 0;  // waves [0, nwaves_builtin) belong to build-time codes
+    struct RtcBucket {
+        int k, n;
+        uint32_t first, count;  // slice of the wave list
+    };
+    std::vector<RtcBucket> rtc;
     uint8_t *mem = nullptr;   // one device allocation: groups | colmap | waves
     rsmi_group *d_groups = nullptr;
     uint32_t *d_colmap = nullptr;
@@ -56,6 +66,8 @@ extern "C" int rsmi_ragged_plan_create(const rsmi_group *g, int64_t ngroups,
     bool bs = ngroups < (int64_t(1) << 20);
     std::vector<int> code_of((size_t)ngroups, -1);
     std::vector<uint8_t> seen(257 * 257, 0);
+    std::map<int, int> rtc_index;  // k*257+n -> position in rtc_codes
+    std::vector<std::pair<int, int>> rtc_codes;
     for (int64_t i = 0; i < ngroups; ++i) {
         const rsmi_group &d = g[i];
         if (d.k < 1 || d.n < d.k || d.n > 256 || d.reserved != 0 || d.offset % 16 ||
@@ -72,11 +84,28 @@ extern "C" int rsmi_ragged_plan_create(const rsmi_group *g, int64_t ngroups,
         const uint64_t end = d.offset + (uint64_t)(d.n - 1) * d.shard_stride +
                              ((d.len + 15u) & ~15u);
         extent = std::max(extent, end);
-        const int ci = rsmi::bitslice_code_index(d.k, d.n);
-        if (ci < 0 || d.len > 65536) bs = false;
+        int ci = rsmi::bitslice_code_index(d.k, d.n);
+        if (ci < 0) {
+            if (rsmi::bitslice_rtc_eligible(d.k, d.n)) {
+                auto it = rtc_index.find(key);
+                if (it == rtc_index.end()) {
+                    it = rtc_index.emplace(key, (int)rtc_codes.size()).first;
+                    rtc_codes.push_back({(int)d.k, (int)d.n});
+                }
+                ci = rsmi::bitslice_builtin_count() + it->second;
+            } else {
+                bs = false;
+            }
+        }
+        if (d.len > 65536) bs = false;
         code_of[(size_t)i] = ci;
     }
     if (extent >= 0x80000000ull) bs = false;
+    // codes without a build-time network: prepare_code above queued their
+    // compiles; the plan takes the bit-sliced path only if every one is ready
+    // now (rsmi_wait_code first to be sure) and never waits for them itself
+    for (auto &c : rtc_codes)
+        if (bs && !rsmi::bitslice_rtc_function(c.first, c.second, true)) bs = false;
 
     rsmi_ragged_plan *P = new rsmi_ragged_plan();
     if (hipGetDevice(&P->device) != hipSuccess) {
@@ -113,12 +142,21 @@ extern "C" int rsmi_ragged_plan_create(const rsmi_group *g, int64_t ngroups,
             for (uint32_t p = 0; p < pcs; ++p) colmap[(size_t)(c + p)] = ((uint32_t)i << 12) | p;
             fill[(size_t)b] += pcs;
         }
-        for (int b = 0; b < nb; ++b)
+        const int nbuiltin = rsmi::bitslice_builtin_count();
+        for (int b = 0; b < nb; ++b) {
+            if (b == nbuiltin) P->nwaves_builtin = (uint32_t)(waves.size() / 2);
+            const uint32_t first = (uint32_t)(waves.size() / 2);
             for (uint64_t w = 0; w < (cols[(size_t)b] + 127) / 128; ++w) {
                 waves.push_back((uint32_t)b);
                 waves.push_back((uint32_t)(base[(size_t)b] + 128 * w));
             }
+            if (b >= nbuiltin && cols[(size_t)b] > 0) {
+                const auto &c = rtc_codes[(size_t)(b - nbuiltin)];
+                P->rtc.push_back({c.first, c.second, first, (uint32_t)(waves.size() / 2) - first});
+            }
+        }
         P->nwaves = (uint32_t)(waves.size() / 2);
+        if (nb <= nbuiltin) P->nwaves_builtin = P->nwaves;
     }
     const size_t gbytes = sizeof(rsmi_group) * (size_t)ngroups;
     const size_t cbytes = sizeof(uint32_t) * colmap.size();
@@ -155,8 +193,14 @@ extern "C" int rsmi_encode_ragged_plan(const rsmi_ragged_plan *P, uint8_t *base,
     hipStream_t s = (hipStream_t)stream;
     hipError_t e;
     if (P->bitslice) {
-        e = rsmi::launch_encode_bitslice_ragged(P->d_groups, P->d_colmap, P->d_waves, P->nwaves,
-                                                base, P->bytes, s);
+        e = rsmi::launch_encode_bitslice_ragged(P->d_groups, P->d_colmap, P->d_waves,
+                                                P->nwaves_builtin, base, P->bytes, s);
+        for (size_t i = 0; e == hipSuccess && i < P->rtc.size(); ++i) {
+            const auto &b = P->rtc[i];
+            e = rsmi::launch_encode_bitslice_ragged_rtc(b.k, b.n, P->d_groups, P->d_colmap,
+                                                        P->d_waves + 2 * (size_t)b.first, b.count,
+                                                        base, P->bytes, s);
+        }
     } else {
         int rc;
         const uint64_t *dir = rsmi::device_code_dir(&rc);

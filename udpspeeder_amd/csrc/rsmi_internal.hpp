@@ -4,6 +4,9 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <string>
+#include <utility>
+#include <vector>
 
 #include "../../include/rsmi.h"
 #include "../../include/rsmi_fec.h"
@@ -63,8 +66,9 @@ hipError_t launch_decode_ragged(const rsmi_group *groups, int64_t ngroups, uint8
                                 const uint8_t *gftab, hipStream_t s);
 
 // Bit-sliced encode kernels specialised at build time for hot (k,n) codes
-// (gen_bitslice.py -> gen/bitslice_codes.inc).  Returns hipErrorNotSupported
-// when (k,n) has no specialised kernel.
+// (gen_bitslice.py -> gen/bitslice_codes.inc), or compiled at run time
+// (bitslice_rtc.cpp).  Returns hipErrorNotSupported when (k,n) has neither
+// (yet).
 hipError_t launch_encode_bitslice(const UniformArgs &a, hipStream_t s);
 bool has_bitslice(int k, int n);
 int bitslice_code_index(int k, int n);  // position in the generated code list, -1 if none
@@ -73,6 +77,20 @@ int bitslice_code_index(int k, int n);  // position in the generated code list, 
 hipError_t launch_encode_bitslice_ragged(const rsmi_group *groups, const uint32_t *colmap,
                                          const uint32_t *waves, uint32_t nwaves, uint8_t *base,
                                          uint32_t bytes, hipStream_t s);
+
+// Codes without a build-time network (bitslice_rtc.cpp): emitted and compiled
+// with hipRTC in the background when first made resident.
+int bitslice_builtin_count();
+bool bitslice_emit(int k, int n, std::string &src, int *nxor);  // gen_bitslice.emit_code's text
+bool bitslice_rtc_eligible(int k, int n);
+void bitslice_rtc_request(const std::vector<std::pair<int, int>> &codes);  // async
+void bitslice_rtc_wait(const std::vector<std::pair<int, int>> &codes);
+int bitslice_rtc_state(int k, int n);  // 0 idle, 1 compiling, 2 ready, 3 failed
+hipFunction_t bitslice_rtc_function(int k, int n, bool ragged);  // nullptr unless ready
+hipError_t launch_encode_bitslice_ragged_rtc(int k, int n, const rsmi_group *groups,
+                                             const uint32_t *colmap, const uint32_t *waves,
+                                             uint32_t nwaves, uint8_t *base, uint32_t bytes,
+                                             hipStream_t s);
 
 constexpr int kPtabDwords = 8;  // per coefficient: T0lo T0hi T1lo T1hi | T2 pad pad pad
 

@@ -248,6 +248,10 @@ def make_groups(ks: Iterable[int], ns: Iterable[int], lens: Iterable[int],
     return arr, int(sizes.sum()) if len(sizes) else 0
 
 
+_GROUP_DT = np.dtype([("offset", "<u8"), ("shard_stride", "<u4"), ("len", "<u4"),
+                      ("k", "<u2"), ("n", "<u2"), ("reserved", "<u4")])  # rsmi_group, 24 B
+
+
 def encode_ragged(base, groups, stream=None) -> None:
     """Encode a ragged batch in one launch.  ``base`` is a 1-D uint8 CUDA tensor,
     ``groups`` a ctypes rsmi_group array from make_groups (host)."""
@@ -260,9 +264,17 @@ def encode_ragged(base, groups, stream=None) -> None:
 class RaggedPlan:
     """A device-resident plan for one ragged batch layout (rsmi_ragged_plan)."""
 
-    def __init__(self, groups):
+    def __init__(self, groups, wait_codes: bool = True):
+        """``wait_codes``: first wait for the run-time bit-sliced networks of
+        the batch's codes (rsmi_wait_code), so the plan takes the bit-sliced
+        path; False makes the plan at once (generic kernel for a batch with a
+        code still compiling)."""
         self._h = C.c_void_p()
         self.ngroups = len(groups)
+        if wait_codes and self.ngroups:
+            arr = np.frombuffer(bytes(groups), dtype=_GROUP_DT)
+            for k, n in sorted(set(zip(arr["k"].tolist(), arr["n"].tolist()))):
+                check(lib().rsmi_wait_code(k, n), "rsmi_wait_code")
         check(lib().rsmi_ragged_plan_create(C.cast(groups, C.c_void_p), len(groups),
                                             C.byref(self._h)), "rsmi_ragged_plan_create")
 
@@ -342,6 +354,38 @@ def decode_ragged(base, groups, present_bits, status=None, stream=None):
 
 def prepare_code(k: int, n: int) -> None:
     check(lib().rsmi_prepare_code(k, n), "rsmi_prepare_code")
+
+
+def wait_code(k: int, n: int) -> None:
+    """prepare_code, then wait for the (k,n) run-time bit-sliced network (if
+    the code gets one) and load it on the current device."""
+    check(lib().rsmi_wait_code(k, n), "rsmi_wait_code")
+
+
+def precompile_code(k: int, n: int) -> None:
+    """Compile the run-time network of (k,n) now (no GPU needed); raises
+    RsmiError for codes that get none (built-in, n == k, too large)."""
+    check(lib().rsmi_precompile_code(k, n), "rsmi_precompile_code")
+
+
+def code_encoder(k: int, n: int) -> int:
+    """Which encoder (k,n) runs now: _lib.ENC_* (generic, build-time bit-sliced,
+    run-time bit-sliced, still compiling)."""
+    r = lib().rsmi_code_encoder(k, n)
+    if r < 0:
+        check(r, "rsmi_code_encoder")
+    return r
+
+
+def bitslice_source(k: int, n: int) -> str:
+    """The XOR-network source of (k,n) as emitted for hipRTC."""
+    L = lib()
+    size = L.rsmi_bitslice_source(k, n, None, 0)
+    if size < 0:
+        check(int(size), "rsmi_bitslice_source")
+    buf = C.create_string_buffer(size + 1)
+    L.rsmi_bitslice_source(k, n, buf, size + 1)
+    return buf.value.decode()
 
 
 def reserve(k: int, n: int, ngroups: int, stream=None) -> None:
