@@ -361,6 +361,7 @@ def rtc_config(u, synth, torch, dev, k=10, m=5, groups=131072):
     buf = torch.zeros((groups, n, 1280), dtype=torch.uint8, device=dev)
     u.fill_data(buf, k, LEN, synth.DATA_SEED)
     ms = _time_ms(torch, lambda: u.encode(buf, k, n, LEN))
+    last = u.lib().rsmi_last_encoder()
     prev = u.rs.set_bitslice(False)
     try:
         ms_generic = _time_ms(torch, lambda: u.encode(buf, k, n, LEN), reps=5)
@@ -369,7 +370,8 @@ def rtc_config(u, synth, torch, dev, k=10, m=5, groups=131072):
     del buf
     alg = groups * n * LEN
     return {"code": f"{k}:{m}", "groups": groups, "len": LEN,
-            "encoder": "bitslice_rtc" if kind == ENC_BITSLICE_RTC else f"kind{kind}",
+            "encoder": "bitslice_rtc" if kind == ENC_BITSLICE_RTC and last == kind else
+                       f"kind{kind}/ran{last}",
             "wait_code_s": round(compile_s, 2), "encode_ms": round(ms, 4),
             "alg_GBps": round(alg / (ms * 1e-3) / 1e9, 1),
             "roofline_frac": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),

@@ -61,8 +61,9 @@ int rsmi_init(void);
 const char *rsmi_last_error(void);
 
 /* Engine options (process-wide).  RSMI_OPT_BITSLICE: 1 (default) uses the
- * build-time specialised bit-sliced encoders where available, 0 forces the
- * generic table kernel (for A/B tests).  Returns the previous value. */
+ * bit-sliced encoders (build-time or run-time compiled, rsmi_code_encoder)
+ * where available, 0 forces the generic table kernel for uniform encodes (for
+ * A/B tests).  Returns the previous value. */
 #define RSMI_OPT_BITSLICE 1
 /* RSMI_OPT_FUSED_DECODE: 1 (default) builds decode matrices and rebuilds the
  * rows in one fused kernel where the code fits it, 0 forces the two-kernel
@@ -105,6 +106,10 @@ int rsmi_prepare_code(int k, int n);
 #define RSMI_ENC_BITSLICE_RTC 3  /* run-time compiled bit-sliced network       */
 #define RSMI_ENC_COMPILING 4     /* generic now; network compiling             */
 int rsmi_code_encoder(int k, int n);
+
+/* The encoder kind this thread's last uniform encode launched (RSMI_ENC_*;
+ * RSMI_ENC_NONE before the first, or when it had nothing to compute). */
+int rsmi_last_encoder(void);
 
 /* rsmi_prepare_code, then block until the (k,n) run-time network (if the code
  * gets one) has compiled or failed, and load it on the current device (do

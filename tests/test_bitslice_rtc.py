@@ -147,6 +147,7 @@ def test_rtc_encode_vs_oracle(gpu, oracle, u, k, n, ln):
     buf = rng.integers(0, 256, (G, n, S), dtype=np.uint8)
     t = torch.from_numpy(buf).to(gpu)
     u.encode(t, k, n, ln)
+    assert u.lib().rsmi_last_encoder() == ENC_BITSLICE_RTC  # the run-time kernel ran
     oracle.encode_batch(k, n, buf.reshape(-1), n * S, S, ln, G)
     out = t.cpu().numpy()
     assert (out[:, :, :ln] == buf[:, :, :ln]).all()
@@ -197,5 +198,7 @@ def test_rtc_before_ready_is_generic_and_exact(gpu, oracle, u):
     u.wait_code(k, n)
     t2 = torch.from_numpy(buf.copy()).to(gpu)
     u.encode(t2, k, n, ln)
+    from udpspeeder_amd._lib import ENC_BITSLICE_RTC
+    assert u.lib().rsmi_last_encoder() == ENC_BITSLICE_RTC
     for t in (t1, t2):
         assert (t.cpu().numpy()[:, :, :ln] == ref[:, :, :ln]).all()

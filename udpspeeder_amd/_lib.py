@@ -90,6 +90,7 @@ def _bind(lib: C.CDLL) -> C.CDLL:
         "rsmi_prepare_code": ([i32, i32], i32),
         "rsmi_reserve": ([i32, i32, i64, vp], i32),
         "rsmi_code_encoder": ([i32, i32], i32),
+        "rsmi_last_encoder": ([], i32),
         "rsmi_wait_code": ([i32, i32], i32),
         "rsmi_precompile_code": ([i32, i32], i32),
         "rsmi_bitslice_source": ([i32, i32, C.c_char_p, i64], i64),

@@ -22,6 +22,7 @@ namespace rsmi {
 namespace {
 
 thread_local std::string g_err;
+thread_local int g_last_enc = RSMI_ENC_NONE;  // rsmi_last_encoder
 std::atomic<int> g_opt_bitslice{1};
 std::atomic<int> g_opt_fused{1};
 
@@ -218,7 +219,12 @@ int encode_dev(int k, int n, uint8_t *base, int64_t gs, int64_t ss, int len, int
     int W;
     UniformArgs a = make_args(k, n, base, gs, ss, len, ngroups, &W);
     hipError_t e = hipErrorNotSupported;
-    if (g_opt_bitslice.load() && has_bitslice(k, n)) e = launch_encode_bitslice(a, s);
+    // build-time network, else the run-time one once compiled (NotSupported
+    // until then), else the generic table kernel
+    if (g_opt_bitslice.load()) e = launch_encode_bitslice(a, s);
+    g_last_enc = e == hipErrorNotSupported ? RSMI_ENC_GENERIC
+                 : has_bitslice(k, n)      ? RSMI_ENC_BITSLICE
+                                           : RSMI_ENC_BITSLICE_RTC;
     if (e == hipErrorNotSupported) e = launch_encode_generic(a, W, C->dev_rows, D->ptab, s);
     if (e != hipSuccess) return hip_fail(e, "encode launch");
     return RSMI_OK;
@@ -616,6 +622,8 @@ int rsmi_decode_matrix(int k, int n, const uint8_t *present, uint8_t *sel, uint8
 }
 
 int rsmi_prepare_code(int k, int n) { return rsmi::prepare_code(k, n); }
+
+int rsmi_last_encoder(void) { return rsmi::g_last_enc; }
 
 int rsmi_reserve(int k, int n, int64_t ngroups, void *stream) {
     return rsmi::reserve(k, n, ngroups, (hipStream_t)stream);

@@ -134,7 +134,8 @@ hipError_t launch_encode_bitslice(const UniformArgs &a, hipStream_t s) {
     const int64_t per = (chunks + slots - 1) / slots;
     waves = (chunks + per - 1) / per;
 #endif
-    const int64_t blocks = (waves + 3) / 4;
+    int64_t blocks = (waves + 3) / 4;
+    if (BS_XCD) blocks = (blocks + 7) & ~int64_t(7);  // the remap needs whole rounds of 8 XCDs
     if (blocks > 0x7fffffff) return hipErrorNotSupported;
     uint8_t *base = a.base;
     int64_t gs = a.group_stride, ss = a.shard_stride;

@@ -35,6 +35,10 @@
 #define BS_ST_SGPR 0  // 1: shard offset of the parity stores in soffset (the round-1 form: wrong
                       // parity dwords under co-resident load, see DevIO::store)
 #endif
+#ifndef BS_XCD
+#define BS_XCD 1  // blocks b, b+8, ... (dispatched to one XCD) take one contiguous range of
+                  // chunks (measured 1.5 % faster than the plain order, scripts/gpu_bench_ab.sh)
+#endif
 #define BS_ACC3(acc, a, b) ((acc) = __builtin_amdgcn_bitop3_b32((acc), (a), (b), 0x96))
 #define BS_ACC2(acc, a) ((acc) ^= (a))
 // keep the generated shard blocks in order so the raw-load ring bounds the
@@ -114,7 +118,9 @@ __device__ __forceinline__ DevIO bs_make_io(uint8_t *base0, int64_t group_stride
     __global__ __launch_bounds__(256, OCC) void NAME(uint8_t *base, int64_t group_stride,     \
                                                         int64_t shard_stride, uint32_t cols,     \
                                                         uint32_t P, uint32_t wstep) {            \
-        for (uint32_t wave = blockIdx.x * 4u + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  \
+        const uint32_t bid = BS_XCD ? (blockIdx.x & 7u) * (gridDim.x >> 3) + (blockIdx.x >> 3)   \
+                                    : blockIdx.x;                                                \
+        for (uint32_t wave = bid * 4u + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);         \
              wave * 128u < cols; wave += wstep) {                                                \
             DevIO io = bs_make_io(base, group_stride, shard_stride, cols, P, wave);               \
             FN(io);                                                                              \

@@ -65,6 +65,9 @@ constexpr int kTile = 1280;    // bytes per lane-tile pass (64 x 16 + 64 x 4)
 #ifndef DEC_NOMEM
 #define DEC_NOMEM 0            // measurement only: survivor loads all hit one cached slot
 #endif
+#ifndef DEC_XCD
+#define DEC_XCD 1              // XCD-contiguous group ranges (see k_decode_fused; ~0.5 %)
+#endif
 #ifndef DEC_PAIR
 #define DEC_PAIR 0             // uniform kernel: fold survivors in pairs (fewer XORs, more VGPRs)
 #endif
@@ -413,7 +416,11 @@ __global__ __launch_bounds__(256, DEC_OCC) void k_decode_fused(UniformArgs a, co
     // DEC_NOMEM (measurement only): every survivor load reads group 0's slot 0
     const __amdgpu_buffer_rsrc_t rsrc0 = __builtin_amdgcn_make_buffer_rsrc(a.base, 0, 4096, 0x00020000);
     const int64_t nwaves = (int64_t)gridDim.x * kWaves;
-    const int64_t g0 = (int64_t)blockIdx.x * kWaves + wid;
+    // DEC_XCD: blocks b, b+8, ... (dispatched to one XCD) take adjacent groups
+    const int64_t bid = (DEC_XCD && (gridDim.x & 7) == 0)
+                            ? (int64_t)(blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3)
+                            : (int64_t)blockIdx.x;
+    const int64_t g0 = bid * kWaves + wid;
     // present flags of the first 64 shards, prefetched one group ahead
     uint32_t pf = (g0 < a.ngroups && lane < n) ? present[g0 * n + lane] : 0u;
     uint32_t pf_next = 0;
