@@ -16,3 +16,5 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/pro
     python3 $R/bench.py --no-cpu-baseline > $O/prof.log 2>&1 || exit 1
 cd $R
 python scripts/kstats.py $O/prof/run_kernel_stats.csv | grep rsmi
+timeout -k 10 300 python -u scripts/e2e_host.py > $O/e2e.json 2> $O/e2e.err || { tail $O/e2e.err; exit 1; }
+tail -5 $O/e2e.json

@@ -52,6 +52,21 @@ struct Workspace {
     size_t bytes = 0;
 };
 
+// Streams and buffers of the pinned host<->device pipelines (rsmi_encode_pinned,
+// rsmi_decode_pinned): one of each per device, one call at a time.
+struct Pipeline {
+    static constexpr int kDepth = 3;
+    std::mutex mu;
+    hipStream_t st[kDepth] = {};
+    uint8_t *dev[kDepth] = {};
+    size_t bytes = 0;
+    int32_t *dstat[kDepth] = {};  // decode: status and present flags per stage
+    uint8_t *dpres[kDepth] = {};
+    int64_t cap = 0;
+    uint8_t *hpin = nullptr;      // decode: pinned copies of present / status (pageable
+    size_t hpin_bytes = 0;        // small copies would block the issuing thread)
+};
+
 struct Device {
     int id = -1;
     std::mutex mu;
@@ -69,6 +84,7 @@ struct Device {
     size_t hdev_bytes = 0;
     int32_t *hstatus_dev = nullptr;
     size_t hstatus_cap = 0;
+    Pipeline penc, pdec;
 };
 
 std::mutex g_devs_mu;
@@ -434,14 +450,7 @@ int host_op(bool decode, int k, int n, uint8_t *base, int64_t gs, int64_t ss, in
     return host_op_ptrs(decode, k, n, p.data(), o.data(), len, ngroups, present, status);
 }
 
-// ---- pipelined host <-> device encode (rsmi_encode_pinned) ----------------
-struct Pipeline {
-    static constexpr int kDepth = 3;
-    hipStream_t st[kDepth] = {};
-    uint8_t *dev[kDepth] = {};
-    size_t bytes = 0;
-};
-
+// ---- pipelined host <-> device encode / decode (rsmi_*_pinned) ------------
 int encode_pinned(int k, int n, const uint8_t *hd, int64_t dgs, uint8_t *hp, int64_t pgs,
                   int64_t ss, int len, int64_t ngroups, int64_t chunk) {
     int rc = check_uniform(k, n, nullptr, 16, ss, len, 0);
@@ -452,9 +461,8 @@ int encode_pinned(int k, int n, const uint8_t *hd, int64_t dgs, uint8_t *hp, int
     if (ngroups == 0 || n == k || len == 0) return RSMI_OK;
     Device *D = current(&rc);
     if (!D) return rc;
-    static std::mutex pmu;  // one pipeline per process at a time
-    static Pipeline P;
-    std::lock_guard<std::mutex> lk(pmu);
+    Pipeline &P = D->penc;  // this device's encode pipeline, one call at a time
+    std::lock_guard<std::mutex> lk(P.mu);
     const int64_t dgs_dev = (int64_t)n * ss;
     const size_t need = (size_t)(dgs_dev * chunk);
     if (P.bytes < need) {
@@ -497,14 +505,13 @@ int decode_pinned(int k, int n, uint8_t *hs, int64_t hgs, int64_t ss, int len, i
     if (ngroups == 0) return RSMI_OK;
     Device *D = current(&rc);
     if (!D) return rc;
-    static std::mutex pmu;
-    static Pipeline P;
-    static int32_t *dstat[Pipeline::kDepth] = {};
-    static uint8_t *dpres[Pipeline::kDepth] = {};
-    static int64_t cap = 0;
-    static uint8_t *hpin = nullptr;  // pinned copies of present / status: pageable
-    static size_t hpin_bytes = 0;    // small copies would block the issuing thread
-    std::lock_guard<std::mutex> lk(pmu);
+    Pipeline &P = D->pdec;  // this device's decode pipeline, one call at a time
+    std::lock_guard<std::mutex> lk(P.mu);
+    int32_t **dstat = P.dstat;
+    uint8_t **dpres = P.dpres;
+    int64_t &cap = P.cap;
+    uint8_t *&hpin = P.hpin;
+    size_t &hpin_bytes = P.hpin_bytes;
     const size_t pin_need = (size_t)(n * ngroups + 64) + sizeof(int32_t) * (size_t)ngroups;
     if (hpin_bytes < pin_need) {
         if (hpin) (void)hipHostFree(hpin);
