@@ -154,6 +154,29 @@ def _gpu_run(chan, cuts, torch):
     return ret, out
 
 
+def _gpu_run_pipelined(chan, cuts, torch):
+    """plan(i+1) and run(i+1) before batch i's outputs are taken, batches on
+    two alternating streams (the decoder's double-buffered batches)."""
+    from udpspeeder_amd.fec import FecDecoder
+    host, lens, offs = _pack(chan)
+    dev = torch.from_numpy(host).cuda()
+    torch.cuda.synchronize()
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    dec = FecDecoder()
+    ret, out = [], []
+    starts = []
+    for bi, (a, b) in enumerate(zip(cuts[:-1], cuts[1:])):
+        p = dec.plan(host, lens[a:b], offs[a:b], dev)
+        ret += list(p.ret)
+        dec.run(stream=streams[bi % 2])
+        starts.append(a)
+        if bi:  # the previous batch's outputs, after this batch was planned and launched
+            out += [(bts, e + starts[bi - 1]) for bts, e in dec.outputs()]
+    out += [(bts, e + starts[-1]) for bts, e in dec.outputs()]
+    dec.close()
+    return ret, out
+
+
 def _cuts(n, nbatch, seed):
     rng = np.random.default_rng(seed)
     if nbatch == 1:
@@ -206,6 +229,19 @@ def test_gpu_decoder_threaded_outputs(gpu, monkeypatch, mode, threads):
     assert g_ret == ret
     assert [e for _, e in g_out] == ev
     assert [b for b, _ in g_out] == out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode,rs", [(0, "20:10"), (1, "1:3,2:4,10:6,20:10")])
+def test_gpu_decoder_pipelined_two_streams(gpu, mode, rs):
+    import torch
+    chan = _long_run(mode, rs, 55 + mode)
+    ret, out, ev = _oracle_run(chan)
+    g_ret, g_out = _gpu_run_pipelined(chan, _cuts(len(chan), 6, 8), torch)
+    assert g_ret == ret
+    assert [e for _, e in g_out] == ev
+    bad = [i for i, ((b, _), x) in enumerate(zip(g_out, out)) if b != x]
+    assert not bad, (len(bad), bad[:5])
 
 
 @pytest.mark.gpu

@@ -169,6 +169,65 @@ def test_gpu_frames_match_oracle_large(gpu, rs, mode, mtu, ql, lmax):
     enc.close()
 
 
+def _run_gpu_pipelined(enc, lens, ev, cuts, torch):
+    """As _run_gpu, but batch i+1 is planned while batch i still runs, and the
+    batches alternate between two streams (the double-buffered plan sets)."""
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    pending = []
+    for bi, (a, b) in enumerate(zip(cuts[:-1], cuts[1:])):
+        ln = lens[a:b]
+        offs = np.zeros(b - a, np.uint64)
+        o = 0
+        chunks = []
+        for i in range(a, b):
+            offs[i - a] = o
+            if ev[i] is not None:
+                chunks.append(ev[i])
+                o += len(ev[i])
+        s = streams[bi % 2]
+        with torch.cuda.stream(s):
+            inbuf = torch.from_numpy(np.frombuffer(b"".join(chunks) + bytes(32), np.uint8).copy()
+                                     ).to("cuda", non_blocking=False)
+            p = enc.plan(ln, offs, inbuf)  # the previous batch may still be on the GPU
+            S = (p.slot_stride_min + 127) // 128 * 128
+            slots = torch.full((max(1, p.n_slots) * S,), 0xEE, dtype=torch.uint8, device="cuda")
+            enc.run(slots, S, stream=s)
+        pending.append((p, slots, S, inbuf, a))
+    torch.cuda.synchronize()
+    out = []
+    for p, slots, S, _, a in pending:
+        h = slots.cpu().numpy()
+        out += [(h[s * S + 120:s * S + 120 + l].tobytes(), int(e) + a) for s, l, e in p.packets]
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rs,mode", [("20:10", 0), ("1:3,2:4,10:6,20:10", 1)])
+def test_gpu_frames_pipelined_two_streams(gpu, rs, mode):
+    """Planning batch i+1 during batch i's GPU run, on two streams, gives the
+    restatement's packets byte for byte."""
+    import torch
+    from udpspeeder_amd.fec import FecEncoder
+    rng = np.random.default_rng(41 + mode)
+    n = 9000
+    lens = rng.integers(0, 1000, n).astype(np.int32)
+    lens[rng.random(n) < 0.01] = -1
+    pay = cook_payloads(0xBEEF + mode, 0, n, np.maximum(lens, 0), 1000)
+    ev = [None if lens[i] < 0 else pay[i, :lens[i]].tobytes() for i in range(n)]
+    enc = FecEncoder(rs, mode, 1250, 200, seq0=5)
+    em = EncodeManager(rs, mode, 1250, 200, 5)
+    exp = []
+    for i, e in enumerate(ev):
+        em.input(e)
+        exp += [(p, i) for p in em.output()]
+    cuts = np.unique(np.concatenate([[0, n], rng.integers(0, n, 7)]))
+    out = _run_gpu_pipelined(enc, lens, ev, cuts, torch)
+    assert len(out) == len(exp)
+    bad = [i for i, (a, b) in enumerate(zip(out, exp)) if a != b]
+    assert not bad, (len(bad), bad[:5])
+    enc.close()
+
+
 @pytest.mark.gpu
 def test_gpu_per_call_interface(gpu):
     """input()/output() one event at a time, as fec_manager's callers use it

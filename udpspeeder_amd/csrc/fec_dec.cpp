@@ -168,14 +168,10 @@ struct Spill {
     }
 };
 
-struct rsmi_fdec {
-    int buff_num = 2000;
-    AntiReplay ar;
-    std::unordered_map<uint32_t, Group> mp;
-    std::vector<RingEnt> ring;
-    int index = 0;
-
-    // ---- last plan
+// One batch's plan and results.  Two alternate: batch i+1 is planned on the
+// host while the GPU still runs batch i, and batch i's outputs stay readable
+// until the plan after that.
+struct Batch {
     std::vector<Job> jobs;
     std::vector<Bucket> buckets;
     std::map<int, int> bucket_of;  // k*257+n -> bucket
@@ -191,30 +187,44 @@ struct rsmi_fdec {
     std::vector<Spill> spills = std::vector<Spill>(1);
     int64_t staging_bytes = 0, d2h_bytes = 0;
     const uint8_t *host_base = nullptr;
-    bool planned = false, ran = false, resolved = false, plan_only = false;
+    bool planned = false, ran = false, resolved = false;
+    uint8_t *hmeta = nullptr, *hblob = nullptr;  // pinned: upload source, rows copied back
+    size_t hmeta_cap = 0, hblob_cap = 0;
+    hipEvent_t done = nullptr;
+    bool in_flight = false;
+};
 
-    // ---- device side
+struct rsmi_fdec {
+    int buff_num = 2000;
+    AntiReplay ar;
+    std::unordered_map<uint32_t, Group> mp;
+    std::vector<RingEnt> ring;
+    int index = 0;
+    bool plan_only = false;
+
+    Batch bat[2];
+    int bi = 1;               // bat[bi] is the batch planned last
+    Batch *B = &bat[1];
+    int out_b = -1;           // batch whose outputs rsmi_fdec_output_list reads
+
+    // ---- device side: shared by the two batches, whose device work is ordered
     int device = -1;
     uint8_t *dcarry = nullptr;  // buff_num x kRingBytes, indexed by ring slot
     size_t dcarry_cap = 0;
     uint8_t *dstage = nullptr, *dmeta = nullptr, *dblob = nullptr;
     size_t stage_cap = 0, meta_cap = 0, blob_cap = 0;
-    uint8_t *hmeta = nullptr, *hblob = nullptr;
-    size_t hmeta_cap = 0, hblob_cap = 0;
     int32_t *dstatus = nullptr;
     size_t status_cap = 0;
-    hipEvent_t done = nullptr;
-    bool in_flight = false;
 
     Group &group(uint32_t seq) { return mp[seq]; }  // operator[] inserts, as the reference
 };
 
 namespace {
 
-int wait_idle(rsmi_fdec *D) {
-    if (D->in_flight) {
-        hipError_t e = hipEventSynchronize(D->done);
-        D->in_flight = false;
+int wait_batch(Batch &X) {
+    if (X.in_flight) {
+        hipError_t e = hipEventSynchronize(X.done);
+        X.in_flight = false;
         if (e != hipSuccess) return fail(RSMI_ERR_HIP, std::string("fdec wait: ") + hipGetErrorString(e));
     }
     return RSMI_OK;
@@ -254,19 +264,19 @@ void plan_decode(rsmi_fdec *D, uint32_t seq, Group &g, int type, int inner, int 
         return;
     }
     const int key = k * 257 + n;
-    auto it = D->bucket_of.find(key);
+    auto it = D->B->bucket_of.find(key);
     int b;
-    if (it == D->bucket_of.end()) {
-        b = (int)D->buckets.size();
-        D->bucket_of[key] = b;
+    if (it == D->B->bucket_of.end()) {
+        b = (int)D->B->buckets.size();
+        D->B->bucket_of[key] = b;
         Bucket B;
         B.k = k;
         B.n = n;
-        D->buckets.push_back(B);
+        D->B->buckets.push_back(B);
     } else {
         b = it->second;
     }
-    Bucket &B = D->buckets[(size_t)b];
+    Bucket &B = D->B->buckets[(size_t)b];
     B.len = std::max(B.len, dlen);
     Job J;
     J.type = type;
@@ -277,18 +287,18 @@ void plan_decode(rsmi_fdec *D, uint32_t seq, Group &g, int type, int inner, int 
     J.event = event;
     J.bucket = b;
     J.row = B.rows++;
-    J.rows0 = (int64_t)D->rows.size();
+    J.rows0 = (int64_t)D->B->rows.size();
     // data rows the host will read: the received packet when this batch's host
     // buffer holds it, else the decoded (or carried) row, copied back
-    const int64_t job = (int64_t)D->jobs.size();
+    const int64_t job = (int64_t)D->B->jobs.size();
     for (int i = 0; i < k; ++i) {
         auto f = g.gm.find(i);
         const RingEnt *r = f != g.gm.end() ? &D->ring[(size_t)f->second] : nullptr;
         if (r && r->host && r->in_batch) {
-            D->rows.push_back(RowRef{r->host, -1});
+            D->B->rows.push_back(RowRef{r->host, -1});
         } else {
-            D->rows.push_back(RowRef{nullptr, (int64_t)D->d2h_rows.size()});
-            D->d2h_rows.emplace_back(job, i);
+            D->B->rows.push_back(RowRef{nullptr, (int64_t)D->B->d2h_rows.size()});
+            D->B->d2h_rows.emplace_back(job, i);
         }
     }
     // survivor copies: dst is patched once the bucket strides are known
@@ -296,13 +306,13 @@ void plan_decode(rsmi_fdec *D, uint32_t seq, Group &g, int type, int inner, int 
         const RingEnt &r = D->ring[(size_t)sv.second];
         GatherCopy G;
         G.src = r.src;
-        G.dst = ((uint64_t)D->jobs.size() << 8) | (uint64_t)sv.first;  // (job, index) until patched
+        G.dst = ((uint64_t)D->B->jobs.size() << 8) | (uint64_t)sv.first;  // (job, index) until patched
         G.len = (uint32_t)r.len;
         G.dst_len = 0;
-        D->gathers.push_back(G);
+        D->B->gathers.push_back(G);
     }
-    D->outs.push_back(Out{event, (int64_t)D->jobs.size(), nullptr, 0});
-    D->jobs.push_back(J);
+    D->B->outs.push_back(Out{event, (int64_t)D->B->jobs.size(), nullptr, 0});
+    D->B->jobs.push_back(J);
     D->ar.set_invalid(seq, now);
 }
 
@@ -372,7 +382,7 @@ int input_packet(rsmi_fdec *D, const uint8_t *s, int len, uint64_t dsrc, int32_t
     if (!end) {
         if (about) plan_decode(D, seq, g, type, inner, len, event, now);
         else if (type == 1 && data_num == 0)  // decode_fast_send (:760-776)
-            D->outs.push_back(Out{event, -1, pay + 2, len - 2});
+            D->B->outs.push_back(Out{event, -1, pay + 2, len - 2});
     }
     if (++D->index == D->buff_num) D->index = 0;
     return 0;
@@ -381,17 +391,17 @@ int input_packet(rsmi_fdec *D, const uint8_t *s, int len, uint64_t dsrc, int32_t
 // Output records of outs[b, e) (fec_manager.cpp:97-129 and :713-755), read from
 // the rows the host holds and the rows copied back; records that straddle two
 // rows are copied into sp.
-void resolve_outputs(const rsmi_fdec *D, size_t b, size_t e, Spill &sp, std::vector<Out> &res) {
+void resolve_outputs(const Batch &X, size_t b, size_t e, Spill &sp, std::vector<Out> &res) {
     for (size_t oi = b; oi < e; ++oi) {
-        const Out &o = D->outs[oi];
+        const Out &o = X.outs[oi];
         if (o.job < 0) {
             res.push_back(o);
             continue;
         }
-        const Job &J = D->jobs[(size_t)o.job];
-        const RowRef *rr = D->rows.data() + J.rows0;
+        const Job &J = X.jobs[(size_t)o.job];
+        const RowRef *rr = X.rows.data() + J.rows0;
         auto row = [&](int i) -> const uint8_t * {
-            return rr[i].host ? rr[i].host : D->hblob + rr[i].d2h;
+            return rr[i].host ? rr[i].host : X.hblob + rr[i].d2h;
         };
         const int64_t L = J.len;
         const int64_t cur = (int64_t)J.k * L;  // the blob: the k data rows back to back
@@ -430,8 +440,8 @@ void resolve_outputs(const rsmi_fdec *D, size_t b, size_t e, Spill &sp, std::vec
                 if ((int)rd_u16(row(i)) > kMaxDataLen) ok = false;
             if (!ok) continue;
             // missed = rows not received + the packet that completed the group
-            const Bucket &B = D->buckets[(size_t)J.bucket];
-            const uint8_t *pres = D->present.data() + B.present_off + J.row * B.n;
+            const Bucket &B = X.buckets[(size_t)J.bucket];
+            const uint8_t *pres = X.present.data() + B.present_off + J.row * B.n;
             for (int i = 0; i < J.k; ++i) {
                 if (pres[i] && i != J.inner) continue;
                 const int64_t l = rd_u16(row(i));
@@ -477,11 +487,13 @@ int rsmi_fdec_create(int32_t buff_num, rsmi_fdec **out) {
 
 void rsmi_fdec_destroy(rsmi_fdec *D) {
     if (!D) return;
-    (void)wait_idle(D);
+    for (Batch &X : D->bat) (void)wait_batch(X);
     for (uint8_t *p : {D->dcarry, D->dstage, D->dmeta, D->dblob}) if (p) (void)hipFree(p);
     if (D->dstatus) (void)hipFree(D->dstatus);
-    for (uint8_t *p : {D->hmeta, D->hblob}) if (p) (void)hipHostFree(p);
-    if (D->done) (void)hipEventDestroy(D->done);
+    for (Batch &X : D->bat) {
+        for (uint8_t *p : {X.hmeta, X.hblob}) if (p) (void)hipHostFree(p);
+        if (X.done) (void)hipEventDestroy(X.done);
+    }
     delete D;
 }
 
@@ -489,27 +501,32 @@ int rsmi_fdec_plan(rsmi_fdec *D, int64_t n, const int32_t *len, const uint64_t *
                    const uint8_t *host_base, const uint8_t *dev_base, int64_t now_ms, int32_t *ret,
                    int64_t *n_decodes) {
     if (!D || n < 0 || (n && (!len || !off || !host_base))) return fail(RSMI_ERR_INVALID, "bad fdec_plan args");
-    if (D->planned && !D->plan_only)
+    if (D->B->planned && !D->plan_only)
         return fail(RSMI_ERR_INVALID, "rsmi_fdec_plan: run the previous plan first (its carry copies)");
     if (!dev_base) {
         D->plan_only = true;  // decisions only; this decoder never runs on a device
     } else if (D->plan_only) {
         return fail(RSMI_ERR_INVALID, "rsmi_fdec_plan: decoder was used plan-only (dev_base NULL)");
     }
-    int rc = wait_idle(D);
+    // plan into the other batch: the one before the last (its outputs, if not
+    // taken yet, are dropped now); the last one may still run on the GPU
+    D->bi ^= 1;
+    D->B = &D->bat[D->bi];
+    if (D->out_b == D->bi) D->out_b = -1;
+    int rc = wait_batch(*D->B);
     if (rc) return rc;
-    D->jobs.clear();
-    D->buckets.clear();
-    D->bucket_of.clear();
-    D->gathers.clear();
-    D->carries.clear();
-    D->outs.clear();
-    D->present.clear();
-    D->rows.clear();
-    D->d2h_rows.clear();
-    for (Spill &sp : D->spills) sp.reset();  // the chunks are reused
-    D->staging_bytes = D->d2h_bytes = 0;
-    D->host_base = host_base;
+    D->B->jobs.clear();
+    D->B->buckets.clear();
+    D->B->bucket_of.clear();
+    D->B->gathers.clear();
+    D->B->carries.clear();
+    D->B->outs.clear();
+    D->B->present.clear();
+    D->B->rows.clear();
+    D->B->d2h_rows.clear();
+    for (Spill &sp : D->B->spills) sp.reset();  // the chunks are reused
+    D->B->staging_bytes = D->B->d2h_bytes = 0;
+    D->B->host_base = host_base;
     for (int64_t i = 0; i < n; ++i) {
         int r;
         if (len[i] < 0 || len[i] + 100 >= kBufLen) {
@@ -522,22 +539,22 @@ int rsmi_fdec_plan(rsmi_fdec *D, int64_t n, const int32_t *len, const uint64_t *
     }
     // staging layout per bucket: rows x n shards x stride, present flags rows x n
     int64_t so = 0, po = 0;
-    for (Bucket &B : D->buckets) {
+    for (Bucket &B : D->B->buckets) {
         B.stride = (B.len + 127) & ~127;
         B.staging_off = so;
         B.present_off = po;
         so += B.rows * B.n * B.stride;
         po += (B.rows * B.n + 15) & ~int64_t(15);
     }
-    D->staging_bytes = so;
-    D->present.assign((size_t)po, 0);
-    for (GatherCopy &G : D->gathers) {
-        const Job &J = D->jobs[(size_t)(G.dst >> 8)];
+    D->B->staging_bytes = so;
+    D->B->present.assign((size_t)po, 0);
+    for (GatherCopy &G : D->B->gathers) {
+        const Job &J = D->B->jobs[(size_t)(G.dst >> 8)];
         const int idx = (int)(G.dst & 0xff);
-        const Bucket &B = D->buckets[(size_t)J.bucket];
+        const Bucket &B = D->B->buckets[(size_t)J.bucket];
         G.dst = (uint64_t)(B.staging_off + (J.row * B.n + idx) * B.stride);  // offset; based at run time
         G.dst_len = (uint32_t)B.stride;
-        D->present[(size_t)(B.present_off + J.row * B.n + idx)] = 1;
+        D->B->present[(size_t)(B.present_off + J.row * B.n + idx)] = 1;
     }
     // live shards of the batch move to the carry area, at their ring slot (:587)
     for (int sidx = 0; sidx < D->buff_num; ++sidx) {
@@ -547,74 +564,89 @@ int rsmi_fdec_plan(rsmi_fdec *D, int64_t n, const int32_t *len, const uint64_t *
         auto it = D->mp.find(r.seq);
         const bool live = it != D->mp.end() && !it->second.fec_done;
         const uint64_t dst = rsmi::kCarryTag | (uint64_t)sidx * kRingBytes;
-        if (live && r.len > 0) D->carries.push_back(CarryCopy{r.src, dst, (uint32_t)r.len, 0});
+        if (live && r.len > 0) D->B->carries.push_back(CarryCopy{r.src, dst, (uint32_t)r.len, 0});
         r.src = dst;
         r.host = nullptr;
     }
-    for (auto &jr : D->d2h_rows) {  // byte offsets of the rows copied back
-        const Job &J = D->jobs[(size_t)jr.first];
-        D->rows[(size_t)(J.rows0 + jr.second)].d2h = D->d2h_bytes;
-        D->d2h_bytes += (J.len + 15) & ~15;
+    for (auto &jr : D->B->d2h_rows) {  // byte offsets of the rows copied back
+        const Job &J = D->B->jobs[(size_t)jr.first];
+        D->B->rows[(size_t)(J.rows0 + jr.second)].d2h = D->B->d2h_bytes;
+        D->B->d2h_bytes += (J.len + 15) & ~15;
     }
-    D->planned = true;
-    D->ran = D->resolved = false;
-    if (n_decodes) *n_decodes = (int64_t)D->jobs.size();
+    D->B->planned = true;
+    D->B->ran = D->B->resolved = false;
+    if (n_decodes) *n_decodes = (int64_t)D->B->jobs.size();
     return RSMI_OK;
 }
 
 int rsmi_fdec_run_dev(rsmi_fdec *D, void *stream) {
-    if (!D || !D->planned) return fail(RSMI_ERR_INVALID, "rsmi_fdec_run_dev without a plan");
+    if (!D || !D->B->planned) return fail(RSMI_ERR_INVALID, "rsmi_fdec_run_dev without a plan");
     if (D->plan_only) return fail(RSMI_ERR_INVALID, "rsmi_fdec_run_dev on a plan-only decoder");
     int cur;
     if (hipGetDevice(&cur) != hipSuccess) return fail(RSMI_ERR_HIP, "fdec: no usable GPU");
     if (D->device < 0) {
-        if (hipEventCreateWithFlags(&D->done, hipEventDisableTiming) != hipSuccess)
-            return fail(RSMI_ERR_HIP, "fdec: hipEventCreate");
+        for (Batch &X : D->bat)
+            if (hipEventCreateWithFlags(&X.done, hipEventDisableTiming) != hipSuccess)
+                return fail(RSMI_ERR_HIP, "fdec: hipEventCreate");
         D->device = cur;
     } else if (cur != D->device) {
         return fail(RSMI_ERR_INVALID, "rsmi_fdec_run_dev on another device than the decoder's");
     }
     hipStream_t s = (hipStream_t)stream;
-    int rc = dev_grow(&D->dcarry, &D->dcarry_cap, (size_t)D->buff_num * kRingBytes);
-    if (!rc) rc = dev_grow(&D->dstage, &D->stage_cap, (size_t)D->staging_bytes + 16);
-    if (!rc) rc = dev_grow(&D->dblob, &D->blob_cap, (size_t)D->d2h_bytes + 16);
-    if (!rc) rc = host_grow(&D->hblob, &D->hblob_cap, (size_t)D->d2h_bytes + 16);
+    // the previous batch reads and writes the shared device buffers: order after
+    // it even on another stream, and never free one of them under it
+    Batch &prev = D->bat[D->bi ^ 1];
+    if (prev.in_flight && hipStreamWaitEvent(s, prev.done, 0) != hipSuccess)
+        return fail(RSMI_ERR_HIP, "fdec: hipStreamWaitEvent");
     int64_t max_rows = 0;
-    for (const Bucket &B : D->buckets) max_rows = std::max(max_rows, B.rows);
+    for (const Bucket &B : D->B->buckets) max_rows = std::max(max_rows, B.rows);
+    if ((size_t)D->buff_num * kRingBytes > D->dcarry_cap || (size_t)D->B->staging_bytes + 16 > D->stage_cap ||
+        (size_t)D->B->d2h_bytes + 16 > D->blob_cap || (size_t)max_rows * 4 + 16 > D->status_cap) {
+        int rcw = wait_batch(prev);
+        if (rcw) return rcw;
+    }
+    int rc = dev_grow(&D->dcarry, &D->dcarry_cap, (size_t)D->buff_num * kRingBytes);
+    if (!rc) rc = dev_grow(&D->dstage, &D->stage_cap, (size_t)D->B->staging_bytes + 16);
+    if (!rc) rc = dev_grow(&D->dblob, &D->blob_cap, (size_t)D->B->d2h_bytes + 16);
+    if (!rc) rc = host_grow(&D->B->hblob, &D->B->hblob_cap, (size_t)D->B->d2h_bytes + 16);
     if (!rc) rc = dev_grow(&D->dstatus, &D->status_cap, (size_t)max_rows * 4 + 16);
     if (rc) return rc;
     // metadata: gathers | present | row copies back | carries, one upload
-    std::vector<CarryCopy> packs(D->d2h_rows.size());
+    std::vector<CarryCopy> packs(D->B->d2h_rows.size());
     int64_t ro = 0;
-    for (size_t j = 0; j < D->d2h_rows.size(); ++j) {
-        const Job &J = D->jobs[(size_t)D->d2h_rows[j].first];
-        const Bucket &B = D->buckets[(size_t)J.bucket];
-        const uint8_t *row = D->dstage + B.staging_off + (J.row * B.n + D->d2h_rows[j].second) * B.stride;
+    for (size_t j = 0; j < D->B->d2h_rows.size(); ++j) {
+        const Job &J = D->B->jobs[(size_t)D->B->d2h_rows[j].first];
+        const Bucket &B = D->B->buckets[(size_t)J.bucket];
+        const uint8_t *row = D->dstage + B.staging_off + (J.row * B.n + D->B->d2h_rows[j].second) * B.stride;
         packs[j] = CarryCopy{(uint64_t)(uintptr_t)row, (uint64_t)(uintptr_t)(D->dblob + ro), (uint32_t)J.len, 0};
         ro += (J.len + 15) & ~15;
     }
-    const size_t gb = D->gathers.size() * sizeof(GatherCopy), pb = D->present.size(),
-                 kb = packs.size() * sizeof(CarryCopy), cb = D->carries.size() * sizeof(CarryCopy);
+    const size_t gb = D->B->gathers.size() * sizeof(GatherCopy), pb = D->B->present.size(),
+                 kb = packs.size() * sizeof(CarryCopy), cb = D->B->carries.size() * sizeof(CarryCopy);
     const size_t go = 0, po = (gb + 255) & ~size_t(255), ko = (po + pb + 255) & ~size_t(255),
                  co = (ko + kb + 255) & ~size_t(255), all = co + cb + 16;
+    if (all > D->meta_cap) {
+        int rcw = wait_batch(prev);
+        if (rcw) return rcw;
+    }
     rc = dev_grow(&D->dmeta, &D->meta_cap, all);
-    if (!rc) rc = host_grow(&D->hmeta, &D->hmeta_cap, all);
+    if (!rc) rc = host_grow(&D->B->hmeta, &D->B->hmeta_cap, all);
     if (rc) return rc;
-    GatherCopy *hg = reinterpret_cast<GatherCopy *>(D->hmeta + go);
-    for (size_t i = 0; i < D->gathers.size(); ++i) {
-        hg[i] = D->gathers[i];
+    GatherCopy *hg = reinterpret_cast<GatherCopy *>(D->B->hmeta + go);
+    for (size_t i = 0; i < D->B->gathers.size(); ++i) {
+        hg[i] = D->B->gathers[i];
         hg[i].dst += (uint64_t)(uintptr_t)D->dstage;
     }
-    if (pb) std::memcpy(D->hmeta + po, D->present.data(), pb);
-    if (kb) std::memcpy(D->hmeta + ko, packs.data(), kb);
-    if (cb) std::memcpy(D->hmeta + co, D->carries.data(), cb);
+    if (pb) std::memcpy(D->B->hmeta + po, D->B->present.data(), pb);
+    if (kb) std::memcpy(D->B->hmeta + ko, packs.data(), kb);
+    if (cb) std::memcpy(D->B->hmeta + co, D->B->carries.data(), cb);
     const rsmi::CarryBase carry{{D->dcarry, D->dcarry}};
-    hipError_t e = hipMemcpyAsync(D->dmeta, D->hmeta, all, hipMemcpyHostToDevice, s);
+    hipError_t e = hipMemcpyAsync(D->dmeta, D->B->hmeta, all, hipMemcpyHostToDevice, s);
     if (e == hipSuccess)
         e = rsmi::launch_gather(reinterpret_cast<const GatherCopy *>(D->dmeta + go),
-                                (int64_t)D->gathers.size(), carry, s);
+                                (int64_t)D->B->gathers.size(), carry, s);
     if (e != hipSuccess) return fail(RSMI_ERR_HIP, std::string("fdec gather: ") + hipGetErrorString(e));
-    for (const Bucket &B : D->buckets) {
+    for (const Bucket &B : D->B->buckets) {
         if (B.len == 0) continue;  // empty shards: nothing to rebuild
         rc = rsmi_decode_dev(B.k, B.n, D->dstage + B.staging_off, (int64_t)B.n * B.stride, B.stride,
                              B.len, B.rows, D->dmeta + po + B.present_off, D->dstatus, stream);
@@ -624,59 +656,65 @@ int rsmi_fdec_run_dev(rsmi_fdec *D, void *stream) {
                            carry, s);
     if (e == hipSuccess)
         e = rsmi::launch_carry(reinterpret_cast<const CarryCopy *>(D->dmeta + co),
-                               (int64_t)D->carries.size(), carry, s);
-    if (e == hipSuccess && D->d2h_bytes)
-        e = hipMemcpyAsync(D->hblob, D->dblob, (size_t)D->d2h_bytes, hipMemcpyDeviceToHost, s);
-    if (e == hipSuccess) e = hipEventRecord(D->done, s);
+                               (int64_t)D->B->carries.size(), carry, s);
+    if (e == hipSuccess && D->B->d2h_bytes)
+        e = hipMemcpyAsync(D->B->hblob, D->dblob, (size_t)D->B->d2h_bytes, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipEventRecord(D->B->done, s);
     if (e != hipSuccess) return fail(RSMI_ERR_HIP, std::string("fdec run: ") + hipGetErrorString(e));
-    D->in_flight = true;
-    D->planned = false;
-    D->ran = true;
+    D->B->in_flight = true;
+    D->B->planned = false;
+    D->B->ran = true;
     return RSMI_OK;
 }
 
 int rsmi_fdec_outputs(rsmi_fdec *D, int64_t *n_out) {
     if (!D) return fail(RSMI_ERR_INVALID, "null decoder");
-    if (!D->resolved) {
-        bool any_job = !D->jobs.empty();
-        if (any_job && !D->ran) return fail(RSMI_ERR_INVALID, "rsmi_fdec_outputs before rsmi_fdec_run_dev");
-        int rc = wait_idle(D);
+    // the older batch first: it ran, and batch i+1 may have been planned since
+    const int xi = (D->bat[D->bi ^ 1].ran && !D->bat[D->bi ^ 1].resolved) ? (D->bi ^ 1) : D->bi;
+    Batch &X = D->bat[xi];
+    if (!X.resolved) {
+        bool any_job = !X.jobs.empty();
+        if (any_job && !X.ran) return fail(RSMI_ERR_INVALID, "rsmi_fdec_outputs before rsmi_fdec_run_dev");
+        int rc = wait_batch(X);
         if (rc) return rc;
-        const size_t N = D->outs.size();
+        const size_t N = X.outs.size();
         int T = N >= (size_t)env_int("RSMI_FDEC_PAR_MIN", 4096) ? host_threads() : 1;
         if (T > (int)N) T = N ? (int)N : 1;
-        if ((int)D->spills.size() < T) D->spills.resize((size_t)T);
+        if ((int)X.spills.size() < T) X.spills.resize((size_t)T);
         std::vector<Out> res;
         if (T == 1) {
             res.reserve(N * 2);
-            resolve_outputs(D, 0, N, D->spills[0], res);
+            resolve_outputs(X, 0, N, X.spills[0], res);
         } else {  // groups resolve independently: T contiguous ranges, joined in order
             std::vector<std::vector<Out>> part((size_t)T);
             std::vector<std::thread> th;
             for (int t = 1; t < T; ++t)
-                th.emplace_back([D, N, T, t, &part] {
-                    resolve_outputs(D, N * t / T, N * (t + 1) / T, D->spills[(size_t)t], part[(size_t)t]);
+                th.emplace_back([&X, N, T, t, &part] {
+                    resolve_outputs(X, N * t / T, N * (t + 1) / T, X.spills[(size_t)t], part[(size_t)t]);
                 });
-            resolve_outputs(D, 0, N / T, D->spills[0], part[0]);
+            resolve_outputs(X, 0, N / T, X.spills[0], part[0]);
             for (std::thread &x : th) x.join();
             size_t tot = 0;
             for (auto &v : part) tot += v.size();
             res.reserve(tot);
             for (auto &v : part) res.insert(res.end(), v.begin(), v.end());
         }
-        D->outs.swap(res);
-        D->resolved = true;
+        X.outs.swap(res);
+        X.resolved = true;
     }
-    if (n_out) *n_out = (int64_t)D->outs.size();
+    D->out_b = xi;
+    if (n_out) *n_out = (int64_t)X.outs.size();
     return RSMI_OK;
 }
 
 int rsmi_fdec_output_list(const rsmi_fdec *D, const uint8_t **ptr, int32_t *len, int32_t *event) {
-    if (!D || !D->resolved) return fail(RSMI_ERR_INVALID, "call rsmi_fdec_outputs first");
-    for (size_t i = 0; i < D->outs.size(); ++i) {
-        if (ptr) ptr[i] = D->outs[i].ptr;
-        if (len) len[i] = D->outs[i].len;
-        if (event) event[i] = D->outs[i].event;
+    if (!D || D->out_b < 0 || !D->bat[D->out_b].resolved)
+        return fail(RSMI_ERR_INVALID, "call rsmi_fdec_outputs first");
+    const Batch &X = D->bat[D->out_b];
+    for (size_t i = 0; i < X.outs.size(); ++i) {
+        if (ptr) ptr[i] = X.outs[i].ptr;
+        if (len) len[i] = X.outs[i].len;
+        if (event) event[i] = X.outs[i].event;
     }
     return RSMI_OK;
 }

@@ -103,6 +103,19 @@ struct Run {
     int k, n, len;
 };
 
+// The pinned arrays one batch's plan is uploaded from, and the event of its
+// device run.  Two sets alternate, so batch i+1 is planned on the host while
+// the GPU still uploads and runs batch i.
+struct PlanSet {
+    HostArr<FrameGroup> jobs;
+    HostArr<FrameSrc> srcs;
+    HostArr<CarryCopy> carry;
+    HostArr<rsmi::ByteRun> stale;       // stale bytes of this batch's groups
+    HostArr<rsmi::ByteRun> shadow_upd;  // the buffer at the batch end -> dshadow
+    hipEvent_t done = nullptr;
+    bool in_flight = false;
+};
+
 }  // namespace
 
 struct rsmi_fenc {
@@ -114,9 +127,9 @@ struct rsmi_fenc {
     std::vector<Pending> pend;  // the open group's inputs, in order
 
     // ---- last plan
-    HostArr<FrameGroup> jobs;
-    HostArr<FrameSrc> srcs;
-    HostArr<CarryCopy> carry;
+    PlanSet ps[2];
+    int pcur = 1;              // ps[pcur] holds the last plan
+    PlanSet *P = &ps[1];
     std::vector<rsmi_fenc_packet> packets;
     std::vector<int64_t> g_slot0;
     std::vector<int32_t> g_k, g_m, g_len;
@@ -131,8 +144,6 @@ struct rsmi_fenc {
     // dshadow holds the buffer as of the batch start (zero beyond shadow_len).
     std::vector<BlobHolder> stack;
     int shadow_len = 0;
-    HostArr<rsmi::ByteRun> stale;       // stale bytes of this batch's groups
-    HostArr<rsmi::ByteRun> shadow_upd;  // the buffer at the batch end -> dshadow
     int64_t n_slots = 0;
     int32_t stride_min = rsmi::kSlotShard;
     bool planned = false;
@@ -147,8 +158,6 @@ struct rsmi_fenc {
     size_t carry_cap[2] = {0, 0};
     int carry_cur = 0;  // pending packets live in dcarry[carry_cur] (or the batch input)
     size_t carry_need = 0;  // bytes of dcarry[carry_cur] the last plan fills
-    hipEvent_t done = nullptr;
-    bool in_flight = false;
 
     int tail_x() const { return cfg.rs_cnt; }
     int y_of(int x) const { return cfg.rs_y[x - 1]; }
@@ -158,11 +167,11 @@ struct rsmi_fenc {
 
 namespace {
 
-int wait_idle(rsmi_fenc *E) {
-    if (E->in_flight) {
-        hipError_t e = hipEventSynchronize(E->done);
+int wait_set(PlanSet &B) {
+    if (B.in_flight) {
+        hipError_t e = hipEventSynchronize(B.done);
         if (e != hipSuccess) return fail(RSMI_ERR_HIP, std::string("fenc wait: ") + hipGetErrorString(e));
-        E->in_flight = false;
+        B.in_flight = false;
     }
     return RSMI_OK;
 }
@@ -186,7 +195,7 @@ void copy_from_holder(rsmi_fenc *E, int64_t slot0, int fec_len, const BlobHolder
     while (a < b) {
         const int doff = a % fec_len, soff = a % H.fec_len;
         const int n = std::min({b - a, fec_len - doff, H.fec_len - soff});
-        E->stale.push_back(rsmi::ByteRun{(uint64_t)(slot0 + a / fec_len),
+        E->P->stale.push_back(rsmi::ByteRun{(uint64_t)(slot0 + a / fec_len),
                                          (uint64_t)(H.slot0 + a / H.fec_len), (uint32_t)doff,
                                          (uint32_t)soff, (uint32_t)n, 0});
         a += n;
@@ -216,7 +225,7 @@ void stale_runs(rsmi_fenc *E, int64_t slot0, int k, int fec_len, int cl) {
             const int q = std::min(end, E->shadow_len);
             for (int a = p; a < q;) {
                 const int doff = a % fec_len, n = std::min(q - a, fec_len - doff);
-                E->stale.push_back(rsmi::ByteRun{(uint64_t)(slot0 + a / fec_len), rsmi::kShadowLoc,
+                E->P->stale.push_back(rsmi::ByteRun{(uint64_t)(slot0 + a / fec_len), rsmi::kShadowLoc,
                                                  (uint32_t)doff, (uint32_t)a, (uint32_t)n, 0});
                 a += n;
             }
@@ -235,7 +244,7 @@ void shadow_update(rsmi_fenc *E) {
         const BlobHolder &H = E->stack[i];
         for (int a = lo; a < H.cl;) {
             const int soff = a % H.fec_len, n = std::min(H.cl - a, H.fec_len - soff);
-            E->shadow_upd.push_back(rsmi::ByteRun{rsmi::kShadowLoc, (uint64_t)(H.slot0 + a / H.fec_len),
+            E->P->shadow_upd.push_back(rsmi::ByteRun{rsmi::kShadowLoc, (uint64_t)(H.slot0 + a / H.fec_len),
                                                   (uint32_t)a, (uint32_t)soff, (uint32_t)n, 0});
             a += n;
         }
@@ -254,7 +263,7 @@ void close_group(rsmi_fenc *E, int k, int m, int fec_len) {
     G.slot0 = (uint64_t)slot0;
     G.seq = E->seq;
     G.fec_len = (uint32_t)fec_len;
-    G.src0 = (uint32_t)E->srcs.size();
+    G.src0 = (uint32_t)E->P->srcs.size();
     G.nsrc = (uint32_t)E->pend.size();
     G.blob_len = (uint32_t)E->blob_len;
     G.nslots = (uint16_t)n;
@@ -266,11 +275,11 @@ void close_group(rsmi_fenc *E, int k, int m, int fec_len) {
     uint32_t off = 4;
     for (size_t j = 0; j < E->pend.size(); ++j) {
         const Pending &p = E->pend[j];
-        E->srcs.push_back(FrameSrc{p.addr, p.len, E->cfg.mode == 0 ? off : 0u});
+        E->P->srcs.push_back(FrameSrc{p.addr, p.len, E->cfg.mode == 0 ? off : 0u});
         off += 2 + p.len;
         if (p.emitted >= 0) E->packets[(size_t)p.emitted].slot = slot0 + (int64_t)j;
     }
-    E->jobs.push_back(G);
+    E->P->jobs.push_back(G);
     if (E->cfg.mode == 0) stale_runs(E, slot0, k, fec_len, E->blob_len);
     E->g_slot0.push_back(slot0);
     E->g_k.push_back(k);
@@ -459,12 +468,13 @@ int rsmi_fenc_set_config(rsmi_fenc *E, const rsmi_fec_config *cfg) {
 
 void rsmi_fenc_destroy(rsmi_fenc *E) {
     if (!E) return;
-    (void)wait_idle(E);
+    for (PlanSet &B : E->ps) (void)wait_set(B);
     if (E->dplan) (void)hipFree(E->dplan);
     if (E->dshadow) (void)hipFree(E->dshadow);
     for (int i = 0; i < 2; ++i)
         if (E->dcarry[i]) (void)hipFree(E->dcarry[i]);
-    if (E->done) (void)hipEventDestroy(E->done);
+    for (PlanSet &B : E->ps)
+        if (B.done) (void)hipEventDestroy(B.done);
     delete E;
 }
 
@@ -472,7 +482,7 @@ int rsmi_fenc_plan(rsmi_fenc *E, int64_t n_events, const int32_t *len, const uin
                    const uint8_t *in_base, int32_t *ret, int64_t *n_slots, int64_t *n_packets,
                    int32_t *slot_stride_min) {
     if (!E || n_events < 0 || (n_events && !len)) return fail(RSMI_ERR_INVALID, "bad fenc_plan args");
-    if (E->planned && !E->plan_only && E->carry.size())
+    if (E->planned && !E->plan_only && E->P->carry.size())
         return fail(RSMI_ERR_INVALID, "rsmi_fenc_plan: run the previous plan first (its carry copies)");
     bool any_packet = false;
     for (int64_t i = 0; i < n_events && !any_packet; ++i) any_packet = len[i] >= 0;
@@ -481,11 +491,15 @@ int rsmi_fenc_plan(rsmi_fenc *E, int64_t n_events, const int32_t *len, const uin
     } else if (E->plan_only && any_packet) {
         return fail(RSMI_ERR_INVALID, "rsmi_fenc_plan: encoder was used plan-only (in_base NULL)");
     }
-    int rc = wait_idle(E);  // the previous batch still reads the plan buffers and carry area
+    // plan into the other set: the batch before the last one read it (its
+    // upload), the last one may still be running on the GPU
+    E->pcur ^= 1;
+    E->P = &E->ps[E->pcur];
+    int rc = wait_set(*E->P);
     if (rc) return rc;
-    E->jobs.clear();
-    E->srcs.clear();
-    E->carry.clear();
+    E->P->jobs.clear();
+    E->P->srcs.clear();
+    E->P->carry.clear();
     E->packets.clear();
     E->g_slot0.clear();
     E->g_k.clear();
@@ -494,8 +508,8 @@ int rsmi_fenc_plan(rsmi_fenc *E, int64_t n_events, const int32_t *len, const uin
     E->g_seq.clear();
     E->runs.clear();
     E->stack.clear();
-    E->stale.clear();
-    E->shadow_upd.clear();
+    E->P->stale.clear();
+    E->P->shadow_upd.clear();
     E->n_slots = 0;
     E->stride_min = rsmi::kSlotShard;
     for (Pending &p : E->pend) p.emitted = -1;  // sent in an earlier batch
@@ -515,14 +529,14 @@ int rsmi_fenc_plan(rsmi_fenc *E, int64_t n_events, const int32_t *len, const uin
         G.slot0 = (uint64_t)slot;
         G.seq = E->seq;
         G.fec_len = p.len + 2;
-        G.src0 = (uint32_t)E->srcs.size();
+        G.src0 = (uint32_t)E->P->srcs.size();
         G.nsrc = 1;
         G.nslots = 1;
         G.nframe = 1;
         G.mode = 1;
         G.idx0 = (uint8_t)j;
-        E->srcs.push_back(FrameSrc{p.addr, p.len, 0});
-        E->jobs.push_back(G);
+        E->P->srcs.push_back(FrameSrc{p.addr, p.len, 0});
+        E->P->jobs.push_back(G);
         E->packets[(size_t)p.emitted].slot = slot;
         E->stride_min = std::max(E->stride_min, (int32_t)((rsmi::kSlotShard + p.len + 2 + 15) & ~15u));
     }
@@ -535,7 +549,7 @@ int rsmi_fenc_plan(rsmi_fenc *E, int64_t n_events, const int32_t *len, const uin
     size_t co = 0;
     for (Pending &p : E->pend) {
         const uint64_t dst = kCarryTag | (nxt ? kCarryBuf1 : 0) | (uint64_t)co;
-        if (p.len) E->carry.push_back(CarryCopy{p.addr, dst, p.len, 0});
+        if (p.len) E->P->carry.push_back(CarryCopy{p.addr, dst, p.len, 0});
         p.addr = dst;
         co += (p.len + 15) & ~15u;
     }
@@ -577,8 +591,9 @@ int rsmi_fenc_run_dev(rsmi_fenc *E, uint8_t *slots, int64_t S, void *stream) {
     int cur;
     if (hipGetDevice(&cur) != hipSuccess) return fail(RSMI_ERR_HIP, "fenc: no usable GPU");
     if (E->device < 0) {
-        if (hipEventCreateWithFlags(&E->done, hipEventDisableTiming) != hipSuccess)
-            return fail(RSMI_ERR_HIP, "fenc: hipEventCreate");
+        for (PlanSet &B : E->ps)
+            if (hipEventCreateWithFlags(&B.done, hipEventDisableTiming) != hipSuccess)
+                return fail(RSMI_ERR_HIP, "fenc: hipEventCreate");
         E->device = cur;
         // start compiling the run-time networks of the -f table's codes now, so
         // they are ready by the time those group sizes come (bitslice_rtc.cpp)
@@ -590,6 +605,17 @@ int rsmi_fenc_run_dev(rsmi_fenc *E, uint8_t *slots, int64_t S, void *stream) {
         return fail(RSMI_ERR_INVALID, "rsmi_fenc_run_dev on another device than the encoder's");
     }
     hipStream_t s = (hipStream_t)stream;
+    // the previous batch (other set) writes the carry area and blob buffer this
+    // one reads: order after it even when it ran on another stream
+    PlanSet &prev = E->ps[E->pcur ^ 1];
+    if (prev.in_flight && hipStreamWaitEvent(s, prev.done, 0) != hipSuccess)
+        return fail(RSMI_ERR_HIP, "fenc: hipStreamWaitEvent");
+    // growing a shared device buffer frees the old one: not under the previous batch
+    const bool grows = E->carry_need > E->carry_cap[E->carry_cur] || !E->dshadow;
+    if (grows) {
+        int rcw = wait_set(prev);
+        if (rcw) return rcw;
+    }
     // carry buffer this batch fills; resolve tagged carry offsets
     int rc0 = grow(&E->dcarry[E->carry_cur], &E->carry_cap[E->carry_cur], E->carry_need, false);
     if (rc0) return rc0;
@@ -600,29 +626,33 @@ int rsmi_fenc_run_dev(rsmi_fenc *E, uint8_t *slots, int64_t S, void *stream) {
         if (hipMemsetAsync(E->dshadow, 0, rsmi::kBlobBufBytes, s) != hipSuccess)
             return fail(RSMI_ERR_HIP, "fenc: clear blob buffer");
     }
-    const size_t gb = E->jobs.size() * sizeof(FrameGroup), sb = E->srcs.size() * sizeof(FrameSrc),
-                 cb = E->carry.size() * sizeof(CarryCopy),
-                 rb = E->stale.size() * sizeof(rsmi::ByteRun),
-                 ub = E->shadow_upd.size() * sizeof(rsmi::ByteRun);
+    const size_t gb = E->P->jobs.size() * sizeof(FrameGroup), sb = E->P->srcs.size() * sizeof(FrameSrc),
+                 cb = E->P->carry.size() * sizeof(CarryCopy),
+                 rb = E->P->stale.size() * sizeof(rsmi::ByteRun),
+                 ub = E->P->shadow_upd.size() * sizeof(rsmi::ByteRun);
     const size_t go = 0, so = (gb + 255) & ~size_t(255), co = (so + sb + 255) & ~size_t(255),
                  ro = (co + cb + 255) & ~size_t(255), uo = (ro + rb + 255) & ~size_t(255);
     const size_t all = uo + ub + 16;
+    if (all > E->plan_cap) {
+        int rcw = wait_set(prev);
+        if (rcw) return rcw;
+    }
     int rc = grow(&E->dplan, &E->plan_cap, all, false);
     if (rc) return rc;
     hipError_t e = hipSuccess;
-    if (gb) e = hipMemcpyAsync(E->dplan + go, E->jobs.p, gb, hipMemcpyHostToDevice, s);
-    if (e == hipSuccess && sb) e = hipMemcpyAsync(E->dplan + so, E->srcs.p, sb, hipMemcpyHostToDevice, s);
-    if (e == hipSuccess && cb) e = hipMemcpyAsync(E->dplan + co, E->carry.p, cb, hipMemcpyHostToDevice, s);
-    if (e == hipSuccess && rb) e = hipMemcpyAsync(E->dplan + ro, E->stale.p, rb, hipMemcpyHostToDevice, s);
+    if (gb) e = hipMemcpyAsync(E->dplan + go, E->P->jobs.p, gb, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess && sb) e = hipMemcpyAsync(E->dplan + so, E->P->srcs.p, sb, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess && cb) e = hipMemcpyAsync(E->dplan + co, E->P->carry.p, cb, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess && rb) e = hipMemcpyAsync(E->dplan + ro, E->P->stale.p, rb, hipMemcpyHostToDevice, s);
     if (e == hipSuccess && ub)
-        e = hipMemcpyAsync(E->dplan + uo, E->shadow_upd.p, ub, hipMemcpyHostToDevice, s);
+        e = hipMemcpyAsync(E->dplan + uo, E->P->shadow_upd.p, ub, hipMemcpyHostToDevice, s);
     if (e == hipSuccess)
-        e = rsmi::launch_frame(reinterpret_cast<const FrameGroup *>(E->dplan + go), (int64_t)E->jobs.size(),
+        e = rsmi::launch_frame(reinterpret_cast<const FrameGroup *>(E->dplan + go), (int64_t)E->P->jobs.size(),
                                reinterpret_cast<const FrameSrc *>(E->dplan + so), carry, slots, S, s);
     // stale bytes past each blob, before the parity is computed over them
     if (e == hipSuccess)
         e = rsmi::launch_byte_runs(reinterpret_cast<const rsmi::ByteRun *>(E->dplan + ro),
-                                   (int64_t)E->stale.size(), slots, S, E->dshadow, s);
+                                   (int64_t)E->P->stale.size(), slots, S, E->dshadow, s);
     if (e != hipSuccess) return fail(RSMI_ERR_HIP, std::string("fenc frame: ") + hipGetErrorString(e));
     // parity of every group
     for (const Run &r : E->runs) {
@@ -632,13 +662,13 @@ int rsmi_fenc_run_dev(rsmi_fenc *E, uint8_t *slots, int64_t S, void *stream) {
     }
     // the blob buffer as this batch leaves it (read by the next batch's stale runs)
     e = rsmi::launch_byte_runs(reinterpret_cast<const rsmi::ByteRun *>(E->dplan + uo),
-                               (int64_t)E->shadow_upd.size(), slots, S, E->dshadow, s);
+                               (int64_t)E->P->shadow_upd.size(), slots, S, E->dshadow, s);
     if (e == hipSuccess)
         e = rsmi::launch_carry(reinterpret_cast<const CarryCopy *>(E->dplan + co),
-                               (int64_t)E->carry.size(), carry, s);
-    if (e == hipSuccess) e = hipEventRecord(E->done, s);
+                               (int64_t)E->P->carry.size(), carry, s);
+    if (e == hipSuccess) e = hipEventRecord(E->P->done, s);
     if (e != hipSuccess) return fail(RSMI_ERR_HIP, std::string("fenc carry: ") + hipGetErrorString(e));
-    E->in_flight = true;
+    E->P->in_flight = true;
     E->planned = false;
     return RSMI_OK;
 }

@@ -113,7 +113,8 @@ class FecEncoder:
             check(lib().rsmi_fenc_groups(self._h, None, g["slot0"].ctypes.data, g["k"].ctypes.data,
                                          g["m"].ctypes.data, g["fec_len"].ctypes.data,
                                          g["seq"].ctypes.data), "rsmi_fenc_groups")
-        self._keep = in_buf  # the input must outlive the run
+        # the input must outlive the run, which may overlap the next plan
+        self._keep = (in_buf, (self._keep or (None,))[0])
         return FencPlan(ns.value, smin.value, ret, packets, g)
 
     def plan_host(self, lens, offsets) -> FencPlan:
@@ -207,7 +208,8 @@ class FecDecoder:
         check(lib().rsmi_fdec_plan(self._h, n, lens.ctypes.data, offsets.ctypes.data,
                                    host_buf.ctypes.data, devp, int(now_ms), ret.ctypes.data,
                                    C.byref(nd)), "rsmi_fdec_plan")
-        self._keep = (host_buf, dev_buf)
+        # batch i's buffers stay referenced while batch i+1 is planned and run
+        self._keep = ((host_buf, dev_buf), (self._keep or (None,))[0])
         return FdecPlan(ret, nd.value)
 
     def run(self, stream=None):
