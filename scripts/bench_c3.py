@@ -25,3 +25,20 @@ t = statistics.median(times)
 alg = int(((ks + ms) * ls).sum())
 print(json.dumps({"bitslice_plan": plan.bitslice, "c3_encode_ms": t, "payload_GiBps": float((ks * ls).sum()) / (t * 1e-3) / 2**30,
                   "alg_GBps": alg / (t * 1e-3) / 1e9, "alg_bytes": alg, "buffer_bytes": total}))
+# C3 decode: min(5, m) random erasures per group on the encoded batch (bench.py's c3 line)
+flags = synth.ragged_erasures(synth.ERASE_SEED, 0, ks + ms, ms, 5)
+bits = torch.from_numpy(synth.present_bits(flags).view(np.int32)).to("cuda")
+st = torch.empty(G, dtype=torch.int32, device="cuda")
+clean = base.clone()
+dtimes = []
+for i in range(15):
+    base.copy_(clean)
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record(); plan.decode(base, bits, status=st); b.record(); torch.cuda.synchronize()
+    if i >= 3:
+        dtimes.append(a.elapsed_time(b))
+assert int((st != 0).sum()) == 0 and torch.equal(base, clean)
+td = statistics.median(dtimes)
+e = ((flags[:, :20] == 0) & (np.arange(20)[None, :] < ks[:, None])).sum(1)
+dalg = int(((ks + e) * ls).sum())
+print(json.dumps({"c3_decode_ms": td, "alg_GBps": dalg / (td * 1e-3) / 1e9, "frac": dalg / (td * 1e-3) / 8e12}))

@@ -284,28 +284,67 @@ __device__ __forceinline__ int gauss_jordan_lds(int k, int e, const WaveLds &L, 
     return RSMI_DEC_OK;
 }
 
+// Tile geometry for W dwords per lane: W = 1, 2, 4 is one 4W-byte load per
+// lane (a 256W-byte tile); W = 5 is a 16-byte load plus a dword load (1280 B).
+template <int W>
+struct TileIO {
+    static_assert(W == 1 || W == 2 || W == 4 || W == 5, "lane pieces must divide 16");
+    static constexpr int kBytes = 256 * W;
+    uint32_t v16, v4;  // per-lane offsets of the two loads (v4 unused for W <= 4)
+    __device__ __forceinline__ void set(int toff, int tlen, int lane) {
+        const int a = (W == 5 ? 16 : 4 * W) * lane;
+        v16 = a < tlen ? (uint32_t)(toff + a) : 0x80000000u;
+        v4 = (W == 5 && 1024 + 4 * lane < tlen) ? (uint32_t)(toff + 1024 + 4 * lane) : 0x80000000u;
+    }
+    __device__ __forceinline__ void load(__amdgpu_buffer_rsrc_t r, uint32_t so, uint32_t (&x)[W]) const {
+        if constexpr (W == 1) {
+            x[0] = __builtin_amdgcn_raw_buffer_load_b32(r, v16, so, DEC_LD_AUX);
+        } else if constexpr (W == 2) {
+            typedef uint32_t u2 __attribute__((ext_vector_type(2)));
+            const u2 v = __builtin_amdgcn_raw_buffer_load_b64(r, v16, so, DEC_LD_AUX);
+            x[0] = v.x; x[1] = v.y;
+        } else {
+            const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, v16, so, DEC_LD_AUX);
+            x[0] = v.x; x[1] = v.y; x[2] = v.z; x[3] = v.w;
+            if constexpr (W == 5) x[4] = __builtin_amdgcn_raw_buffer_load_b32(r, v4, so, DEC_LD_AUX);
+        }
+    }
+    // offsets in the VGPR, soffset 0 (see bitslice_kern.hpp DevIO::store)
+    __device__ __forceinline__ void store(__amdgpu_buffer_rsrc_t r, uint32_t so, const uint32_t (&y)[W]) const {
+        if constexpr (W == 1) {
+            __builtin_amdgcn_raw_buffer_store_b32(y[0], r, v16 + so, 0, DEC_ST_AUX);
+        } else if constexpr (W == 2) {
+            typedef uint32_t u2 __attribute__((ext_vector_type(2)));
+            const u2 v = {y[0], y[1]};
+            __builtin_amdgcn_raw_buffer_store_b64(v, r, v16 + so, 0, DEC_ST_AUX);
+        } else {
+            const u32x4 v = {y[0], y[1], y[2], y[3]};
+            __builtin_amdgcn_raw_buffer_store_b128(v, r, v16 + so, 0, DEC_ST_AUX);
+            if constexpr (W == 5) __builtin_amdgcn_raw_buffer_store_b32(y[4], r, v4 + so, 0, DEC_ST_AUX);
+        }
+    }
+};
+
 // ---- 2 + 4. survivor streaming ---------------------------------------------------
 // One group's reconstruction: the wave-uniform descriptor covers the group's
 // n slots; survivor j's slot offset sits in lane j of so_lane, missing row
-// r's in lane r of mo_lane.
+// r's in lane r of mo_lane.  W dwords per lane: the ragged kernel picks the
+// narrowest tile that covers a short group, so its MACs do not run over empty
+// lanes.
+template <int W>
 struct Rebuild {
     __amdgpu_buffer_rsrc_t rsrc;
     uint32_t so_lane, mo_lane;
     int k, e, len, lpad;
-    uint32_t v16, v4;
-    u32x4 rq[kRing];
-    uint32_t rd[kRing];
+    TileIO<W> io;
+    uint32_t rq[kRing][W];
 
     __device__ __forceinline__ void load(int q, int j) {
-        const uint32_t so = __builtin_amdgcn_readlane(so_lane, j);
-        rq[q] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, v16, so, DEC_LD_AUX);
-        rd[q] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, v4, so, DEC_LD_AUX);
+        io.load(rsrc, __builtin_amdgcn_readlane(so_lane, j), rq[q]);
     }
     // whole cache lines where the slot has room (rsmi.h padding rule)
     __device__ __forceinline__ void start_tile(int toff, int lane) {
-        const int tlen = lpad - toff;
-        v16 = (16 * lane < tlen) ? (uint32_t)(toff + 16 * lane) : 0x80000000u;
-        v4 = (1024 + 4 * lane < tlen) ? (uint32_t)(toff + 1024 + 4 * lane) : 0x80000000u;
+        io.set(toff, lpad - toff, lane);
 #pragma unroll
         for (int q = 0; q < kRing; ++q)
             if (q < k) load(q, q);
@@ -313,27 +352,26 @@ struct Rebuild {
     // passes over (tile, block of kPass rows); tile 0's first loads were
     // issued by start_tile(0) before the Gauss-Jordan
     __device__ __forceinline__ void run(const uint32_t *tab, int lane) {
-        for (int toff = 0; toff < len; toff += kTile) {
+        for (int toff = 0; toff < len; toff += TileIO<W>::kBytes) {
             for (int rb = 0; rb < e; rb += kPass) {
                 if (toff || rb) start_tile(toff, lane);
-                uint32_t acc[kPass][5];
+                uint32_t acc[kPass][W];
 #pragma unroll
                 for (int r = 0; r < kPass; ++r)
 #pragma unroll
-                    for (int w = 0; w < 5; ++w) acc[r][w] = 0;
+                    for (int w = 0; w < W; ++w) acc[r][w] = 0;
                 for (int jb = 0; jb < k; jb += kRing) {
 #pragma unroll
                     for (int q = 0; q < kRing; ++q) {
                         const int j = jb + q;
                         if (j < k) {
-                            // the 3-bit split selectors of the survivor's 5 dwords
-                            const uint32_t x[5] = {rq[q].x, rq[q].y, rq[q].z, rq[q].w, rd[q]};
-                            uint32_t a0[5], a1[5], a2[5];
+                            // the 3-bit split selectors of the survivor's W dwords
+                            uint32_t a0[W], a1[W], a2[W];
 #pragma unroll
-                            for (int w = 0; w < 5; ++w) {
-                                a0[w] = x[w] & 0x07070707u;
-                                a1[w] = (x[w] >> 3) & 0x07070707u;
-                                a2[w] = (x[w] >> 6) & 0x03030303u;
+                            for (int w = 0; w < W; ++w) {
+                                a0[w] = rq[q][w] & 0x07070707u;
+                                a1[w] = (rq[q][w] >> 3) & 0x07070707u;
+                                a2[w] = (rq[q][w] >> 6) & 0x03030303u;
                             }
                             // ring slot q took survivor j: load survivor j + kRing into it
                             if (j + kRing < k) load(q, j + kRing);
@@ -344,7 +382,7 @@ struct Rebuild {
                                     const uint4 t = reinterpret_cast<const uint4 *>(ta + r * 8)[0];
                                     const uint32_t t2 = ta[r * 8 + 4];
 #pragma unroll
-                                    for (int w = 0; w < 5; ++w)
+                                    for (int w = 0; w < W; ++w)
                                         acc[r][w] ^= xor3(__builtin_amdgcn_perm(t.y, t.x, a0[w]),
                                                           __builtin_amdgcn_perm(t.w, t.z, a1[w]),
                                                           __builtin_amdgcn_perm(t2, t2, a2[w]));
@@ -354,19 +392,8 @@ struct Rebuild {
                     }
                 }
 #pragma unroll
-                for (int r = 0; r < kPass; ++r) {
-                    if (rb + r < e) {
-                        const uint32_t so = __builtin_amdgcn_readlane(mo_lane, rb + r);
-                        const u32x4 v = {acc[r][0], acc[r][1], acc[r][2], acc[r][3]};
-#if DEC_ST_SGPR
-                        __builtin_amdgcn_raw_buffer_store_b128(v, rsrc, v16, so, DEC_ST_AUX);
-                        __builtin_amdgcn_raw_buffer_store_b32(acc[r][4], rsrc, v4, so, DEC_ST_AUX);
-#else
-                        __builtin_amdgcn_raw_buffer_store_b128(v, rsrc, v16 + so, 0, DEC_ST_AUX);
-                        __builtin_amdgcn_raw_buffer_store_b32(acc[r][4], rsrc, v4 + so, 0, DEC_ST_AUX);
-#endif
-                    }
-                }
+                for (int r = 0; r < kPass; ++r)
+                    if (rb + r < e) io.store(rsrc, __builtin_amdgcn_readlane(mo_lane, rb + r), acc[r]);
             }
         }
     }
@@ -711,7 +738,14 @@ __global__ __launch_bounds__(256, DEC_OCC) void k_decode_fused(UniformArgs a, co
 // words: bit j of word j/32 = shard j received), parity rows through the
 // device code directory.  Groups this form cannot take (e > kRows, k > kmax,
 // or n slots spanning >= 2 GiB) get kDefer for k_decode_ragged_big.
-__global__ __launch_bounds__(256, DEC_OCC) void k_decode_ragged(
+#ifndef DEC_RAG_W
+#define DEC_RAG_W 1  // ragged kernel: tile width per group (0: always 1280-byte tiles)
+#endif
+#ifndef DEC_RAG_OCC
+#define DEC_RAG_OCC DEC_OCC  // waves per SIMD the ragged kernel's registers are cut for
+#endif
+
+__global__ __launch_bounds__(256, DEC_RAG_OCC) void k_decode_ragged(
     const rsmi_group *groups, int64_t ngroups, uint8_t *base, const uint32_t *present,
     int32_t *status_out, const uint64_t *code_dir, const uint32_t *ptab, const uint8_t *gftab,
     int kmax) {
@@ -759,24 +793,34 @@ __global__ __launch_bounds__(256, DEC_OCC) void k_decode_ragged(
             continue;
         }
         auto prow = [&](uint32_t R) { return rows + (R - k) * k; };
-        Rebuild B;
-        B.rsrc = group_rsrc(base + off, (uint32_t)(n * ss));
-        B.k = k;
-        B.e = e;
-        B.len = len;
-        B.lpad = (int)(((uint32_t)len + 127) / 128 * 128 < ss ? ((uint32_t)len + 127) / 128 * 128 : ss);
+        const int lpad = (int)(((uint32_t)len + 127) / 128 * 128 < ss ? ((uint32_t)len + 127) / 128 * 128 : ss);
         const uint32_t sel_lane = lane < k ? (uint32_t)L.sel[lane] : 0u;
-        B.so_lane = sel_lane * ss;
-        B.mo_lane = (lane < e ? (uint32_t)L.miss[lane] : 0u) * ss;
-        if (len > 0) B.start_tile(0, lane);
-        const int st = (e + k <= 64) ? gauss_jordan_regs(k, e, sel_lane, L, T, prow, lane)
-                                     : gauss_jordan_lds(k, e, L, T, prow, lane);
-        if (st != RSMI_DEC_OK) {
-            if (lane == 0) status_out[g] = st;
-            continue;
-        }
-        if (len > 0) B.run(L.tab, lane);
-        if (lane == 0) status_out[g] = RSMI_DEC_OK;
+        auto rebuild = [&](auto wc) {
+            constexpr int W = decltype(wc)::value;
+            Rebuild<W> B;
+            B.rsrc = group_rsrc(base + off, (uint32_t)(n * ss));
+            B.k = k;
+            B.e = e;
+            B.len = len;
+            B.lpad = lpad;
+            B.so_lane = sel_lane * ss;
+            B.mo_lane = (lane < e ? (uint32_t)L.miss[lane] : 0u) * ss;
+            if (len > 0) B.start_tile(0, lane);
+            const int st = (e + k <= 64) ? gauss_jordan_regs(k, e, sel_lane, L, T, prow, lane)
+                                         : gauss_jordan_lds(k, e, L, T, prow, lane);
+            if (st == RSMI_DEC_OK && len > 0) B.run(L.tab, lane);
+            return st;
+        };
+        // the narrowest tile that covers the group (one pass), else 1280-byte
+        // tiles.  Lane pieces of 4, 8 or 16 bytes divide lpad (a multiple of
+        // 16), so no lane straddles pad_end; 12-byte pieces would.
+        const int nw = DEC_RAG_W ? (lpad + 255) / 256 : 5;
+        int st;
+        if (nw <= 1) st = rebuild(std::integral_constant<int, 1>{});
+        else if (nw == 2) st = rebuild(std::integral_constant<int, 2>{});
+        else if (nw <= 4) st = rebuild(std::integral_constant<int, 4>{});
+        else st = rebuild(std::integral_constant<int, 5>{});
+        if (lane == 0) status_out[g] = st;
         wave_sync();  // the LDS slice is rewritten by the next group
     }
 }
