@@ -59,9 +59,18 @@ def test_exports_rsmi_fec_h():
     assert not missing, missing
 
 
+def test_exports_rsmi_io_h():
+    ex = _exports()
+    decl = _declared("rsmi_io.h")
+    assert "rsmi_udp_recv_batch" in decl and "rsmi_udp_send_batch" in decl
+    missing = [d for d in decl if d not in ex]
+    assert not missing, missing
+
+
 def test_every_header_is_checked():
     assert sorted(os.listdir(os.path.join(ROOT, "include"))) == ["rs_compat.h", "rsmi.h",
-                                                                 "rsmi_cook.h", "rsmi_fec.h"]
+                                                                 "rsmi_cook.h", "rsmi_fec.h",
+                                                                 "rsmi_io.h"]
 
 
 def test_exports_rs_compat_h_mangled():
