@@ -51,6 +51,10 @@ constexpr int kWaves = 4;      // waves per block (one group each)
 constexpr int kRing = DEC_RING;  // survivors in flight per wave
 constexpr int kRows = 10;      // max e handled by the one-wave kernels
 constexpr int kPass = 5;       // rows accumulated per pass over the survivors
+#ifndef DEC_REG_ROWS
+#define DEC_REG_ROWS 5
+#endif
+constexpr int kRegRows = DEC_REG_ROWS;  // fused kernel: register Gauss-Jordan up to this e (LDS form above)
 constexpr int kTile = 1280;    // bytes per lane-tile pass (64 x 16 + 64 x 4)
 #ifndef DEC_ST_SGPR
 #define DEC_ST_SGPR 0          // 1: row offset of the rebuilt-row stores in soffset (see bitslice.hip
@@ -527,13 +531,13 @@ __global__ __launch_bounds__(256, DEC_OCC) void k_decode_fused(UniformArgs a, co
 
         // ---- 3. Gauss-Jordan on [A | M], e x (e+k) ------------------------------
         const int W = e + k;
-        if (W <= 64) {
+        if (W <= 64 && e <= kRegRows) {
             // lane c holds column c: a missing data index (c < e) or survivor c - e
             const uint32_t col = lane < e ? (uint32_t)L.miss[lane]
                                           : (lane < W ? (uint32_t)L.sel[lane - e] : 0u);
-            uint32_t a[kRows];
+            uint32_t a[kRegRows];
 #pragma unroll
-            for (int r = 0; r < kRows; ++r) {
+            for (int r = 0; r < kRegRows; ++r) {
                 a[r] = 0;
                 if (r < e) {
                     const uint32_t R = __builtin_amdgcn_readlane(sel_lane, k - e + r);
@@ -543,7 +547,7 @@ __global__ __launch_bounds__(256, DEC_OCC) void k_decode_fused(UniformArgs a, co
                 }
             }
 #pragma unroll
-            for (int p = 0; p < kRows; ++p) {
+            for (int p = 0; p < kRegRows; ++p) {
                 if (p < e) {
                     const uint32_t piv = __builtin_amdgcn_readlane(a[p], p);
                     if (piv == 0) {
@@ -553,7 +557,7 @@ __global__ __launch_bounds__(256, DEC_OCC) void k_decode_fused(UniformArgs a, co
                     const uint32_t ip = __builtin_amdgcn_readfirstlane(linv[piv]);
                     a[p] = gmul_t(s01[ip], s2[ip], a[p]);
 #pragma unroll
-                    for (int r = 0; r < kRows; ++r) {
+                    for (int r = 0; r < kRegRows; ++r) {
                         if (r < e && r != p) {
                             const uint32_t f = __builtin_amdgcn_readlane(a[r], p);
                             a[r] ^= gmul_t(s01[f], s2[f], a[p]);
@@ -571,7 +575,7 @@ __global__ __launch_bounds__(256, DEC_OCC) void k_decode_fused(UniformArgs a, co
             if (lane >= e && lane < W) {
                 uint32_t *dst = L.tab + (lane - e) * kRows * 8;
 #pragma unroll
-                for (int r = 0; r < kRows; ++r) {
+                for (int r = 0; r < kRegRows; ++r) {
                     if (r < e) {
                         reinterpret_cast<uint4 *>(dst + r * 8)[0] = s01[a[r]];
                         dst[r * 8 + 4] = s2[a[r]];
