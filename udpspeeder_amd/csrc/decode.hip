@@ -69,6 +69,9 @@ constexpr int kTile = 1280;    // bytes per lane-tile pass (64 x 16 + 64 x 4)
 #ifndef DEC_NOMEM
 #define DEC_NOMEM 0            // measurement only: survivor loads all hit one cached slot
 #endif
+#ifndef DEC_RAG_DEEP
+#define DEC_RAG_DEEP 1  // ragged kernel: 16 / W survivors in flight for 4- and 8-byte lane pieces
+#endif
 #ifndef DEC_XCD
 #define DEC_XCD 1              // XCD-contiguous group ranges (see k_decode_fused; ~0.5 %)
 #endif
@@ -337,11 +340,14 @@ struct TileIO {
 // lanes.
 template <int W>
 struct Rebuild {
+    // narrow tiles keep more survivors in flight in the same registers (16
+    // dwords of ring): short groups are latency-bound, not VGPR-bound
+    static constexpr int R = DEC_RAG_DEEP && W <= 2 ? 16 / W : kRing;
     __amdgpu_buffer_rsrc_t rsrc;
     uint32_t so_lane, mo_lane;
     int k, e, len, lpad;
     TileIO<W> io;
-    uint32_t rq[kRing][W];
+    uint32_t rq[R][W];
 
     __device__ __forceinline__ void load(int q, int j) {
         io.load(rsrc, __builtin_amdgcn_readlane(so_lane, j), rq[q]);
@@ -350,7 +356,7 @@ struct Rebuild {
     __device__ __forceinline__ void start_tile(int toff, int lane) {
         io.set(toff, lpad - toff, lane);
 #pragma unroll
-        for (int q = 0; q < kRing; ++q)
+        for (int q = 0; q < R; ++q)
             if (q < k) load(q, q);
     }
     // passes over (tile, block of kPass rows); tile 0's first loads were
@@ -364,9 +370,9 @@ struct Rebuild {
                 for (int r = 0; r < kPass; ++r)
 #pragma unroll
                     for (int w = 0; w < W; ++w) acc[r][w] = 0;
-                for (int jb = 0; jb < k; jb += kRing) {
+                for (int jb = 0; jb < k; jb += R) {
 #pragma unroll
-                    for (int q = 0; q < kRing; ++q) {
+                    for (int q = 0; q < R; ++q) {
                         const int j = jb + q;
                         if (j < k) {
                             // the 3-bit split selectors of the survivor's W dwords
@@ -377,8 +383,8 @@ struct Rebuild {
                                 a1[w] = (rq[q][w] >> 3) & 0x07070707u;
                                 a2[w] = (rq[q][w] >> 6) & 0x03030303u;
                             }
-                            // ring slot q took survivor j: load survivor j + kRing into it
-                            if (j + kRing < k) load(q, j + kRing);
+                            // ring slot q took survivor j: load survivor j + R into it
+                            if (j + R < k) load(q, j + R);
                             const uint32_t *ta = tab + (j * kRows + rb) * 8;
 #pragma unroll
                             for (int r = 0; r < kPass; ++r) {
