@@ -13,7 +13,11 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
+#include <condition_variable>
 #include <cstdlib>
+#include <functional>
+#include <mutex>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -471,6 +475,66 @@ int host_threads() {
     return t;
 }
 
+// Resolver threads, started once and kept (starting 15 threads per batch cost
+// more than resolving a 30 K-packet batch).  One batch at a time: a caller
+// that finds the pool busy (another connection's decoder) resolves alone.
+class ResolvePool {
+  public:
+    static ResolvePool &get() {
+        static ResolvePool *p = new ResolvePool();  // never torn down: threads are detached
+        return *p;
+    }
+    // f(t) for t in [0, n) over the pool and the calling thread; false if busy
+    bool try_run(int n, const std::function<void(int)> &f) {
+        std::unique_lock<std::mutex> busy(run_mu_, std::try_to_lock);
+        if (!busy.owns_lock()) return false;
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            while ((int)workers_ < n - 1) {
+                std::thread(&ResolvePool::loop, this).detach();
+                ++workers_;
+            }
+            job_ = &f;
+            n_ = n;
+            next_.store(0);
+            left_ = (int)workers_;  // every worker checks in once per job
+            ++gen_;
+        }
+        cv_.notify_all();
+        for (int t; (t = next_.fetch_add(1)) < n;) f(t);
+        std::unique_lock<std::mutex> lk(mu_);
+        done_.wait(lk, [&] { return left_ == 0; });  // no worker still inside f
+        job_ = nullptr;
+        return true;
+    }
+
+  private:
+    void loop() {
+        uint64_t seen = 0;
+        for (;;) {
+            const std::function<void(int)> *f;
+            int n;
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [&] { return gen_ != seen; });
+                seen = gen_;
+                f = job_;
+                n = n_;
+            }
+            for (int t; (t = next_.fetch_add(1)) < n;) (*f)(t);
+            std::lock_guard<std::mutex> lk(mu_);
+            if (--left_ == 0) done_.notify_all();
+        }
+    }
+    std::mutex run_mu_, mu_;
+    std::condition_variable cv_, done_;
+    const std::function<void(int)> *job_ = nullptr;
+    int n_ = 0, left_ = 0;
+    std::atomic<int> next_{0};
+    uint64_t gen_ = 0;
+    unsigned workers_ = 0;
+};
+
 }  // namespace
 
 extern "C" {
@@ -687,13 +751,11 @@ int rsmi_fdec_outputs(rsmi_fdec *D, int64_t *n_out) {
             resolve_outputs(X, 0, N, X.spills[0], res);
         } else {  // groups resolve independently: T contiguous ranges, joined in order
             std::vector<std::vector<Out>> part((size_t)T);
-            std::vector<std::thread> th;
-            for (int t = 1; t < T; ++t)
-                th.emplace_back([&X, N, T, t, &part] {
-                    resolve_outputs(X, N * t / T, N * (t + 1) / T, X.spills[(size_t)t], part[(size_t)t]);
-                });
-            resolve_outputs(X, 0, N / T, X.spills[0], part[0]);
-            for (std::thread &x : th) x.join();
+            const std::function<void(int)> range = [&X, N, T, &part](int t) {
+                resolve_outputs(X, N * t / T, N * (t + 1) / T, X.spills[(size_t)t], part[(size_t)t]);
+            };
+            if (!ResolvePool::get().try_run(T, range))
+                for (int t = 0; t < T; ++t) range(t);  // pool busy: this thread alone
             size_t tot = 0;
             for (auto &v : part) tot += v.size();
             res.reserve(tot);
