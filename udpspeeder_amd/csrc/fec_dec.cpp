@@ -14,6 +14,8 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
+#include <cstdio>
 #include <condition_variable>
 #include <cstdlib>
 #include <functional>
@@ -739,10 +741,16 @@ int rsmi_fdec_outputs(rsmi_fdec *D, int64_t *n_out) {
     if (!X.resolved) {
         bool any_job = !X.jobs.empty();
         if (any_job && !X.ran) return fail(RSMI_ERR_INVALID, "rsmi_fdec_outputs before rsmi_fdec_run_dev");
+        static const bool prof = env_int("RSMI_FDEC_PROFILE", 0) != 0;
+        const auto t0 = std::chrono::steady_clock::now();
         int rc = wait_batch(X);
         if (rc) return rc;
+        const auto t1 = std::chrono::steady_clock::now();
         const size_t N = X.outs.size();
-        int T = N >= (size_t)env_int("RSMI_FDEC_PAR_MIN", 4096) ? host_threads() : 1;
+        // work ~ records, not groups: a mode-0 group yields up to k records
+        size_t work = N;
+        for (const Job &J : X.jobs) work += (size_t)J.k;
+        int T = work >= (size_t)env_int("RSMI_FDEC_PAR_MIN", 4096) ? host_threads() : 1;
         if (T > (int)N) T = N ? (int)N : 1;
         if ((int)X.spills.size() < T) X.spills.resize((size_t)T);
         std::vector<Out> res;
@@ -763,6 +771,12 @@ int rsmi_fdec_outputs(rsmi_fdec *D, int64_t *n_out) {
         }
         X.outs.swap(res);
         X.resolved = true;
+        if (prof) {
+            const auto t2 = std::chrono::steady_clock::now();
+            fprintf(stderr, "fdec outputs: wait %.3f ms, resolve %.3f ms (%zu records, %d threads)\n",
+                    std::chrono::duration<double, std::milli>(t1 - t0).count(),
+                    std::chrono::duration<double, std::milli>(t2 - t1).count(), X.outs.size(), T);
+        }
     }
     D->out_b = xi;
     if (n_out) *n_out = (int64_t)X.outs.size();
