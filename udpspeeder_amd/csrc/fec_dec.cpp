@@ -85,9 +85,36 @@ struct AntiReplay {
     }
 };
 
+// inner index -> ring slot in ascending index order: the reference's
+// std::map<int,int> (fec_manager.h:382), kept as one sorted vector per group
+// (indices mostly arrive in order, so inserts append).
+struct SlotMap {
+    std::vector<std::pair<int, int>> v;
+    typedef std::vector<std::pair<int, int>>::const_iterator It;
+    It begin() const { return v.begin(); }
+    It end() const { return v.end(); }
+    size_t size() const { return v.size(); }
+    It find(int key) const {
+        It it = std::lower_bound(v.begin(), v.end(), key,
+                                 [](const std::pair<int, int> &a, int b) { return a.first < b; });
+        return it != v.end() && it->first == key ? it : v.end();
+    }
+    bool count(int key) const { return find(key) != v.end(); }
+    void set(int key, int slot) {  // key not present (checked by the caller)
+        if (v.empty()) v.reserve(32);
+        if (v.empty() || v.back().first < key) {
+            v.emplace_back(key, slot);
+            return;
+        }
+        auto it = std::lower_bound(v.begin(), v.end(), key,
+                                   [](const std::pair<int, int> &a, int b) { return a.first < b; });
+        v.insert(it, std::make_pair(key, slot));
+    }
+};
+
 struct Group {  // fec_group_t (fec_manager.h:376-384)
     int type = -1, data_num = -1, red = -1, len = -1, fec_done = 0;
-    std::map<int, int> gm;  // inner index -> ring slot
+    SlotMap gm;  // inner index -> ring slot
 };
 
 struct RingEnt {  // fec_data_t (fec_manager.h:366-375), bytes on the device
@@ -336,8 +363,9 @@ int input_packet(rsmi_fdec *D, const uint8_t *s, int len, uint64_t dsrc, int32_t
     if (type == 0 && data_num == 0) return -1;
     if (data_num + red >= RSMI_FEC_MAX_PACKETS) return -1;
     if (!D->ar.valid(seq, now)) return 0;
+    Group *gp = &D->group(seq);  // operator[]: inserts, as the reference's mp[seq]
     {
-        Group &g = D->group(seq);
+        Group &g = *gp;
         if (g.fec_done) return -1;
         if (g.gm.count(inner)) return -1;
         if (g.type == -1) g.type = type;
@@ -357,7 +385,7 @@ int input_packet(rsmi_fdec *D, const uint8_t *s, int len, uint64_t dsrc, int32_t
         const uint32_t tmp_seq = slot.seq;
         D->ar.set_invalid(tmp_seq, now);
         auto it = D->mp.find(tmp_seq);
-        if (it != D->mp.end()) D->mp.erase(it);
+        if (it != D->mp.end()) D->mp.erase(it);  // other groups' references stay valid
         if (tmp_seq == seq) return -1;
     }
     slot.used = true;
@@ -366,8 +394,8 @@ int input_packet(rsmi_fdec *D, const uint8_t *s, int len, uint64_t dsrc, int32_t
     slot.src = dsrc;
     slot.host = pay;
     slot.in_batch = true;
-    Group &g = D->group(seq);
-    g.gm[inner] = D->index;
+    Group &g = *gp;
+    g.gm.set(inner, D->index);
     const int size = (int)g.gm.size();
     bool about = false, end = false;
     if (type == 0) {
