@@ -39,6 +39,7 @@ METRIC = "device-resident RS encode+decode GiB/s (payload bytes) & FEC-groups/s,
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 K, M, LEN, STRIDE, ERASURES = 20, 10, 1250, 1280, 5
 C4_GROUPS = 1 << 20
+SETTLE_EXTRA_MS = 150.0  # untimed calls before each other_configs measurement (clock ramp)
 TRAFFIC = {"encode": os.path.join(ROOT, "profiles", "traffic.json"),
            "decode": os.path.join(ROOT, "profiles", "traffic_decode.json")}
 
@@ -48,6 +49,10 @@ def parse(argv=None):
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--settle-ms", type=float, default=400.0,
+                   help="untimed steps for at least this long before the --warmup steps: the GPU "
+                        "clocks ramp over the first tens of ms of load, and the VALU-heavy decode "
+                        "runs ~15%% slower until they have (never part of the timed region)")
     p.add_argument("--groups", type=int, default=65536, help="groups per GPU (weak scaling)")
     p.add_argument("--scaling", choices=["weak", "strong"], default=None,
                    help="default: weak at N=1 (C1+C2), strong over --total-groups at N>1 (C4)")
@@ -136,6 +141,14 @@ def main():
         if i is not None:
             ev[i][2].record(stream)
 
+    # settle: untimed steps until the clocks have ramped (see --settle-ms)
+    t_settle = time.perf_counter()
+    settle_steps = 0
+    while (time.perf_counter() - t_settle) * 1e3 < args.settle_ms:
+        for _ in range(8):
+            step()
+        settle_steps += 8
+        torch.cuda.synchronize()
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -194,6 +207,7 @@ def main():
         line = {
             "metric": METRIC, "value": round(value, 2), "unit": "GiB/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup,
+            "settle": {"ms": args.settle_ms, "steps": settle_steps},
             "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
             "scaling": scaling, "vs_baseline": None, "dtype": "u8",
             "data": "synthetic: SplitMix64 payload bytes, seeded 5-of-30 erasures per group",
@@ -272,16 +286,27 @@ def rehearse(args, world, rank, scaling):
 
 
 def _time_ms(torch, fn, reps=10, warm=2):
-    ts = []
-    for i in range(reps + warm):
-        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    """Median per-call GPU time of fn, calls enqueued back to back.  With a
+    synchronise before every call, the start event would fire on an idle GPU
+    while the host is still in fn's launch path (~0.1 ms of Python and HIP
+    calls), and that gap would be counted as kernel time.  The warm calls run
+    for at least SETTLE_EXTRA_MS, so the clocks are up again after the host
+    work between configs (see --settle-ms)."""
+    t0 = time.perf_counter()
+    i = 0
+    while i < warm or (time.perf_counter() - t0) * 1e3 < SETTLE_EXTRA_MS:
+        fn()
+        i += 1
+        if i % 8 == 0:
+            torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(reps + 1)]
+    for a, b in ev:
         a.record()
         fn()
         b.record()
-        torch.cuda.synchronize()
-        if i >= warm:
-            ts.append(a.elapsed_time(b))
-    return statistics.median(ts)
+    torch.cuda.synchronize()
+    return statistics.median(a.elapsed_time(b) for a, b in ev[1:])  # the first call waits on the host
 
 
 def extra_configs(u, synth, torch, dev, buf, G):

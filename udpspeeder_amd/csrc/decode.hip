@@ -75,6 +75,9 @@ constexpr int kTile = 1280;    // bytes per lane-tile pass (64 x 16 + 64 x 4)
 #ifndef DEC_XCD
 #define DEC_XCD 1              // XCD-contiguous group ranges (see k_decode_fused; ~0.5 %)
 #endif
+#ifndef DEC_ROWGUARD
+#define DEC_ROWGUARD 1         // fused kernel: row guards on an opaque SGPR (see the MAC loop)
+#endif
 #ifndef DEC_PAIR
 #define DEC_PAIR 0             // uniform kernel: fold survivors in pairs (fewer XORs, more VGPRs)
 #endif
@@ -706,9 +709,15 @@ __global__ __launch_bounds__(256, DEC_OCC) void k_decode_fused(UniformArgs a, co
                             split(rq[q], rd[q], a0, a1, a2);
                             refill(q, j);
                             const uint32_t *ta = L.tab + (j * kRows + rb) * 8;
+                            // rows in this pass, as an opaque SGPR per survivor: a
+                            // loop-invariant "rb + r < e" is hoisted as a lane-mask
+                            // boolean and re-materialised with v_cndmask + v_cmp at
+                            // every use (2 VALU per row and survivor)
+                            int nr = e - rb;
+                            if (DEC_ROWGUARD) asm volatile("" : "+s"(nr));
 #pragma unroll
                             for (int r = 0; r < kPass; ++r) {
-                                if (DEC_FAKE ? r < DEC_FAKE : rb + r < e) {  // DEC_FAKE: measurement only
+                                if (DEC_FAKE ? r < DEC_FAKE : r < nr) {  // DEC_FAKE: measurement only
                                     const uint4 t = reinterpret_cast<const uint4 *>(ta + r * 8)[0];
                                     const uint32_t t2 = ta[r * 8 + 4];
 #pragma unroll
