@@ -15,13 +15,26 @@ u.rs.fill_ragged(base, dg, G, synth.DATA_SEED)
 for kk in set(zip(ks.tolist(), (ks + ms).tolist())):
     u.prepare_code(*kk)
 plan = u.rs.RaggedPlan(groups)
-times = []
-for i in range(15):
-    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    a.record(); plan.encode(base); b.record(); torch.cuda.synchronize()
-    if i >= 3:
-        times.append(a.elapsed_time(b))
-t = statistics.median(times)
+
+
+def time_ms(fn, reps=20, settle_ms=150.0):
+    """median per-call time, calls back to back after a clock-settle phase
+    (bench.py's _time_ms)"""
+    import time
+    t0 = time.perf_counter()
+    while (time.perf_counter() - t0) * 1e3 < settle_ms:
+        for _ in range(8):
+            fn()
+        torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(reps + 1)]
+    for a, b in ev:
+        a.record(); fn(); b.record()
+    torch.cuda.synchronize()
+    return statistics.median(a.elapsed_time(b) for a, b in ev[1:])
+
+
+t = time_ms(lambda: plan.encode(base))
 alg = int(((ks + ms) * ls).sum())
 print(json.dumps({"bitslice_plan": plan.bitslice, "c3_encode_ms": t, "payload_GiBps": float((ks * ls).sum()) / (t * 1e-3) / 2**30,
                   "alg_GBps": alg / (t * 1e-3) / 1e9, "alg_bytes": alg, "buffer_bytes": total}))
@@ -30,15 +43,9 @@ flags = synth.ragged_erasures(synth.ERASE_SEED, 0, ks + ms, ms, 5)
 bits = torch.from_numpy(synth.present_bits(flags).view(np.int32)).to("cuda")
 st = torch.empty(G, dtype=torch.int32, device="cuda")
 clean = base.clone()
-dtimes = []
-for i in range(15):
-    base.copy_(clean)
-    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    a.record(); plan.decode(base, bits, status=st); b.record(); torch.cuda.synchronize()
-    if i >= 3:
-        dtimes.append(a.elapsed_time(b))
+# rebuilt rows equal the erased ones, so repeated decodes leave the batch unchanged
+td = time_ms(lambda: plan.decode(base, bits, status=st))
 assert int((st != 0).sum()) == 0 and torch.equal(base, clean)
-td = statistics.median(dtimes)
 e = ((flags[:, :20] == 0) & (np.arange(20)[None, :] < ks[:, None])).sum(1)
 dalg = int(((ks + e) * ls).sum())
 print(json.dumps({"c3_decode_ms": td, "alg_GBps": dalg / (td * 1e-3) / 1e9, "frac": dalg / (td * 1e-3) / 8e12}))
