@@ -333,6 +333,22 @@ int decode_ragged_dev(const rsmi_group *dg, int64_t ngroups, uint8_t *base,
     return RSMI_OK;
 }
 
+int decode_ragged_cls_dev(const rsmi_group *dg, int64_t ngroups, const uint32_t *cls_idx,
+                          const int64_t cls_first[5], uint8_t *base, const uint32_t *present_bits,
+                          int32_t *status, int kmax, hipStream_t s) {
+    if (ngroups <= 0) return RSMI_OK;
+    if (!base || !present_bits || !status)
+        return fail(RSMI_ERR_INVALID, "null base/present_bits/status");
+    if (((uintptr_t)base) % 16) return fail(RSMI_ERR_INVALID, "base must be 16-aligned");
+    int rc;
+    Device *D = current(&rc);
+    if (!D) return rc;
+    hipError_t e = launch_decode_ragged_cls(dg, ngroups, cls_idx, cls_first, base, present_bits,
+                                            status, kmax, D->code_dir, D->ptab, D->gftab, s);
+    if (e != hipSuccess) return hip_fail(e, "ragged decode launch");
+    return RSMI_OK;
+}
+
 uint64_t *device_code_dir(int *rc) {
     Device *D = current(rc);
     return D ? D->code_dir : nullptr;

@@ -69,6 +69,9 @@ constexpr int kTile = 1280;    // bytes per lane-tile pass (64 x 16 + 64 x 4)
 #ifndef DEC_NOMEM
 #define DEC_NOMEM 0            // measurement only: survivor loads all hit one cached slot
 #endif
+#ifndef DEC_RAG_RING45
+#define DEC_RAG_RING45 DEC_RING  // ragged kernels: survivors in flight for 16- and 20-byte lane pieces
+#endif
 #ifndef DEC_RAG_DEEP
 #define DEC_RAG_DEEP 1  // ragged kernel: 16 / W survivors in flight for 4- and 8-byte lane pieces
 #endif
@@ -135,7 +138,12 @@ __device__ __forceinline__ uint32_t gmul(const uint8_t *lexp, const uint8_t *llo
 
 struct WaveLds {  // per-wave LDS slice
     uint8_t *sel, *miss, *aug;
-    uint32_t *tab;  // [k][kRows] entries of 8 dwords (T0lo T0hi T1lo T1hi T2 - - -)
+    uint32_t *tab;  // k_decode_fused: [k][kRows] entries of 8 dwords (T0lo T0hi T1lo T1hi T2 - - -)
+    // ragged kernels: coefficient (j, r)'s split table is t01[j * rows + r]
+    // (T0lo T0hi T1lo T1hi) and t2[j * rows + r] (T2): 20 bytes, not 32
+    uint4 *t01;
+    uint32_t *t2;
+    int rows;
 };
 
 __host__ __device__ inline int aug_bytes(int k) { return (kRows * (kRows + k) + 15) & ~15; }
@@ -145,8 +153,14 @@ __host__ __device__ inline int wave_lds_bytes(int k) {
     return 512 + aug_bytes(k) + k * kRows * 32;
 }
 
-__device__ __forceinline__ WaveLds wave_slice(uint8_t *wl, int k) {
-    return WaveLds{wl, wl + 256, wl + 512, reinterpret_cast<uint32_t *>(wl + 512 + aug_bytes(k))};
+// Ragged kernels' slice: sel[64] miss[64] t01[k*rows] t2[k*rows] (k <= 32,
+// e <= rows: the register Gauss-Jordan always applies, no aug matrix).
+__host__ __device__ inline int rag_lds_bytes(int k, int rows) { return 128 + k * rows * 20; }
+
+__device__ __forceinline__ WaveLds rag_slice(uint8_t *wl, int k, int rows) {
+    uint4 *t01 = reinterpret_cast<uint4 *>(wl + 128);
+    return WaveLds{wl, wl + 64, nullptr, nullptr, t01,
+                   reinterpret_cast<uint32_t *>(t01 + k * rows), rows};
 }
 
 // ---- 1. survivor selection (rs.cpp:24-39) ------------------------------------
@@ -184,8 +198,9 @@ __device__ __forceinline__ int select_survivors(int k, int n, Flag flag, const W
 // ---- 3. Gauss-Jordan ------------------------------------------------------------
 // prow(R) points at the code's parity row R (R >= k: row R - k of the parity
 // rows).  Register form: lane c holds column c of [A | M], W = e + k <= 64.
-// Leaves coef[r][j] expanded into its split table at tab[j][r].
-template <class Row>
+// Leaves coef[r][j] expanded into its split table at (t01, t2)[j * rows + r];
+// NR >= e is the number of row registers.
+template <int NR, class Row>
 __device__ __forceinline__ int gauss_jordan_regs(int k, int e, uint32_t sel_lane, const WaveLds &L,
                                                  const Tables &T, Row prow, int lane) {
     int st = RSMI_DEC_OK;
@@ -193,9 +208,9 @@ __device__ __forceinline__ int gauss_jordan_regs(int k, int e, uint32_t sel_lane
     // lane c holds column c: a missing data index (c < e) or survivor c - e
     const uint32_t col = lane < e ? (uint32_t)L.miss[lane]
                                   : (lane < W ? (uint32_t)L.sel[lane - e] : 0u);
-    uint32_t a[kRows];
+    uint32_t a[NR];
 #pragma unroll
-    for (int r = 0; r < kRows; ++r) {
+    for (int r = 0; r < NR; ++r) {
         a[r] = 0;
         if (r < e) {
             const uint32_t R = __builtin_amdgcn_readlane(sel_lane, k - e + r);
@@ -204,7 +219,7 @@ __device__ __forceinline__ int gauss_jordan_regs(int k, int e, uint32_t sel_lane
         }
     }
 #pragma unroll
-    for (int p = 0; p < kRows; ++p) {
+    for (int p = 0; p < NR; ++p) {
         if (p < e) {
             const uint32_t piv = __builtin_amdgcn_readlane(a[p], p);
             if (piv == 0) {
@@ -214,7 +229,7 @@ __device__ __forceinline__ int gauss_jordan_regs(int k, int e, uint32_t sel_lane
             const uint32_t ip = __builtin_amdgcn_readfirstlane(T.linv[piv]);
             a[p] = gmul_t(T.s01[ip], T.s2[ip], a[p]);
 #pragma unroll
-            for (int r = 0; r < kRows; ++r) {
+            for (int r = 0; r < NR; ++r) {
                 if (r < e && r != p) {
                     const uint32_t f = __builtin_amdgcn_readlane(a[r], p);
                     a[r] ^= gmul_t(T.s01[f], T.s2[f], a[p]);
@@ -225,70 +240,16 @@ __device__ __forceinline__ int gauss_jordan_regs(int k, int e, uint32_t sel_lane
     }
     st = __builtin_amdgcn_readfirstlane(st);
     if (st != RSMI_DEC_OK) return st;
-    // coef[r][j] sits in lane e + j: expand into split tables tab[j][r]
+    // coef[r][j] sits in lane e + j: expand into its split table
     if (lane >= e && lane < W) {
-        uint32_t *dst = L.tab + (lane - e) * kRows * 8;
+        const int base = (lane - e) * L.rows;
 #pragma unroll
-        for (int r = 0; r < kRows; ++r) {
+        for (int r = 0; r < NR; ++r) {
             if (r < e) {
-                reinterpret_cast<uint4 *>(dst + r * 8)[0] = T.s01[a[r]];
-                dst[r * 8 + 4] = T.s2[a[r]];
+                L.t01[base + r] = T.s01[a[r]];
+                L.t2[base + r] = T.s2[a[r]];
             }
         }
-    }
-    wave_sync();
-    return RSMI_DEC_OK;
-}
-
-// LDS form for W > 64 (k <= 64, e <= kRows): [A | M] in the wave's aug slice.
-template <class Row>
-__device__ __forceinline__ int gauss_jordan_lds(int k, int e, const WaveLds &L, const Tables &T,
-                                                Row prow, int lane) {
-    int st = RSMI_DEC_OK;
-    const int W = e + k;
-    for (int t = lane; t < e * W; t += 64) {
-        const int r = t / W, c = t - r * W;
-        const int R = L.sel[k - e + r];
-        const uint8_t *pr = prow(R);
-        uint8_t v;
-        if (c < e) {
-            v = pr[L.miss[c]];
-        } else {
-            const int s = L.sel[c - e];
-            v = (s >= k) ? (uint8_t)(s == R) : pr[s];
-        }
-        L.aug[t] = v;
-    }
-    wave_sync();
-    for (int p = 0; p < e && st == RSMI_DEC_OK; ++p) {
-        const uint32_t piv = __builtin_amdgcn_readfirstlane(L.aug[p * W + p]);
-        if (piv == 0) {
-            st = RSMI_DEC_SINGULAR;
-            break;
-        }
-        const uint32_t ipiv = __builtin_amdgcn_readfirstlane(T.lexp[255 - T.llog[piv]]);
-        for (int c = p + 1 + lane; c < W; c += 64)
-            L.aug[p * W + c] = (uint8_t)gmul(T.lexp, T.llog, ipiv, L.aug[p * W + c]);
-        wave_sync();
-        const int cols = W - p - 1;
-        for (int t = lane; t < e * cols; t += 64) {
-            const int r = t / cols;
-            if (r == p) continue;
-            const int c = p + 1 + (t - r * cols);
-            const uint32_t f = L.aug[r * W + p];
-            if (f) L.aug[r * W + c] ^= (uint8_t)gmul(T.lexp, T.llog, f, L.aug[p * W + c]);
-        }
-        wave_sync();
-    }
-    st = __builtin_amdgcn_readfirstlane(st);
-    if (st != RSMI_DEC_OK) return st;
-    // expand coef[r][j] = aug[r][e + j] into split tables tab[j][r]
-    for (int t = lane; t < e * k; t += 64) {
-        const int r = t / k, j = t - r * k;
-        const uint32_t c = L.aug[r * W + e + j];
-        uint32_t *dst = L.tab + (j * kRows + r) * 8;
-        reinterpret_cast<uint4 *>(dst)[0] = T.s01[c];
-        dst[4] = T.s2[c];
     }
     wave_sync();
     return RSMI_DEC_OK;
@@ -345,7 +306,7 @@ template <int W>
 struct Rebuild {
     // narrow tiles keep more survivors in flight in the same registers (16
     // dwords of ring): short groups are latency-bound, not VGPR-bound
-    static constexpr int R = DEC_RAG_DEEP && W <= 2 ? 16 / W : kRing;
+    static constexpr int R = DEC_RAG_DEEP && W <= 2 ? 16 / W : DEC_RAG_RING45;
     __amdgpu_buffer_rsrc_t rsrc;
     uint32_t so_lane, mo_lane;
     int k, e, len, lpad;
@@ -364,7 +325,7 @@ struct Rebuild {
     }
     // passes over (tile, block of kPass rows); tile 0's first loads were
     // issued by start_tile(0) before the Gauss-Jordan
-    __device__ __forceinline__ void run(const uint32_t *tab, int lane) {
+    __device__ __forceinline__ void run(const WaveLds &L, int lane) {
         for (int toff = 0; toff < len; toff += TileIO<W>::kBytes) {
             for (int rb = 0; rb < e; rb += kPass) {
                 if (toff || rb) start_tile(toff, lane);
@@ -388,12 +349,15 @@ struct Rebuild {
                             }
                             // ring slot q took survivor j: load survivor j + R into it
                             if (j + R < k) load(q, j + R);
-                            const uint32_t *ta = tab + (j * kRows + rb) * 8;
+                            const uint4 *ta = L.t01 + j * L.rows + rb;
+                            const uint32_t *ta2 = L.t2 + j * L.rows + rb;
+                            int nr = e - rb;  // opaque SGPR: see k_decode_fused's row guards
+                            asm volatile("" : "+s"(nr));
 #pragma unroll
                             for (int r = 0; r < kPass; ++r) {
-                                if (rb + r < e) {
-                                    const uint4 t = reinterpret_cast<const uint4 *>(ta + r * 8)[0];
-                                    const uint32_t t2 = ta[r * 8 + 4];
+                                if (r < nr) {
+                                    const uint4 t = ta[r];
+                                    const uint32_t t2 = ta2[r];
 #pragma unroll
                                     for (int w = 0; w < W; ++w)
                                         acc[r][w] ^= xor3(__builtin_amdgcn_perm(t.y, t.x, a0[w]),
@@ -755,91 +719,144 @@ __global__ __launch_bounds__(256, DEC_OCC) void k_decode_fused(UniformArgs a, co
 // One wave per group; each group its own (k, n, len, shard_stride, offset) from
 // its rsmi_group descriptor, present flags as a 256-bit mask per group (8
 // words: bit j of word j/32 = shard j received), parity rows through the
-// device code directory.  Groups this form cannot take (e > kRows, k > kmax,
-// or n slots spanning >= 2 GiB) get kDefer for k_decode_ragged_big.
+// device code directory.  Groups this form cannot take (e > NR, k > kmax, or
+// n slots spanning >= 2 GiB) get kDefer for k_decode_ragged_big.
 #ifndef DEC_RAG_W
 #define DEC_RAG_W 1  // ragged kernel: tile width per group (0: always 1280-byte tiles)
 #endif
 #ifndef DEC_RAG_OCC
 #define DEC_RAG_OCC DEC_OCC  // waves per SIMD the ragged kernel's registers are cut for
 #endif
+// class kernels (plans): waves per SIMD per tile width
+#ifndef DEC_CLS_OCC1
+#define DEC_CLS_OCC1 8
+#endif
+#ifndef DEC_CLS_OCC2
+#define DEC_CLS_OCC2 8
+#endif
+#ifndef DEC_CLS_OCC4
+#define DEC_CLS_OCC4 6
+#endif
+#ifndef DEC_CLS_OCC5
+#define DEC_CLS_OCC5 5
+#endif
+constexpr int kClsRows = 5;  // class kernels: e <= 5 in registers, more is deferred
 
+// One group.  WC = tile width (1, 2, 4, 5), or 0: chosen per group.  The
+// descriptor d is wave-uniform (scalar loads).
+template <int WC, int NR>
+__device__ __forceinline__ void ragged_group(int64_t g, const rsmi_group &d, uint32_t w8,
+                                             uint8_t *base, int32_t *status_out,
+                                             const uint64_t *code_dir, const Tables &T,
+                                             const WaveLds &L, int kmax, int lane) {
+    const int k = __builtin_amdgcn_readfirstlane(d.k);
+    const int n = __builtin_amdgcn_readfirstlane(d.n);
+    const int len = __builtin_amdgcn_readfirstlane(d.len);
+    const uint32_t ss = __builtin_amdgcn_readfirstlane(d.shard_stride);
+    const uint64_t off = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(d.offset >> 32)) << 32) |
+                         (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)d.offset);
+    const uint8_t *rows = (k >= 1 && n > k && n <= 256)
+                              ? reinterpret_cast<const uint8_t *>(code_dir[k * 257 + n])
+                              : nullptr;
+    if (k < 1 || n < k || n > 256 || (n > k && !rows)) {
+        if (lane == 0) status_out[g] = RSMI_DEC_UNSUPPORTED;
+        return;
+    }
+    int e;
+    const int cnt = select_survivors(
+        k, n,
+        [&](int b, int idx) {
+            // words b/32 and b/32 + 1 cover shards b..b+63 (readlane ignores exec)
+            const uint32_t lo = __builtin_amdgcn_readlane(w8, (b >> 5) & 7);
+            const uint32_t hi = __builtin_amdgcn_readlane(w8, ((b >> 5) + 1) & 7);
+            return ((((idx & 32) ? hi : lo) >> (idx & 31)) & 1u) != 0;
+        },
+        L, lane, e);
+    wave_sync();
+    if (cnt < k || e == 0) {
+        if (lane == 0) status_out[g] = cnt < k ? RSMI_DEC_TOO_FEW : RSMI_DEC_OK;
+        return;
+    }
+    if (e > NR || k > kmax || (uint64_t)n * ss >= 0x80000000ull) {
+        if (lane == 0) status_out[g] = kDefer;
+        return;
+    }
+    auto prow = [&](uint32_t R) { return rows + (R - k) * k; };
+    const int lpad = rag_lpad((uint32_t)len, ss);
+    const uint32_t sel_lane = lane < k ? (uint32_t)L.sel[lane] : 0u;
+    auto rebuild = [&](auto wc) {
+        constexpr int W = decltype(wc)::value;
+        Rebuild<W> B;
+        B.rsrc = group_rsrc(base + off, (uint32_t)(n * ss));
+        B.k = k;
+        B.e = e;
+        B.len = len;
+        B.lpad = lpad;
+        B.so_lane = sel_lane * ss;
+        B.mo_lane = (lane < e ? (uint32_t)L.miss[lane] : 0u) * ss;
+        if (len > 0) B.start_tile(0, lane);
+        const int st = gauss_jordan_regs<NR>(k, e, sel_lane, L, T, prow, lane);
+        if (st == RSMI_DEC_OK && len > 0) B.run(L, lane);
+        return st;
+    };
+    int st;
+    if constexpr (WC != 0) {
+        st = rebuild(std::integral_constant<int, WC>{});
+    } else {
+        const int w = DEC_RAG_W ? rag_width(lpad) : 5;
+        if (w == 1) st = rebuild(std::integral_constant<int, 1>{});
+        else if (w == 2) st = rebuild(std::integral_constant<int, 2>{});
+        else if (w == 4) st = rebuild(std::integral_constant<int, 4>{});
+        else st = rebuild(std::integral_constant<int, 5>{});
+    }
+    if (lane == 0) status_out[g] = st;
+}
+
+// Every group of the batch, tile width chosen per group (rsmi_decode_ragged_dev:
+// descriptors on the device, no plan).
 __global__ __launch_bounds__(256, DEC_RAG_OCC) void k_decode_ragged(
-    const rsmi_group *groups, int64_t ngroups, uint8_t *base, const uint32_t *present,
-    int32_t *status_out, const uint64_t *code_dir, const uint32_t *ptab, const uint8_t *gftab,
-    int kmax) {
+    const rsmi_group *__restrict__ groups, int64_t ngroups, uint8_t *base,
+    const uint32_t *__restrict__ present, int32_t *status_out, const uint64_t *__restrict__ code_dir,
+    const uint32_t *ptab, const uint8_t *gftab, int kmax) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const Tables T = load_tables(smem, ptab, gftab);
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane0 = threadIdx.x & 63;
+    const WaveLds L = rag_slice(smem + kTabBytes + wid * rag_lds_bytes(kmax, kRows), kmax, kRows);
+    __syncthreads();
+    const int64_t nwaves = (int64_t)gridDim.x * kWaves;
+    for (int64_t g = (int64_t)blockIdx.x * kWaves + wid; g < ngroups; g += nwaves) {
+        // lane-derived values are recomputed per group: hoisted out of the
+        // loop they stay live across the four tile-width bodies and spill
+        int lane = lane0;
+        asm volatile("" : "+v"(lane));
+        const rsmi_group d = groups[g];
+        ragged_group<0, kRows>(g, d, present[g * 8 + (lane & 7)], base, status_out, code_dir, T, L,
+                               kmax, lane);
+        wave_sync();  // the LDS slice is rewritten by the next group
+    }
+}
+
+// Plans: the groups of one tile-width class (idx[0..count)), registers cut
+// for that width so short groups run at up to 8 waves per SIMD: C3's groups
+// are latency-bound (descriptor -> code rows -> inversion -> a few survivors).
+template <int W, int OCC>
+__global__ __launch_bounds__(256, OCC) void k_decode_ragged_cls(
+    const rsmi_group *__restrict__ groups, const uint32_t *__restrict__ idx, int64_t count,
+    uint8_t *base, const uint32_t *__restrict__ present, int32_t *status_out,
+    const uint64_t *__restrict__ code_dir, const uint32_t *ptab, const uint8_t *gftab, int kmax) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const Tables T = load_tables(smem, ptab, gftab);
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
-    const WaveLds L = wave_slice(smem + kTabBytes + wid * wave_lds_bytes(kmax), kmax);
+    const WaveLds L = rag_slice(smem + kTabBytes + wid * rag_lds_bytes(kmax, kClsRows), kmax, kClsRows);
     __syncthreads();
-
     const int64_t nwaves = (int64_t)gridDim.x * kWaves;
-    for (int64_t g = (int64_t)blockIdx.x * kWaves + wid; g < ngroups; g += nwaves) {
+    for (int64_t i = (int64_t)blockIdx.x * kWaves + wid; i < count; i += nwaves) {
+        const int64_t g = __builtin_amdgcn_readfirstlane(idx[i]);
         const rsmi_group d = groups[g];
-        const int k = __builtin_amdgcn_readfirstlane(d.k);
-        const int n = __builtin_amdgcn_readfirstlane(d.n);
-        const int len = __builtin_amdgcn_readfirstlane(d.len);
-        const uint32_t ss = __builtin_amdgcn_readfirstlane(d.shard_stride);
-        const uint64_t off = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(d.offset >> 32)) << 32) |
-                             (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)d.offset);
-        const uint8_t *rows = (k >= 1 && n > k && n <= 256)
-                                  ? reinterpret_cast<const uint8_t *>(code_dir[k * 257 + n])
-                                  : nullptr;
-        if (k < 1 || n < k || n > 256 || (n > k && !rows)) {
-            if (lane == 0) status_out[g] = RSMI_DEC_UNSUPPORTED;
-            continue;
-        }
-        const uint32_t w8 = present[g * 8 + (lane & 7)];  // lane i (< 8) holds word i of the mask
-        int e;
-        const int cnt = select_survivors(
-            k, n,
-            [&](int b, int idx) {
-                // words b/32 and b/32 + 1 cover shards b..b+63 (readlane ignores exec)
-                const uint32_t lo = __builtin_amdgcn_readlane(w8, (b >> 5) & 7);
-                const uint32_t hi = __builtin_amdgcn_readlane(w8, ((b >> 5) + 1) & 7);
-                return ((((idx & 32) ? hi : lo) >> (idx & 31)) & 1u) != 0;
-            },
-            L, lane, e);
-        wave_sync();
-        if (cnt < k || e == 0) {
-            if (lane == 0) status_out[g] = cnt < k ? RSMI_DEC_TOO_FEW : RSMI_DEC_OK;
-            continue;
-        }
-        if (e > kRows || k > kmax || k > 64 || (uint64_t)n * ss >= 0x80000000ull) {
-            if (lane == 0) status_out[g] = kDefer;
-            continue;
-        }
-        auto prow = [&](uint32_t R) { return rows + (R - k) * k; };
-        const int lpad = (int)(((uint32_t)len + 127) / 128 * 128 < ss ? ((uint32_t)len + 127) / 128 * 128 : ss);
-        const uint32_t sel_lane = lane < k ? (uint32_t)L.sel[lane] : 0u;
-        auto rebuild = [&](auto wc) {
-            constexpr int W = decltype(wc)::value;
-            Rebuild<W> B;
-            B.rsrc = group_rsrc(base + off, (uint32_t)(n * ss));
-            B.k = k;
-            B.e = e;
-            B.len = len;
-            B.lpad = lpad;
-            B.so_lane = sel_lane * ss;
-            B.mo_lane = (lane < e ? (uint32_t)L.miss[lane] : 0u) * ss;
-            if (len > 0) B.start_tile(0, lane);
-            const int st = (e + k <= 64) ? gauss_jordan_regs(k, e, sel_lane, L, T, prow, lane)
-                                         : gauss_jordan_lds(k, e, L, T, prow, lane);
-            if (st == RSMI_DEC_OK && len > 0) B.run(L.tab, lane);
-            return st;
-        };
-        // the narrowest tile that covers the group (one pass), else 1280-byte
-        // tiles.  Lane pieces of 4, 8 or 16 bytes divide lpad (a multiple of
-        // 16), so no lane straddles pad_end; 12-byte pieces would.
-        const int nw = DEC_RAG_W ? (lpad + 255) / 256 : 5;
-        int st;
-        if (nw <= 1) st = rebuild(std::integral_constant<int, 1>{});
-        else if (nw == 2) st = rebuild(std::integral_constant<int, 2>{});
-        else if (nw <= 4) st = rebuild(std::integral_constant<int, 4>{});
-        else st = rebuild(std::integral_constant<int, 5>{});
-        if (lane == 0) status_out[g] = st;
+        ragged_group<W, kClsRows>(g, d, present[g * 8 + (lane & 7)], base, status_out, code_dir, T,
+                                  L, kmax, lane);
         wave_sync();  // the LDS slice is rewritten by the next group
     }
 }
@@ -986,19 +1003,60 @@ hipError_t launch_decode_fused(const UniformArgs &a, const uint8_t *present,
     return hipGetLastError();
 }
 
+hipError_t launch_decode_ragged_big(const rsmi_group *groups, int64_t ngroups, uint8_t *base,
+                                    const uint32_t *present_bits, int32_t *status,
+                                    const uint64_t *code_dir, const uint32_t *ptab,
+                                    const uint8_t *gftab, hipStream_t s);
+
 hipError_t launch_decode_ragged(const rsmi_group *groups, int64_t ngroups, uint8_t *base,
                                 const uint32_t *present_bits, int32_t *status, int kmax,
                                 const uint64_t *code_dir, const uint32_t *ptab,
                                 const uint8_t *gftab, hipStream_t s) {
     if (ngroups <= 0) return hipSuccess;
     kmax = kmax < 1 ? 1 : (kmax > 32 ? 32 : kmax);  // larger k: the workgroup kernel
-    const size_t lds = kTabBytes + (size_t)kWaves * wave_lds_bytes(kmax);
+    const size_t lds = kTabBytes + (size_t)kWaves * rag_lds_bytes(kmax, kRows);
     int64_t blocks = (ngroups + kWaves - 1) / kWaves;
     if (blocks > 256 * 8) blocks = 256 * 8;
     k_decode_ragged<<<(unsigned)blocks, 64 * kWaves, lds, s>>>(groups, ngroups, base, present_bits,
                                                               status, code_dir, ptab, gftab, kmax);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
+    return launch_decode_ragged_big(groups, ngroups, base, present_bits, status, code_dir, ptab,
+                                    gftab, s);
+}
+
+hipError_t launch_decode_ragged_cls(const rsmi_group *groups, int64_t ngroups,
+                                    const uint32_t *cls_idx, const int64_t cls_first[5],
+                                    uint8_t *base, const uint32_t *present_bits, int32_t *status,
+                                    int kmax, const uint64_t *code_dir, const uint32_t *ptab,
+                                    const uint8_t *gftab, hipStream_t s) {
+    if (ngroups <= 0) return hipSuccess;
+    kmax = kmax < 1 ? 1 : (kmax > 32 ? 32 : kmax);  // larger k: the workgroup kernel
+    const size_t lds = kTabBytes + (size_t)kWaves * rag_lds_bytes(kmax, kClsRows);
+    auto launch = [&](auto kern, int c, int occ) {
+        const int64_t count = cls_first[c + 1] - cls_first[c];
+        if (count <= 0) return hipSuccess;
+        int64_t blocks = (count + kWaves - 1) / kWaves;
+        const int64_t cap = 256 * (int64_t)occ;  // one round of resident blocks
+        if (blocks > cap) blocks = cap;
+        kern<<<(unsigned)blocks, 64 * kWaves, lds, s>>>(groups, cls_idx + cls_first[c], count, base,
+                                                       present_bits, status, code_dir, ptab, gftab,
+                                                       kmax);
+        return hipGetLastError();
+    };
+    hipError_t e = launch(k_decode_ragged_cls<5, DEC_CLS_OCC5>, 3, DEC_CLS_OCC5);
+    if (e == hipSuccess) e = launch(k_decode_ragged_cls<4, DEC_CLS_OCC4>, 2, DEC_CLS_OCC4);
+    if (e == hipSuccess) e = launch(k_decode_ragged_cls<2, DEC_CLS_OCC2>, 1, DEC_CLS_OCC2);
+    if (e == hipSuccess) e = launch(k_decode_ragged_cls<1, DEC_CLS_OCC1>, 0, DEC_CLS_OCC1);
+    if (e != hipSuccess) return e;
+    return launch_decode_ragged_big(groups, ngroups, base, present_bits, status, code_dir, ptab,
+                                    gftab, s);
+}
+
+hipError_t launch_decode_ragged_big(const rsmi_group *groups, int64_t ngroups, uint8_t *base,
+                                    const uint32_t *present_bits, int32_t *status,
+                                    const uint64_t *code_dir, const uint32_t *ptab,
+                                    const uint8_t *gftab, hipStream_t s) {
     const int64_t bb = ngroups < 256 * 4 ? ngroups : 256 * 4;
     k_decode_ragged_big<<<(unsigned)bb, 256, kTabBytes + 512 + kBigAug, s>>>(
         groups, ngroups, base, present_bits, status, code_dir, ptab, gftab);

@@ -19,12 +19,19 @@
 
 #include "rsmi_internal.hpp"
 
+#ifndef RSMI_DEC_CLASSES
+#define RSMI_DEC_CLASSES 1  // plan decodes: one register-cut kernel per tile-width class
+#endif
+
 namespace rsmi {
 int prepare_code(int k, int n);
 void set_error(const std::string &m);
 uint64_t *device_code_dir(int *rc);
 int decode_ragged_dev(const rsmi_group *dg, int64_t ngroups, uint8_t *base,
                       const uint32_t *present_bits, int32_t *status, int kmax, hipStream_t s);
+int decode_ragged_cls_dev(const rsmi_group *dg, int64_t ngroups, const uint32_t *cls_idx,
+                          const int64_t cls_first[5], uint8_t *base, const uint32_t *present_bits,
+                          int32_t *status, int kmax, hipStream_t s);
 const uint32_t *device_ptab(int *rc);
 }  // namespace rsmi
 
@@ -45,6 +52,10 @@ struct rsmi_ragged_plan {
     rsmi_group *d_groups = nullptr;
     uint32_t *d_colmap = nullptr;
     uint32_t *d_waves = nullptr;
+    // decode: group indices by tile-width class (rag_width), class c at
+    // [cls_first[c], cls_first[c+1]) of d_cls
+    int64_t cls_first[5] = {0, 0, 0, 0, 0};
+    uint32_t *d_cls = nullptr;
 };
 
 namespace {
@@ -158,12 +169,28 @@ extern "C" int rsmi_ragged_plan_create(const rsmi_group *g, int64_t ngroups,
         P->nwaves = (uint32_t)(waves.size() / 2);
         if (nb <= nbuiltin) P->nwaves_builtin = P->nwaves;
     }
+    // decode classes: the width each group's tiles take (decode.hip)
+    std::vector<uint32_t> cls((size_t)ngroups);
+    {
+        int64_t cnt[4] = {0, 0, 0, 0};
+        std::vector<uint8_t> c_of((size_t)ngroups);
+        for (int64_t i = 0; i < ngroups; ++i) {
+            const int c = rsmi::rag_width_class(rsmi::rag_width(rsmi::rag_lpad(g[i].len, g[i].shard_stride)));
+            c_of[(size_t)i] = (uint8_t)c;
+            ++cnt[c];
+        }
+        for (int c = 0; c < 4; ++c) P->cls_first[c + 1] = P->cls_first[c] + cnt[c];
+        int64_t fill[4] = {P->cls_first[0], P->cls_first[1], P->cls_first[2], P->cls_first[3]};
+        for (int64_t i = 0; i < ngroups; ++i) cls[(size_t)fill[c_of[(size_t)i]]++] = (uint32_t)i;
+    }
     const size_t gbytes = sizeof(rsmi_group) * (size_t)ngroups;
     const size_t cbytes = sizeof(uint32_t) * colmap.size();
     const size_t wbytes = sizeof(uint32_t) * waves.size();
+    const size_t dbytes = sizeof(uint32_t) * cls.size();
     const size_t goff = 0, coff = (gbytes + 255) & ~size_t(255),
-                 woff = (coff + cbytes + 255) & ~size_t(255);
-    const size_t all = woff + wbytes + 16;
+                 woff = (coff + cbytes + 255) & ~size_t(255),
+                 doff = (woff + wbytes + 255) & ~size_t(255);
+    const size_t all = doff + dbytes + 16;
     if (hipMalloc(&P->mem, all) != hipSuccess) {
         delete P;
         return fail(RSMI_ERR_NOMEM, "hipMalloc(ragged plan)");
@@ -171,11 +198,14 @@ extern "C" int rsmi_ragged_plan_create(const rsmi_group *g, int64_t ngroups,
     P->d_groups = reinterpret_cast<rsmi_group *>(P->mem + goff);
     P->d_colmap = reinterpret_cast<uint32_t *>(P->mem + coff);
     P->d_waves = reinterpret_cast<uint32_t *>(P->mem + woff);
+    P->d_cls = reinterpret_cast<uint32_t *>(P->mem + doff);
     hipError_t e = hipSuccess;
     if (gbytes) e = hipMemcpy(P->d_groups, g, gbytes, hipMemcpyHostToDevice);
     if (e == hipSuccess && cbytes) e = hipMemcpy(P->d_colmap, colmap.data(), cbytes,
                                                  hipMemcpyHostToDevice);
     if (e == hipSuccess && wbytes) e = hipMemcpy(P->d_waves, waves.data(), wbytes,
+                                                 hipMemcpyHostToDevice);
+    if (e == hipSuccess && dbytes) e = hipMemcpy(P->d_cls, cls.data(), dbytes,
                                                  hipMemcpyHostToDevice);
     if (e != hipSuccess) {
         (void)hipFree(P->mem);
@@ -217,6 +247,9 @@ extern "C" int rsmi_decode_ragged_plan(const rsmi_ragged_plan *P, uint8_t *base,
                                        const uint32_t *present_bits, int32_t *status,
                                        void *stream) {
     if (!P) return fail(RSMI_ERR_INVALID, "null plan");
+    if (RSMI_DEC_CLASSES)
+        return rsmi::decode_ragged_cls_dev(P->d_groups, P->ngroups, P->d_cls, P->cls_first, base,
+                                           present_bits, status, P->kmax, (hipStream_t)stream);
     return rsmi::decode_ragged_dev(P->d_groups, P->ngroups, base, present_bits, status, P->kmax,
                                    (hipStream_t)stream);
 }

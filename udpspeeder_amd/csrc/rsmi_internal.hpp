@@ -64,6 +64,25 @@ hipError_t launch_decode_ragged(const rsmi_group *groups, int64_t ngroups, uint8
                                 const uint32_t *present_bits, int32_t *status, int kmax,
                                 const uint64_t *code_dir, const uint32_t *ptab,
                                 const uint8_t *gftab, hipStream_t s);
+// Tile width of a ragged group (lane dwords: 1, 2, 4 or 5): the narrowest
+// that covers its padded length in one pass, else 1280-byte tiles.  Lane
+// pieces of 4, 8 or 16 bytes divide the padded length (a multiple of 16).
+__host__ __device__ inline int rag_lpad(uint32_t len, uint32_t ss) {
+    const uint32_t l128 = (len + 127) / 128 * 128;  // whole lines where the slot has room
+    return (int)(l128 < ss ? l128 : ss);
+}
+__host__ __device__ inline int rag_width(int lpad) {
+    const int nw = (lpad + 255) / 256;
+    return nw <= 1 ? 1 : (nw == 2 ? 2 : (nw <= 4 ? 4 : 5));
+}
+__host__ __device__ inline int rag_width_class(int w) { return w == 1 ? 0 : (w == 2 ? 1 : (w == 4 ? 2 : 3)); }
+// Plans: the groups sorted into the four width classes (cls_idx, class c's
+// groups at [cls_first[c], cls_first[c+1])), one register-cut kernel per class.
+hipError_t launch_decode_ragged_cls(const rsmi_group *groups, int64_t ngroups,
+                                    const uint32_t *cls_idx, const int64_t cls_first[5],
+                                    uint8_t *base, const uint32_t *present_bits, int32_t *status,
+                                    int kmax, const uint64_t *code_dir, const uint32_t *ptab,
+                                    const uint8_t *gftab, hipStream_t s);
 
 // Bit-sliced encode kernels specialised at build time for hot (k,n) codes
 // (gen_bitslice.py -> gen/bitslice_codes.inc), or compiled at run time
