@@ -196,6 +196,9 @@ enum : int { kIdle = 0, kBusy = 1, kReady = 2, kFailed = 3 };
 
 struct Unit {  // one hipRTC program: one or more codes
     std::vector<std::pair<int, int>> codes;
+    // set by whoever compiles the unit: its worker thread, or a thread that
+    // waits for one of its codes before the worker got a compile slot
+    std::atomic<bool> claimed{false};
     std::vector<char> co;  // code object
     std::mutex mu;         // guards mod[]
     hipModule_t mod[kMaxDev] = {};
@@ -354,6 +357,21 @@ bool compile_unit(Unit &U, std::string &err) {
 
 constexpr int kMaxCompileThreads = 4;
 
+// Compiles U (the caller has claimed it) and publishes its codes' state.
+void compile_and_publish(Unit &U) {
+    Registry &R = reg();
+    std::string err;
+    const bool ok = compile_unit(U, err);
+    if (!ok && getenv("RSMI_RTC_VERBOSE")) fprintf(stderr, "rsmi: runtime bit-slice compile failed: %s\n", err.c_str());
+    std::lock_guard<std::mutex> lk(R.mu);
+    for (auto &c : U.codes) {
+        RtcCode *rc = R.table[c.first * 257 + c.second].load();
+        rc->err = err;
+        rc->state.store(ok ? kReady : kFailed);
+    }
+    R.cv.notify_all();
+}
+
 void worker(std::shared_ptr<Unit> U) {
     Registry &R = reg();
     {
@@ -369,17 +387,15 @@ void worker(std::shared_ptr<Unit> U) {
             R.cv.notify_all();
             return;
         }
+        if (U->claimed.exchange(true)) {  // a waiting thread compiled it
+            --R.inflight;
+            R.cv.notify_all();
+            return;
+        }
         ++R.running;
     }
-    std::string err;
-    const bool ok = compile_unit(*U, err);
-    if (!ok && getenv("RSMI_RTC_VERBOSE")) fprintf(stderr, "rsmi: runtime bit-slice compile failed: %s\n", err.c_str());
+    compile_and_publish(*U);
     std::lock_guard<std::mutex> lk(R.mu);
-    for (auto &c : U->codes) {
-        RtcCode *rc = R.table[c.first * 257 + c.second].load();
-        rc->err = err;
-        rc->state.store(ok ? kReady : kFailed);
-    }
     --R.running;
     --R.inflight;
     R.cv.notify_all();
@@ -446,9 +462,20 @@ void bitslice_rtc_request(const std::vector<std::pair<int, int>> &codes) {
     }
 }
 
-// Block until every listed code's compile has finished (ready or failed).
+// Block until every listed code's compile has finished (ready or failed).  A
+// code whose unit is still queued behind kMaxCompileThreads running compiles
+// is compiled on the calling thread instead of waiting its turn.
 void bitslice_rtc_wait(const std::vector<std::pair<int, int>> &codes) {
     Registry &R = reg();
+    for (auto &c : codes) {
+        std::shared_ptr<Unit> U;
+        {
+            std::lock_guard<std::mutex> lk(R.mu);
+            RtcCode *rc = R.table[c.first * 257 + c.second].load();
+            if (rc && rc->state.load() == kBusy) U = rc->unit;
+        }
+        if (U && !U->claimed.exchange(true)) compile_and_publish(*U);
+    }
     std::unique_lock<std::mutex> lk(R.mu);
     R.cv.wait(lk, [&] {
         for (auto &c : codes) {
