@@ -874,108 +874,119 @@ __global__ __launch_bounds__(256) void k_decode_ragged_big(
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const Tables T = load_tables(smem, ptab, gftab);
     uint8_t *sel = smem + kTabBytes, *miss = sel + 256, *aug = miss + 256;
-    __shared__ int s_e;
+    __shared__ int s_e, s_n;
+    __shared__ int64_t s_list[256];
     const int tid = threadIdx.x, lane = tid & 63;
-    __syncthreads();
-    for (int64_t g = blockIdx.x; g < ngroups; g += gridDim.x) {
-        if (status_out[g] != kDefer) continue;  // uniform per block
-        const rsmi_group d = groups[g];
-        const int k = d.k, n = d.n, len = (int)d.len;
-        const uint64_t ss = d.shard_stride;
-        uint8_t *gb = base + d.offset;
-        const uint8_t *rows = reinterpret_cast<const uint8_t *>(code_dir[k * 257 + n]);
-        const uint32_t *pw = present + g * 8;
-        if (tid < 64) {  // wave 0 selects (the one-wave kernel found >= k present)
-            const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
-            int cnt = 0, e = 0;
-            for (int b = 0; b < n && cnt < k; b += 64) {
-                const int idx = b + lane;
-                const bool f = idx < n && ((pw[idx >> 5] >> (idx & 31)) & 1u);
-                const uint64_t mk = __ballot(f);
-                const int rank = cnt + __popcll(mk & lt);
-                if (f && rank < k) sel[rank] = (uint8_t)idx;
-                cnt += __popcll(mk);
-            }
-            for (int b = 0; b < k; b += 64) {
-                const int idx = b + lane;
-                const bool ms = idx < k && !((pw[idx >> 5] >> (idx & 31)) & 1u);
-                const uint64_t mk = __ballot(ms);
-                if (ms) miss[e + __popcll(mk & lt)] = (uint8_t)idx;
-                e += __popcll(mk);
-            }
-            if (lane == 0) s_e = e;
-        }
+    // Each block takes 256 consecutive statuses at a time (one coalesced load)
+    // and works through the deferred ones among them: usually none, and a
+    // group-at-a-time scan cost a dependent load per group.
+    for (int64_t g0 = (int64_t)blockIdx.x * 256; g0 < ngroups; g0 += (int64_t)gridDim.x * 256) {
+        if (tid == 0) s_n = 0;
         __syncthreads();
-        const int e = s_e, W = e + k;
-        for (int t = tid; t < e * W; t += 256) {
-            const int r = t / W, c = t - r * W;
-            const int R = sel[k - e + r];
-            const uint8_t *pr = rows + (R - k) * k;
-            uint8_t v;
-            if (c < e) {
-                v = pr[miss[c]];
-            } else {
-                const int s = sel[c - e];
-                v = (s >= k) ? (uint8_t)(s == R) : pr[s];
-            }
-            aug[t] = v;
-        }
+        if (g0 + tid < ngroups && status_out[g0 + tid] == kDefer)
+            s_list[atomicAdd(&s_n, 1)] = g0 + tid;
         __syncthreads();
-        int st = RSMI_DEC_OK;
-        for (int p = 0; p < e; ++p) {
-            const uint32_t piv = aug[p * W + p];
-            if (piv == 0) {
-                st = RSMI_DEC_SINGULAR;
-                break;
-            }
-            const uint32_t ipiv = T.lexp[255 - T.llog[piv]];
-            for (int c = p + 1 + tid; c < W; c += 256)
-                aug[p * W + c] = (uint8_t)gmul(T.lexp, T.llog, ipiv, aug[p * W + c]);
-            __syncthreads();
-            const int cols = W - p - 1;
-            for (int t = tid; t < e * cols; t += 256) {
-                const int r = t / cols;
-                if (r == p) continue;
-                const int c = p + 1 + (t - r * cols);
-                const uint32_t f = aug[r * W + p];
-                if (f) aug[r * W + c] ^= (uint8_t)gmul(T.lexp, T.llog, f, aug[p * W + c]);
+        const int nlist = s_n;
+        for (int li = 0; li < nlist; ++li) {
+            const int64_t g = s_list[li];
+            const rsmi_group d = groups[g];
+            const int k = d.k, n = d.n, len = (int)d.len;
+            const uint64_t ss = d.shard_stride;
+            uint8_t *gb = base + d.offset;
+            const uint8_t *rows = reinterpret_cast<const uint8_t *>(code_dir[k * 257 + n]);
+            const uint32_t *pw = present + g * 8;
+            if (tid < 64) {  // wave 0 selects (the one-wave kernel found >= k present)
+                const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+                int cnt = 0, e = 0;
+                for (int b = 0; b < n && cnt < k; b += 64) {
+                    const int idx = b + lane;
+                    const bool f = idx < n && ((pw[idx >> 5] >> (idx & 31)) & 1u);
+                    const uint64_t mk = __ballot(f);
+                    const int rank = cnt + __popcll(mk & lt);
+                    if (f && rank < k) sel[rank] = (uint8_t)idx;
+                    cnt += __popcll(mk);
+                }
+                for (int b = 0; b < k; b += 64) {
+                    const int idx = b + lane;
+                    const bool ms = idx < k && !((pw[idx >> 5] >> (idx & 31)) & 1u);
+                    const uint64_t mk = __ballot(ms);
+                    if (ms) miss[e + __popcll(mk & lt)] = (uint8_t)idx;
+                    e += __popcll(mk);
+                }
+                if (lane == 0) s_e = e;
             }
             __syncthreads();
-        }
-        if (st == RSMI_DEC_OK) {
-            // coef[r][j] = aug[r][e + j]; rows in blocks of kBigRows, dwords per thread
-            const int words = (len + 3) >> 2;
-            for (int rb = 0; rb < e; rb += kBigRows) {
-                for (int w = tid; w < words; w += 256) {
-                    uint32_t acc[kBigRows];
-#pragma unroll
-                    for (int r = 0; r < kBigRows; ++r) acc[r] = 0;
-                    for (int j = 0; j < k; ++j) {
-                        const uint32_t x =
-                            *reinterpret_cast<const uint32_t *>(gb + sel[j] * ss + 4 * w);
-                        const uint32_t a0 = x & 0x07070707u, a1 = (x >> 3) & 0x07070707u,
-                                       a2 = (x >> 6) & 0x03030303u;
-#pragma unroll
-                        for (int r = 0; r < kBigRows; ++r) {
-                            if (rb + r < e) {
-                                const uint32_t c = aug[(rb + r) * W + e + j];
-                                const uint4 t = T.s01[c];
-                                const uint32_t t2 = T.s2[c];
-                                acc[r] ^= xor3(__builtin_amdgcn_perm(t.y, t.x, a0),
-                                               __builtin_amdgcn_perm(t.w, t.z, a1),
-                                               __builtin_amdgcn_perm(t2, t2, a2));
+            const int e = s_e, W = e + k;
+            for (int t = tid; t < e * W; t += 256) {
+                const int r = t / W, c = t - r * W;
+                const int R = sel[k - e + r];
+                const uint8_t *pr = rows + (R - k) * k;
+                uint8_t v;
+                if (c < e) {
+                    v = pr[miss[c]];
+                } else {
+                    const int s = sel[c - e];
+                    v = (s >= k) ? (uint8_t)(s == R) : pr[s];
+                }
+                aug[t] = v;
+            }
+            __syncthreads();
+            int st = RSMI_DEC_OK;
+            for (int p = 0; p < e; ++p) {
+                const uint32_t piv = aug[p * W + p];
+                if (piv == 0) {
+                    st = RSMI_DEC_SINGULAR;
+                    break;
+                }
+                const uint32_t ipiv = T.lexp[255 - T.llog[piv]];
+                for (int c = p + 1 + tid; c < W; c += 256)
+                    aug[p * W + c] = (uint8_t)gmul(T.lexp, T.llog, ipiv, aug[p * W + c]);
+                __syncthreads();
+                const int cols = W - p - 1;
+                for (int t = tid; t < e * cols; t += 256) {
+                    const int r = t / cols;
+                    if (r == p) continue;
+                    const int c = p + 1 + (t - r * cols);
+                    const uint32_t f = aug[r * W + p];
+                    if (f) aug[r * W + c] ^= (uint8_t)gmul(T.lexp, T.llog, f, aug[p * W + c]);
+                }
+                __syncthreads();
+            }
+            if (st == RSMI_DEC_OK) {
+                // coef[r][j] = aug[r][e + j]; rows in blocks of kBigRows, dwords per thread
+                const int words = (len + 3) >> 2;
+                for (int rb = 0; rb < e; rb += kBigRows) {
+                    for (int w = tid; w < words; w += 256) {
+                        uint32_t acc[kBigRows];
+    #pragma unroll
+                        for (int r = 0; r < kBigRows; ++r) acc[r] = 0;
+                        for (int j = 0; j < k; ++j) {
+                            const uint32_t x =
+                                *reinterpret_cast<const uint32_t *>(gb + sel[j] * ss + 4 * w);
+                            const uint32_t a0 = x & 0x07070707u, a1 = (x >> 3) & 0x07070707u,
+                                           a2 = (x >> 6) & 0x03030303u;
+    #pragma unroll
+                            for (int r = 0; r < kBigRows; ++r) {
+                                if (rb + r < e) {
+                                    const uint32_t c = aug[(rb + r) * W + e + j];
+                                    const uint4 t = T.s01[c];
+                                    const uint32_t t2 = T.s2[c];
+                                    acc[r] ^= xor3(__builtin_amdgcn_perm(t.y, t.x, a0),
+                                                   __builtin_amdgcn_perm(t.w, t.z, a1),
+                                                   __builtin_amdgcn_perm(t2, t2, a2));
+                                }
                             }
                         }
+    #pragma unroll
+                        for (int r = 0; r < kBigRows; ++r)
+                            if (rb + r < e)
+                                *reinterpret_cast<uint32_t *>(gb + miss[rb + r] * ss + 4 * w) = acc[r];
                     }
-#pragma unroll
-                    for (int r = 0; r < kBigRows; ++r)
-                        if (rb + r < e)
-                            *reinterpret_cast<uint32_t *>(gb + miss[rb + r] * ss + 4 * w) = acc[r];
                 }
             }
+            if (tid == 0) status_out[g] = st;
+            __syncthreads();  // sel / miss / aug are rewritten by the next group
         }
-        if (tid == 0) status_out[g] = st;
-        __syncthreads();  // sel / miss / aug are rewritten by the next group
     }
 }
 
@@ -1057,7 +1068,8 @@ hipError_t launch_decode_ragged_big(const rsmi_group *groups, int64_t ngroups, u
                                     const uint32_t *present_bits, int32_t *status,
                                     const uint64_t *code_dir, const uint32_t *ptab,
                                     const uint8_t *gftab, hipStream_t s) {
-    const int64_t bb = ngroups < 256 * 4 ? ngroups : 256 * 4;
+    int64_t bb = (ngroups + 255) / 256;
+    if (bb > 256 * 4) bb = 256 * 4;
     k_decode_ragged_big<<<(unsigned)bb, 256, kTabBytes + 512 + kBigAug, s>>>(
         groups, ngroups, base, present_bits, status, code_dir, ptab, gftab);
     return hipGetLastError();
