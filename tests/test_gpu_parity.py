@@ -448,6 +448,51 @@ def test_ragged_decode_vs_oracle_mixed(gpu, oracle):
         assert (got[k:] == org[k:]).all(), i  # parity slots untouched
 
 
+def test_ragged_plan_decode_graph_capture(gpu, oracle):
+    """A ragged plan decode forks its width classes over extra streams and joins
+    them back (event fork/join): it captures into a graph, and every replay
+    matches the oracle on the batch's current contents."""
+    import torch
+    import udpspeeder_amd as u
+    from udpspeeder_amd import synth
+    rng = np.random.default_rng(33)
+    G = 700
+    ks = rng.integers(1, 21, G)
+    ms = rng.integers(1, 11, G)
+    ls = rng.integers(1, 1300, G)  # all four tile widths
+    groups, total = u.make_groups(ks, ks + ms, ls)
+    flags = np.zeros((G, 256), np.uint8)
+    for i in range(G):
+        n = int(ks[i] + ms[i])
+        flags[i, :n] = 1
+        flags[i, rng.choice(n, min(5, int(ms[i])), replace=False)] = 0
+    plan = u.rs.RaggedPlan(groups, wait_codes=False)  # decode needs no encode networks
+    base = torch.zeros(total, dtype=torch.uint8, device=gpu)
+    bits = torch.from_numpy(synth.present_bits(flags).view(np.int32)).to(gpu)
+    st = torch.empty(G, dtype=torch.int32, device=gpu)
+    plan.decode(base, bits, status=st)  # warm-up outside capture
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        plan.decode(base, bits, status=st)
+    for seed in (4, 5):
+        host = np.random.default_rng(seed).integers(0, 256, total, dtype=np.uint8)
+        base.copy_(torch.from_numpy(host).to(gpu))
+        st.fill_(7)
+        g.replay()
+        torch.cuda.synchronize()
+        out = base.cpu().numpy()
+        sts = st.cpu().numpy()
+        for i in range(0, G, 7):
+            d = groups[i]
+            n, k = d.n, d.k
+            seg = host[d.offset:d.offset + n * d.shard_stride].copy()
+            ost = oracle.decode_batch(k, n, seg, 0, d.shard_stride, d.len, 1, flags[i:i + 1, :n])
+            assert sts[i] == ost[0], (seed, i)
+            got = out[d.offset:d.offset + n * d.shard_stride].reshape(n, d.shard_stride)
+            assert (got[:k, :d.len] == seg.reshape(n, d.shard_stride)[:k, :d.len]).all(), (seed, i)
+
+
 def test_ragged_decode_dev_unresident_code(gpu, oracle):
     """The device-descriptor form: resident codes decode, a code that was
     never made resident reports RSMI_DEC_UNSUPPORTED and is left alone."""

@@ -343,8 +343,14 @@ int decode_ragged_cls_dev(const rsmi_group *dg, int64_t ngroups, const uint32_t 
     int rc;
     Device *D = current(&rc);
     if (!D) return rc;
+    // Classes run one after another on s: forking them over four streams
+    // (event fork/join) measured slower, 0.240 vs 0.217 ms for C3.
+    const hipStream_t cs[4] = {s, s, s, s};
     hipError_t e = launch_decode_ragged_cls(dg, ngroups, cls_idx, cls_first, base, present_bits,
-                                            status, kmax, D->code_dir, D->ptab, D->gftab, s);
+                                            status, kmax, D->code_dir, D->ptab, D->gftab, s, cs);
+    if (e == hipSuccess)
+        e = launch_decode_ragged_big(dg, ngroups, base, present_bits, status, D->code_dir, D->ptab,
+                                     D->gftab, s);
     if (e != hipSuccess) return hip_fail(e, "ragged decode launch");
     return RSMI_OK;
 }

@@ -1040,7 +1040,7 @@ hipError_t launch_decode_ragged_cls(const rsmi_group *groups, int64_t ngroups,
                                     const uint32_t *cls_idx, const int64_t cls_first[5],
                                     uint8_t *base, const uint32_t *present_bits, int32_t *status,
                                     int kmax, const uint64_t *code_dir, const uint32_t *ptab,
-                                    const uint8_t *gftab, hipStream_t s) {
+                                    const uint8_t *gftab, hipStream_t s, const hipStream_t cs[4]) {
     if (ngroups <= 0) return hipSuccess;
     kmax = kmax < 1 ? 1 : (kmax > 32 ? 32 : kmax);  // larger k: the workgroup kernel
     const size_t lds = kTabBytes + (size_t)kWaves * rag_lds_bytes(kmax, kClsRows);
@@ -1050,7 +1050,7 @@ hipError_t launch_decode_ragged_cls(const rsmi_group *groups, int64_t ngroups,
         int64_t blocks = (count + kWaves - 1) / kWaves;
         const int64_t cap = 256 * (int64_t)occ;  // one round of resident blocks
         if (blocks > cap) blocks = cap;
-        kern<<<(unsigned)blocks, 64 * kWaves, lds, s>>>(groups, cls_idx + cls_first[c], count, base,
+        kern<<<(unsigned)blocks, 64 * kWaves, lds, cs[c]>>>(groups, cls_idx + cls_first[c], count, base,
                                                        present_bits, status, code_dir, ptab, gftab,
                                                        kmax);
         return hipGetLastError();
@@ -1059,9 +1059,7 @@ hipError_t launch_decode_ragged_cls(const rsmi_group *groups, int64_t ngroups,
     if (e == hipSuccess) e = launch(k_decode_ragged_cls<4, DEC_CLS_OCC4>, 2, DEC_CLS_OCC4);
     if (e == hipSuccess) e = launch(k_decode_ragged_cls<2, DEC_CLS_OCC2>, 1, DEC_CLS_OCC2);
     if (e == hipSuccess) e = launch(k_decode_ragged_cls<1, DEC_CLS_OCC1>, 0, DEC_CLS_OCC1);
-    if (e != hipSuccess) return e;
-    return launch_decode_ragged_big(groups, ngroups, base, present_bits, status, code_dir, ptab,
-                                    gftab, s);
+    return e;
 }
 
 hipError_t launch_decode_ragged_big(const rsmi_group *groups, int64_t ngroups, uint8_t *base,

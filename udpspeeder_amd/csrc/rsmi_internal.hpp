@@ -78,10 +78,17 @@ __host__ __device__ inline int rag_width(int lpad) {
 __host__ __device__ inline int rag_width_class(int w) { return w == 1 ? 0 : (w == 2 ? 1 : (w == 4 ? 2 : 3)); }
 // Plans: the groups sorted into the four width classes (cls_idx, class c's
 // groups at [cls_first[c], cls_first[c+1])), one register-cut kernel per class.
+// Class c runs on cs[c]; the caller orders cs[] against s and then runs
+// launch_decode_ragged_big on s.
 hipError_t launch_decode_ragged_cls(const rsmi_group *groups, int64_t ngroups,
                                     const uint32_t *cls_idx, const int64_t cls_first[5],
                                     uint8_t *base, const uint32_t *present_bits, int32_t *status,
                                     int kmax, const uint64_t *code_dir, const uint32_t *ptab,
+                                    const uint8_t *gftab, hipStream_t s, const hipStream_t cs[4]);
+// The workgroup-per-group kernel for the groups the one-wave kernels deferred.
+hipError_t launch_decode_ragged_big(const rsmi_group *groups, int64_t ngroups, uint8_t *base,
+                                    const uint32_t *present_bits, int32_t *status,
+                                    const uint64_t *code_dir, const uint32_t *ptab,
                                     const uint8_t *gftab, hipStream_t s);
 
 // Bit-sliced encode kernels specialised at build time for hot (k,n) codes
