@@ -1,7 +1,7 @@
 """Decode timing under different launch patterns (C1 encode + C2 decode, RS(20,10)):
 back-to-back steps as bench.py runs them, synchronised steps as ab_encode.py
 runs them, decode-only back-to-back, and the C2 worst case (5 data erasures
-per group) decode-only.  Prints per-pattern mean / median ms."""
+per group) decode-only, and encode-only.  Prints per-pattern mean / median ms."""
 import os, sys, statistics
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
@@ -25,7 +25,8 @@ def run(pattern, steps=30):
         if pattern not in ("dec_only", "worst"):
             u.encode(t, k, n, ln, stream=s)
         ev[i][1].record(s)
-        u.decode(t, worst if pattern == "worst" else pres, k, n, ln, status=st, stream=s)
+        if pattern != "enc_only":
+            u.decode(t, worst if pattern == "worst" else pres, k, n, ln, status=st, stream=s)
         ev[i][2].record(s)
         if pattern == "sync":
             torch.cuda.synchronize()
@@ -37,5 +38,6 @@ def run(pattern, steps=30):
           f"decode mean {statistics.mean(dec):.4f} med {statistics.median(dec):.4f}", flush=True)
 
 
-for p in ("b2b", "sync", "dec_only", "b2b", "worst"):
+for p in (sys.argv[1].split(",") if len(sys.argv) > 1 else
+          ("b2b", "sync", "dec_only", "b2b", "worst", "enc_only")):
     run(p)
