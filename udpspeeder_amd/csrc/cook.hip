@@ -42,6 +42,9 @@ constexpr int kPpl = 96 / kLpp;         // pieces per lane per round
 #ifndef COOK_OCC
 #define COOK_OCC (kLpp == 8 ? 4 : kLpp == 16 ? 5 : 6)  // waves per SIMD the register budget is cut for
 #endif
+#ifndef COOK_ABS_LDS
+#define COOK_ABS_LDS 1  // CRC tables addressed from LDS address 0 (see tab_byte)
+#endif
 #ifndef COOK_SB
 #define COOK_SB 1  // scheduling fence every COOK_SB pieces (0: none), bounds registers
 #endif
@@ -70,14 +73,30 @@ __device__ __forceinline__ void st_piece(uint8_t *p, u32x4 v) {
     *reinterpret_cast<u32x4_a4 *>(p) = v;
 }
 
+// Table word at word index w + byte b of x (b = 0..3): the tables sit at LDS
+// address 0 (the kernels' only LDS is the dynamic array, tables first), so the
+// address is ((x >> 8b) & 0xff) * 4 + 4w -- the table base goes into the
+// ds_read offset and the byte scale into one SDWA shift.  Through the generic
+// pointer LLVM added the array's base as a register: v_bfe + v_lshl_add per
+// lookup.
+#if COOK_ABS_LDS
+typedef const __attribute__((address_space(3))) uint32_t *lds_u32p;
+__device__ __forceinline__ uint32_t tab_byte(const uint32_t *, int w, uint32_t x, int b) {
+    return *(lds_u32p)(size_t)(4 * w + (((x >> (8 * b)) & 0xffu) << 2));
+}
+#else
+__device__ __forceinline__ uint32_t tab_byte(const uint32_t *T, int w, uint32_t x, int b) {
+    return T[w + ((x >> (8 * b)) & 0xffu)];
+}
+#endif
+
 // CRC register after 8 bytes (dwords a, b little-endian) from register c.
 __device__ __forceinline__ uint32_t slice8(const uint32_t *T, uint32_t c, uint32_t a, uint32_t b) {
     const uint32_t x = c ^ a;
-    uint32_t r = xor3(T[7 * 256 + (x & 0xff)], T[6 * 256 + ((x >> 8) & 0xff)],
-                      T[5 * 256 + ((x >> 16) & 0xff)]);
-    r = xor3(r, T[4 * 256 + (x >> 24)], T[3 * 256 + (b & 0xff)]);
-    r = xor3(r, T[2 * 256 + ((b >> 8) & 0xff)], T[256 + ((b >> 16) & 0xff)]);
-    return r ^ T[b >> 24];
+    uint32_t r = xor3(tab_byte(T, 7 * 256, x, 0), tab_byte(T, 6 * 256, x, 1), tab_byte(T, 5 * 256, x, 2));
+    r = xor3(r, tab_byte(T, 4 * 256, x, 3), tab_byte(T, 3 * 256, b, 0));
+    r = xor3(r, tab_byte(T, 2 * 256, b, 1), tab_byte(T, 256, b, 2));
+    return r ^ tab_byte(T, 0, b, 3);
 }
 
 // A linear map of the CRC register held as 8 nibble tables of 16 words.
@@ -171,9 +190,9 @@ __device__ __forceinline__ uint32_t crc16(const uint32_t *T, u32x4 v) {
 #else
 // Z_{16 kLpp} as four byte tables.
 __device__ __forceinline__ uint32_t zh(const uint32_t *T, uint32_t c) {
-    const uint32_t *B = T + kCookZH;
-    return xor3(B[c & 0xff], B[256 + ((c >> 8) & 0xff)], B[512 + ((c >> 16) & 0xff)]) ^
-           B[768 + (c >> 24)];
+    return xor3(tab_byte(T, kCookZH, c, 0), tab_byte(T, kCookZH + 256, c, 1),
+                tab_byte(T, kCookZH + 512, c, 2)) ^
+           tab_byte(T, kCookZH + 768, c, 3);
 }
 
 // Raw CRC of one 16-byte piece.
