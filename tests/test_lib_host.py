@@ -173,3 +173,35 @@ def test_fec_grammar_matches_reference(oracle):
         else:
             assert crc == 0 and cfg.rs_cnt == len(want), s
             assert [cfg.rs_y[i] for i in range(cfg.rs_cnt)] == [y for _, y in want], s
+
+
+# fec_decode's error path (lib/fec.cpp:851-856): the shuffle permutes the
+# caller's pkt/index arrays first, and an index >= n is only rejected afterwards
+# by build_decode_matrix (:809-816).  No GPU work happens on this path, so the
+# drop-in and the reference library (oracle/_ref, the checker) are compared here.
+@pytest.mark.parametrize("index", [[7, 0, 12, 1, 3], [3, 2, 1, 0, 40], [9, 4, 3, 2, 1],
+                                   [4, 3, 2, 1, 0], [1, 0, 3, 2, 200]])
+def test_fec_decode_invalid_index_permutes_like_reference(index):
+    import ctypes as C
+    from oracle.cpu import REF_SO
+    if not os.path.exists(REF_SO):
+        pytest.skip("oracle/_ref not built")
+    ref = C.CDLL(REF_SO)
+    ref._Z7fec_newii.restype = C.c_void_p
+    ref._Z7fec_newii.argtypes = [C.c_int, C.c_int]
+    ref._Z10fec_decodePvPS_Pii.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
+    k, n, ln = 5, 9, 8
+    if max(index) < n:
+        pytest.skip("valid indices reach the GPU")
+    bufs = [C.create_string_buffer(ln) for _ in range(k)]
+    arr = (C.c_void_p * k)(*[C.addressof(b) for b in bufs])
+    idx = (C.c_int * k)(*index)
+    rc_ref = ref._Z10fec_decodePvPS_Pii(ref._Z7fec_newii(k, n), arr, idx, ln)
+    ref_slots = [[C.addressof(b) for b in bufs].index(arr[i]) for i in range(k)]
+    pkt = [bytearray(ln) for _ in range(k)]
+    ours = list(pkt)
+    oidx = list(index)
+    rc = u.fec_decode(u.fec_new(k, n), ours, oidx, ln)
+    assert rc == rc_ref == 1
+    assert oidx == list(idx)
+    assert [next(i for i, b in enumerate(pkt) if b is p) for p in ours] == ref_slots

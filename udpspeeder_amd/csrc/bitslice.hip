@@ -120,6 +120,9 @@ hipError_t launch_encode_bitslice(const UniformArgs &a, hipStream_t s) {
         return hipErrorNotSupported;
     const int64_t chunks = (cols + 127) / 128;
     int64_t waves = chunks;
+#ifdef BS_CPW
+    waves = (chunks + BS_CPW - 1) / BS_CPW;  // measurement knob: chunks per wave
+#endif
 #if BS_PERSIST
     // balanced persistent grid: every resident wave slot takes ceil(chunks /
     // slots) chunks, and only as many waves run as that needs

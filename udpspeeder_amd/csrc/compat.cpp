@@ -58,12 +58,22 @@ int shuffle_slots(void **pkt, int *index, int k) {
 // buffers sitting in slots row < k after the shuffle (fec.cpp:872-877).
 int decode_packets(const CodeHandle *c, void **pkt, int *index, int sz) {
     const int k = c->k, n = c->n;
+    // A negative index would make the reference's shuffle read index[c < 0]
+    // (undefined); reject it before anything moves.
     for (int i = 0; i < k; ++i)
-        if (index[i] < 0 || index[i] >= n) {
+        if (index[i] < 0) {
             std::fprintf(stderr, "decode: invalid index %d (max %d)\n", index[i], n - 1);
             return 1;
         }
+    // The shuffle runs first, as in fec_decode (fec.cpp:851-856): an index >= n
+    // is only rejected afterwards by build_decode_matrix (fec.cpp:809-816), so
+    // on that error path the caller's arrays are left permuted the same way.
     if (shuffle_slots(pkt, index, k)) return 1;
+    for (int i = 0; i < k; ++i)
+        if (index[i] >= n) {
+            std::fprintf(stderr, "decode: invalid index %d (max %d)\n", index[i], n - 1);
+            return 1;
+        }
     std::vector<uint8_t> present((size_t)n, 0);
     std::vector<uint8_t *> shards((size_t)n, nullptr);
     for (int i = 0; i < k; ++i) {
