@@ -77,6 +77,52 @@ __global__ __launch_bounds__(256, 3) void shaped(uint8_t *dbase, uint8_t *pbase,
   }
 }
 
+
+// HALF = 1: one wave per 64 columns (each lane one 16-B piece): half the
+// footprint per wave.  SPLITK = 1: two waves per 128 columns, wave h reads data
+// rows 10h..10h+9 and writes parity rows 20+5h..20+5h+4.
+template <int HALF, int SPLITK>
+__global__ __launch_bounds__(256, 3) void shaped2(uint8_t *dbase, uint32_t cols, uint32_t dgs) {
+    const uint32_t bid = (blockIdx.x & 7u) * (gridDim.x >> 3) + (blockIdx.x >> 3);
+    const uint32_t w = bid * 4u + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t cpw = HALF ? 64u : 128u;
+    const uint32_t wave = SPLITK ? w >> 1 : w, h = SPLITK ? (w & 1u) : 0u;
+    if (wave * cpw >= cols) return;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t P = 80;
+    const uint32_t cfirst = wave * cpw, gfirst = cfirst / P;
+    auto rs = __builtin_amdgcn_make_buffer_rsrc(dbase + (uint64_t)gfirst * dgs, 0, 4 * dgs, 0x00020000);
+    uint32_t c0 = cfirst + lane, c1 = c0 + 64;
+    uint32_t g0 = c0 / P, g1 = c1 / P;
+    uint32_t d0 = c0 < cols ? (g0 - gfirst) * dgs + (c0 - g0 * P) * 16 : 0x80000000u;
+    uint32_t d1 = (!HALF && c1 < cols) ? (g1 - gfirst) * dgs + (c1 - g1 * P) * 16 : 0x80000000u;
+    const int J = SPLITK ? 10 : 20, I = SPLITK ? 5 : 10;
+    const uint32_t jo = h * 10 * 1280, io = 20 * 1280 + h * 5 * 1280;
+    u32x4 acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0};
+    u32x4 r0[4], r1[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        r0[q] = __builtin_amdgcn_raw_buffer_load_b128(rs, d0 + jo + q * 1280, 0, 2);
+        if (!HALF) r1[q] = __builtin_amdgcn_raw_buffer_load_b128(rs, d1 + jo + q * 1280, 0, 2);
+    }
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+        const int q = j % 4;
+        acc0 ^= r0[q];
+        if (!HALF) acc1 ^= r1[q];
+        if (j + 4 < J) {
+            r0[q] = __builtin_amdgcn_raw_buffer_load_b128(rs, d0 + jo + (j + 4) * 1280, 0, 2);
+            if (!HALF) r1[q] = __builtin_amdgcn_raw_buffer_load_b128(rs, d1 + jo + (j + 4) * 1280, 0, 2);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int i = 0; i < I; ++i) {
+        __builtin_amdgcn_raw_buffer_store_b128(acc0 + i, rs, d0 + io + i * 1280, 0, 2);
+        if (!HALF) __builtin_amdgcn_raw_buffer_store_b128(acc1 + i, rs, d1 + io + i * 1280, 0, 2);
+    }
+}
+
 template <class F>
 float time_ms(F f, int reps = 30) {
     hipEvent_t a, b;
@@ -144,6 +190,13 @@ int main() {
         SHAPEDC("inplace cpw14", 4, 2, 2, true, buf, 30 * 1280, 20 * 1280, cols, 14)
         // tail: exactly 13 and 12 rounds of 3072 wave slots (time scaled to 65536 groups);
         // COLS must stay <= G * 80: the buffer holds G groups
+        {
+            const uint32_t wv = cols / 64, bl = ((wv + 3) / 4 + 7) & ~7u;
+            report("inplace half-footprint (64 col)", time_ms([&] { shaped2<1, 0><<<bl, 256>>>(buf, cols, DGS); }));
+            const uint32_t wv2 = cols / 128 * 2, bl2 = ((wv2 + 3) / 4 + 7) & ~7u;
+            report("inplace split-k (2 waves/128 col)", time_ms([&] { shaped2<0, 1><<<bl2, 256>>>(buf, cols, DGS); }));
+            report("inplace ring4 nt xcd (again)", time_ms([&] { shaped<4, 2, 2, true><<<blocks, 256>>>(buf, buf, cols, DGS, 30 * 1280, 20 * 1280, blocks * 4); }));
+        }
         SHAPEDC("inplace 13 rounds", 4, 2, 2, true, buf, 30 * 1280, 20 * 1280, 3072u * 13 * 128, 1)
         SHAPEDC("inplace 12 rounds", 4, 2, 2, true, buf, 30 * 1280, 20 * 1280, 3072u * 12 * 128, 1)
     }

@@ -104,6 +104,34 @@ def test_encode_c1_full_sha(gpu, golden):
     assert h_p.hexdigest() == F["parity_sha256"]
 
 
+def _split_codes():
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "udpspeeder_amd", "csrc"))
+    import gen_bitslice as gb
+    return [c for c in gb.default_codes() if gb.split_ok(*c)]
+
+
+@pytest.mark.parametrize("k,n", _split_codes())
+def test_encode_split_k_codes(gpu, oracle, k, n):
+    """Every code with a split-k network (two waves per chunk, partial parities
+    swapped over LDS): odd lengths, a ragged last chunk, against the oracle."""
+    import udpspeeder_amd as u
+    for G, ln in ((41, 1250), (7, 333), (1, 16)):
+        S = stride_for(ln)
+        rng = np.random.default_rng(k * 257 + n + ln)
+        buf = rng.integers(0, 256, (G, n, S), dtype=np.uint8)
+        t = upload(buf, gpu)
+        u.encode(t, k, n, ln)
+        oracle.encode_batch(k, n, buf.reshape(-1), n * S, S, ln, G)
+        out = t.cpu().numpy()
+        assert (out[:, :, :ln] == buf[:, :, :ln]).all(), (G, ln)
+        pad = pad_end(ln, S)
+        assert (out[:, :, pad:] == buf[:, :, pad:]).all(), (G, ln)
+    from udpspeeder_amd._lib import ENC_BITSLICE
+    assert u.lib().rsmi_last_encoder() == ENC_BITSLICE
+
+
 @pytest.mark.parametrize("bitslice", [True, False])
 @pytest.mark.parametrize("k,n,ln", [(20, 30, 1250), (13, 21, 700), (1, 11, 64), (5, 15, 17)])
 def test_encode_paths_agree(gpu, oracle, bitslice, k, n, ln):

@@ -129,16 +129,33 @@ def emit_block(w0, ind, k, P, r0, r1):
     """One pass: load every input shard once, accumulate parity rows r0..r1-1."""
     def w(line):
         w0(ind + line)
-    nxor = 0
     for i in range(r0, r1):
         w("uint32_t " + ", ".join(f"o{i}_{u} = 0" for u in range(8)) + ";")
-    R = min(RING, k)
+    nxor = emit_shards(w, P, r0, r1, 0, k)
+    for i in range(r0, r1):
+        emit_store(w, k, i)
+    return nxor
+
+
+def emit_store(w, k, i):
+    w(f"{{")
+    w(f"    uint32_t q[8] = {{" + ", ".join(f"o{i}_{u}" for u in range(8)) + "};")
+    w(f"    bs_transpose8(q);")
+    w(f"    io.store({k + i}, q);")
+    w(f"}}")
+
+
+def emit_shards(w, P, r0, r1, j0, j1):
+    """Input shards j0..j1-1 through a RING-deep raw-load ring, accumulated into
+    parity rows r0..r1-1 (o<row>_<plane>, declared by the caller)."""
+    nxor = 0
+    R = min(RING, j1 - j0)
     w("uint32_t " + ", ".join(f"rb{r}[8]" for r in range(R)) + ";")
     for r in range(R):
-        w(f"io.load({r}, rb{r});")
-    for j in range(k):
+        w(f"io.load({j0 + r}, rb{r});")
+    for j in range(j0, j1):
         w(f"{{  // input shard {j}")
-        w(f"    uint32_t (&p)[8] = rb{j % R};")
+        w(f"    uint32_t (&p)[8] = rb{(j - j0) % R};")
         w(f"    bs_transpose8(p);")
         need_lo, need_hi = {}, {}
         terms = {}
@@ -173,9 +190,11 @@ def emit_block(w0, ind, k, P, r0, r1):
                 nxor += 1
                 names[mm] = nm
                 return nm
+
             for mask in sorted(needed, key=lambda x: bin(x).count("1")):
                 get(mask)
             return names
+
         lo_names = build(need_lo, 0, "l")
         hi_names = build(need_hi, 4, "h")
         for i in range(r0, r1):
@@ -190,17 +209,56 @@ def emit_block(w0, ind, k, P, r0, r1):
                 elif a or b:
                     w(f"    BS_ACC2({acc}, {a or b});")
                     nxor += 1
-        if j + R < k:
-            w(f"    io.load({j + R}, rb{j % R});")
+        if j + R < j1:
+            w(f"    io.load({j + R}, rb{(j - j0) % R});")
         w(f"}}")
         w(f"BS_SCHED_BARRIER();")
-    for i in range(r0, r1):
-        w(f"{{")
-        w(f"    uint32_t q[8] = {{" + ", ".join(f"o{i}_{u}" for u in range(8)) + "};")
-        w(f"    bs_transpose8(q);")
-        w(f"    io.store({k + i}, q);")
-        w(f"}}")
     return nxor
+
+
+# ---------------------------------------------------------------- split-k form
+# Two waves per 128-column chunk: wave h accumulates ALL m parity rows over its
+# half of the input shards (h = 0: shards 0..ka-1, h = 1: ka..k-1), hands the
+# partial sums of the partner's rows over LDS (x.send / x.sync / x.recv), adds
+# the partner's partials of its own rows, and stores those (h = 0: rows
+# 0..mh-1, h = 1: mh..m-1).  Each wave then touches half the shard rows of the
+# chunk: the chip's concurrent HBM footprint per wave halves
+# (scripts/probes/mix_probe.hip "split-k": 3 % faster access pattern).
+SPLIT_MAX_ROWS = 5  # rows handed over per wave: the kernel's LDS exchange is sized for this
+
+
+def split_ok(k: int, n: int) -> bool:
+    m = n - k
+    return k >= 10 and 2 <= m <= 2 * SPLIT_MAX_ROWS
+
+
+def emit_split(k: int, n: int):
+    m = n - k
+    P = enc_matrix(k, n)
+    ka, mh = (k + 1) // 2, (m + 1) // 2
+    L = [f"// RS(k={k}, n={n}) split-k: shards 0..{ka - 1} | {ka}..{k - 1}, rows 0..{mh - 1} | {mh}..{m - 1}",
+         "template <class IO, class XCH>",
+         f"__device__ __forceinline__ void bs_split_{k}_{n}(IO &io, uint32_t h, XCH &x) {{"]
+    nxor = 0
+    for h, (j0, j1), (own0, own1), (oth0, oth1) in (
+            (0, (0, ka), (0, mh), (mh, m)), (1, (ka, k), (mh, m), (0, mh))):
+        L.append("    if (h == 0) {" if h == 0 else "    } else {")
+
+        def w(line):
+            L.append("        " + line)
+        for i in range(m):
+            w("uint32_t " + ", ".join(f"o{i}_{u} = 0" for u in range(8)) + ";")
+        nxor += emit_shards(w, P, 0, m, j0, j1)
+        for r, i in enumerate(range(oth0, oth1)):
+            w(f"x.send({r}, " + ", ".join(f"o{i}_{u}" for u in range(8)) + ");")
+        w("x.sync();")
+        for r, i in enumerate(range(own0, own1)):
+            w(f"x.recv({r}, " + ", ".join(f"o{i}_{u}" for u in range(8)) + ");")
+        for i in range(own0, own1):
+            emit_store(w, k, i)
+    L.append("    }")
+    L.append(f"}}  // {nxor} XOR ops + {8 * m} exchange XORs")
+    return "\n".join(L), nxor
 
 
 def default_codes():
@@ -254,6 +312,13 @@ def main():
         stats.append((k, n, nx))
     parts.append("#define BS_FOR_EACH_CODE(X) \\")
     parts.append(" \\\n".join(f"    X({k}, {n})" for (k, n) in codes))
+    split = [(k, n) for (k, n) in codes if split_ok(k, n)]
+    parts.append("#ifdef __HIPCC__  // device-only: the split form synchronises a wave pair")
+    for (k, n) in split:
+        parts.append(emit_split(k, n)[0])
+    parts.append("#define BS_FOR_EACH_SPLIT(X) \\")
+    parts.append(" \\\n".join(f"    X({k}, {n})" for (k, n) in split))
+    parts.append("#endif")
     parts.append("")
     txt = "\n".join(parts) + "\n"
     if os.path.exists(args.out) and open(args.out).read() == txt:
