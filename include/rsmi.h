@@ -129,6 +129,11 @@ int rsmi_precompile_code(int k, int n);
  * RSMI_ERR_INVALID. */
 int64_t rsmi_bitslice_source(int k, int n, char *buf, int64_t cap);
 
+/* The two-wave split-k form of the same network (bs_split_<k>_<n>, codes with
+ * k >= 10 and 2 <= n-k <= 10; identical to gen_bitslice.emit_split's text),
+ * same buffer convention; RSMI_ERR_INVALID for codes without one. */
+int64_t rsmi_bitslice_split_source(int k, int n, char *buf, int64_t cap);
+
 /* Make (k,n) resident and pre-size the decode workspace that calls on
  * `stream` use, for up to `ngroups` groups (needed before graph capture). */
 int rsmi_reserve(int k, int n, int64_t ngroups, void *stream);

@@ -81,12 +81,12 @@ __global__ __launch_bounds__(256, 3) void shaped(uint8_t *dbase, uint8_t *pbase,
 // HALF = 1: one wave per 64 columns (each lane one 16-B piece): half the
 // footprint per wave.  SPLITK = 1: two waves per 128 columns, wave h reads data
 // rows 10h..10h+9 and writes parity rows 20+5h..20+5h+4.
-template <int HALF, int SPLITK>
+template <int HALF, int SPLITK, int NS = 2>
 __global__ __launch_bounds__(256, 3) void shaped2(uint8_t *dbase, uint32_t cols, uint32_t dgs) {
     const uint32_t bid = (blockIdx.x & 7u) * (gridDim.x >> 3) + (blockIdx.x >> 3);
     const uint32_t w = bid * 4u + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t cpw = HALF ? 64u : 128u;
-    const uint32_t wave = SPLITK ? w >> 1 : w, h = SPLITK ? (w & 1u) : 0u;
+    const uint32_t wave = SPLITK ? w / NS : w, h = SPLITK ? (w % NS) : 0u;
     if (wave * cpw >= cols) return;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t P = 80;
@@ -96,8 +96,8 @@ __global__ __launch_bounds__(256, 3) void shaped2(uint8_t *dbase, uint32_t cols,
     uint32_t g0 = c0 / P, g1 = c1 / P;
     uint32_t d0 = c0 < cols ? (g0 - gfirst) * dgs + (c0 - g0 * P) * 16 : 0x80000000u;
     uint32_t d1 = (!HALF && c1 < cols) ? (g1 - gfirst) * dgs + (c1 - g1 * P) * 16 : 0x80000000u;
-    const int J = SPLITK ? 10 : 20, I = SPLITK ? 5 : 10;
-    const uint32_t jo = h * 10 * 1280, io = 20 * 1280 + h * 5 * 1280;
+    const int J = SPLITK ? 20 / NS : 20, I = SPLITK ? (NS == 4 ? (h < 2 ? 3 : 2) : 5) : 10;
+    const uint32_t jo = h * (20 / NS) * 1280, io = 20 * 1280 + (NS == 4 ? (h < 2 ? 3 * h : 6 + 2 * (h - 2)) : h * 5) * 1280;
     u32x4 acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0};
     u32x4 r0[4], r1[4];
 #pragma unroll
@@ -195,6 +195,8 @@ int main() {
             report("inplace half-footprint (64 col)", time_ms([&] { shaped2<1, 0><<<bl, 256>>>(buf, cols, DGS); }));
             const uint32_t wv2 = cols / 128 * 2, bl2 = ((wv2 + 3) / 4 + 7) & ~7u;
             report("inplace split-k (2 waves/128 col)", time_ms([&] { shaped2<0, 1><<<bl2, 256>>>(buf, cols, DGS); }));
+            const uint32_t wv4 = cols / 128 * 4, bl4 = ((wv4 + 3) / 4 + 7) & ~7u;
+            report("inplace split-4 (4 waves/128 col)", time_ms([&] { shaped2<0, 1, 4><<<bl4, 256>>>(buf, cols, DGS); }));
             report("inplace ring4 nt xcd (again)", time_ms([&] { shaped<4, 2, 2, true><<<blocks, 256>>>(buf, buf, cols, DGS, 30 * 1280, 20 * 1280, blocks * 4); }));
         }
         SHAPEDC("inplace 13 rounds", 4, 2, 2, true, buf, 30 * 1280, 20 * 1280, 3072u * 13 * 128, 1)

@@ -42,6 +42,20 @@ def test_emitters_agree(u, kn):
     assert u.bitslice_source(*kn) == gen_bitslice.emit_code(*kn)[0]
 
 
+@pytest.mark.parametrize("kn", [(10, 15), (20, 30), (10, 12), (13, 23), (40, 50), (31, 36)])
+def test_split_emitters_agree(u, kn):
+    assert gen_bitslice.split_ok(*kn)
+    assert u.bitslice_source(*kn, split=True) == gen_bitslice.emit_split(*kn)[0]
+
+
+def test_split_eligibility(u):
+    from udpspeeder_amd._lib import RsmiError
+    for kn in [(9, 15), (10, 11), (10, 21), (20, 31)]:
+        assert not gen_bitslice.split_ok(*kn)
+        with pytest.raises(RsmiError):
+            u.bitslice_source(*kn, split=True)
+
+
 def test_row_blocks():
     assert gen_bitslice.row_blocks(10) == [(0, 10)]
     assert gen_bitslice.row_blocks(11) == [(0, 6), (6, 11)]
@@ -131,7 +145,7 @@ def test_precompile_rejects(u):
 
 # ---------------------------------------------------------------- GPU
 GPU_CASES = [(10, 15, 1250), (10, 15, 17), (10, 40, 1250), (5, 17, 333), (7, 9, 4000),
-             (40, 60, 1280), (1, 2, 1), (2, 200, 100)]
+             (40, 60, 1280), (1, 2, 1), (2, 200, 100), (12, 20, 1250), (31, 36, 777)]
 
 
 @pytest.mark.gpu

@@ -94,6 +94,7 @@ def _bind(lib: C.CDLL) -> C.CDLL:
         "rsmi_wait_code": ([i32, i32], i32),
         "rsmi_precompile_code": ([i32, i32], i32),
         "rsmi_bitslice_source": ([i32, i32, C.c_char_p, i64], i64),
+        "rsmi_bitslice_split_source": ([i32, i32, C.c_char_p, i64], i64),
         "rsmi_encode_dev": ([i32, i32, vp, i64, i64, i32, i64, vp], i32),
         "rsmi_decode_dev": ([i32, i32, vp, i64, i64, i32, i64, vp, vp, vp], i32),
         "rsmi_encode_ragged": ([vp, i64, vp, vp], i32),

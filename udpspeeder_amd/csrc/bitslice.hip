@@ -35,46 +35,7 @@ namespace {
 BS_FOR_EACH_CODE(BS_KERNEL)
 #undef BS_KERNEL
 
-// ---- split-k form (gen_bitslice.py emit_split) ------------------------------
-// A 2-wave workgroup per 128-column chunk: wave h reads half of the data
-// shards, the two waves swap the partial sums of each other's parity rows
-// through LDS, and each stores half of the rows.  Partials go out as two
-// 16-byte writes per lane per row (a wave writes 1 KiB contiguous per
-// instruction: conflict-free).
-struct BsXch {
-    bs_u32x4 (*out)[64];
-    const bs_u32x4 (*in)[64];
-    __device__ __forceinline__ void send(int r, uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3,
-                                         uint32_t a4, uint32_t a5, uint32_t a6, uint32_t a7) const {
-        const uint32_t lane = threadIdx.x & 63u;
-        out[2 * r][lane] = bs_u32x4{a0, a1, a2, a3};
-        out[2 * r + 1][lane] = bs_u32x4{a4, a5, a6, a7};
-    }
-    __device__ __forceinline__ void sync() const { __syncthreads(); }
-    __device__ __forceinline__ void recv(int r, uint32_t &a0, uint32_t &a1, uint32_t &a2, uint32_t &a3,
-                                         uint32_t &a4, uint32_t &a5, uint32_t &a6, uint32_t &a7) const {
-        const uint32_t lane = threadIdx.x & 63u;
-        const bs_u32x4 x = in[2 * r][lane], y = in[2 * r + 1][lane];
-        a0 ^= x.x; a1 ^= x.y; a2 ^= x.z; a3 ^= x.w;
-        a4 ^= y.x; a5 ^= y.y; a6 ^= y.z; a7 ^= y.w;
-    }
-};
-
-// Block b (XCD-contiguous order as BS_DEFINE_UNIFORM) = chunk b; both waves of
-// a block leave together past the last chunk, so the barrier always pairs up.
-#define BS_DEFINE_SPLIT(NAME, FN, OCC)                                                           \
-    __global__ __launch_bounds__(128, OCC) void NAME(uint8_t *base, int64_t group_stride,       \
-                                                        int64_t shard_stride, uint32_t cols,     \
-                                                        uint32_t P) {                            \
-        __shared__ bs_u32x4 xch[2][2 * 5][64];                                                   \
-        const uint32_t bid = BS_XCD ? (blockIdx.x & 7u) * (gridDim.x >> 3) + (blockIdx.x >> 3)   \
-                                    : blockIdx.x;                                                \
-        if (bid * 128u >= cols) return;                                                          \
-        const uint32_t h = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);                     \
-        DevIO io = bs_make_io(base, group_stride, shard_stride, cols, P, bid);                  \
-        BsXch x{xch[h], xch[h ^ 1u]};                                                            \
-        FN(io, h, x);                                                                            \
-    }
+// ---- split-k form: BsXch and BS_DEFINE_SPLIT in bitslice_kern.hpp ----------
 #define BS_SPLIT_KERNEL(K, N) BS_DEFINE_SPLIT(k_bs2_##K##_##N, bs_split_##K##_##N, BS_OCC)
 BS_FOR_EACH_SPLIT(BS_SPLIT_KERNEL)
 #undef BS_SPLIT_KERNEL
@@ -128,7 +89,7 @@ hipError_t launch_encode_bitslice_ragged_rtc(int k, int n, const rsmi_group *gro
                                              uint32_t nwaves, uint8_t *base, uint32_t bytes,
                                              hipStream_t s) {
     if (nwaves == 0) return hipSuccess;
-    hipFunction_t f = bitslice_rtc_function(k, n, true);
+    hipFunction_t f = bitslice_rtc_function(k, n, kRtcRagged);
     if (!f) return hipErrorNotSupported;
     const BsGroup *g = reinterpret_cast<const BsGroup *>(groups);
     void *args[] = {&g, &colmap, &waves, &nwaves, &base, &bytes};
@@ -149,7 +110,7 @@ bool has_bitslice(int k, int n) {
 hipError_t launch_encode_bitslice(const UniformArgs &a, hipStream_t s) {
     hipFunction_t rtc = nullptr;
     if (!has_bitslice(a.k, a.n)) {
-        rtc = bitslice_rtc_function(a.k, a.n, false);
+        rtc = bitslice_rtc_function(a.k, a.n, kRtcUniform);
         if (!rtc) return hipErrorNotSupported;
     }
     // Columns per group: whole 128-B lines when the slot has room (measured
@@ -190,6 +151,16 @@ hipError_t launch_encode_bitslice(const UniformArgs &a, hipStream_t s) {
     uint8_t *base = a.base;
     int64_t gs = a.group_stride, ss = a.shard_stride;
     uint32_t ucols = (uint32_t)cols, uP = (uint32_t)P, wstep = (uint32_t)(blocks * 4);
+    if (BS_SPLIT && rtc) {
+        hipFunction_t f2 = bitslice_rtc_function(a.k, a.n, kRtcSplit);
+        if (f2) {
+            int64_t sblocks = chunks;
+            if (BS_XCD) sblocks = (sblocks + 7) & ~int64_t(7);
+            if (sblocks > 0x7fffffff) return hipErrorNotSupported;
+            void *args[] = {&base, &gs, &ss, &ucols, &uP};
+            return hipModuleLaunchKernel(f2, (unsigned)sblocks, 1, 1, 128, 1, 1, 0, s, args, nullptr);
+        }
+    }
     if (BS_SPLIT && !rtc) {
         // one 2-wave block per chunk
         int64_t sblocks = chunks;

@@ -193,3 +193,46 @@ __device__ __forceinline__ bool bs_rag_setup(const BsGroup *groups, const uint32
         if (!bs_rag_setup(groups, colmap, waves, nwaves, base, bytes, io, code)) return;         \
         FN(io);                                                                                  \
     }
+
+#if defined(__HIPCC__) || defined(__HIPCC_RTC__)
+// ---- split-k form (gen_bitslice.py emit_split) --------------------------------
+// A 2-wave workgroup per 128-column chunk: wave h reads half of the data
+// shards, the two waves swap the partial sums of each other's parity rows
+// through LDS, and each stores half of the rows.  Partials go out as two
+// 16-byte writes per lane per row (a wave writes 1 KiB contiguous per
+// instruction: conflict-free).
+struct BsXch {
+    bs_u32x4 (*out)[64];
+    const bs_u32x4 (*in)[64];
+    __device__ __forceinline__ void send(int r, uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3,
+                                         uint32_t a4, uint32_t a5, uint32_t a6, uint32_t a7) const {
+        const uint32_t lane = threadIdx.x & 63u;
+        out[2 * r][lane] = bs_u32x4{a0, a1, a2, a3};
+        out[2 * r + 1][lane] = bs_u32x4{a4, a5, a6, a7};
+    }
+    __device__ __forceinline__ void sync() const { __syncthreads(); }
+    __device__ __forceinline__ void recv(int r, uint32_t &a0, uint32_t &a1, uint32_t &a2, uint32_t &a3,
+                                         uint32_t &a4, uint32_t &a5, uint32_t &a6, uint32_t &a7) const {
+        const uint32_t lane = threadIdx.x & 63u;
+        const bs_u32x4 x = in[2 * r][lane], y = in[2 * r + 1][lane];
+        a0 ^= x.x; a1 ^= x.y; a2 ^= x.z; a3 ^= x.w;
+        a4 ^= y.x; a5 ^= y.y; a6 ^= y.z; a7 ^= y.w;
+    }
+};
+
+// Block b (XCD-contiguous order as BS_DEFINE_UNIFORM) = chunk b; both waves of
+// a block leave together past the last chunk, so the barrier always pairs up.
+#define BS_DEFINE_SPLIT(NAME, FN, OCC)                                                           \
+    __global__ __launch_bounds__(128, OCC) void NAME(uint8_t *base, int64_t group_stride,       \
+                                                        int64_t shard_stride, uint32_t cols,     \
+                                                        uint32_t P) {                            \
+        __shared__ bs_u32x4 xch[2][2 * 5][64];                                                   \
+        const uint32_t bid = BS_XCD ? (blockIdx.x & 7u) * (gridDim.x >> 3) + (blockIdx.x >> 3)   \
+                                    : blockIdx.x;                                                \
+        if (bid * 128u >= cols) return;                                                          \
+        const uint32_t h = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);                     \
+        DevIO io = bs_make_io(base, group_stride, shard_stride, cols, P, bid);                  \
+        BsXch x{xch[h], xch[h ^ 1u]};                                                            \
+        FN(io, h, x);                                                                            \
+    }
+#endif

@@ -45,6 +45,7 @@ namespace {
 
 constexpr int kMaxRows = 10;  // gen_bitslice.MAX_ROWS
 constexpr int kRing = 4;      // gen_bitslice.RING
+constexpr int kSplitRows = 5;  // gen_bitslice.SPLIT_MAX_ROWS
 constexpr int kMaxDev = 64;
 
 // ---------------------------------------------------------------- emitter
@@ -74,24 +75,21 @@ void bit_rows(uint8_t c, int lo[8], int hi[8]) {
 
 std::string S(long v) { return std::to_string(v); }
 
-void emit_block(Emitter &E, const std::string &ind, int k, const uint8_t *par, int r0, int r1) {
-    auto w = [&](const std::string &s) { E.line(ind, s); };
-    for (int i = r0; i < r1; ++i) {
-        std::string s = "uint32_t ";
-        for (int u = 0; u < 8; ++u) s += (u ? ", o" : "o") + S(i) + "_" + S(u) + " = 0";
-        w(s + ";");
-    }
-    const int R = std::min(kRing, k);
+// Input shards j0..j1-1 through the raw-load ring into parity rows r0..r1-1
+// (gen_bitslice.emit_shards).
+template <class Wf>
+void emit_shards(Emitter &E, Wf &w, int k, const uint8_t *par, int r0, int r1, int j0, int j1) {
+    const int R = std::min(kRing, j1 - j0);
     {
         std::string s = "uint32_t ";
         for (int r = 0; r < R; ++r) s += (r ? ", rb" : "rb") + S(r) + "[8]";
         w(s + ";");
     }
-    for (int r = 0; r < R; ++r) w("io.load(" + S(r) + ", rb" + S(r) + ");");
+    for (int r = 0; r < R; ++r) w("io.load(" + S(j0 + r) + ", rb" + S(r) + ");");
     std::vector<int> tlo((size_t)(r1 - r0) * 8), thi((size_t)(r1 - r0) * 8);
-    for (int j = 0; j < k; ++j) {
+    for (int j = j0; j < j1; ++j) {
         w("{  // input shard " + S(j));
-        w("    uint32_t (&p)[8] = rb" + S(j % R) + ";");
+        w("    uint32_t (&p)[8] = rb" + S((j - j0) % R) + ";");
         w("    bs_transpose8(p);");
         std::vector<int> need_lo, need_hi;  // first-seen order (Python dict)
         bool seen_lo[16] = {}, seen_hi[16] = {};
@@ -140,19 +138,41 @@ void emit_block(Emitter &E, const std::string &ind, int k, const uint8_t *par, i
                     E.nxor += 1;
                 }
             }
-        if (j + R < k) w("    io.load(" + S(j + R) + ", rb" + S(j % R) + ");");
+        if (j + R < j1) w("    io.load(" + S(j + R) + ", rb" + S((j - j0) % R) + ");");
         w("}");
         w("BS_SCHED_BARRIER();");
     }
+}
+
+std::string row_list(int i) {
+    std::string s;
+    for (int u = 0; u < 8; ++u) s += (u ? ", o" : "o") + S(i) + "_" + S(u);
+    return s;
+}
+
+template <class Wf>
+void emit_acc_decl(Wf &w, int r0, int r1) {
     for (int i = r0; i < r1; ++i) {
-        w("{");
-        std::string q = "    uint32_t q[8] = {";
-        for (int u = 0; u < 8; ++u) q += (u ? ", o" : "o") + S(i) + "_" + S(u);
-        w(q + "};");
-        w("    bs_transpose8(q);");
-        w("    io.store(" + S(k + i) + ", q);");
-        w("}");
+        std::string s = "uint32_t ";
+        for (int u = 0; u < 8; ++u) s += (u ? ", o" : "o") + S(i) + "_" + S(u) + " = 0";
+        w(s + ";");
     }
+}
+
+template <class Wf>
+void emit_store(Wf &w, int k, int i) {
+    w("{");
+    w("    uint32_t q[8] = {" + row_list(i) + "};");
+    w("    bs_transpose8(q);");
+    w("    io.store(" + S(k + i) + ", q);");
+    w("}");
+}
+
+void emit_block(Emitter &E, const std::string &ind, int k, const uint8_t *par, int r0, int r1) {
+    auto w = [&](const std::string &s) { E.line(ind, s); };
+    emit_acc_decl(w, r0, r1);
+    emit_shards(E, w, k, par, r0, r1, 0, k);
+    for (int i = r0; i < r1; ++i) emit_store(w, k, i);
 }
 
 }  // namespace
@@ -189,6 +209,43 @@ bool bitslice_emit(int k, int n, std::string &src, int *nxor) {
     return true;
 }
 
+// gen_bitslice.split_ok: codes that get the two-wave split-k form
+bool bitslice_split_ok(int k, int n) {
+    const int m = n - k;
+    return k >= 10 && m >= 2 && m <= 2 * kSplitRows;
+}
+
+// Text of bs_split_<k>_<n> exactly as gen_bitslice.emit_split prints it.
+bool bitslice_emit_split(int k, int n, std::string &src) {
+    std::vector<uint8_t> enc;
+    if (!bitslice_split_ok(k, n) || !build_enc_matrix(k, n, enc)) return false;
+    const int m = n - k, ka = (k + 1) / 2, mh = (m + 1) / 2;
+    const uint8_t *par = enc.data() + (size_t)k * k;
+    Emitter E;
+    E.line("", "// RS(k=" + S(k) + ", n=" + S(n) + ") split-k: shards 0.." + S(ka - 1) + " | " +
+                   S(ka) + ".." + S(k - 1) + ", rows 0.." + S(mh - 1) + " | " + S(mh) + ".." +
+                   S(m - 1));
+    E.line("", "template <class IO, class XCH>");
+    E.line("", "__device__ __forceinline__ void bs_split_" + S(k) + "_" + S(n) +
+                   "(IO &io, uint32_t h, XCH &x) {");
+    for (int h = 0; h < 2; ++h) {
+        const int j0 = h ? ka : 0, j1 = h ? k : ka;
+        const int own0 = h ? mh : 0, own1 = h ? m : mh, oth0 = h ? 0 : mh, oth1 = h ? mh : m;
+        E.line("", h == 0 ? "    if (h == 0) {" : "    } else {");
+        auto w = [&](const std::string &s) { E.line("        ", s); };
+        emit_acc_decl(w, 0, m);
+        emit_shards(E, w, k, par, 0, m, j0, j1);
+        for (int i = oth0; i < oth1; ++i) w("x.send(" + S(i - oth0) + ", " + row_list(i) + ");");
+        w("x.sync();");
+        for (int i = own0; i < own1; ++i) w("x.recv(" + S(i - own0) + ", " + row_list(i) + ");");
+        for (int i = own0; i < own1; ++i) emit_store(w, k, i);
+    }
+    E.line("", "    }");
+    E.line("", "}  // " + S(E.nxor) + " XOR ops + " + S(8 * m) + " exchange XORs");
+    src.swap(E.out);
+    return true;
+}
+
 namespace {
 
 // ---------------------------------------------------------------- registry
@@ -209,11 +266,12 @@ struct RtcCode {
     std::atomic<int> state{kIdle};
     std::shared_ptr<Unit> unit;
     std::string err;
-    std::atomic<hipFunction_t> fu[kMaxDev], fr[kMaxDev];
+    std::atomic<hipFunction_t> fu[kMaxDev], fr[kMaxDev], fs[kMaxDev];
     RtcCode() {
         for (int d = 0; d < kMaxDev; ++d) {
             fu[d].store(nullptr);
             fr[d].store(nullptr);
+            fs[d].store(nullptr);
         }
     }
 };
@@ -306,6 +364,10 @@ std::string unit_source(const Unit &U) {
              ")\n";
         s += "extern \"C\" BS_DEFINE_RAGGED_ONE(rsmi_bs_r_" + kn + ", bs_code_" + kn + ", " + occ +
              ")\n";
+        if (bitslice_emit_split(c.first, c.second, src)) {
+            s += src;
+            s += "\nextern \"C\" BS_DEFINE_SPLIT(rsmi_bs_s_" + kn + ", bs_split_" + kn + ", 3)\n";
+        }
     }
     return s;
 }
@@ -494,13 +556,15 @@ int bitslice_rtc_state(int k, int n) {
 
 // The compiled kernel for (k,n) on the current device (module loaded on first
 // use), or nullptr while the code is not ready.
-hipFunction_t bitslice_rtc_function(int k, int n, bool ragged) {
+hipFunction_t bitslice_rtc_function(int k, int n, RtcKind kind) {
     if (k < 1 || n > 256 || k >= n) return nullptr;
+    if (kind == kRtcSplit && !bitslice_split_ok(k, n)) return nullptr;
     RtcCode *rc = reg().table[k * 257 + n].load();
     if (!rc || rc->state.load(std::memory_order_acquire) != kReady) return nullptr;
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) return nullptr;
-    hipFunction_t f = (ragged ? rc->fr : rc->fu)[dev].load(std::memory_order_acquire);
+    std::atomic<hipFunction_t> *slot = kind == kRtcRagged ? rc->fr : (kind == kRtcSplit ? rc->fs : rc->fu);
+    hipFunction_t f = slot[dev].load(std::memory_order_acquire);
     if (f) return f;
     Unit &U = *rc->unit;
     std::lock_guard<std::mutex> lk(U.mu);
@@ -511,15 +575,18 @@ hipFunction_t bitslice_rtc_function(int k, int n, bool ragged) {
         return nullptr;
     }
     const std::string kn = S(k) + "_" + S(n);
-    hipFunction_t fu = nullptr, fr = nullptr;
+    hipFunction_t fu = nullptr, fr = nullptr, fs = nullptr;
     if (hipModuleGetFunction(&fu, U.mod[dev], ("rsmi_bs_u_" + kn).c_str()) != hipSuccess ||
-        hipModuleGetFunction(&fr, U.mod[dev], ("rsmi_bs_r_" + kn).c_str()) != hipSuccess) {
+        hipModuleGetFunction(&fr, U.mod[dev], ("rsmi_bs_r_" + kn).c_str()) != hipSuccess ||
+        (bitslice_split_ok(k, n) &&
+         hipModuleGetFunction(&fs, U.mod[dev], ("rsmi_bs_s_" + kn).c_str()) != hipSuccess)) {
         U.load_failed[dev] = true;
         return nullptr;
     }
     rc->fu[dev].store(fu, std::memory_order_release);
     rc->fr[dev].store(fr, std::memory_order_release);
-    return ragged ? fr : fu;
+    rc->fs[dev].store(fs, std::memory_order_release);
+    return kind == kRtcRagged ? fr : (kind == kRtcSplit ? fs : fu);
 }
 
 std::string bitslice_rtc_error(int k, int n) {
@@ -539,7 +606,7 @@ extern "C" int rsmi_wait_code(int k, int n) {
     if (rc) return rc;
     rsmi::bitslice_rtc_wait({{k, n}});
     // load the module on this device now, so a later graph capture never does
-    if (rsmi::bitslice_rtc_state(k, n) == rsmi::kReady) (void)rsmi::bitslice_rtc_function(k, n, false);
+    if (rsmi::bitslice_rtc_state(k, n) == rsmi::kReady) (void)rsmi::bitslice_rtc_function(k, n, rsmi::kRtcUniform);
     return RSMI_OK;
 }
 
@@ -576,6 +643,17 @@ extern "C" int64_t rsmi_bitslice_source(int k, int n, char *buf, int64_t cap) {
         const size_t c = std::min<size_t>((size_t)cap - 1, s.size());
         memcpy(buf, s.data(), c);
         buf[c] = '\0';
+    }
+    return (int64_t)s.size();
+}
+
+extern "C" int64_t rsmi_bitslice_split_source(int k, int n, char *buf, int64_t cap) {
+    std::string s;
+    if (k < 1 || n <= k || n > 256 || !rsmi::bitslice_emit_split(k, n, s)) return RSMI_ERR_INVALID;
+    if (buf && cap > 0) {
+        const size_t c = std::min((size_t)(cap - 1), s.size());
+        std::memcpy(buf, s.data(), c);
+        buf[c] = 0;
     }
     return (int64_t)s.size();
 }

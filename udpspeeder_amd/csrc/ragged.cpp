@@ -116,7 +116,7 @@ extern "C" int rsmi_ragged_plan_create(const rsmi_group *g, int64_t ngroups,
     // compiles; the plan takes the bit-sliced path only if every one is ready
     // now (rsmi_wait_code first to be sure) and never waits for them itself
     for (auto &c : rtc_codes)
-        if (bs && !rsmi::bitslice_rtc_function(c.first, c.second, true)) bs = false;
+        if (bs && !rsmi::bitslice_rtc_function(c.first, c.second, rsmi::kRtcRagged)) bs = false;
 
     rsmi_ragged_plan *P = new rsmi_ragged_plan();
     if (hipGetDevice(&P->device) != hipSuccess) {

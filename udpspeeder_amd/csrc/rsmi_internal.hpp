@@ -112,7 +112,10 @@ bool bitslice_rtc_eligible(int k, int n);
 void bitslice_rtc_request(const std::vector<std::pair<int, int>> &codes);  // async
 void bitslice_rtc_wait(const std::vector<std::pair<int, int>> &codes);
 int bitslice_rtc_state(int k, int n);  // 0 idle, 1 compiling, 2 ready, 3 failed
-hipFunction_t bitslice_rtc_function(int k, int n, bool ragged);  // nullptr unless ready
+enum RtcKind { kRtcUniform = 0, kRtcRagged = 1, kRtcSplit = 2 };
+hipFunction_t bitslice_rtc_function(int k, int n, RtcKind kind);  // nullptr unless ready
+bool bitslice_split_ok(int k, int n);                                // gen_bitslice.split_ok
+bool bitslice_emit_split(int k, int n, std::string &src);           // gen_bitslice.emit_split's text
 hipError_t launch_encode_bitslice_ragged_rtc(int k, int n, const rsmi_group *groups,
                                              const uint32_t *colmap, const uint32_t *waves,
                                              uint32_t nwaves, uint8_t *base, uint32_t bytes,

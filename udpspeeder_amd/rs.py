@@ -377,14 +377,16 @@ def code_encoder(k: int, n: int) -> int:
     return r
 
 
-def bitslice_source(k: int, n: int) -> str:
-    """The XOR-network source of (k,n) as emitted for hipRTC."""
+def bitslice_source(k: int, n: int, split: bool = False) -> str:
+    """The XOR-network source of (k,n) as emitted for hipRTC (split=True: the
+    two-wave split-k form)."""
     L = lib()
-    size = L.rsmi_bitslice_source(k, n, None, 0)
+    fn = L.rsmi_bitslice_split_source if split else L.rsmi_bitslice_source
+    size = fn(k, n, None, 0)
     if size < 0:
-        check(int(size), "rsmi_bitslice_source")
+        check(int(size), fn.__name__)
     buf = C.create_string_buffer(size + 1)
-    L.rsmi_bitslice_source(k, n, buf, size + 1)
+    fn(k, n, buf, size + 1)
     return buf.value.decode()
 
 
