@@ -182,7 +182,7 @@ def main():
     e_rows = (pres_np[:, :K] == 0).sum(1)
     dec_alg = int(((e_rows > 0) * K * LEN).sum() + (e_rows * LEN).sum())  # k*len read + e*len written
     roof = {
-        "encode": roofline("encode", "k_bs_20_30: bit-sliced RS(20,10) encode", enc_alg, enc_ms, G),
+        "encode": roofline("encode", "k_bs2_20_30: split-k bit-sliced RS(20,10) encode", enc_alg, enc_ms, G),
         "decode": roofline("decode", "k_decode_fused: RS(20,10) decode, 5 random erasures",
                            dec_alg, dec_ms, G),
     }
@@ -236,7 +236,8 @@ def roofline(which, kernel, alg_bytes, ms, G):
     if os.path.exists(path):
         try:
             tj = json.load(open(path))
-            if tj.get("groups") == G:
+            # only counters of the kernel this build launches
+            if tj.get("groups") == G and kernel.split(":")[0] == tj.get("kernel"):
                 traffic = tj.get("hbm_bytes_per_launch")
         except (OSError, ValueError):
             traffic = None
