@@ -144,6 +144,16 @@ def test_precompile_rejects(u):
 
 
 # ---------------------------------------------------------------- GPU
+@pytest.mark.gpu
+def test_precompile_then_gpu_in_one_process(tmp_path):
+    """rsmi_precompile_code before any GPU use, then rsmi_init, in a fresh
+    process (hipRTC used to leave the shared HIP runtime without devices)."""
+    env = dict(os.environ, RSMI_RTC_CACHE=str(tmp_path))
+    r = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "scripts", "precompile_then_gpu.py")],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=150)
+    assert r.returncode == 0 and "rsmi_init ok" in r.stdout, r.stdout + r.stderr
+
+
 GPU_CASES = [(10, 15, 1250), (10, 15, 17), (10, 40, 1250), (5, 17, 333), (7, 9, 4000),
              (40, 60, 1280), (1, 2, 1), (2, 200, 100), (12, 20, 1250), (31, 36, 777)]
 

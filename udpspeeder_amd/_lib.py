@@ -162,8 +162,28 @@ def lib() -> C.CDLL:
                 raise RsmiError(
                     f"{LIB_PATH} not found: build it with `make -C udpspeeder_amd/csrc` "
                     "(or __graft_entry__.build()); there is no CPU fallback")
+            _share_torch_hip_runtime()
             _lib = _bind(C.CDLL(LIB_PATH))
         return _lib
+
+
+def _share_torch_hip_runtime() -> None:
+    """Load torch's HIP runtime before librsmi, so the process has ONE.
+
+    librsmi.so needs libamdhip64.so.7; torch's ROCm libraries need the
+    unversioned libamdhip64.so from torch/lib.  Loaded first, librsmi pulls in
+    /opt/rocm's runtime and torch later maps its own copy: two HIP runtimes
+    (two ROCr instances) in one process, and only the one that initialises
+    first sees the GPU -- rsmi_init then fails with "no ROCm-capable device"
+    behind a working torch, or torch.cuda.is_available() turns False
+    (scripts/rt_order_probe.py on the GPU box).  With torch imported first,
+    librsmi's libamdhip64.so.7 resolves to torch's already-loaded runtime
+    (same SONAME).  Without torch installed there is only one runtime anyway.
+    """
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
 
 
 def check(rc: int, what: str) -> None:
