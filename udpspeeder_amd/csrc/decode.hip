@@ -81,6 +81,9 @@ constexpr int kTile = 1280;    // bytes per lane-tile pass (64 x 16 + 64 x 4)
 #ifndef DEC_ROWGUARD
 #define DEC_ROWGUARD 1         // fused kernel: row guards on an opaque SGPR (see the MAC loop)
 #endif
+#ifndef DEC_GRID_BLOCKS_PER_CU
+#define DEC_GRID_BLOCKS_PER_CU 16  // fused kernel's grid (see launch_decode_fused)
+#endif
 #ifndef DEC_PAIR
 #define DEC_PAIR 0             // uniform kernel: fold survivors in pairs (fewer XORs, more VGPRs)
 #endif
@@ -1006,7 +1009,10 @@ hipError_t launch_decode_fused(const UniformArgs &a, const uint8_t *present,
     const size_t lds = kTabBytes + (size_t)(((a.n - a.k) * a.k + 15) & ~15) +
                        (size_t)kWaves * wave_lds_bytes(a.k);
     int64_t blocks = (a.ngroups + kWaves - 1) / kWaves;
-    const int64_t cap = 256 * 8;
+    // 16 blocks per CU: four resident rounds of 4 blocks, so a wave takes 4 of
+    // C2's 65,536 groups and the last round's tail is short (8 blocks per CU:
+    // +0.5-1.5 % decode time, 64: +6 %, profiles/r02/probes/dec_grid*_ab.txt)
+    const int64_t cap = 256 * DEC_GRID_BLOCKS_PER_CU;
     if (blocks > cap) blocks = cap;
     if (blocks < 1) blocks = 1;
     k_decode_fused<<<(unsigned)blocks, 64 * kWaves, lds, s>>>(a, present, parity_rows, status,
