@@ -81,9 +81,6 @@ constexpr int kTile = 1280;    // bytes per lane-tile pass (64 x 16 + 64 x 4)
 #ifndef DEC_ROWGUARD
 #define DEC_ROWGUARD 1         // fused kernel: row guards on an opaque SGPR (see the MAC loop)
 #endif
-#ifndef DEC_GRID_BLOCKS_PER_CU
-#define DEC_GRID_BLOCKS_PER_CU 16  // fused kernel's grid (see launch_decode_fused)
-#endif
 #ifndef DEC_PAIR
 #define DEC_PAIR 0             // uniform kernel: fold survivors in pairs (fewer XORs, more VGPRs)
 #endif
@@ -1008,17 +1005,9 @@ hipError_t launch_decode_fused(const UniformArgs &a, const uint8_t *present,
                                const uint32_t *ptab, const uint8_t *gftab, hipStream_t s) {
     const size_t lds = kTabBytes + (size_t)(((a.n - a.k) * a.k + 15) & ~15) +
                        (size_t)kWaves * wave_lds_bytes(a.k);
-    // Balanced grid: at most 16 blocks per CU (four resident rounds), sized so
-    // every wave takes the same number q of groups -- C2's 65,536 groups give
-    // q = 4 on 4,096 blocks.  Grids that leave some waves one group more than
-    // the rest pay that group at the end: 12 or 24 blocks per CU (q = 5.3 /
-    // 2.7) ran the C2 decode 8 % slower, 8 blocks per CU (q = 8) 1 % slower,
-    // one group per wave 6 % slower (profiles/r02/probes/dec_grid*_ab.txt).
-    const int64_t maxw = 256 * (int64_t)DEC_GRID_BLOCKS_PER_CU * kWaves;
-    const int64_t q = a.ngroups > 0 ? (a.ngroups + maxw - 1) / maxw : 1;
-    const int64_t waves = a.ngroups > 0 ? (a.ngroups + q - 1) / q : 1;
-    int64_t blocks = (waves + kWaves - 1) / kWaves;
-    if (blocks >= 64) blocks = (blocks + 7) & ~int64_t(7);  // whole XCD rounds (DEC_XCD)
+    int64_t blocks = (a.ngroups + kWaves - 1) / kWaves;
+    const int64_t cap = 256 * 8;
+    if (blocks > cap) blocks = cap;
     if (blocks < 1) blocks = 1;
     k_decode_fused<<<(unsigned)blocks, 64 * kWaves, lds, s>>>(a, present, parity_rows, status,
                                                              ptab, gftab);
