@@ -241,9 +241,8 @@ def test_decode_vs_oracle_random(gpu, oracle, k, n, ln, ner):
 
 @pytest.mark.parametrize("G", [4095, 50001, 65537, 131071])
 def test_decode_grid_sizes(gpu, oracle, G):
-    """Batch sizes around the fused decode's balanced grid (every wave the same
-    number of groups, whole XCD rounds of blocks): 1, 4, 5 and 8 groups per
-    wave, blocks rounded up past the last group."""
+    """Batch sizes that split unevenly over the fused decode's persistent grid
+    (2,048 blocks at most: 1 to 16 groups per wave, some waves one group short)."""
     import udpspeeder_amd as u
     k, n, ln = 20, 30, 48
     S = stride_for(ln)
