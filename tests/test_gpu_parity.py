@@ -239,26 +239,6 @@ def test_decode_vs_oracle_random(gpu, oracle, k, n, ln, ner):
     assert (out[:, k:] == buf[:, k:]).all()
 
 
-@pytest.mark.parametrize("G", [4095, 50001, 65537, 131071])
-def test_decode_grid_sizes(gpu, oracle, G):
-    """Batch sizes that split unevenly over the fused decode's persistent grid
-    (2,048 blocks at most: 1 to 16 groups per wave, some waves one group short)."""
-    import udpspeeder_amd as u
-    k, n, ln = 20, 30, 48
-    S = stride_for(ln)
-    rng = np.random.default_rng(G)
-    buf = rng.integers(0, 256, (G, n, S), dtype=np.uint8)
-    present = np.ones((G, n), np.uint8)
-    er = np.argsort(rng.random((G, n)), axis=1)[:, :5]
-    np.put_along_axis(present, er, 0, axis=1)
-    ref = buf.copy()
-    st_ref = oracle.decode_batch(k, n, ref.reshape(-1), n * S, S, ln, G, present)
-    t = upload(buf, gpu)
-    st = u.decode(t, upload(present, gpu), k, n, ln).cpu().numpy()
-    assert (st == st_ref).all()
-    assert (t.cpu().numpy()[:, :k, :ln] == ref[:, :k, :ln]).all()
-
-
 @pytest.mark.parametrize("fused", [True, False])
 @pytest.mark.parametrize("k,n,ln", [(20, 30, 1250), (20, 30, 3000), (7, 13, 100), (1, 2, 1280),
                                     (10, 20, 1281), (40, 50, 64)])
