@@ -123,6 +123,21 @@ int rsmi_wait_code(int k, int n);
  * over RSMI_RTC_MAX_COEFS, RSMI_RTC=0), RSMI_ERR_HIP when hipRTC fails. */
 int rsmi_precompile_code(int k, int n);
 
+/* Queue the run-time networks of count codes (k[i], n[i]) for the background
+ * compile pool and return at once, without touching any GPU (codes with no
+ * run-time network are skipped).  Returns how many of the codes get one. */
+int rsmi_precompile_codes_async(const int32_t *k, const int32_t *n, int count);
+
+/* Stop run-time compilation: queued compiles are dropped (their codes stay on
+ * the generic kernel), and the call returns once every compile already inside
+ * hipRTC has finished (one code each, at most 4 pool threads plus waiting
+ * callers).  Later requests compile nothing.  The library calls it itself at
+ * process exit, from the main thread's exit path before any atexit handler,
+ * so comgr/LLVM is never torn down under a running compile; a host that exits
+ * some other way (or wants a bounded exit) calls it first.  The Python binding
+ * registers it with Python's atexit. */
+void rsmi_rtc_shutdown(void);
+
 /* The bit-sliced XOR network source of (k,n) (n > k) as emitted for hipRTC
  * (identical to the build-time generator's text).  Copies at most cap-1 bytes
  * plus a NUL into buf (may be NULL); returns the full length, or

@@ -13,8 +13,10 @@ compiled by oracle/Makefile) and writes small data fixtures:
   decode_small.npz      rs_decode2 results for erasure patterns, incl. non-codeword
                         inputs (random parity) that pin the lowest-k-survivors rule,
                         extra survivors, too-few survivors, and the pointer permutation
-  full_hashes.json      sha256 over full-size C1 encode parity, C3 ragged parity and a
-                        C2 non-codeword decode (pins the PRNG definitions too)
+  full_hashes.json      sha256 over full-size C1 encode parity, C3 ragged parity, a
+                        C2 non-codeword decode (pins the PRNG definitions too), and
+                        the C4 rank slices 3/8 and 7/8 of 2^20 groups (encode parity
+                        + non-codeword decode), python -m oracle.gen_golden --c4
 
 Inputs are regenerated from the PRNG definitions in oracle/cpu.py, so the fixtures
 hold outputs (plus sha256 of inputs to pin the generator).
@@ -234,10 +236,57 @@ def c3_ragged_decode(ref: Reference, ora: Oracle):
             "data_out_sha256": h.hexdigest()}
 
 
+C4_GROUPS = 1 << 20
+C4_WORLD = 8
+C4_RANKS = (3, 7)
+
+
+def c4_rank_slices(ref: Reference, nthreads: int):
+    """C4 (RS(20,10), 1250 B, 2^20 groups over 8 ranks): for ranks 3 and 7 of
+    8, the slice [g0, g1) = shard.strong_range(r, 8, 2^20) as one rank encodes
+    and decodes it (global group ids g0.. drive the PRNG streams):
+      parity_sha256   rs_encode2 parity of the slice's DATA_SEED data;
+      data_out_sha256 rs_decode2 of the non-codeword slice (DATA_SEED data,
+                      DATA_SEED ^ 0xFFFF parity, 5 erasures per group from
+                      ERASE_SEED), digest of the k data rows (len bytes each).
+    Groups are independent (connection.h:244-245), so each slice's digest is
+    what the 8-GPU job's rank r must produce."""
+    k, n, ln = 20, 30, 1250
+    chunk = 8192
+    out = {"k": k, "n": n, "len": ln, "groups": C4_GROUPS, "world": C4_WORLD,
+           "seed": DATA_SEED, "parity_seed": DATA_SEED ^ 0xFFFF, "erase_seed": ERASE_SEED,
+           "erasures": 5, "ranks": {}}
+    for r in C4_RANKS:
+        g0, g1 = C4_GROUPS * r // C4_WORLD, C4_GROUPS * (r + 1) // C4_WORLD
+        hp = hashlib.sha256(); hx = hashlib.sha256()
+        for c0 in range(g0, g1, chunk):
+            m = min(chunk, g1 - c0)
+            buf = np.zeros((m, n, ln), np.uint8)
+            buf[:, :k] = group_data(DATA_SEED, c0, m, k, ln)
+            ref.encode_batch(k, n, buf.reshape(-1), n * ln, ln, ln, m, nthreads)
+            hp.update(buf[:, k:].tobytes())
+            buf[:, k:] = group_data(DATA_SEED ^ 0xFFFF, c0, m, n - k, ln)
+            pres = present_from_erasures(erasures(ERASE_SEED, c0, m, n, 5), n)
+            st = ref.decode_batch(k, n, buf.reshape(-1), n * ln, ln, ln, m, pres, True, nthreads)
+            assert (st == 0).all()
+            hx.update(buf[:, :k].tobytes())
+        out["ranks"][str(r)] = {"g0": g0, "g1": g1, "parity_sha256": hp.hexdigest(),
+                                "data_out_sha256": hx.hexdigest()}
+    return out
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
     ref = Reference()
     ora = Oracle()
+    if sys.argv[1:] == ["--c4"]:  # add/refresh only the C4 rank-slice digests
+        path = os.path.join(OUT, "full_hashes.json")
+        full = json.load(open(path))
+        full["c4_rank_slices"] = c4_rank_slices(ref, os.cpu_count() or 1)
+        with open(path, "w") as f:
+            json.dump(full, f, indent=1)
+        print("c4_rank_slices written to", path)
+        return
     if sys.argv[1:] == ["--c3-decode"]:  # add/refresh only the C3 decode digest
         path = os.path.join(OUT, "full_hashes.json")
         full = json.load(open(path))
@@ -253,8 +302,10 @@ def main():
     np.savez_compressed(os.path.join(OUT, "matrices.npz"), **mats)
     np.savez_compressed(os.path.join(OUT, "encode_small.npz"), **encode_small(ref))
     np.savez_compressed(os.path.join(OUT, "decode_small.npz"), **decode_small(ref))
+    full = full_hashes(ref, ora, os.cpu_count() or 1)
+    full["c4_rank_slices"] = c4_rank_slices(ref, os.cpu_count() or 1)
     with open(os.path.join(OUT, "full_hashes.json"), "w") as f:
-        json.dump(full_hashes(ref, ora, os.cpu_count() or 1), f, indent=1)
+        json.dump(full, f, indent=1)
     print("golden fixtures written to", OUT)
 
 

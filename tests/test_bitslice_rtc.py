@@ -27,9 +27,16 @@ RTC_CODES = [(10, 15), (1, 2), (3, 4), (10, 40), (5, 17), (30, 42), (7, 9), (2, 
 
 @pytest.fixture(scope="module")
 def u(tmp_path_factory):
+    """This module's compiles go to a private cache; the variable is restored
+    afterwards, so later modules keep the default (warm) cache."""
+    old = os.environ.get("RSMI_RTC_CACHE")
     os.environ["RSMI_RTC_CACHE"] = str(tmp_path_factory.mktemp("rtc_cache"))
     import udpspeeder_amd
-    return udpspeeder_amd
+    yield udpspeeder_amd
+    if old is None:
+        del os.environ["RSMI_RTC_CACHE"]
+    else:
+        os.environ["RSMI_RTC_CACHE"] = old
 
 
 def test_codes_are_not_builtin():
@@ -141,6 +148,106 @@ def test_precompile_rejects(u):
     finally:
         del os.environ["RSMI_RTC_MAX_COEFS"]
     assert u.code_encoder(5, 5) == ENC_NONE
+
+
+# A process that exits while a run-time compile is inside hipRTC must exit
+# cleanly and promptly: comgr/LLVM is loaded by libhiprtc on first use, so its
+# static destructors are registered after (and run before) any atexit handler
+# librsmi registers earlier; tearing LLVM down under a running compile crashed
+# or hung the round-2 GPU test process at exit.  The library now stops
+# compiles from Python's atexit and from the main thread's exit path, ahead
+# of every atexit handler (bitslice_rtc.cpp shutdown_compiles).
+_EXIT_PY = r"""
+import os, sys, threading, time
+sys.path.insert(0, {root!r})
+from udpspeeder_amd._lib import lib
+L = lib()
+def go():
+    L.rsmi_precompile_code({k}, {n})
+for _ in range({threads}):
+    threading.Thread(target=go, daemon=True).start()
+{extra}
+time.sleep({sleep})
+print("main returns", flush=True)
+"""
+
+_EXIT_C = r"""
+#include <pthread.h>
+#include <stdio.h>
+#include <unistd.h>
+int rsmi_precompile_code(int k, int n);
+static void *go(void *p) { (void)p; rsmi_precompile_code(40, 60); return 0; }
+int main(void) {
+    pthread_t t;
+    pthread_create(&t, 0, go, 0);
+    usleep(1500 * 1000);   /* inside hipRTC by now */
+    printf("main returns\n");
+    fflush(stdout);
+    return 0;              /* exit() with the compile still running */
+}
+"""
+
+
+def _run_exit(args, tmp_path, bound, expect_cached=True):
+    env = dict(os.environ, RSMI_RTC_CACHE=str(tmp_path / "cold"))
+    t0 = time.time()
+    r = subprocess.run(args, env=env, capture_output=True, text=True, timeout=bound + 60)
+    dt = time.time() - t0
+    assert r.returncode == 0, (r.returncode, r.stdout, r.stderr[-2000:])
+    assert "main returns" in r.stdout
+    assert dt < bound, dt
+    if expect_cached:
+        # the compile that was inside hipRTC finished before the process went
+        # away (the round-2 library exited under it: nothing cached, or SIGSEGV)
+        cold = tmp_path / "cold"
+        files = os.listdir(cold) if cold.exists() else []
+        assert any(f.startswith("bs-") and f.endswith(".co") for f in files), files
+    return dt
+
+
+@pytest.mark.parametrize("case", ["one", "queue", "waiter"])
+def test_exit_during_compile_python(u, tmp_path, case):
+    """Interpreter exit mid-compile: a daemon thread in rsmi_precompile_code
+    (40,60) (800 coefficients, ~10 s cold); 'queue' also has a 40-code -f
+    table queued behind the pool; 'waiter' has six threads compiling on their
+    own (caller-side compiles).  rc 0, and the exit waits for at most the
+    compiles already inside hipRTC (one code each)."""
+    extra = ""
+    threads = 1
+    if case == "queue":
+        extra = ("import ctypes\n"
+                 "ks = [x for x in range(11, 51)]; ns = [x + max(1, x // 2) for x in ks]\n"
+                 "A = ctypes.c_int32 * len(ks)\n"
+                 "assert L.rsmi_precompile_codes_async(A(*ks), A(*ns), len(ks)) >= 30\n")
+    if case == "waiter":
+        threads = 6
+    src = _EXIT_PY.format(root=ROOT, k=40, n=60, threads=threads, extra=extra, sleep=1.5)
+    _run_exit([sys.executable, "-c", src], tmp_path, bound=90)
+
+
+def test_exit_during_compile_c(u, tmp_path):
+    """The same from a C program linked against librsmi: main() returns while
+    a pthread is inside hipRTC; the main thread's exit path waits for it."""
+    c = tmp_path / "exit_mid_compile.c"
+    c.write_text(_EXIT_C)
+    exe = str(tmp_path / "exit_mid_compile")
+    libdir = os.path.join(ROOT, "udpspeeder_amd")
+    subprocess.run(["gcc", "-O1", "-o", exe, str(c), "-L" + libdir, "-lrsmi", "-lpthread",
+                    "-Wl,-rpath," + libdir], check=True)
+    _run_exit([exe], tmp_path, bound=90)
+
+
+def test_shutdown_stops_compiles(u, tmp_path):
+    """After rsmi_rtc_shutdown nothing new compiles: precompile fails and the
+    code stays on the generic kernel (in a child, so this process keeps
+    compiling)."""
+    src = (f"import sys; sys.path.insert(0, {ROOT!r})\n"
+           "from udpspeeder_amd._lib import lib, ENC_GENERIC\n"
+           "L = lib(); L.rsmi_rtc_shutdown()\n"
+           "assert L.rsmi_precompile_code(10, 14) != 0\n"
+           "assert L.rsmi_code_encoder(10, 14) == ENC_GENERIC, L.rsmi_code_encoder(10, 14)\n"
+           "print('main returns')\n")
+    _run_exit([sys.executable, "-c", src], tmp_path, bound=60, expect_cached=False)
 
 
 # ---------------------------------------------------------------- GPU

@@ -239,6 +239,33 @@ def test_decode_vs_oracle_random(gpu, oracle, k, n, ln, ner):
     assert (out[:, k:] == buf[:, k:]).all()
 
 
+@pytest.mark.parametrize("G", [4095, 50001, 65537, 131071])
+def test_decode_grid_sizes(gpu, oracle, G):
+    """Batch sizes that split unevenly over the fused decode's persistent grid
+    (2,048 blocks at most: 1 to 16 groups per wave, some waves one group short).
+    Round 2 dropped this test when the GPU test process crashed at exit with it
+    in the suite; the cause was run-time compiles still inside hipRTC at exit
+    (tests/test_bitslice_rtc.py::test_exit_during_compile_*), not this kernel."""
+    import udpspeeder_amd as u
+    k, n, ln = 20, 30, 48
+    S = stride_for(ln)
+    rng = np.random.default_rng(G)
+    buf = rng.integers(0, 256, (G, n, S), dtype=np.uint8)
+    present = np.ones((G, n), np.uint8)
+    er = np.argsort(rng.random((G, n)), axis=1)[:, :5]
+    np.put_along_axis(present, er, 0, axis=1)
+    ref = buf.copy()
+    st_ref = oracle.decode_batch(k, n, ref.reshape(-1), n * S, S, ln, G, present)
+    t = upload(buf, gpu)
+    st = u.decode(t, upload(present, gpu), k, n, ln).cpu().numpy()
+    assert (st == st_ref).all()
+    out = t.cpu().numpy()
+    assert (out[:, :k, :ln] == ref[:, :k, :ln]).all()
+    # nothing outside the rebuilt rows' slots changed: parity rows and the
+    # survivors are the input bytes
+    assert (out[:, k:] == buf[:, k:]).all()
+
+
 @pytest.mark.parametrize("fused", [True, False])
 @pytest.mark.parametrize("k,n,ln", [(20, 30, 1250), (20, 30, 3000), (7, 13, 100), (1, 2, 1280),
                                     (10, 20, 1281), (40, 50, 64)])
@@ -823,3 +850,35 @@ def test_concurrent_ragged_and_decode(gpu, oracle):
         oracle.encode_batch(d.k, d.n, seg, 0, d.shard_stride, d.len, 1)
         got = out[d.offset:d.offset + d.n * d.shard_stride].reshape(d.n, d.shard_stride)
         assert (got[:, :d.len] == seg.reshape(d.n, d.shard_stride)[:, :d.len]).all(), i
+
+
+def test_decode_wrappers_reject_bad_status_and_masks(gpu):
+    """The kernels write status[g] for every g < G and read 8 mask words per
+    group: the Python wrappers refuse a short / wrong-dtype status tensor and
+    a misshaped present_bits before anything is launched."""
+    import torch
+    import udpspeeder_amd as u
+    from udpspeeder_amd import synth
+    k, n, ln, G = 20, 30, 64, 8
+    t = torch.zeros((G, n, 64), dtype=torch.uint8, device=gpu)
+    pres = torch.ones((G, n), dtype=torch.uint8, device=gpu)
+    for bad in (torch.zeros(G - 1, dtype=torch.int32, device=gpu),
+                torch.zeros(G, dtype=torch.int64, device=gpu)):
+        with pytest.raises((ValueError, TypeError)):
+            u.decode(t, pres, k, n, ln, status=bad)
+    groups, total = u.make_groups([3] * G, [5] * G, [40] * G)
+    base = torch.zeros(total, dtype=torch.uint8, device=gpu)
+    flags = np.ones((G, 5), np.uint8)
+    bits = torch.from_numpy(synth.present_bits(flags).view(np.int32)).to(gpu)
+    u.prepare_code(3, 5)
+    with pytest.raises(ValueError):
+        u.rs.decode_ragged(base, groups, bits[:G - 1])
+    with pytest.raises(ValueError):
+        u.rs.decode_ragged(base, groups, bits, status=torch.zeros(G - 1, dtype=torch.int32, device=gpu))
+    dg = u.rs.groups_to_device(groups, gpu)
+    with pytest.raises(ValueError):
+        u.rs.decode_ragged_dev(base, dg[:24 * (G - 1)], G, bits)
+    with pytest.raises(ValueError):
+        u.rs.decode_ragged_dev(base, dg, G, bits, status=torch.zeros(2, dtype=torch.int32, device=gpu))
+    st = u.rs.decode_ragged_dev(base, dg, G, bits, kmax=3)
+    assert (st.cpu().numpy() == 0).all()

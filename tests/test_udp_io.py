@@ -110,3 +110,40 @@ def test_bad_args():
     slab = io.Slab(2, 64)
     with pytest.raises(RsmiError):
         io.recv_batch(rx, slab, 0, 64, 2, timeout_ms=0)  # slot needs max_len + 1 bytes
+
+
+def test_one_bad_datagram_does_not_stop_the_batch():
+    """A datagram the kernel rejects on its own (EMSGSIZE here; ECONNREFUSED
+    after an ICMP port-unreachable is the same case) is dropped and the rest of
+    the batch still goes out, as the reference's per-packet sendto does
+    (packet.cpp:149-162); only a batch of which nothing went out is an error."""
+    from udpspeeder_amd._lib import RsmiError
+    rx, tx = _pair()
+    S = 70000
+    src = io.Slab(4, S)
+    for i in range(4):
+        src.slot(i)[:] = i + 1
+    to = io.addr_of(*rx.getsockname())
+    assert io.send_batch(tx, src, 0, [10, 66000, 20, 30], to=to) == 3
+    dst = io.Slab(4, 64)
+    got = io.recv_batch(rx, dst, 0, 32, 4, timeout_ms=2000)
+    assert list(got) == [10, 20, 30]
+    assert (dst.slot(1, 0, 20) == 3).all() and (dst.slot(2, 0, 30) == 4).all()
+    with pytest.raises(RsmiError):
+        io.send_batch(tx, src, 0, [66000, 66000], to=to)
+
+
+def test_connection_refused_mid_batch():
+    """Connected socket, peer port closed: the ICMP error surfaces on a later
+    send as ECONNREFUSED for one datagram; the call still returns a count."""
+    rx, tx = _pair()
+    port = rx.getsockname()[1]
+    rx.close()
+    tx.connect(("127.0.0.1", port))
+    src = io.Slab(64, 64)
+    total = 0
+    for _ in range(4):
+        n = io.send_batch(tx, src, 0, np.full(64, 16, np.int32))
+        assert 0 < n <= 64
+        total += n
+    assert total < 4 * 64  # at least one refused datagram was skipped, not fatal

@@ -6,6 +6,7 @@ reports HIP errors (no device, launch failure) as exceptions.
 """
 from __future__ import annotations
 
+import atexit
 import ctypes as C
 import os
 import threading
@@ -93,6 +94,8 @@ def _bind(lib: C.CDLL) -> C.CDLL:
         "rsmi_last_encoder": ([], i32),
         "rsmi_wait_code": ([i32, i32], i32),
         "rsmi_precompile_code": ([i32, i32], i32),
+        "rsmi_rtc_shutdown": ([], None),
+        "rsmi_precompile_codes_async": ([vp, vp, i32], i32),
         "rsmi_bitslice_source": ([i32, i32, C.c_char_p, i64], i64),
         "rsmi_bitslice_split_source": ([i32, i32, C.c_char_p, i64], i64),
         "rsmi_encode_dev": ([i32, i32, vp, i64, i64, i32, i64, vp], i32),
@@ -164,6 +167,9 @@ def lib() -> C.CDLL:
                     "(or __graft_entry__.build()); there is no CPU fallback")
             _share_torch_hip_runtime()
             _lib = _bind(C.CDLL(LIB_PATH))
+            # run-time compiles still inside hipRTC finish before the
+            # interpreter (and then comgr/LLVM) tears down (bitslice_rtc.cpp)
+            atexit.register(_lib.rsmi_rtc_shutdown)
         return _lib
 
 

@@ -19,12 +19,14 @@
 #include <hip/hiprtc.h>
 
 #include <sys/stat.h>
+#include <sys/syscall.h>
 #include <unistd.h>
 
 #include <algorithm>
 #include <atomic>
 #include <condition_variable>
 #include <cstdio>
+#include <deque>
 #include <cstdlib>
 #include <cstring>
 #include <functional>
@@ -251,10 +253,10 @@ namespace {
 // ---------------------------------------------------------------- registry
 enum : int { kIdle = 0, kBusy = 1, kReady = 2, kFailed = 3 };
 
-struct Unit {  // one hipRTC program: one or more codes
+struct Unit {  // one hipRTC program: one code (so an exit waits for one compile at most)
     std::vector<std::pair<int, int>> codes;
-    // set by whoever compiles the unit: its worker thread, or a thread that
-    // waits for one of its codes before the worker got a compile slot
+    // set by whoever compiles the unit (a pool worker, or a thread that waits
+    // for its code before a worker took it), or by the shutdown that drops it
     std::atomic<bool> claimed{false};
     std::vector<char> co;  // code object
     std::mutex mu;         // guards mod[]
@@ -279,10 +281,11 @@ struct RtcCode {
 struct Registry {
     std::mutex mu;
     std::condition_variable cv;
-    int inflight = 0;  // units being compiled or queued
-    int running = 0;   // compile threads inside hipRTC
+    std::deque<std::shared_ptr<Unit>> queue;  // units no one has claimed yet
+    int workers = 0;  // pool threads alive
+    int running = 0;  // threads inside compile_unit (pool workers and waiting callers)
     bool atexit_set = false;
-    bool exiting = false;  // set at exit: queued units are dropped, running ones finish
+    bool exiting = false;  // rsmi_rtc_shutdown ran: nothing new enters hipRTC
     std::atomic<RtcCode *> table[257 * 257];
     Registry() {
         for (auto &t : table) t.store(nullptr);
@@ -419,7 +422,8 @@ bool compile_unit(Unit &U, std::string &err) {
 
 constexpr int kMaxCompileThreads = 4;
 
-// Compiles U (the caller has claimed it) and publishes its codes' state.
+// Compiles U (the caller has claimed it and counted itself in R.running) and
+// publishes its codes' state.
 void compile_and_publish(Unit &U) {
     Registry &R = reg();
     std::string err;
@@ -431,49 +435,82 @@ void compile_and_publish(Unit &U) {
         rc->err = err;
         rc->state.store(ok ? kReady : kFailed);
     }
-    R.cv.notify_all();
-}
-
-void worker(std::shared_ptr<Unit> U) {
-    Registry &R = reg();
-    {
-        std::unique_lock<std::mutex> lk(R.mu);
-        R.cv.wait(lk, [&] { return R.running < kMaxCompileThreads || R.exiting; });
-        if (R.exiting) {  // process exit: drop queued units (their codes stay generic)
-            for (auto &c : U->codes) {
-                RtcCode *rc = R.table[c.first * 257 + c.second].load();
-                rc->err = "process exiting";
-                rc->state.store(kFailed);
-            }
-            --R.inflight;
-            R.cv.notify_all();
-            return;
-        }
-        if (U->claimed.exchange(true)) {  // a waiting thread compiled it
-            --R.inflight;
-            R.cv.notify_all();
-            return;
-        }
-        ++R.running;
-    }
-    compile_and_publish(*U);
-    std::lock_guard<std::mutex> lk(R.mu);
     --R.running;
-    --R.inflight;
     R.cv.notify_all();
 }
 
-// Runs before hipRTC's own teardown (registered after it was loaded): lets
-// the at most kMaxCompileThreads compiles inside hipRTC finish.
-void wait_all_at_exit() {
+// A unit that will never compile: its codes stay on the generic kernel.
+// Caller holds R.mu and has claimed U.
+void drop_unit_locked(Registry &R, Unit &U, const char *why) {
+    for (auto &c : U.codes) {
+        RtcCode *rc = R.table[c.first * 257 + c.second].load();
+        rc->err = why;
+        rc->state.store(kFailed);
+    }
+}
+
+// Pool thread: takes queued units until the queue is empty or shutdown began.
+void worker() {
+    Registry &R = reg();
+    std::unique_lock<std::mutex> lk(R.mu);
+    while (!R.exiting && !R.queue.empty()) {
+        std::shared_ptr<Unit> U = R.queue.front();
+        R.queue.pop_front();
+        if (U->claimed.exchange(true)) continue;  // a waiting thread compiles it
+        ++R.running;
+        lk.unlock();
+        compile_and_publish(*U);
+        lk.lock();
+    }
+    --R.workers;
+    R.cv.notify_all();
+}
+
+// Shutdown: nothing new enters hipRTC, queued units are dropped, and the call
+// returns once every compile already inside hipRTC (at most kMaxCompileThreads
+// pool workers plus any waiting callers, one code each) has left it.  It must
+// run before comgr/LLVM (dlopen'ed by libhiprtc on first use, so registered
+// AFTER any atexit handler of ours) runs its static destructors: an exit that
+// tears LLVM down under a running compile crashes or hangs the process.
+void shutdown_compiles_impl() {
     Registry &R = reg();
     std::unique_lock<std::mutex> lk(R.mu);
     R.exiting = true;
+    for (auto &U : R.queue)
+        if (!U->claimed.exchange(true)) drop_unit_locked(R, *U, "process exiting");
+    R.queue.clear();
     R.cv.notify_all();
-    R.cv.wait(lk, [&] { return R.inflight == 0; });
+    R.cv.wait(lk, [&] { return R.running == 0; });
+}
+
+// The exit hooks, earliest first:
+//  1. the Python binding registers rsmi_rtc_shutdown with Python's atexit
+//     (before interpreter finalisation);
+//  2. a thread_local guard on the main thread: glibc's exit() runs the exiting
+//     thread's TLS destructors before ANY atexit/__cxa_atexit handler, so this
+//     runs ahead of comgr's static destructors whatever the load order;
+//  3. a plain atexit handler, in case exit() is called from another thread.
+struct MainThreadExitGuard {
+    ~MainThreadExitGuard() { shutdown_compiles_impl(); }
+};
+
+void arm_exit_hooks_locked(Registry &R) {
+    if (R.atexit_set) return;
+    R.atexit_set = true;
+    atexit(shutdown_compiles_impl);
 }
 
 }  // namespace
+
+void shutdown_compiles() { shutdown_compiles_impl(); }
+
+// Touch the guard on the thread that loads the library (the main thread, for
+// a Python import or a linked program) so its destructor is registered there.
+__attribute__((constructor)) static void rsmi_rtc_arm_main_guard() {
+    if ((pid_t)syscall(SYS_gettid) != getpid()) return;
+    static thread_local MainThreadExitGuard guard;
+    (void)&guard;
+}
 
 bool bitslice_rtc_eligible(int k, int n) {
     const int m = n - k;
@@ -481,52 +518,48 @@ bool bitslice_rtc_eligible(int k, int n) {
            !env_off("RSMI_RTC");
 }
 
-// Queue the codes that are eligible and not yet requested, in up to
-// kMaxCompileThreads units of about equal size (k*m), and return at once.
+// Queue the codes that are eligible and not yet requested (smallest k*m
+// first, one code per hipRTC program) for the kMaxCompileThreads pool threads,
+// and return at once.
 void bitslice_rtc_request(const std::vector<std::pair<int, int>> &codes) {
     Registry &R = reg();
     std::vector<std::pair<int, int>> todo;
-    {
-        std::lock_guard<std::mutex> lk(R.mu);
-        for (auto &c : codes) {
-            if (!bitslice_rtc_eligible(c.first, c.second)) continue;
-            auto &slot = R.table[c.first * 257 + c.second];
-            if (slot.load()) continue;
-            RtcCode *rc = new RtcCode();
-            rc->state.store(kBusy);
-            slot.store(rc);
-            todo.push_back(c);
-        }
-        if (todo.empty()) return;
-        if (!R.atexit_set) {
-            R.atexit_set = true;
-            atexit(wait_all_at_exit);
-        }
-    }
-    // largest first into the lightest unit
-    std::sort(todo.begin(), todo.end(), [](const std::pair<int, int> &a, const std::pair<int, int> &b) {
-        return (long)a.first * (a.second - a.first) > (long)b.first * (b.second - b.first);
-    });
-    const int nu = std::min<int>(kMaxCompileThreads, (int)todo.size());
-    std::vector<std::shared_ptr<Unit>> units;
-    std::vector<long> load((size_t)nu, 0);
-    for (int u = 0; u < nu; ++u) units.push_back(std::make_shared<Unit>());
-    for (auto &c : todo) {
-        const int u = (int)(std::min_element(load.begin(), load.end()) - load.begin());
-        units[(size_t)u]->codes.push_back(c);
-        load[(size_t)u] += (long)c.first * (c.second - c.first);
-    }
     std::lock_guard<std::mutex> lk(R.mu);
-    for (auto &U : units) {
-        for (auto &c : U->codes) R.table[c.first * 257 + c.second].load()->unit = U;
-        ++R.inflight;
-        std::thread(worker, U).detach();
+    for (auto &c : codes) {
+        if (!bitslice_rtc_eligible(c.first, c.second)) continue;
+        auto &slot = R.table[c.first * 257 + c.second];
+        if (slot.load()) continue;
+        RtcCode *rc = new RtcCode();
+        rc->state.store(kBusy);
+        slot.store(rc);
+        todo.push_back(c);
+    }
+    if (todo.empty()) return;
+    arm_exit_hooks_locked(R);
+    std::stable_sort(todo.begin(), todo.end(), [](const std::pair<int, int> &a, const std::pair<int, int> &b) {
+        return (long)a.first * (a.second - a.first) < (long)b.first * (b.second - b.first);
+    });
+    for (auto &c : todo) {
+        auto U = std::make_shared<Unit>();
+        U->codes.push_back(c);
+        RtcCode *rc = R.table[c.first * 257 + c.second].load();
+        rc->unit = U;
+        if (R.exiting) {
+            U->claimed.store(true);
+            drop_unit_locked(R, *U, "process exiting");
+            continue;
+        }
+        R.queue.push_back(U);
+    }
+    while (R.workers < kMaxCompileThreads && R.workers < (int)R.queue.size()) {
+        ++R.workers;
+        std::thread(worker).detach();
     }
 }
 
 // Block until every listed code's compile has finished (ready or failed).  A
-// code whose unit is still queued behind kMaxCompileThreads running compiles
-// is compiled on the calling thread instead of waiting its turn.
+// code whose unit is still queued is compiled on the calling thread instead of
+// waiting its turn.
 void bitslice_rtc_wait(const std::vector<std::pair<int, int>> &codes) {
     Registry &R = reg();
     for (auto &c : codes) {
@@ -534,9 +567,12 @@ void bitslice_rtc_wait(const std::vector<std::pair<int, int>> &codes) {
         {
             std::lock_guard<std::mutex> lk(R.mu);
             RtcCode *rc = R.table[c.first * 257 + c.second].load();
-            if (rc && rc->state.load() == kBusy) U = rc->unit;
+            if (rc && rc->state.load() == kBusy && !R.exiting && !rc->unit->claimed.exchange(true)) {
+                U = rc->unit;
+                ++R.running;
+            }
         }
-        if (U && !U->claimed.exchange(true)) compile_and_publish(*U);
+        if (U) compile_and_publish(*U);
     }
     std::unique_lock<std::mutex> lk(R.mu);
     R.cv.wait(lk, [&] {
@@ -601,6 +637,8 @@ void set_error(const std::string &m);
 
 }  // namespace rsmi
 
+extern "C" void rsmi_rtc_shutdown(void) { rsmi::shutdown_compiles(); }
+
 extern "C" int rsmi_wait_code(int k, int n) {
     int rc = rsmi::prepare_code(k, n);
     if (rc) return rc;
@@ -623,6 +661,19 @@ extern "C" int rsmi_precompile_code(int k, int n) {
         return RSMI_ERR_HIP;
     }
     return RSMI_OK;
+}
+
+extern "C" int rsmi_precompile_codes_async(const int32_t *k, const int32_t *n, int count) {
+    if (count < 0 || (count && (!k || !n))) {
+        rsmi::set_error("rsmi_precompile_codes_async: bad arrays");
+        return RSMI_ERR_INVALID;
+    }
+    std::vector<std::pair<int, int>> codes;
+    for (int i = 0; i < count; ++i)
+        if (k[i] >= 1 && n[i] > k[i] && n[i] <= 256 && rsmi::bitslice_rtc_eligible(k[i], n[i]))
+            codes.push_back({k[i], n[i]});
+    rsmi::bitslice_rtc_request(codes);
+    return (int)codes.size();
 }
 
 extern "C" int rsmi_code_encoder(int k, int n) {

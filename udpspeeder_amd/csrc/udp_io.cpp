@@ -134,7 +134,7 @@ int send_all(int fd, int32_t n, const int32_t *len, Addr addr, const rsmi_udp_ad
     std::vector<iovec> iov;
     msgs.reserve((size_t)std::min(n, kChunk));
     iov.reserve(msgs.capacity());
-    int sent = 0;
+    int sent = 0, failed = 0, err = 0;
     int i = 0;
     while (i < n) {
         msgs.clear();
@@ -164,11 +164,22 @@ int send_all(int fd, int32_t n, const int32_t *len, Addr addr, const rsmi_udp_ad
                     (void)poll(&p, 1, 10);
                     continue;
                 }
-                return io_fail("sendmmsg");
+                // msgs[done] failed on its own (ECONNREFUSED after an ICMP
+                // port-unreachable, EMSGSIZE, ...): drop that one datagram and
+                // go on, as the reference's per-packet sendto/send does
+                // (packet.cpp:143-162 logs and carries on)
+                if (!failed) err = errno;
+                ++failed;
+                ++done;
+                continue;
             }
             done += (size_t)r;
+            sent += r;
         }
-        sent += (int)msgs.size();
+    }
+    if (failed && sent == 0) {
+        errno = err;
+        return io_fail("sendmmsg");
     }
     return sent;
 }

@@ -196,6 +196,26 @@ def _check_dev(t, name, dtype=None):
         raise TypeError(f"{name} must be {dtype}")
 
 
+def _status_out(status, G, device):
+    """The caller's status tensor checked (int32, contiguous, >= G entries, on
+    ``device``: the kernels write status[g] for every g < G), or a new one."""
+    import torch
+    if status is None:
+        return torch.empty(G, dtype=torch.int32, device=device)
+    _check_dev(status, "status", torch.int32)
+    if status.device != device or not status.is_contiguous() or status.numel() < G:
+        raise ValueError(f"status must be a contiguous int32 tensor of >= {G} entries on {device}")
+    return status
+
+
+def _present_bits(present_bits, G, device):
+    import torch
+    _check_dev(present_bits, "present_bits", torch.int32)
+    if tuple(present_bits.shape) != (G, 8) or not present_bits.is_contiguous() or \
+            present_bits.device != device:
+        raise ValueError("present_bits must be a contiguous [G, 8] int32 tensor on the base's device")
+
+
 def _shard_geometry(shards, n):
     import torch
     _check_dev(shards, "shards", torch.uint8)
@@ -223,10 +243,9 @@ def decode(shards, present, k: int, n: int, length: Optional[int] = None, status
     import torch
     G, gs, ss, S = _shard_geometry(shards, n)
     _check_dev(present, "present", torch.uint8)
-    if tuple(present.shape) != (G, n) or not present.is_contiguous():
-        raise ValueError("present must be a contiguous [G, n] uint8 tensor")
-    if status is None:
-        status = torch.empty(G, dtype=torch.int32, device=shards.device)
+    if tuple(present.shape) != (G, n) or not present.is_contiguous() or present.device != shards.device:
+        raise ValueError("present must be a contiguous [G, n] uint8 tensor on the shards' device")
+    status = _status_out(status, G, shards.device)
     L = S if length is None else int(length)
     check(lib().rsmi_decode_dev(k, n, shards.data_ptr(), gs, ss, L, G, present.data_ptr(),
                                 status.data_ptr(), _stream_handle(stream)), "rsmi_decode_dev")
@@ -291,13 +310,9 @@ class RaggedPlan:
         """rs_decode2 on every group of the plan's layout; ``present_bits`` an
         int32 [G, 8] CUDA tensor of 256-bit masks (synth.present_bits).
         Returns the int32 [G] status tensor."""
-        import torch
         _check_dev(base, "base")
-        _check_dev(present_bits, "present_bits", torch.int32)
-        if tuple(present_bits.shape) != (self.ngroups, 8) or not present_bits.is_contiguous():
-            raise ValueError("present_bits must be a contiguous [G, 8] int32 tensor")
-        if status is None:
-            status = torch.empty(self.ngroups, dtype=torch.int32, device=base.device)
+        _present_bits(present_bits, self.ngroups, base.device)
+        status = _status_out(status, self.ngroups, base.device)
         check(lib().rsmi_decode_ragged_plan(self._h, base.data_ptr(), present_bits.data_ptr(),
                                             status.data_ptr(), _stream_handle(stream)),
               "rsmi_decode_ragged_plan")
@@ -330,9 +345,13 @@ def decode_ragged_dev(base, dev_groups, ngroups: int, present_bits, status=None,
     """Graph-capturable ragged decode with a device descriptor tensor (24
     bytes per group); codes must be resident (prepare_code).  Returns status."""
     import torch
-    _check_dev(present_bits, "present_bits", torch.int32)
-    if status is None:
-        status = torch.empty(ngroups, dtype=torch.int32, device=base.device)
+    _check_dev(base, "base", torch.uint8)
+    _check_dev(dev_groups, "dev_groups", torch.uint8)
+    if dev_groups.device != base.device or not dev_groups.is_contiguous() or \
+            dev_groups.numel() < 24 * ngroups:
+        raise ValueError(f"dev_groups must be a contiguous uint8 tensor of >= {24 * ngroups} bytes")
+    _present_bits(present_bits, ngroups, base.device)
+    status = _status_out(status, ngroups, base.device)
     check(lib().rsmi_decode_ragged_dev(dev_groups.data_ptr(), ngroups, base.data_ptr(),
                                        present_bits.data_ptr(), status.data_ptr(), kmax,
                                        _stream_handle(stream)), "rsmi_decode_ragged_dev")
@@ -343,9 +362,9 @@ def decode_ragged(base, groups, present_bits, status=None, stream=None):
     """rs_decode2 on every group of a ragged batch described by a host ctypes
     rsmi_group array (make_groups); synchronous.  Returns status."""
     import torch
-    _check_dev(present_bits, "present_bits", torch.int32)
-    if status is None:
-        status = torch.empty(len(groups), dtype=torch.int32, device=base.device)
+    _check_dev(base, "base", torch.uint8)
+    _present_bits(present_bits, len(groups), base.device)
+    status = _status_out(status, len(groups), base.device)
     check(lib().rsmi_decode_ragged(C.cast(groups, C.c_void_p), len(groups), base.data_ptr(),
                                    present_bits.data_ptr(), status.data_ptr(),
                                    _stream_handle(stream)), "rsmi_decode_ragged")
