@@ -333,7 +333,7 @@ def extra_configs(u, synth, torch, dev, buf, G):
     out["c4_one_gpu"] = c4_one_gpu(u, synth, torch, dev)
     out["rtc_f10_5_encode"] = rtc_config(u, synth, torch, dev)
     out["f2_cook_decook"] = cook_config(torch, dev, buf, G)
-    out["dropin_latency_us"] = dropin_latency(u)
+    out["dropin_latency_us"] = dropin_latency_both(u)
     return out
 
 
@@ -496,7 +496,25 @@ def dropin_latency(u, calls=300):
     return {"rs_encode2": round(statistics.median(te[20:]) * 1e6, 1),
             "rs_decode2": round(statistics.median(td[20:]) * 1e6, 1),
             "calls": calls, "what": "one RS(20,10) 1250-B group per call, host buffers, "
-                                    "synchronous (pinned staging, H2D, kernel, D2H)"}
+                                    "synchronous"}
+
+
+def dropin_latency_both(u):
+    """The drop-in per-call latency through the one-kernel path (default:
+    pinned staging read over PCIe by one kernel, completion flag polled) and
+    through the staged copy path (H2D, kernel, D2H, stream sync)."""
+    L = u.lib()
+    prev = L.rsmi_set_option(3, 1)
+    try:
+        one = dropin_latency(u)
+        L.rsmi_set_option(3, 0)
+        staged = dropin_latency(u)
+    finally:
+        L.rsmi_set_option(3, prev)
+    one["what"] += ": one kernel reads pinned staging over PCIe, flag polled (oneshot.hip)"
+    one["staged_copy_path"] = {"rs_encode2": staged["rs_encode2"], "rs_decode2": staged["rs_decode2"],
+                               "what": "pinned staging, H2D, kernel, D2H, stream sync"}
+    return one
 
 
 def cpu_baseline(buf, present, G, threads):

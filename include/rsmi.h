@@ -69,6 +69,11 @@ const char *rsmi_last_error(void);
  * rows in one fused kernel where the code fits it, 0 forces the two-kernel
  * path (plan kernel + apply kernel). */
 #define RSMI_OPT_FUSED_DECODE 2
+/* RSMI_OPT_ONE_GROUP: 1 (default) runs single-group host calls (the level-1
+ * drop-in rs_encode2 / rs_decode2 / fec_*) as ONE kernel that reads pinned
+ * staging over PCIe and raises a completion flag (oneshot.hip); 0 takes the
+ * staged copy path (H2D, kernel, D2H). */
+#define RSMI_OPT_ONE_GROUP 3
 int rsmi_set_option(int option, int value);
 
 /* Host copy of fec_new(k,n)'s n x k systematic encoding matrix (row-major),
@@ -246,15 +251,27 @@ int rsmi_encode_pinned(int k, int n, const uint8_t *host_data, int64_t data_gs,
                        uint8_t *host_parity, int64_t parity_gs, int64_t shard_stride,
                        int len, int64_t ngroups, int64_t chunk_groups);
 
-/* Pipelined end-to-end decode from host memory: group g's n shard slots at
- * host_shards + g*shards_gs + j*shard_stride (erased slots may hold junk;
- * only the first k present are sent), present flags [ngroups][n]; missing
- * data rows are written back into their own host slots, status[g] receives
- * RSMI_DEC_*.  Only the k selected survivors travel H2D and only the rebuilt
- * rows travel D2H. */
+/* End-to-end decode from host memory: group g's n shard slots at
+ * host_shards + g*shards_gs + j*shard_stride (erased slots may hold junk),
+ * present flags [ngroups][n]; missing data rows are written back into their
+ * own host slots (the slot padding rule above applies to them), status[g]
+ * receives RSMI_DEC_*.  Synchronous.
+ *
+ * Pinned, device-mapped shards (hipHostMalloc, torch pin_memory,
+ * hipHostRegister) take the zero-copy path: the decode kernel reads only the
+ * k survivors it selects (the first k present, lib/rs.cpp:24-39) straight
+ * from host memory over PCIe and writes only the rebuilt rows back -- no
+ * staging copy.  Any other memory, or a code the fused kernel does not take,
+ * goes through the staged pipeline: chunks of chunk_groups groups H2D ->
+ * decode -> D2H of the data rows on three streams. */
 int rsmi_decode_pinned(int k, int n, uint8_t *host_shards, int64_t shards_gs,
                        int64_t shard_stride, int len, int64_t ngroups,
                        const uint8_t *present, int32_t *status, int64_t chunk_groups);
+
+/* Which path this thread's last rsmi_decode_pinned took. */
+#define RSMI_PINNED_ZERO_COPY 1
+#define RSMI_PINNED_STAGED 2
+int rsmi_last_decode_pinned_path(void);
 
 /* ---- synthetic inputs (bench / tests) ----------------------------------- */
 

@@ -9,7 +9,7 @@ root, names = sys.argv[1], sys.argv[2:]
 for p in sorted(glob.glob(f"{root}/p*/run_counter_collection.csv")):
     agg = collections.defaultdict(lambda: collections.defaultdict(float))
     for row in csv.DictReader(open(p)):
-        k = row["Kernel_Name"]
+        k = row["Kernel_Name"].replace("(anonymous namespace)", "anon")
         hit = [n for n in names if ("::" + n + "(") in k or ("::" + n + "<") in k
                or k.startswith(n + "(") or k.startswith(n + "<")]
         if not hit:

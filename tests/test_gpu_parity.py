@@ -626,6 +626,52 @@ def test_compat_pointer_permutation(gpu, golden, name):
     assert sha(after) == D[f"{name}__ptr_bufs_sha"].tobytes().hex()
 
 
+@pytest.mark.parametrize("one_group", [True, False])
+@pytest.mark.parametrize("k,n,ln", [(20, 30, 1250), (3, 6, 3), (1, 2, 1), (40, 60, 700),
+                                    (10, 16, 5000), (128, 255, 64), (7, 13, 100), (20, 30, 17)])
+def test_dropin_one_group_vs_oracle(gpu, oracle, one_group, k, n, ln):
+    """rs_encode2 / rs_decode2 of one group on non-codeword inputs, through
+    the one-kernel latency path (RSMI_OPT_ONE_GROUP, oneshot.hip: pinned
+    staging read over PCIe, completion flag) and through the staged copy path:
+    both bit-exact with the oracle.  Covers survivors beyond one register
+    chunk (k = 40), shards longer than 4 KiB (several column blocks), e > 8
+    (several row blocks) and a code outside the kernel's LDS budget
+    (k = 128, n = 255: it falls back)."""
+    import udpspeeder_amd as u
+    L = u.lib()
+    prev = L.rsmi_set_option(3, int(one_group))
+    try:
+        rng = np.random.default_rng(k * 31 + n + ln)
+        for trial in range(3):
+            rows = rng.integers(0, 256, (n, ln), dtype=np.uint8)
+            # encode
+            data = [bytearray(rows[j].tobytes()) for j in range(n)]
+            u.rs_encode2(k, n, data, ln)
+            ref = np.zeros((n, ln), np.uint8)
+            ref[:k] = rows[:k]
+            oracle.encode_batch(k, n, ref.reshape(-1), 0, ln, ln, 1)
+            for j in range(n):
+                assert bytes(data[j]) == ref[j].tobytes(), ("encode", trial, j)
+            # decode a non-codeword: up to min(k, m) erasures, data first
+            m = n - k
+            e = min(k, m, 1 + trial * 4)
+            er = [int(x) for x in rng.choice(k, e, replace=False)]
+            if m > e:  # and one parity shard, so the survivors skip it
+                er.append(k + int(rng.integers(0, m)))
+            present = np.ones(n, np.uint8)
+            present[er] = 0
+            buf = np.ascontiguousarray(rows.copy())
+            st_ref = oracle.decode_batch(k, n, buf.reshape(-1), 0, ln, ln, 1, present[None, :])
+            arr = [bytearray(rows[j].tobytes()) for j in range(n)]
+            ptrs = [arr[j] if present[j] else None for j in range(n)]
+            rc = u.rs_decode2(k, n, ptrs, ln)
+            assert rc == int(st_ref[0])
+            for j in range(k):
+                assert bytes(ptrs[j]) == buf[j].tobytes(), ("decode", trial, j)
+    finally:
+        L.rsmi_set_option(3, prev)
+
+
 def test_compat_lower_api(gpu, oracle):
     import udpspeeder_amd as u
     k, n, ln = 5, 9, 40
@@ -684,9 +730,51 @@ def test_decode_pinned_pipeline(gpu, oracle):
     orig = h[:, :k, :ln].clone()
     pres = synth.erasure_present(21, 0, G, n, 6)
     h[torch.from_numpy(pres == 0)] = 0xA5
+    before = h.clone()
     st = u.rs.decode_pinned(h, pres, k, n, ln, chunk_groups=1000)
+    assert u.lib().rsmi_last_decode_pinned_path() == 1  # zero-copy: pinned torch memory
     assert (st == 0).all()
     assert torch.equal(h[:, :k, :ln], orig)
+    # only the rebuilt data rows were written: every other slot is as it was
+    # (erased parity slots still hold the 0xA5 junk)
+    rebuilt = torch.from_numpy(pres == 0)
+    rebuilt[:, k:] = False
+    assert torch.equal(h[~rebuilt], before[~rebuilt])
+
+
+@pytest.mark.parametrize("pinned", [True, False])
+@pytest.mark.parametrize("k,n,ln,S,off", [(20, 30, 1250, 1280, 0), (10, 16, 1283, 1296, 7),
+                                          (7, 13, 100, 112, 3), (20, 30, 1250, 1280, 5)])
+def test_decode_pinned_noncodeword(gpu, oracle, pinned, k, n, ln, S, off):
+    """rsmi_decode_pinned on non-codewords (random parity, so the bytes pin
+    which survivors are used, lib/rs.cpp:24-39) against the oracle: pinned
+    torch memory (zero-copy path, also from an interior offset of the
+    allocation) and pageable numpy memory (staged path)."""
+    import torch
+    import udpspeeder_amd as u
+    from udpspeeder_amd import synth
+    G = 1500
+    rng = np.random.default_rng(k * 1000 + S + off)
+    raw = rng.integers(0, 256, ((G + off) * n * S,), dtype=np.uint8)
+    pres = synth.erasure_present(77 + k, 0, G, n, min(n - k, 6))
+    ref = raw[off * n * S:].copy()
+    st_ref = oracle.decode_batch(k, n, ref, n * S, S, ln, G, pres)
+    if pinned:
+        big = torch.from_numpy(raw).pin_memory()
+        h = big[off * n * S:].view(G, n, S)  # an interior pointer of the pinned block
+        st = u.rs.decode_pinned(h, pres, k, n, ln, chunk_groups=512)
+        out = h.numpy().reshape(-1)
+        want = 1
+    else:
+        h = raw[off * n * S:].reshape(G, n, S)
+        st = u.rs.decode_pinned(h, pres, k, n, ln, chunk_groups=512)
+        out = h.reshape(-1)
+        want = 2
+    assert u.lib().rsmi_last_decode_pinned_path() == want
+    assert (st == st_ref).all()
+    o = out.reshape(G, n, S)
+    r = ref.reshape(G, n, S)
+    assert (o[:, :k, :ln] == r[:, :k, :ln]).all()
 
 
 def test_host_batched_api(gpu, oracle):

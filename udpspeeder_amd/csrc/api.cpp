@@ -6,6 +6,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -23,6 +24,7 @@ namespace {
 
 thread_local std::string g_err;
 thread_local int g_last_enc = RSMI_ENC_NONE;  // rsmi_last_encoder
+std::atomic<int> g_opt_oneshot{1};              // RSMI_OPT_ONE_GROUP
 std::atomic<int> g_opt_bitslice{1};
 std::atomic<int> g_opt_fused{1};
 
@@ -84,7 +86,14 @@ struct Device {
     size_t hdev_bytes = 0;
     int32_t *hstatus_dev = nullptr;
     size_t hstatus_cap = 0;
-    Pipeline penc, pdec;
+    Pipeline penc, pdec, pzc;  // pzc: rsmi_decode_pinned's zero-copy path
+    // one group per call (oneshot.hip): pinned staging the kernel reads and
+    // writes over PCIe, a completion flag, guarded by one_mu
+    std::mutex one_mu;
+    hipStream_t one_stream = nullptr;
+    uint8_t *one_pin = nullptr, *one_dev = nullptr;  // host / device address of the staging
+    size_t one_bytes = 0;
+    uint32_t one_seq = 0;
 };
 
 std::mutex g_devs_mu;
@@ -333,9 +342,8 @@ int decode_ragged_dev(const rsmi_group *dg, int64_t ngroups, uint8_t *base,
     return RSMI_OK;
 }
 
-int decode_ragged_cls_dev(const rsmi_group *dg, int64_t ngroups, const uint32_t *cls_idx,
-                          const int64_t cls_first[5], uint8_t *base, const uint32_t *present_bits,
-                          int32_t *status, int kmax, hipStream_t s) {
+int decode_ragged_cls_dev(const rsmi_group *dg, int64_t ngroups, const ClsLaunch &C, uint8_t *base,
+                          const uint32_t *present_bits, int32_t *status, int kmax, hipStream_t s) {
     if (ngroups <= 0) return RSMI_OK;
     if (!base || !present_bits || !status)
         return fail(RSMI_ERR_INVALID, "null base/present_bits/status");
@@ -346,8 +354,8 @@ int decode_ragged_cls_dev(const rsmi_group *dg, int64_t ngroups, const uint32_t 
     // Classes run one after another on s: forking them over four streams
     // (event fork/join) measured slower, 0.240 vs 0.217 ms for C3.
     const hipStream_t cs[4] = {s, s, s, s};
-    hipError_t e = launch_decode_ragged_cls(dg, ngroups, cls_idx, cls_first, base, present_bits,
-                                            status, kmax, D->code_dir, D->ptab, D->gftab, s, cs);
+    hipError_t e = launch_decode_ragged_cls(dg, C, base, present_bits, status, kmax, D->code_dir,
+                                            D->ptab, D->gftab, s, cs);
     if (e == hipSuccess)
         e = launch_decode_ragged_big(dg, ngroups, base, present_bits, status, D->code_dir, D->ptab,
                                      D->gftab, s);
@@ -395,6 +403,95 @@ int host_buffers(Device &D, size_t bytes, int64_t ngroups) {
 }
 }  // namespace
 
+// One group, host buffers, one kernel (oneshot.hip): the shards the kernel
+// needs are copied into pinned staging, the kernel reads them over PCIe,
+// writes the output rows back into staging and raises a flag this thread
+// spins on.  Returns 1 when the code/shape is outside the kernel's range (the
+// caller takes the staged path), else RSMI_OK or an error.
+int one_group_op(Device &D, bool decode, int k, int n, uint8_t *const *ptrs, uint8_t *const *out,
+                 int len, const uint8_t *present, int32_t *status) {
+    const int ss = (len + 15) & ~15;
+    if (!one_group_ok(k, n, len, ss > 0 ? ss : 16, !decode)) return 1;
+    const Code *C;
+    int rc;
+    {
+        std::lock_guard<std::mutex> lk(D.mu);
+        rc = ensure_code(D, k, n, &C);
+        if (rc) return rc;
+    }
+    std::lock_guard<std::mutex> lk(D.one_mu);
+    const int m = n - k;
+    const size_t in_bytes = (size_t)n * ss, out_bytes = (size_t)(decode ? k : m) * ss;
+    const size_t need = in_bytes + out_bytes + 64;
+    if (!D.one_stream)
+        RSMI_HIP(hipStreamCreateWithFlags(&D.one_stream, hipStreamNonBlocking), "hipStreamCreate(one)");
+    if (D.one_bytes < need) {
+        if (D.one_pin) (void)hipHostFree(D.one_pin);
+        D.one_pin = D.one_dev = nullptr;
+        D.one_bytes = 0;
+        const size_t cap = std::max<size_t>(need, 64 * 1024);
+        RSMI_HIP(hipHostMalloc(&D.one_pin, cap, hipHostMallocDefault), "hipHostMalloc(one)");
+        void *dp = nullptr;
+        RSMI_HIP(hipHostGetDevicePointer(&dp, D.one_pin, 0), "hipHostGetDevicePointer(one)");
+        D.one_dev = static_cast<uint8_t *>(dp);
+        D.one_bytes = cap;
+        std::memset(D.one_pin, 0, cap);
+    }
+    uint8_t *in = D.one_pin, *rows = D.one_pin + in_bytes;
+    uint8_t *tail = D.one_pin + D.one_bytes - 64;  // status | flag
+    volatile uint32_t *flag = reinterpret_cast<volatile uint32_t *>(tail + 32);
+    OneArgs a{};
+    a.in = D.one_dev;
+    a.out = D.one_dev + in_bytes;
+    a.rows = C->dev_rows;
+    a.ptab = D.ptab;
+    a.gftab = D.gftab;
+    a.status = reinterpret_cast<int32_t *>(D.one_dev + (tail - D.one_pin));
+    a.flag = reinterpret_cast<uint32_t *>(D.one_dev + (tail + 32 - D.one_pin));
+    a.seq = ++D.one_seq;
+    a.k = k;
+    a.n = n;
+    a.len = len;
+    a.ss = ss > 0 ? ss : 16;
+    a.encode = decode ? 0 : 1;
+    if (decode) {
+        // only the survivors the kernel will read: the first k present (rs.cpp:24-39)
+        int cnt = 0;
+        for (int j = 0; j < n; ++j) {
+            if (!present[j]) continue;
+            a.present[j >> 5] |= 1u << (j & 31);
+            if (cnt++ < k && len) std::memcpy(in + (size_t)j * ss, ptrs[j], (size_t)len);
+        }
+    } else if (len) {
+        for (int j = 0; j < k; ++j) std::memcpy(in + (size_t)j * ss, ptrs[j], (size_t)len);
+    }
+    std::atomic_thread_fence(std::memory_order_release);
+    hipError_t e = launch_one_group(a, D.one_stream);
+    if (e != hipSuccess) return hip_fail(e, "one-group kernel launch");
+    // spin on the flag; a kernel that never raises it surfaces its error
+    // through the stream after a bound
+    const auto t0 = std::chrono::steady_clock::now();
+    while (*flag != a.seq) {
+        __builtin_ia32_pause();
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) {
+            RSMI_HIP(hipStreamSynchronize(D.one_stream), "one-group kernel");
+            if (*flag != a.seq) return fail(RSMI_ERR_HIP, "one-group kernel did not complete");
+        }
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
+    const int32_t st = *reinterpret_cast<volatile int32_t *>(tail);
+    if (status) *status = st;
+    if (decode) {
+        if (st != RSMI_DEC_OK || !len) return RSMI_OK;
+        int r = 0;  // rebuilt rows come out in ascending missing-index order
+        for (int j = 0; j < k; ++j)
+            if (!present[j]) std::memcpy(out[j], rows + (size_t)(r++) * ss, (size_t)len);
+    } else if (len) {
+        for (int j = k; j < n; ++j) std::memcpy(ptrs[j], rows + (size_t)(j - k) * ss, (size_t)len);
+    }
+    return RSMI_OK;
+}
+
 // Gather host shards into a packed device layout [g][n][ss] (ss =
 // round_up(len,16)), run the device op on the internal stream, scatter back.
 // ptrs[g*n + j] is shard j of group g (may be null for an erased shard when
@@ -409,6 +506,10 @@ int host_op_ptrs(bool decode, int k, int n, uint8_t *const *ptrs, uint8_t *const
     int rc;
     Device *D = current(&rc);
     if (!D) return rc;
+    if (ngroups == 1 && n > k && g_opt_oneshot.load()) {
+        rc = one_group_op(*D, decode, k, n, ptrs, out, len, present, status);
+        if (rc != 1) return rc;
+    }
     std::lock_guard<std::mutex> hl(D->hmu);
     const int64_t ss = len > 0 ? (len + 15) / 16 * 16 : 16;
     const int64_t dgs = ss * n;
@@ -518,6 +619,116 @@ int encode_pinned(int k, int n, const uint8_t *hd, int64_t dgs, uint8_t *hp, int
     return RSMI_OK;
 }
 
+int decode_zero_copy(Device &D, int k, int n, uint8_t *hs_dev, int64_t hgs, int64_t ss, int len,
+                     int64_t ngroups, const uint8_t *present, int32_t *status) {
+    Pipeline &P = D.pzc;  // one call at a time per device
+    std::lock_guard<std::mutex> lk(P.mu);
+    const Code *C;
+    int rc;
+    {
+        std::lock_guard<std::mutex> dl(D.mu);
+        rc = ensure_code(D, k, n, &C);
+        if (rc) return rc;
+    }
+    // present flags and statuses go through pinned staging in chunks of up
+    // to kChunk groups (a few MB of device buffers, whatever the batch)
+    constexpr int64_t kChunk = 1 << 18;
+    const int64_t cap = std::min<int64_t>(ngroups, kChunk);
+    if (P.cap < cap) {
+        for (int i = 0; i < 2; ++i) {
+            if (P.dstat[i]) (void)hipFree(P.dstat[i]);
+            if (P.dpres[i]) (void)hipFree(P.dpres[i]);
+            P.dstat[i] = nullptr;
+            P.dpres[i] = nullptr;
+        }
+        if (P.hpin) (void)hipHostFree(P.hpin);
+        P.hpin = nullptr;
+        P.cap = 0;
+        for (int i = 0; i < 2; ++i) {
+            RSMI_HIP(hipMalloc(&P.dstat[i], sizeof(int32_t) * (size_t)cap), "hipMalloc(status)");
+            RSMI_HIP(hipMalloc(&P.dpres[i], (size_t)(256 * cap)), "hipMalloc(present)");
+        }
+        RSMI_HIP(hipHostMalloc(&P.hpin, 2 * (size_t)(256 + 4) * (size_t)cap, hipHostMallocDefault),
+                 "hipHostMalloc(pin)");
+        P.cap = cap;
+    }
+    for (int i = 0; i < 2; ++i)
+        if (!P.st[i]) RSMI_HIP(hipStreamCreateWithFlags(&P.st[i], hipStreamNonBlocking),
+                               "hipStreamCreate(zero-copy)");
+    // two chunks in flight: staging of chunk c+1's flags overlaps chunk c's kernel
+    uint8_t *hp[2] = {P.hpin, P.hpin + (size_t)(256 + 4) * (size_t)cap};
+    int64_t prev_g0[2] = {-1, -1}, prev_cnt[2] = {0, 0};
+    auto finish = [&](int b) -> int {
+        if (prev_g0[b] < 0) return RSMI_OK;
+        RSMI_HIP(hipStreamSynchronize(P.st[b]), "hipStreamSynchronize(zero-copy)");
+        if (status)
+            std::memcpy(status + prev_g0[b], hp[b] + (size_t)n * cap, sizeof(int32_t) * (size_t)prev_cnt[b]);
+        prev_g0[b] = -1;
+        return RSMI_OK;
+    };
+    int64_t c = 0;
+    for (int64_t g0 = 0; g0 < ngroups; g0 += cap, ++c) {
+        const int64_t cnt = std::min(cap, ngroups - g0);
+        const int b = (int)(c & 1);
+        rc = finish(b);
+        if (rc) return rc;
+        hipStream_t s = P.st[b];
+        std::memcpy(hp[b], present + g0 * n, (size_t)(n * cnt));
+        RSMI_HIP(hipMemcpyAsync(P.dpres[b], hp[b], (size_t)(n * cnt), hipMemcpyHostToDevice, s),
+                 "H2D present");
+        int W;
+        UniformArgs a = make_args(k, n, hs_dev + g0 * hgs, hgs, ss, len, cnt, &W);
+        hipError_t e = launch_decode_fused(a, P.dpres[b], C->dev_rows, P.dstat[b], D.ptab, D.gftab, s,
+                                           /*host_shards=*/true);
+        if (e != hipSuccess) return hip_fail(e, "zero-copy decode launch");
+        RSMI_HIP(hipMemcpyAsync(hp[b] + (size_t)n * cap, P.dstat[b], sizeof(int32_t) * (size_t)cnt,
+                                hipMemcpyDeviceToHost, s), "D2H status");
+        prev_g0[b] = g0;
+        prev_cnt[b] = cnt;
+    }
+    for (int b = 0; b < 2; ++b) {
+        rc = finish(b);
+        if (rc) return rc;
+    }
+    return RSMI_OK;
+}
+
+// The device address of host range [p, p + bytes) when all of it lies in one
+// pinned, device-mapped allocation (hipHostMalloc, torch pin_memory,
+// hipHostRegister'ed), else nullptr: a kernel may then read and write it over
+// PCIe.  Anything else (pageable memory, a range running past the allocation)
+// never reaches a kernel.
+uint8_t *mapped_host_range(uint8_t *p, size_t bytes) {
+    const bool dbg = getenv("RSMI_DEBUG_PINNED") != nullptr;
+    hipPointerAttribute_t at;
+    hipError_t e = hipPointerGetAttributes(&at, p);
+    if (e != hipSuccess) {
+        if (dbg) fprintf(stderr, "rsmi: pinned? %p: hipPointerGetAttributes %d\n", (void *)p, (int)e);
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    if (dbg)
+        fprintf(stderr, "rsmi: pinned? %p: type %d dev %p host %p flags %u\n", (void *)p, (int)at.type,
+                at.devicePointer, at.hostPointer, at.allocationFlags);
+    if (at.type != hipMemoryTypeHost || !at.devicePointer || !at.hostPointer) return nullptr;
+    void *start = nullptr;
+    size_t size = 0;
+    hipError_t e1 = hipPointerGetAttribute(&start, HIP_POINTER_ATTRIBUTE_RANGE_START_ADDR, (hipDeviceptr_t)p);
+    hipError_t e2 = hipPointerGetAttribute(&size, HIP_POINTER_ATTRIBUTE_RANGE_SIZE, (hipDeviceptr_t)p);
+    if (dbg)
+        fprintf(stderr, "rsmi: pinned? range %d %d start %p size %zu need %zu\n", (int)e1, (int)e2, start,
+                size, bytes);
+    if (e1 != hipSuccess || e2 != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    const uint8_t *s0 = static_cast<const uint8_t *>(start);
+    if (!s0 || p < s0 || p + bytes > s0 + size) return nullptr;
+    return static_cast<uint8_t *>(at.devicePointer) + (p - static_cast<uint8_t *>(at.hostPointer));
+}
+
+thread_local int g_last_pinned = 0;  // rsmi_last_decode_pinned_path
+
 int decode_pinned(int k, int n, uint8_t *hs, int64_t hgs, int64_t ss, int len, int64_t ngroups,
                   const uint8_t *present, int32_t *status, int64_t chunk) {
     int rc = check_uniform(k, n, nullptr, 16, ss, len, 0);
@@ -527,6 +738,15 @@ int decode_pinned(int k, int n, uint8_t *hs, int64_t hgs, int64_t ss, int len, i
     if (ngroups == 0) return RSMI_OK;
     Device *D = current(&rc);
     if (!D) return rc;
+    // Zero-copy: shards in pinned host memory are read by the fused decode
+    // kernel itself over PCIe -- only the k survivors it selects (lib/rs.cpp:
+    // 24-39) -- and it writes only the rebuilt rows back; nothing is staged.
+    uint8_t *hs_dev = nullptr;
+    if (g_opt_fused.load() && n > k && decode_fused_ok(k, n, hgs, ss, len) && hgs % 16 == 0 &&
+        (uintptr_t)hs % 16 == 0)
+        hs_dev = mapped_host_range(hs, (size_t)((ngroups - 1) * hgs + (int64_t)n * ss));
+    g_last_pinned = hs_dev ? RSMI_PINNED_ZERO_COPY : RSMI_PINNED_STAGED;
+    if (hs_dev) return decode_zero_copy(*D, k, n, hs_dev, hgs, ss, len, ngroups, present, status);
     Pipeline &P = D->pdec;  // this device's decode pipeline, one call at a time
     std::lock_guard<std::mutex> lk(P.mu);
     int32_t **dstat = P.dstat;
@@ -610,6 +830,7 @@ int rsmi_version(void) { return 0x000100; }
 int rsmi_set_option(int option, int value) {
     if (option == RSMI_OPT_BITSLICE) return rsmi::g_opt_bitslice.exchange(value ? 1 : 0);
     if (option == RSMI_OPT_FUSED_DECODE) return rsmi::g_opt_fused.exchange(value ? 1 : 0);
+    if (option == RSMI_OPT_ONE_GROUP) return rsmi::g_opt_oneshot.exchange(value ? 1 : 0);
     rsmi::set_error("unknown option");
     return RSMI_ERR_INVALID;
 }
@@ -653,6 +874,8 @@ int rsmi_decode_matrix(int k, int n, const uint8_t *present, uint8_t *sel, uint8
 int rsmi_prepare_code(int k, int n) { return rsmi::prepare_code(k, n); }
 
 int rsmi_last_encoder(void) { return rsmi::g_last_enc; }
+
+int rsmi_last_decode_pinned_path(void) { return rsmi::g_last_pinned; }
 
 int rsmi_reserve(int k, int n, int64_t ngroups, void *stream) {
     return rsmi::reserve(k, n, ngroups, (hipStream_t)stream);

@@ -387,6 +387,11 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t group_rsrc(const uint8_t *gbas
 
 // The uniform kernel keeps its own straight-line form (not Rebuild / the
 // helper functions): written that way it fits 4 waves/SIMD without spills.
+// LDAUX / STAUX: cache policy of the survivor loads and rebuilt-row stores --
+// DEC_LD_AUX / DEC_ST_AUX for HBM; sc0|sc1 (system scope, coherent with the
+// host) when the shards are pinned host memory read over PCIe
+// (rsmi_decode_pinned's zero-copy path).
+template <int LDAUX, int STAUX>
 __global__ __launch_bounds__(256, DEC_OCC) void k_decode_fused(UniformArgs a, const uint8_t *present,
                                                       const uint8_t *prows, int32_t *status_out,
                                                       const uint32_t *ptab, const uint8_t *gftab) {
@@ -495,8 +500,8 @@ __global__ __launch_bounds__(256, DEC_OCC) void k_decode_fused(UniformArgs a, co
             for (int q = 0; q < kRing; ++q) {
                 if (q < k) {
                     const uint32_t so = __builtin_amdgcn_readlane(so_lane, q);
-                    rq[q] = __builtin_amdgcn_raw_buffer_load_b128(DEC_NOMEM ? rsrc0 : rsrc, v16, DEC_NOMEM ? 0u : so, DEC_LD_AUX);
-                    rd[q] = __builtin_amdgcn_raw_buffer_load_b32(DEC_NOMEM ? rsrc0 : rsrc, v4, DEC_NOMEM ? 0u : so, DEC_LD_AUX);
+                    rq[q] = __builtin_amdgcn_raw_buffer_load_b128(DEC_NOMEM ? rsrc0 : rsrc, v16, DEC_NOMEM ? 0u : so, LDAUX);
+                    rd[q] = __builtin_amdgcn_raw_buffer_load_b32(DEC_NOMEM ? rsrc0 : rsrc, v4, DEC_NOMEM ? 0u : so, LDAUX);
                 }
             }
         };
@@ -624,8 +629,8 @@ __global__ __launch_bounds__(256, DEC_OCC) void k_decode_fused(UniformArgs a, co
         auto refill = [&](int q, int j) {
             if (j + kRing < k) {
                 const uint32_t so = __builtin_amdgcn_readlane(so_lane, j + kRing);
-                rq[q] = __builtin_amdgcn_raw_buffer_load_b128(DEC_NOMEM ? rsrc0 : rsrc, v16, DEC_NOMEM ? 0u : so, DEC_LD_AUX);
-                rd[q] = __builtin_amdgcn_raw_buffer_load_b32(DEC_NOMEM ? rsrc0 : rsrc, v4, DEC_NOMEM ? 0u : so, DEC_LD_AUX);
+                rq[q] = __builtin_amdgcn_raw_buffer_load_b128(DEC_NOMEM ? rsrc0 : rsrc, v16, DEC_NOMEM ? 0u : so, LDAUX);
+                rd[q] = __builtin_amdgcn_raw_buffer_load_b32(DEC_NOMEM ? rsrc0 : rsrc, v4, DEC_NOMEM ? 0u : so, LDAUX);
             }
         };
         for (int toff = 0; toff < a.len; toff += kTile) {
@@ -700,11 +705,11 @@ __global__ __launch_bounds__(256, DEC_OCC) void k_decode_fused(UniformArgs a, co
                         const uint32_t so = __builtin_amdgcn_readlane(mo_lane, rb + r);
                         const u32x4 v = {acc[r][0], acc[r][1], acc[r][2], acc[r][3]};
 #if DEC_ST_SGPR
-                        __builtin_amdgcn_raw_buffer_store_b128(v, rsrc, v16, so, DEC_ST_AUX);
-                        __builtin_amdgcn_raw_buffer_store_b32(acc[r][4], rsrc, v4, so, DEC_ST_AUX);
+                        __builtin_amdgcn_raw_buffer_store_b128(v, rsrc, v16, so, STAUX);
+                        __builtin_amdgcn_raw_buffer_store_b32(acc[r][4], rsrc, v4, so, STAUX);
 #else
-                        __builtin_amdgcn_raw_buffer_store_b128(v, rsrc, v16 + so, 0, DEC_ST_AUX);
-                        __builtin_amdgcn_raw_buffer_store_b32(acc[r][4], rsrc, v4 + so, 0, DEC_ST_AUX);
+                        __builtin_amdgcn_raw_buffer_store_b128(v, rsrc, v16 + so, 0, STAUX);
+                        __builtin_amdgcn_raw_buffer_store_b32(acc[r][4], rsrc, v4 + so, 0, STAUX);
 #endif
                     }
                 }
@@ -837,22 +842,27 @@ __global__ __launch_bounds__(256, DEC_RAG_OCC) void k_decode_ragged(
     }
 }
 
-// Plans: the groups of one tile-width class (idx[0..count)), registers cut
-// for that width so short groups run at up to 8 waves per SIMD: C3's groups
-// are latency-bound (descriptor -> code rows -> inversion -> a few survivors).
+// Plans: the groups of one tile-width class, registers cut for that width so
+// short groups run at up to 8 waves per SIMD: C3's groups are latency-bound
+// (descriptor -> code rows -> inversion -> a few survivors).  Wave w takes the
+// groups idx[wst[w] .. wst[w+1]) the plan dealt it (ragged.cpp: balanced so
+// that the one resident round of waves ends together).
 template <int W, int OCC>
 __global__ __launch_bounds__(256, OCC) void k_decode_ragged_cls(
-    const rsmi_group *__restrict__ groups, const uint32_t *__restrict__ idx, int64_t count,
-    uint8_t *base, const uint32_t *__restrict__ present, int32_t *status_out,
-    const uint64_t *__restrict__ code_dir, const uint32_t *ptab, const uint8_t *gftab, int kmax) {
+    const rsmi_group *__restrict__ groups, const uint32_t *__restrict__ idx,
+    const uint32_t *__restrict__ wst, int nw, uint8_t *base, const uint32_t *__restrict__ present,
+    int32_t *status_out, const uint64_t *__restrict__ code_dir, const uint32_t *ptab,
+    const uint8_t *gftab, int kmax) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const Tables T = load_tables(smem, ptab, gftab);
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     const WaveLds L = rag_slice(smem + kTabBytes + wid * rag_lds_bytes(kmax, kClsRows), kmax, kClsRows);
     __syncthreads();
-    const int64_t nwaves = (int64_t)gridDim.x * kWaves;
-    for (int64_t i = (int64_t)blockIdx.x * kWaves + wid; i < count; i += nwaves) {
+    const int w = blockIdx.x * kWaves + wid;
+    if (w >= nw) return;
+    const uint32_t i1 = wst[w + 1];
+    for (uint32_t i = wst[w]; i < i1; ++i) {
         const int64_t g = __builtin_amdgcn_readfirstlane(idx[i]);
         const rsmi_group d = groups[g];
         ragged_group<W, kClsRows>(g, d, present[g * 8 + (lane & 7)], base, status_out, code_dir, T,
@@ -1002,15 +1012,20 @@ bool decode_fused_ok(int k, int n, int64_t group_stride, int64_t shard_stride, i
 
 hipError_t launch_decode_fused(const UniformArgs &a, const uint8_t *present,
                                const uint8_t *parity_rows, int32_t *status,
-                               const uint32_t *ptab, const uint8_t *gftab, hipStream_t s) {
+                               const uint32_t *ptab, const uint8_t *gftab, hipStream_t s,
+                               bool host_shards) {
     const size_t lds = kTabBytes + (size_t)(((a.n - a.k) * a.k + 15) & ~15) +
                        (size_t)kWaves * wave_lds_bytes(a.k);
     int64_t blocks = (a.ngroups + kWaves - 1) / kWaves;
     const int64_t cap = 256 * 8;
     if (blocks > cap) blocks = cap;
     if (blocks < 1) blocks = 1;
-    k_decode_fused<<<(unsigned)blocks, 64 * kWaves, lds, s>>>(a, present, parity_rows, status,
-                                                             ptab, gftab);
+    if (host_shards)
+        k_decode_fused<3, 3><<<(unsigned)blocks, 64 * kWaves, lds, s>>>(a, present, parity_rows,
+                                                                      status, ptab, gftab);
+    else
+        k_decode_fused<DEC_LD_AUX, DEC_ST_AUX><<<(unsigned)blocks, 64 * kWaves, lds, s>>>(
+            a, present, parity_rows, status, ptab, gftab);
     return hipGetLastError();
 }
 
@@ -1036,29 +1051,28 @@ hipError_t launch_decode_ragged(const rsmi_group *groups, int64_t ngroups, uint8
                                     gftab, s);
 }
 
-hipError_t launch_decode_ragged_cls(const rsmi_group *groups, int64_t ngroups,
-                                    const uint32_t *cls_idx, const int64_t cls_first[5],
-                                    uint8_t *base, const uint32_t *present_bits, int32_t *status,
-                                    int kmax, const uint64_t *code_dir, const uint32_t *ptab,
+int decode_cls_occupancy(int c) {
+    static const int occ[4] = {DEC_CLS_OCC1, DEC_CLS_OCC2, DEC_CLS_OCC4, DEC_CLS_OCC5};
+    return occ[c & 3];
+}
+
+hipError_t launch_decode_ragged_cls(const rsmi_group *groups, const ClsLaunch &C, uint8_t *base,
+                                    const uint32_t *present_bits, int32_t *status, int kmax,
+                                    const uint64_t *code_dir, const uint32_t *ptab,
                                     const uint8_t *gftab, hipStream_t s, const hipStream_t cs[4]) {
-    if (ngroups <= 0) return hipSuccess;
     kmax = kmax < 1 ? 1 : (kmax > 32 ? 32 : kmax);  // larger k: the workgroup kernel
     const size_t lds = kTabBytes + (size_t)kWaves * rag_lds_bytes(kmax, kClsRows);
-    auto launch = [&](auto kern, int c, int occ) {
-        const int64_t count = cls_first[c + 1] - cls_first[c];
-        if (count <= 0) return hipSuccess;
-        int64_t blocks = (count + kWaves - 1) / kWaves;
-        const int64_t cap = 256 * (int64_t)occ;  // one round of resident blocks
-        if (blocks > cap) blocks = cap;
-        kern<<<(unsigned)blocks, 64 * kWaves, lds, cs[c]>>>(groups, cls_idx + cls_first[c], count, base,
-                                                       present_bits, status, code_dir, ptab, gftab,
-                                                       kmax);
+    auto launch = [&](auto kern, int c) {
+        const int nw = C.nw[c];
+        if (nw <= 0) return hipSuccess;
+        kern<<<(unsigned)((nw + kWaves - 1) / kWaves), 64 * kWaves, lds, cs[c]>>>(
+            groups, C.idx, C.wst[c], nw, base, present_bits, status, code_dir, ptab, gftab, kmax);
         return hipGetLastError();
     };
-    hipError_t e = launch(k_decode_ragged_cls<5, DEC_CLS_OCC5>, 3, DEC_CLS_OCC5);
-    if (e == hipSuccess) e = launch(k_decode_ragged_cls<4, DEC_CLS_OCC4>, 2, DEC_CLS_OCC4);
-    if (e == hipSuccess) e = launch(k_decode_ragged_cls<2, DEC_CLS_OCC2>, 1, DEC_CLS_OCC2);
-    if (e == hipSuccess) e = launch(k_decode_ragged_cls<1, DEC_CLS_OCC1>, 0, DEC_CLS_OCC1);
+    hipError_t e = launch(k_decode_ragged_cls<5, DEC_CLS_OCC5>, 3);
+    if (e == hipSuccess) e = launch(k_decode_ragged_cls<4, DEC_CLS_OCC4>, 2);
+    if (e == hipSuccess) e = launch(k_decode_ragged_cls<2, DEC_CLS_OCC2>, 1);
+    if (e == hipSuccess) e = launch(k_decode_ragged_cls<1, DEC_CLS_OCC1>, 0);
     return e;
 }
 

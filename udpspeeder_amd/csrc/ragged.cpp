@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <utility>
 #include <cstring>
 #include <map>
 #include <string>
@@ -29,9 +30,8 @@ void set_error(const std::string &m);
 uint64_t *device_code_dir(int *rc);
 int decode_ragged_dev(const rsmi_group *dg, int64_t ngroups, uint8_t *base,
                       const uint32_t *present_bits, int32_t *status, int kmax, hipStream_t s);
-int decode_ragged_cls_dev(const rsmi_group *dg, int64_t ngroups, const uint32_t *cls_idx,
-                          const int64_t cls_first[5], uint8_t *base, const uint32_t *present_bits,
-                          int32_t *status, int kmax, hipStream_t s);
+int decode_ragged_cls_dev(const rsmi_group *dg, int64_t ngroups, const ClsLaunch &C, uint8_t *base,
+                          const uint32_t *present_bits, int32_t *status, int kmax, hipStream_t s);
 const uint32_t *device_ptab(int *rc);
 }  // namespace rsmi
 
@@ -52,9 +52,9 @@ struct rsmi_ragged_plan {
     rsmi_group *d_groups = nullptr;
     uint32_t *d_colmap = nullptr;
     uint32_t *d_waves = nullptr;
-    // decode: group indices by tile-width class (rag_width), class c at
-    // [cls_first[c], cls_first[c+1]) of d_cls
-    int64_t cls_first[5] = {0, 0, 0, 0, 0};
+    // decode: group indices by tile-width class (rag_width), dealt to waves
+    // (d_cls, wave-major; class c's wave offsets at d_wst + wst_first[c])
+    rsmi::ClsLaunch cls{};
     uint32_t *d_cls = nullptr;
 };
 
@@ -169,28 +169,69 @@ extern "C" int rsmi_ragged_plan_create(const rsmi_group *g, int64_t ngroups,
         P->nwaves = (uint32_t)(waves.size() / 2);
         if (nb <= nbuiltin) P->nwaves_builtin = P->nwaves;
     }
-    // decode classes: the width each group's tiles take (decode.hip)
-    std::vector<uint32_t> cls((size_t)ngroups);
+    // decode classes: the width each group's tiles take (decode.hip).  Each
+    // class kernel runs one resident round of waves; the class's groups are
+    // dealt to those waves longest-first onto the least-loaded wave, on an
+    // estimated cost, so the round ends together (a strided deal left the
+    // average wave alive for 53-67 % of its kernel: profiles/r03).
+    std::vector<uint32_t> cls, wst;
+    int64_t wst_first[4] = {0, 0, 0, 0};
     {
-        int64_t cnt[4] = {0, 0, 0, 0};
-        std::vector<uint8_t> c_of((size_t)ngroups);
-        for (int64_t i = 0; i < ngroups; ++i) {
-            const int c = rsmi::rag_width_class(rsmi::rag_width(rsmi::rag_lpad(g[i].len, g[i].shard_stride)));
-            c_of[(size_t)i] = (uint8_t)c;
-            ++cnt[c];
+        int ncu = 0;
+        if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, P->device) != hipSuccess ||
+            ncu < 1)
+            ncu = 256;
+        std::vector<std::vector<uint32_t>> by((size_t)4);
+        for (int64_t i = 0; i < ngroups; ++i)
+            by[(size_t)rsmi::rag_width_class(
+                   rsmi::rag_width(rsmi::rag_lpad(g[i].len, g[i].shard_stride)))]
+                .push_back((uint32_t)i);
+        cls.reserve((size_t)ngroups);
+        for (int c = 0; c < 4; ++c) {
+            auto &v = by[(size_t)c];
+            const int W = c == 0 ? 1 : (c == 1 ? 2 : (c == 2 ? 4 : 5));
+            const int64_t slots = (int64_t)ncu * 4 * rsmi::decode_cls_occupancy(c);
+            const int nw = (int)std::min<int64_t>((int64_t)v.size(), slots);
+            P->cls.nw[c] = nw;
+            wst_first[c] = (int64_t)wst.size();
+            if (nw == 0) {
+                wst.push_back((uint32_t)cls.size());
+                continue;
+            }
+            // cost: a fixed chain (descriptor, flags, code rows, elimination)
+            // plus per survivor a load and a W-dword multiply
+            auto cost = [&](uint32_t i) { return 24.0 + g[i].k * (2.0 + W); };
+            std::stable_sort(v.begin(), v.end(), [&](uint32_t a, uint32_t b) { return cost(a) > cost(b); });
+            std::vector<std::vector<uint32_t>> lists((size_t)nw);
+            std::vector<std::pair<double, int>> heap;  // (load, wave), min-heap
+            heap.reserve((size_t)nw);
+            for (int w = 0; w < nw; ++w) heap.push_back({0.0, w});
+            auto gt = [](const std::pair<double, int> &a, const std::pair<double, int> &b) {
+                return a.first > b.first || (a.first == b.first && a.second > b.second);
+            };
+            for (uint32_t i : v) {
+                std::pop_heap(heap.begin(), heap.end(), gt);
+                heap.back().first += cost(i);
+                lists[(size_t)heap.back().second].push_back(i);
+                std::push_heap(heap.begin(), heap.end(), gt);
+            }
+            for (int w = 0; w < nw; ++w) {
+                wst.push_back((uint32_t)cls.size());
+                cls.insert(cls.end(), lists[(size_t)w].begin(), lists[(size_t)w].end());
+            }
+            wst.push_back((uint32_t)cls.size());
         }
-        for (int c = 0; c < 4; ++c) P->cls_first[c + 1] = P->cls_first[c] + cnt[c];
-        int64_t fill[4] = {P->cls_first[0], P->cls_first[1], P->cls_first[2], P->cls_first[3]};
-        for (int64_t i = 0; i < ngroups; ++i) cls[(size_t)fill[c_of[(size_t)i]]++] = (uint32_t)i;
     }
     const size_t gbytes = sizeof(rsmi_group) * (size_t)ngroups;
     const size_t cbytes = sizeof(uint32_t) * colmap.size();
     const size_t wbytes = sizeof(uint32_t) * waves.size();
     const size_t dbytes = sizeof(uint32_t) * cls.size();
+    const size_t sbytes = sizeof(uint32_t) * wst.size();
     const size_t goff = 0, coff = (gbytes + 255) & ~size_t(255),
                  woff = (coff + cbytes + 255) & ~size_t(255),
-                 doff = (woff + wbytes + 255) & ~size_t(255);
-    const size_t all = doff + dbytes + 16;
+                 doff = (woff + wbytes + 255) & ~size_t(255),
+                 soff = (doff + dbytes + 255) & ~size_t(255);
+    const size_t all = soff + sbytes + 16;
     if (hipMalloc(&P->mem, all) != hipSuccess) {
         delete P;
         return fail(RSMI_ERR_NOMEM, "hipMalloc(ragged plan)");
@@ -199,6 +240,9 @@ extern "C" int rsmi_ragged_plan_create(const rsmi_group *g, int64_t ngroups,
     P->d_colmap = reinterpret_cast<uint32_t *>(P->mem + coff);
     P->d_waves = reinterpret_cast<uint32_t *>(P->mem + woff);
     P->d_cls = reinterpret_cast<uint32_t *>(P->mem + doff);
+    uint32_t *d_wst = reinterpret_cast<uint32_t *>(P->mem + soff);
+    P->cls.idx = P->d_cls;
+    for (int c = 0; c < 4; ++c) P->cls.wst[c] = d_wst + wst_first[c];
     hipError_t e = hipSuccess;
     if (gbytes) e = hipMemcpy(P->d_groups, g, gbytes, hipMemcpyHostToDevice);
     if (e == hipSuccess && cbytes) e = hipMemcpy(P->d_colmap, colmap.data(), cbytes,
@@ -207,6 +251,7 @@ extern "C" int rsmi_ragged_plan_create(const rsmi_group *g, int64_t ngroups,
                                                  hipMemcpyHostToDevice);
     if (e == hipSuccess && dbytes) e = hipMemcpy(P->d_cls, cls.data(), dbytes,
                                                  hipMemcpyHostToDevice);
+    if (e == hipSuccess && sbytes) e = hipMemcpy(d_wst, wst.data(), sbytes, hipMemcpyHostToDevice);
     if (e != hipSuccess) {
         (void)hipFree(P->mem);
         delete P;
@@ -248,8 +293,8 @@ extern "C" int rsmi_decode_ragged_plan(const rsmi_ragged_plan *P, uint8_t *base,
                                        void *stream) {
     if (!P) return fail(RSMI_ERR_INVALID, "null plan");
     if (RSMI_DEC_CLASSES)
-        return rsmi::decode_ragged_cls_dev(P->d_groups, P->ngroups, P->d_cls, P->cls_first, base,
-                                           present_bits, status, P->kmax, (hipStream_t)stream);
+        return rsmi::decode_ragged_cls_dev(P->d_groups, P->ngroups, P->cls, base, present_bits, status,
+                                           P->kmax, (hipStream_t)stream);
     return rsmi::decode_ragged_dev(P->d_groups, P->ngroups, base, present_bits, status, P->kmax,
                                    (hipStream_t)stream);
 }

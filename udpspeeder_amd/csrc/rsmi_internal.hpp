@@ -54,9 +54,12 @@ hipError_t launch_fill_ragged(const rsmi_group *groups, int64_t ngroups, uint8_t
 
 // Fused decode (plan + reconstruction in one wave per group, decode.hip).
 bool decode_fused_ok(int k, int n, int64_t group_stride, int64_t shard_stride, int len);
+// host_shards: a.base is pinned host memory the kernel reads and writes over
+// PCIe (system-scope loads and stores)
 hipError_t launch_decode_fused(const UniformArgs &a, const uint8_t *present,
                                const uint8_t *parity_rows, int32_t *status,
-                               const uint32_t *ptab, const uint8_t *gftab, hipStream_t s);
+                               const uint32_t *ptab, const uint8_t *gftab, hipStream_t s,
+                               bool host_shards = false);
 
 // Ragged decode (decode.hip): one-wave-per-group kernel, then the
 // workgroup-per-group kernel for the groups it defers.
@@ -76,14 +79,22 @@ __host__ __device__ inline int rag_width(int lpad) {
     return nw <= 1 ? 1 : (nw == 2 ? 2 : (nw <= 4 ? 4 : 5));
 }
 __host__ __device__ inline int rag_width_class(int w) { return w == 1 ? 0 : (w == 2 ? 1 : (w == 4 ? 2 : 3)); }
-// Plans: the groups sorted into the four width classes (cls_idx, class c's
-// groups at [cls_first[c], cls_first[c+1])), one register-cut kernel per class.
+// Plans: the groups sorted into the four width classes, one register-cut
+// kernel per class.  Within class c the groups are dealt to nw[c] waves
+// (about one resident round: decode_cls_occupancy) by longest-processing-time
+// first on an estimated cost, so the waves of the one round finish together;
+// wave w of class c takes idx[wst[c][w] .. wst[c][w+1]).
+struct ClsLaunch {
+    const uint32_t *idx;     // device: group indices, wave-major within each class
+    const uint32_t *wst[4];  // device: per class, nw[c] + 1 offsets into idx
+    int nw[4];
+};
+int decode_cls_occupancy(int c);  // waves per SIMD class c's kernel is cut for
 // Class c runs on cs[c]; the caller orders cs[] against s and then runs
 // launch_decode_ragged_big on s.
-hipError_t launch_decode_ragged_cls(const rsmi_group *groups, int64_t ngroups,
-                                    const uint32_t *cls_idx, const int64_t cls_first[5],
-                                    uint8_t *base, const uint32_t *present_bits, int32_t *status,
-                                    int kmax, const uint64_t *code_dir, const uint32_t *ptab,
+hipError_t launch_decode_ragged_cls(const rsmi_group *groups, const ClsLaunch &L, uint8_t *base,
+                                    const uint32_t *present_bits, int32_t *status, int kmax,
+                                    const uint64_t *code_dir, const uint32_t *ptab,
                                     const uint8_t *gftab, hipStream_t s, const hipStream_t cs[4]);
 // The workgroup-per-group kernel for the groups the one-wave kernels deferred.
 hipError_t launch_decode_ragged_big(const rsmi_group *groups, int64_t ngroups, uint8_t *base,
@@ -122,6 +133,24 @@ hipError_t launch_encode_bitslice_ragged_rtc(int k, int n, const rsmi_group *gro
                                              hipStream_t s);
 
 constexpr int kPtabDwords = 8;  // per coefficient: T0lo T0hi T1lo T1hi | T2 pad pad pad
+
+// ---- one group per call, latency path (oneshot.hip) ------------------------------
+constexpr int kOneAug = 16384;  // LDS bytes for [A | M] (e * (e + k)) or the encode coefficients
+struct OneArgs {
+    const uint8_t *in;      // device address of pinned staging: slot j at in + j * ss
+    uint8_t *out;           // device address of pinned rows: output row r at out + r * ss
+    const uint8_t *rows;    // the code's (n-k) x k parity rows (device)
+    const uint32_t *ptab;   // v_perm split tables (device)
+    const uint8_t *gftab;   // exp[512] | log[256] (device)
+    int32_t *status;        // device address of a pinned word: RSMI_DEC_*
+    uint32_t *flag;         // device address of a pinned word: set to seq when done
+    uint32_t seq;
+    int k, n, len, ss;
+    int encode;             // 1: out rows = parity rows k..n-1; 0: rebuilt data rows, miss order
+    uint32_t present[8];    // decode: bit j = shard j received
+};
+bool one_group_ok(int k, int n, int len, int ss, bool encode);
+hipError_t launch_one_group(const OneArgs &a, hipStream_t s);
 
 // ---- packet cook / de_cook (cook.hip, cook_host.cpp) -------------------------------
 // A packet is walked by kCookLpp lanes of a wave (8: eight packets per wave;
