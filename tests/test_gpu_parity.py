@@ -503,6 +503,44 @@ def test_ragged_decode_vs_oracle_mixed(gpu, oracle):
         assert (got[k:] == org[k:]).all(), i  # parity slots untouched
 
 
+def test_ragged_plan_decode_many_codes_vs_oracle(gpu, oracle):
+    """Plan decode (the width-class kernels, 8-dword group records read out of
+    registers) over groups of ~200 different codes against the oracle: every
+    code's parity rows sit at their own device address, so the records'
+    64-bit pointers and offsets are rebuilt from many different low dwords
+    (a sign-extended low dword with bit 31 set faulted the GPU once)."""
+    import torch
+    import udpspeeder_amd as u
+    from udpspeeder_amd import synth
+    rng = np.random.default_rng(77)
+    codes = sorted({(int(k), int(k + m)) for k, m in zip(rng.integers(1, 33, 400), rng.integers(1, 21, 400))})
+    G = 3 * len(codes)
+    pick = rng.integers(0, len(codes), G)
+    ks = np.array([codes[i][0] for i in pick]); ns = np.array([codes[i][1] for i in pick])
+    ls = rng.integers(1, 1300, G)
+    groups, total = u.make_groups(ks, ns, ls)
+    host = rng.integers(0, 256, total, dtype=np.uint8)
+    flags = np.zeros((G, 256), np.uint8)
+    for i in range(G):
+        n, m = int(ns[i]), int(ns[i] - ks[i])
+        flags[i, :n] = 1
+        flags[i, rng.choice(n, min(5, m), replace=False)] = 0
+    plan = u.rs.RaggedPlan(groups, wait_codes=False)
+    base = upload(host, gpu)
+    bits = torch.from_numpy(synth.present_bits(flags).view(np.int32)).to(gpu)
+    st = plan.decode(base, bits).cpu().numpy()
+    plan.close()
+    out = base.cpu().numpy()
+    for i in range(G):
+        d = groups[i]
+        n, k = d.n, d.k
+        seg = host[d.offset:d.offset + n * d.shard_stride].copy()
+        ost = oracle.decode_batch(k, n, seg, 0, d.shard_stride, d.len, 1, flags[i:i + 1, :n])
+        assert st[i] == ost[0], (i, k, n)
+        got = out[d.offset:d.offset + n * d.shard_stride].reshape(n, d.shard_stride)
+        assert (got[:k, :d.len] == seg.reshape(n, d.shard_stride)[:k, :d.len]).all(), (i, k, n)
+
+
 def test_ragged_plan_decode_graph_capture(gpu, oracle):
     """A ragged plan decode forks its width classes over extra streams and joins
     them back (event fork/join): it captures into a graph, and every replay

@@ -363,6 +363,15 @@ int decode_ragged_cls_dev(const rsmi_group *dg, int64_t ngroups, const ClsLaunch
     return RSMI_OK;
 }
 
+const uint8_t *device_code_rows(int k, int n) {
+    int rc;
+    Device *D = current(&rc);
+    if (!D) return nullptr;
+    std::lock_guard<std::mutex> lk(D->mu);
+    auto it = D->codes.find(k * 257 + n);
+    return it == D->codes.end() ? nullptr : it->second.dev_rows;
+}
+
 uint64_t *device_code_dir(int *rc) {
     Device *D = current(rc);
     return D ? D->code_dir : nullptr;
@@ -711,19 +720,26 @@ uint8_t *mapped_host_range(uint8_t *p, size_t bytes) {
         fprintf(stderr, "rsmi: pinned? %p: type %d dev %p host %p flags %u\n", (void *)p, (int)at.type,
                 at.devicePointer, at.hostPointer, at.allocationFlags);
     if (at.type != hipMemoryTypeHost || !at.devicePointer || !at.hostPointer) return nullptr;
-    void *start = nullptr;
-    size_t size = 0;
+    // [p, p + bytes) lies in ONE allocation when its first and last bytes
+    // report the same range start (RANGE_SIZE reads 0 for a 4 GiB pinned
+    // block on ROCm 7.2, so the size is not trusted)
+    void *start = nullptr, *start_last = nullptr;
     hipError_t e1 = hipPointerGetAttribute(&start, HIP_POINTER_ATTRIBUTE_RANGE_START_ADDR, (hipDeviceptr_t)p);
-    hipError_t e2 = hipPointerGetAttribute(&size, HIP_POINTER_ATTRIBUTE_RANGE_SIZE, (hipDeviceptr_t)p);
+    hipError_t e2 = hipPointerGetAttribute(&start_last, HIP_POINTER_ATTRIBUTE_RANGE_START_ADDR,
+                                           (hipDeviceptr_t)(p + bytes - 1));
     if (dbg)
-        fprintf(stderr, "rsmi: pinned? range %d %d start %p size %zu need %zu\n", (int)e1, (int)e2, start,
-                size, bytes);
+        fprintf(stderr, "rsmi: pinned? range %d %d start %p start(last byte) %p need %zu\n", (int)e1, (int)e2,
+                start, start_last, bytes);
     if (e1 != hipSuccess || e2 != hipSuccess) {
         (void)hipGetLastError();
         return nullptr;
     }
-    const uint8_t *s0 = static_cast<const uint8_t *>(start);
-    if (!s0 || p < s0 || p + bytes > s0 + size) return nullptr;
+    if (!start || start != start_last || p < static_cast<const uint8_t *>(start)) return nullptr;
+    hipPointerAttribute_t at_last;
+    if (hipPointerGetAttributes(&at_last, p + bytes - 1) != hipSuccess || at_last.type != hipMemoryTypeHost) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
     return static_cast<uint8_t *>(at.devicePointer) + (p - static_cast<uint8_t *>(at.hostPointer));
 }
 

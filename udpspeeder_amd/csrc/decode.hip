@@ -747,36 +747,32 @@ __global__ __launch_bounds__(256, DEC_OCC) void k_decode_fused(UniformArgs a, co
 #endif
 constexpr int kClsRows = 5;  // class kernels: e <= 5 in registers, more is deferred
 
-// One group.  WC = tile width (1, 2, 4, 5), or 0: chosen per group.  The
-// descriptor d is wave-uniform (scalar loads).
-template <int WC, int NR>
-__device__ __forceinline__ void ragged_group(int64_t g, const rsmi_group &d, uint32_t w8,
-                                             uint8_t *base, int32_t *status_out,
-                                             const uint64_t *code_dir, const Tables &T,
-                                             const WaveLds &L, int kmax, int lane) {
-    const int k = __builtin_amdgcn_readfirstlane(d.k);
-    const int n = __builtin_amdgcn_readfirstlane(d.n);
-    const int len = __builtin_amdgcn_readfirstlane(d.len);
-    const uint32_t ss = __builtin_amdgcn_readfirstlane(d.shard_stride);
-    const uint64_t off = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(d.offset >> 32)) << 32) |
-                         (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)d.offset);
-    const uint8_t *rows = (k >= 1 && n > k && n <= 256)
-                              ? reinterpret_cast<const uint8_t *>(code_dir[k * 257 + n])
-                              : nullptr;
+// One group's wave-uniform description.
+struct GroupDesc {
+    int64_t g;          // status index
+    int k, n, len;
+    uint32_t ss;
+    uint64_t off;
+    const uint8_t *rows;  // the code's parity rows, (n-k) x k (nullptr when n == k)
+};
+
+// One group.  WC = tile width (1, 2, 4, 5), or 0: chosen per group.
+// flag(b, idx) is shard idx's present flag (b = idx rounded down to 64).
+template <int WC, int NR, class Flag>
+__device__ __forceinline__ void ragged_group_run(const GroupDesc &D, Flag flag, uint8_t *base,
+                                                 int32_t *status_out, const Tables &T,
+                                                 const WaveLds &L, int kmax, int lane) {
+    const int64_t g = D.g;
+    const int k = D.k, n = D.n, len = D.len;
+    const uint32_t ss = D.ss;
+    const uint64_t off = D.off;
+    const uint8_t *rows = D.rows;
     if (k < 1 || n < k || n > 256 || (n > k && !rows)) {
         if (lane == 0) status_out[g] = RSMI_DEC_UNSUPPORTED;
         return;
     }
     int e;
-    const int cnt = select_survivors(
-        k, n,
-        [&](int b, int idx) {
-            // words b/32 and b/32 + 1 cover shards b..b+63 (readlane ignores exec)
-            const uint32_t lo = __builtin_amdgcn_readlane(w8, (b >> 5) & 7);
-            const uint32_t hi = __builtin_amdgcn_readlane(w8, ((b >> 5) + 1) & 7);
-            return ((((idx & 32) ? hi : lo) >> (idx & 31)) & 1u) != 0;
-        },
-        L, lane, e);
+    const int cnt = select_survivors(k, n, flag, L, lane, e);
     wave_sync();
     if (cnt < k || e == 0) {
         if (lane == 0) status_out[g] = cnt < k ? RSMI_DEC_TOO_FEW : RSMI_DEC_OK;
@@ -817,6 +813,35 @@ __device__ __forceinline__ void ragged_group(int64_t g, const rsmi_group &d, uin
     if (lane == 0) status_out[g] = st;
 }
 
+// One group from its rsmi_group descriptor (scalar loads) and the code
+// directory; w8 is present word (lane & 7) of the group.
+template <int WC, int NR>
+__device__ __forceinline__ void ragged_group(int64_t g, const rsmi_group &d, uint32_t w8,
+                                             uint8_t *base, int32_t *status_out,
+                                             const uint64_t *code_dir, const Tables &T,
+                                             const WaveLds &L, int kmax, int lane) {
+    GroupDesc D;
+    D.g = g;
+    D.k = __builtin_amdgcn_readfirstlane(d.k);
+    D.n = __builtin_amdgcn_readfirstlane(d.n);
+    D.len = __builtin_amdgcn_readfirstlane(d.len);
+    D.ss = __builtin_amdgcn_readfirstlane(d.shard_stride);
+    D.off = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(d.offset >> 32)) << 32) |
+            (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)d.offset);
+    D.rows = (D.k >= 1 && D.n > D.k && D.n <= 256)
+                 ? reinterpret_cast<const uint8_t *>(code_dir[D.k * 257 + D.n])
+                 : nullptr;
+    ragged_group_run<WC, NR>(
+        D,
+        [&](int b, int idx) {
+            // words b/32 and b/32 + 1 cover shards b..b+63 (readlane ignores exec)
+            const uint32_t lo = __builtin_amdgcn_readlane(w8, (b >> 5) & 7);
+            const uint32_t hi = __builtin_amdgcn_readlane(w8, ((b >> 5) + 1) & 7);
+            return ((((idx & 32) ? hi : lo) >> (idx & 31)) & 1u) != 0;
+        },
+        base, status_out, T, L, kmax, lane);
+}
+
 // Every group of the batch, tile width chosen per group (rsmi_decode_ragged_dev:
 // descriptors on the device, no plan).
 __global__ __launch_bounds__(256, DEC_RAG_OCC) void k_decode_ragged(
@@ -844,14 +869,17 @@ __global__ __launch_bounds__(256, DEC_RAG_OCC) void k_decode_ragged(
 
 // Plans: the groups of one tile-width class, registers cut for that width so
 // short groups run at up to 8 waves per SIMD: C3's groups are latency-bound
-// (descriptor -> code rows -> inversion -> a few survivors).  Wave w takes the
-// groups idx[wst[w] .. wst[w+1]) the plan dealt it (ragged.cpp: balanced so
-// that the one resident round of waves ends together).
+// (a chain of dependent round trips per group).  Wave w takes the groups the
+// plan dealt it (ragged.cpp: balanced so that the one resident round of waves
+// ends together), as 8-dword records {offset lo, hi, stride, len, k | n << 16,
+// status index, parity-rows pointer lo, hi} at rec[wst[w] .. wst[w+1]): eight
+// records and their present masks come in with two wave-wide loads, and each
+// group's fields are read out of registers -- no descriptor, index or code
+// directory round trip per group.
 template <int W, int OCC>
 __global__ __launch_bounds__(256, OCC) void k_decode_ragged_cls(
-    const rsmi_group *__restrict__ groups, const uint32_t *__restrict__ idx,
-    const uint32_t *__restrict__ wst, int nw, uint8_t *base, const uint32_t *__restrict__ present,
-    int32_t *status_out, const uint64_t *__restrict__ code_dir, const uint32_t *ptab,
+    const uint32_t *__restrict__ rec, const uint32_t *__restrict__ wst, int nw, uint8_t *base,
+    const uint32_t *__restrict__ present, int32_t *status_out, const uint32_t *ptab,
     const uint8_t *gftab, int kmax) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const Tables T = load_tables(smem, ptab, gftab);
@@ -861,13 +889,41 @@ __global__ __launch_bounds__(256, OCC) void k_decode_ragged_cls(
     __syncthreads();
     const int w = blockIdx.x * kWaves + wid;
     if (w >= nw) return;
-    const uint32_t i1 = wst[w + 1];
-    for (uint32_t i = wst[w]; i < i1; ++i) {
-        const int64_t g = __builtin_amdgcn_readfirstlane(idx[i]);
-        const rsmi_group d = groups[g];
-        ragged_group<W, kClsRows>(g, d, present[g * 8 + (lane & 7)], base, status_out, code_dir, T,
-                                  L, kmax, lane);
-        wave_sync();  // the LDS slice is rewritten by the next group
+    const uint32_t i0 = wst[w], i1 = wst[w + 1];
+    for (uint32_t b0 = i0; b0 < i1; b0 += 8) {
+        const uint32_t nb = i1 - b0 < 8u ? i1 - b0 : 8u;
+        // lane l: dword (l & 7) of record (l >> 3), then present word (l & 7)
+        // of that record's group
+        uint32_t r = 0, pw = 0;
+        if ((uint32_t)(lane >> 3) < nb) r = rec[(size_t)(b0 + (lane >> 3)) * 8 + (lane & 7)];
+        const uint32_t gl = (uint32_t)__shfl(r, (lane & ~7) | 5);
+        if ((uint32_t)(lane >> 3) < nb) pw = present[(size_t)gl * 8 + (lane & 7)];
+        for (uint32_t i = 0; i < nb; ++i) {
+            int q = (int)i * 8;
+            asm volatile("" : "+s"(q));  // the record's lane base, a scalar
+            GroupDesc D;
+            // (readlane returns int: every dword goes through uint32_t before it
+            // is widened, or a low half with bit 31 set sign-extends into the
+            // high half of a 64-bit offset or pointer)
+            auto dw = [&](int f) { return (uint32_t)__builtin_amdgcn_readlane(r, q + f); };
+            const uint32_t kn = dw(4);
+            D.g = (int64_t)dw(5);
+            D.k = (int)(kn & 0xFFFFu);
+            D.n = (int)(kn >> 16);
+            D.len = (int)dw(3);
+            D.ss = dw(2);
+            D.off = ((uint64_t)dw(1) << 32) | (uint64_t)dw(0);
+            D.rows = reinterpret_cast<const uint8_t *>((uintptr_t)(((uint64_t)dw(7) << 32) | (uint64_t)dw(6)));
+            ragged_group_run<W, kClsRows>(
+                D,
+                [&](int b, int idx) {
+                    const uint32_t lo = __builtin_amdgcn_readlane(pw, q + ((b >> 5) & 7));
+                    const uint32_t hi = __builtin_amdgcn_readlane(pw, q + (((b >> 5) + 1) & 7));
+                    return ((((idx & 32) ? hi : lo) >> (idx & 31)) & 1u) != 0;
+                },
+                base, status_out, T, L, kmax, lane);
+            wave_sync();  // the LDS slice is rewritten by the next group
+        }
     }
 }
 
@@ -1066,7 +1122,7 @@ hipError_t launch_decode_ragged_cls(const rsmi_group *groups, const ClsLaunch &C
         const int nw = C.nw[c];
         if (nw <= 0) return hipSuccess;
         kern<<<(unsigned)((nw + kWaves - 1) / kWaves), 64 * kWaves, lds, cs[c]>>>(
-            groups, C.idx, C.wst[c], nw, base, present_bits, status, code_dir, ptab, gftab, kmax);
+            C.rec, C.wst[c], nw, base, present_bits, status, ptab, gftab, kmax);
         return hipGetLastError();
     };
     hipError_t e = launch(k_decode_ragged_cls<5, DEC_CLS_OCC5>, 3);

@@ -26,6 +26,7 @@
 
 namespace rsmi {
 int prepare_code(int k, int n);
+const uint8_t *device_code_rows(int k, int n);
 void set_error(const std::string &m);
 uint64_t *device_code_dir(int *rc);
 int decode_ragged_dev(const rsmi_group *dg, int64_t ngroups, uint8_t *base,
@@ -52,7 +53,7 @@ struct rsmi_ragged_plan {
     rsmi_group *d_groups = nullptr;
     uint32_t *d_colmap = nullptr;
     uint32_t *d_waves = nullptr;
-    // decode: group indices by tile-width class (rag_width), dealt to waves
+    // decode: group records by tile-width class (rag_width), dealt to waves
     // (d_cls, wave-major; class c's wave offsets at d_wst + wst_first[c])
     rsmi::ClsLaunch cls{};
     uint32_t *d_cls = nullptr;
@@ -186,7 +187,7 @@ extern "C" int rsmi_ragged_plan_create(const rsmi_group *g, int64_t ngroups,
             by[(size_t)rsmi::rag_width_class(
                    rsmi::rag_width(rsmi::rag_lpad(g[i].len, g[i].shard_stride)))]
                 .push_back((uint32_t)i);
-        cls.reserve((size_t)ngroups);
+        cls.reserve((size_t)ngroups * 8);
         for (int c = 0; c < 4; ++c) {
             auto &v = by[(size_t)c];
             const int W = c == 0 ? 1 : (c == 1 ? 2 : (c == 2 ? 4 : 5));
@@ -195,7 +196,7 @@ extern "C" int rsmi_ragged_plan_create(const rsmi_group *g, int64_t ngroups,
             P->cls.nw[c] = nw;
             wst_first[c] = (int64_t)wst.size();
             if (nw == 0) {
-                wst.push_back((uint32_t)cls.size());
+                wst.push_back((uint32_t)(cls.size() / 8));
                 continue;
             }
             // cost: a fixed chain (descriptor, flags, code rows, elimination)
@@ -216,10 +217,17 @@ extern "C" int rsmi_ragged_plan_create(const rsmi_group *g, int64_t ngroups,
                 std::push_heap(heap.begin(), heap.end(), gt);
             }
             for (int w = 0; w < nw; ++w) {
-                wst.push_back((uint32_t)cls.size());
-                cls.insert(cls.end(), lists[(size_t)w].begin(), lists[(size_t)w].end());
+                wst.push_back((uint32_t)(cls.size() / 8));
+                for (uint32_t i : lists[(size_t)w]) {  // the group's 8-dword record (decode.hip)
+                    const rsmi_group &d = g[i];
+                    const uint64_t rows = (uint64_t)(uintptr_t)rsmi::device_code_rows(d.k, d.n);
+                    const uint32_t r8[8] = {(uint32_t)d.offset, (uint32_t)(d.offset >> 32), d.shard_stride,
+                                            d.len, (uint32_t)d.k | ((uint32_t)d.n << 16), i,
+                                            (uint32_t)rows, (uint32_t)(rows >> 32)};
+                    cls.insert(cls.end(), r8, r8 + 8);
+                }
             }
-            wst.push_back((uint32_t)cls.size());
+            wst.push_back((uint32_t)(cls.size() / 8));
         }
     }
     const size_t gbytes = sizeof(rsmi_group) * (size_t)ngroups;
@@ -241,7 +249,7 @@ extern "C" int rsmi_ragged_plan_create(const rsmi_group *g, int64_t ngroups,
     P->d_waves = reinterpret_cast<uint32_t *>(P->mem + woff);
     P->d_cls = reinterpret_cast<uint32_t *>(P->mem + doff);
     uint32_t *d_wst = reinterpret_cast<uint32_t *>(P->mem + soff);
-    P->cls.idx = P->d_cls;
+    P->cls.rec = P->d_cls;
     for (int c = 0; c < 4; ++c) P->cls.wst[c] = d_wst + wst_first[c];
     hipError_t e = hipSuccess;
     if (gbytes) e = hipMemcpy(P->d_groups, g, gbytes, hipMemcpyHostToDevice);

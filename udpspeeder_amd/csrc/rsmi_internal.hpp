@@ -83,12 +83,14 @@ __host__ __device__ inline int rag_width_class(int w) { return w == 1 ? 0 : (w =
 // kernel per class.  Within class c the groups are dealt to nw[c] waves
 // (about one resident round: decode_cls_occupancy) by longest-processing-time
 // first on an estimated cost, so the waves of the one round finish together;
-// wave w of class c takes idx[wst[c][w] .. wst[c][w+1]).
+// wave w of class c takes records rec[wst[c][w] .. wst[c][w+1]).
 struct ClsLaunch {
-    const uint32_t *idx;     // device: group indices, wave-major within each class
-    const uint32_t *wst[4];  // device: per class, nw[c] + 1 offsets into idx
+    const uint32_t *rec;     // device: 8-dword group records (decode.hip), wave-major per class
+    const uint32_t *wst[4];  // device: per class, nw[c] + 1 offsets into rec (in records)
     int nw[4];
 };
+// The (k,n) code's parity rows on the current device (nullptr: not resident).
+const uint8_t *device_code_rows(int k, int n);
 int decode_cls_occupancy(int c);  // waves per SIMD class c's kernel is cut for
 // Class c runs on cs[c]; the caller orders cs[] against s and then runs
 // launch_decode_ragged_big on s.
