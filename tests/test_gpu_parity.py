@@ -513,7 +513,7 @@ def test_ragged_plan_decode_many_codes_vs_oracle(gpu, oracle):
     import udpspeeder_amd as u
     from udpspeeder_amd import synth
     rng = np.random.default_rng(77)
-    codes = sorted({(int(k), int(k + m)) for k, m in zip(rng.integers(1, 33, 400), rng.integers(1, 21, 400))})
+    codes = sorted({(int(k), int(k + m)) for k, m in zip(rng.integers(1, 61, 400), rng.integers(1, 21, 400))})
     G = 3 * len(codes)
     pick = rng.integers(0, len(codes), G)
     ks = np.array([codes[i][0] for i in pick]); ns = np.array([codes[i][1] for i in pick])
@@ -524,11 +524,20 @@ def test_ragged_plan_decode_many_codes_vs_oracle(gpu, oracle):
     for i in range(G):
         n, m = int(ns[i]), int(ns[i] - ks[i])
         flags[i, :n] = 1
-        flags[i, rng.choice(n, min(5, m), replace=False)] = 0
+        # up to 10 erasures, so e > 5 groups (and k > 32 ones) are deferred
+        # to the workgroup kernel, whose launch the plan gates on a mark
+        flags[i, rng.choice(n, min(int(rng.integers(1, 11)), m), replace=False)] = 0
     plan = u.rs.RaggedPlan(groups, wait_codes=False)
     base = upload(host, gpu)
     bits = torch.from_numpy(synth.present_bits(flags).view(np.int32)).to(gpu)
     st = plan.decode(base, bits).cpu().numpy()
+    # a second call that defers nothing (all present), then the first again
+    allp = torch.from_numpy(synth.present_bits((np.arange(256)[None, :] < ns[:, None]).astype(np.uint8))
+                            .view(np.int32)).to(gpu)
+    assert (plan.decode(base, allp).cpu().numpy() == 0).all()
+    base.copy_(upload(host, gpu))
+    st2 = plan.decode(base, bits).cpu().numpy()
+    assert (st2 == st).all()
     plan.close()
     out = base.cpu().numpy()
     for i in range(G):

@@ -358,7 +358,7 @@ int decode_ragged_cls_dev(const rsmi_group *dg, int64_t ngroups, const ClsLaunch
                                             D->ptab, D->gftab, s, cs);
     if (e == hipSuccess)
         e = launch_decode_ragged_big(dg, ngroups, base, present_bits, status, D->code_dir, D->ptab,
-                                     D->gftab, s);
+                                     D->gftab, s, C.defer, C.epoch);
     if (e != hipSuccess) return hip_fail(e, "ragged decode launch");
     return RSMI_OK;
 }

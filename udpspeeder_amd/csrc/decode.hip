@@ -758,10 +758,20 @@ struct GroupDesc {
 
 // One group.  WC = tile width (1, 2, 4, 5), or 0: chosen per group.
 // flag(b, idx) is shard idx's present flag (b = idx rounded down to 64).
+// A deferral mark: the class kernels raise *word to `epoch` (atomic max) when
+// they leave a group for k_decode_ragged_big, which does nothing unless
+// *word >= its epoch.  Calls number their epochs upwards, so concurrent calls
+// on one plan can only make the big kernel scan needlessly, never skip.
+struct DeferMark {
+    uint32_t *word;  // nullptr: no mark (the big kernel always scans)
+    uint32_t epoch;
+};
+
 template <int WC, int NR, class Flag>
 __device__ __forceinline__ void ragged_group_run(const GroupDesc &D, Flag flag, uint8_t *base,
                                                  int32_t *status_out, const Tables &T,
-                                                 const WaveLds &L, int kmax, int lane) {
+                                                 const WaveLds &L, int kmax, int lane,
+                                                 DeferMark dm = DeferMark{nullptr, 0}) {
     const int64_t g = D.g;
     const int k = D.k, n = D.n, len = D.len;
     const uint32_t ss = D.ss;
@@ -779,7 +789,10 @@ __device__ __forceinline__ void ragged_group_run(const GroupDesc &D, Flag flag, 
         return;
     }
     if (e > NR || k > kmax || (uint64_t)n * ss >= 0x80000000ull) {
-        if (lane == 0) status_out[g] = kDefer;
+        if (lane == 0) {
+            status_out[g] = kDefer;
+            if (dm.word) atomicMax(dm.word, dm.epoch);
+        }
         return;
     }
     auto prow = [&](uint32_t R) { return rows + (R - k) * k; };
@@ -880,7 +893,7 @@ template <int W, int OCC>
 __global__ __launch_bounds__(256, OCC) void k_decode_ragged_cls(
     const uint32_t *__restrict__ rec, const uint32_t *__restrict__ wst, int nw, uint8_t *base,
     const uint32_t *__restrict__ present, int32_t *status_out, const uint32_t *ptab,
-    const uint8_t *gftab, int kmax) {
+    const uint8_t *gftab, int kmax, DeferMark dm) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const Tables T = load_tables(smem, ptab, gftab);
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -921,7 +934,7 @@ __global__ __launch_bounds__(256, OCC) void k_decode_ragged_cls(
                     const uint32_t hi = __builtin_amdgcn_readlane(pw, q + (((b >> 5) + 1) & 7));
                     return ((((idx & 32) ? hi : lo) >> (idx & 31)) & 1u) != 0;
                 },
-                base, status_out, T, L, kmax, lane);
+                base, status_out, T, L, kmax, lane, dm);
             wave_sync();  // the LDS slice is rewritten by the next group
         }
     }
@@ -936,7 +949,10 @@ constexpr int kBigRows = 8;
 
 __global__ __launch_bounds__(256) void k_decode_ragged_big(
     const rsmi_group *groups, int64_t ngroups, uint8_t *base, const uint32_t *present,
-    int32_t *status_out, const uint64_t *code_dir, const uint32_t *ptab, const uint8_t *gftab) {
+    int32_t *status_out, const uint64_t *code_dir, const uint32_t *ptab, const uint8_t *gftab,
+    const uint32_t *defer_word, uint32_t epoch) {
+    // plans: nothing to do unless a class kernel marked a deferral this call
+    if (defer_word && (uint32_t)__builtin_amdgcn_readfirstlane(*defer_word) < epoch) return;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const Tables T = load_tables(smem, ptab, gftab);
     uint8_t *sel = smem + kTabBytes, *miss = sel + 256, *aug = miss + 256;
@@ -1088,7 +1104,8 @@ hipError_t launch_decode_fused(const UniformArgs &a, const uint8_t *present,
 hipError_t launch_decode_ragged_big(const rsmi_group *groups, int64_t ngroups, uint8_t *base,
                                     const uint32_t *present_bits, int32_t *status,
                                     const uint64_t *code_dir, const uint32_t *ptab,
-                                    const uint8_t *gftab, hipStream_t s);
+                                    const uint8_t *gftab, hipStream_t s, const uint32_t *defer_word,
+                                    uint32_t epoch);
 
 hipError_t launch_decode_ragged(const rsmi_group *groups, int64_t ngroups, uint8_t *base,
                                 const uint32_t *present_bits, int32_t *status, int kmax,
@@ -1122,7 +1139,8 @@ hipError_t launch_decode_ragged_cls(const rsmi_group *groups, const ClsLaunch &C
         const int nw = C.nw[c];
         if (nw <= 0) return hipSuccess;
         kern<<<(unsigned)((nw + kWaves - 1) / kWaves), 64 * kWaves, lds, cs[c]>>>(
-            C.rec, C.wst[c], nw, base, present_bits, status, ptab, gftab, kmax);
+            C.rec, C.wst[c], nw, base, present_bits, status, ptab, gftab, kmax,
+            DeferMark{C.defer, C.epoch});
         return hipGetLastError();
     };
     hipError_t e = launch(k_decode_ragged_cls<5, DEC_CLS_OCC5>, 3);
@@ -1135,11 +1153,12 @@ hipError_t launch_decode_ragged_cls(const rsmi_group *groups, const ClsLaunch &C
 hipError_t launch_decode_ragged_big(const rsmi_group *groups, int64_t ngroups, uint8_t *base,
                                     const uint32_t *present_bits, int32_t *status,
                                     const uint64_t *code_dir, const uint32_t *ptab,
-                                    const uint8_t *gftab, hipStream_t s) {
+                                    const uint8_t *gftab, hipStream_t s, const uint32_t *defer_word,
+                                    uint32_t epoch) {
     int64_t bb = (ngroups + 255) / 256;
     if (bb > 256 * 4) bb = 256 * 4;
     k_decode_ragged_big<<<(unsigned)bb, 256, kTabBytes + 512 + kBigAug, s>>>(
-        groups, ngroups, base, present_bits, status, code_dir, ptab, gftab);
+        groups, ngroups, base, present_bits, status, code_dir, ptab, gftab, defer_word, epoch);
     return hipGetLastError();
 }
 

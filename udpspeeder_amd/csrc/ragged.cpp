@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <utility>
 #include <cstring>
 #include <map>
@@ -57,6 +58,7 @@ struct rsmi_ragged_plan {
     // (d_cls, wave-major; class c's wave offsets at d_wst + wst_first[c])
     rsmi::ClsLaunch cls{};
     uint32_t *d_cls = nullptr;
+    std::atomic<uint32_t> epoch{0};  // decode calls so far (the deferral mark, ClsLaunch)
 };
 
 namespace {
@@ -239,7 +241,7 @@ extern "C" int rsmi_ragged_plan_create(const rsmi_group *g, int64_t ngroups,
                  woff = (coff + cbytes + 255) & ~size_t(255),
                  doff = (woff + wbytes + 255) & ~size_t(255),
                  soff = (doff + dbytes + 255) & ~size_t(255);
-    const size_t all = soff + sbytes + 16;
+    const size_t all = soff + sbytes + 256;  // + the deferral word
     if (hipMalloc(&P->mem, all) != hipSuccess) {
         delete P;
         return fail(RSMI_ERR_NOMEM, "hipMalloc(ragged plan)");
@@ -250,6 +252,7 @@ extern "C" int rsmi_ragged_plan_create(const rsmi_group *g, int64_t ngroups,
     P->d_cls = reinterpret_cast<uint32_t *>(P->mem + doff);
     uint32_t *d_wst = reinterpret_cast<uint32_t *>(P->mem + soff);
     P->cls.rec = P->d_cls;
+    P->cls.defer = reinterpret_cast<uint32_t *>(P->mem + ((soff + sbytes + 127) & ~size_t(127)));
     for (int c = 0; c < 4; ++c) P->cls.wst[c] = d_wst + wst_first[c];
     hipError_t e = hipSuccess;
     if (gbytes) e = hipMemcpy(P->d_groups, g, gbytes, hipMemcpyHostToDevice);
@@ -260,6 +263,7 @@ extern "C" int rsmi_ragged_plan_create(const rsmi_group *g, int64_t ngroups,
     if (e == hipSuccess && dbytes) e = hipMemcpy(P->d_cls, cls.data(), dbytes,
                                                  hipMemcpyHostToDevice);
     if (e == hipSuccess && sbytes) e = hipMemcpy(d_wst, wst.data(), sbytes, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemset(P->cls.defer, 0, sizeof(uint32_t));
     if (e != hipSuccess) {
         (void)hipFree(P->mem);
         delete P;
@@ -300,9 +304,15 @@ extern "C" int rsmi_decode_ragged_plan(const rsmi_ragged_plan *P, uint8_t *base,
                                        const uint32_t *present_bits, int32_t *status,
                                        void *stream) {
     if (!P) return fail(RSMI_ERR_INVALID, "null plan");
-    if (RSMI_DEC_CLASSES)
-        return rsmi::decode_ragged_cls_dev(P->d_groups, P->ngroups, P->cls, base, present_bits, status,
+    if (RSMI_DEC_CLASSES) {
+        rsmi::ClsLaunch C = P->cls;
+        // a rising mark per call: the big kernel runs only if a call at or
+        // after this one deferred (graph replays keep their captured mark and
+        // may scan needlessly; never the reverse)
+        C.epoch = const_cast<rsmi_ragged_plan *>(P)->epoch.fetch_add(1) + 1;
+        return rsmi::decode_ragged_cls_dev(P->d_groups, P->ngroups, C, base, present_bits, status,
                                            P->kmax, (hipStream_t)stream);
+    }
     return rsmi::decode_ragged_dev(P->d_groups, P->ngroups, base, present_bits, status, P->kmax,
                                    (hipStream_t)stream);
 }

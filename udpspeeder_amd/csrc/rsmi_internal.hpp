@@ -88,6 +88,8 @@ struct ClsLaunch {
     const uint32_t *rec;     // device: 8-dword group records (decode.hip), wave-major per class
     const uint32_t *wst[4];  // device: per class, nw[c] + 1 offsets into rec (in records)
     int nw[4];
+    uint32_t *defer;         // device word: set to epoch when a group is left for the big kernel
+    uint32_t epoch;          // this call's mark (plans count calls)
 };
 // The (k,n) code's parity rows on the current device (nullptr: not resident).
 const uint8_t *device_code_rows(int k, int n);
@@ -98,11 +100,13 @@ hipError_t launch_decode_ragged_cls(const rsmi_group *groups, const ClsLaunch &L
                                     const uint32_t *present_bits, int32_t *status, int kmax,
                                     const uint64_t *code_dir, const uint32_t *ptab,
                                     const uint8_t *gftab, hipStream_t s, const hipStream_t cs[4]);
-// The workgroup-per-group kernel for the groups the one-wave kernels deferred.
+// The workgroup-per-group kernel for the groups the one-wave kernels deferred
+// (defer_word: skip everything unless *defer_word == epoch; nullptr: scan).
 hipError_t launch_decode_ragged_big(const rsmi_group *groups, int64_t ngroups, uint8_t *base,
                                     const uint32_t *present_bits, int32_t *status,
                                     const uint64_t *code_dir, const uint32_t *ptab,
-                                    const uint8_t *gftab, hipStream_t s);
+                                    const uint8_t *gftab, hipStream_t s,
+                                    const uint32_t *defer_word = nullptr, uint32_t epoch = 0);
 
 // Bit-sliced encode kernels specialised at build time for hot (k,n) codes
 // (gen_bitslice.py -> gen/bitslice_codes.inc), or compiled at run time
