@@ -286,7 +286,7 @@ def rehearse(args, world, rank, scaling):
         dist.destroy_process_group()
 
 
-def _time_ms(torch, fn, reps=10, warm=2):
+def _time_ms(torch, fn, reps=10, warm=2, spread=None):
     """Median per-call GPU time of fn, calls enqueued back to back.  With a
     synchronise before every call, the start event would fire on an idle GPU
     while the host is still in fn's launch path (~0.1 ms of Python and HIP
@@ -307,7 +307,10 @@ def _time_ms(torch, fn, reps=10, warm=2):
         fn()
         b.record()
     torch.cuda.synchronize()
-    return statistics.median(a.elapsed_time(b) for a, b in ev[1:])  # the first call waits on the host
+    ts = [a.elapsed_time(b) for a, b in ev[1:]]  # the first call waits on the host
+    if spread is not None:  # min / max per-call time: how far one box's reps scatter
+        spread["spread_ms"] = [round(min(ts), 4), round(max(ts), 4)]
+    return statistics.median(ts)
 
 
 def extra_configs(u, synth, torch, dev, buf, G):
@@ -350,21 +353,22 @@ def c3_configs(u, synth, torch, dev, G):
     dg = u.rs.groups_to_device(groups, dev)
     u.rs.fill_ragged(base, dg, G, synth.DATA_SEED)
     plan = u.rs.RaggedPlan(groups)
-    t = _time_ms(torch, lambda: plan.encode(base))
+    sp_e, sp_d = {}, {}
+    t = _time_ms(torch, lambda: plan.encode(base), spread=sp_e)
     alg = int(((ks + ms_) * ls).sum())
     out["c3_ragged_encode"] = {
-        "encode_ms": round(t, 4), "groups": G, "bitslice_plan": plan.bitslice,
+        "encode_ms": round(t, 4), **sp_e, "groups": G, "bitslice_plan": plan.bitslice,
         "payload_GiBps": round(float((ks * ls).sum()) / (t * 1e-3) / 2**30, 1),
         "alg_GBps": round(alg / (t * 1e-3) / 1e9, 1), "alg_bytes": alg,
         "roofline_frac": round(alg / (t * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
     flags = synth.ragged_erasures(synth.ERASE_SEED, 0, ks + ms_, ms_, ERASURES)
     bits = torch.from_numpy(synth.present_bits(flags).view(np.int32)).to(dev)
     st = torch.empty(G, dtype=torch.int32, device=dev)
-    t = _time_ms(torch, lambda: plan.decode(base, bits, status=st))
+    t = _time_ms(torch, lambda: plan.decode(base, bits, status=st), spread=sp_d)
     e = ((flags[:, :20] == 0) & (np.arange(20)[None, :] < ks[:, None])).sum(1)
     alg = int((((e > 0) * ks + e) * ls).sum())  # k*len read + e*len written, groups with e > 0
     out["c3_ragged_decode"] = {
-        "decode_ms": round(t, 4), "groups": G, "rebuilt_rows": int(e.sum()),
+        "decode_ms": round(t, 4), **sp_d, "groups": G, "rebuilt_rows": int(e.sum()),
         "payload_GiBps": round(float((ks * ls).sum()) / (t * 1e-3) / 2**30, 1),
         "alg_GBps": round(alg / (t * 1e-3) / 1e9, 1), "alg_bytes": alg,
         "roofline_frac": round(alg / (t * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),

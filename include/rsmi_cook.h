@@ -84,6 +84,19 @@ int rsmi_cook_dev(const rsmi_cook_ctx *ctx, const rsmi_packet_batch *batch,
  * reference's de_cook returns -1 (the buffer then holds what it leaves). */
 int rsmi_decook_dev(const rsmi_cook_ctx *ctx, const rsmi_packet_batch *batch, void *stream);
 
+/* Out of place: packet i is read at batch->base + offset_i and its output
+ * written at out + offset_i (same offsets, cap and alignment; out 16-aligned).
+ * out may be device memory or pinned host memory mapped for the device
+ * (hipHostMalloc, or hipHostRegister'd): the kernel's own stores then carry
+ * the cooked packets over PCIe, so the transform and the D2H copy are one
+ * pass (the send side: cooked packets land where sendmmsg reads them).  For
+ * rsmi_decook_to, batch->base may likewise be pinned host memory read over
+ * PCIe (the receive side: the H2D copy and de_cook are one pass). */
+int rsmi_cook_to(const rsmi_cook_ctx *ctx, const rsmi_packet_batch *batch, uint8_t *out,
+                 const uint8_t *iv, const uint8_t *iv_len, uint64_t seed, void *stream);
+int rsmi_decook_to(const rsmi_cook_ctx *ctx, const rsmi_packet_batch *batch, uint8_t *out,
+                   void *stream);
+
 /* Synchronous host-memory forms (one H2D, one launch, one D2H; packet i at
  * host + i*stride): the per-packet mirror of do_cook/de_cook for callers that
  * have not moved to device batches. */

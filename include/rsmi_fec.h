@@ -119,6 +119,25 @@ int rsmi_fenc_groups(const rsmi_fenc *enc, int64_t *n_groups, int64_t *slot0, in
  * the shard rows line-aligned).  Asynchronous. */
 int rsmi_fenc_run_dev(rsmi_fenc *enc, uint8_t *slots_base, int64_t slot_stride, void *stream);
 
+/* rsmi_fenc_run_dev, then do_cook on every planned packet in the same stream
+ * of work -- what the reference does to each packet output() returns before
+ * it goes to the socket (fec_manager.cpp:364-460 -> my_send -> do_cook,
+ * packet.cpp:165-168, 303-308).  Packet p (rsmi_fenc_packets order) is read
+ * from its slot and written cooked at out + slot * slot_stride +
+ * RSMI_FEC_SLOT_PACKET; out_len[p] (device int32, n_packets entries) receives
+ * its cooked length (-1: it did not fit).  IVs are drawn on the device from
+ * (seed, p), iv_len in [4, 32] as the reference draws it.  out: device memory
+ * or pinned host memory (n_slots * slot_stride bytes, 16-aligned): with pinned
+ * host memory the cook's stores are the D2H transfer.  NULL cooks in place in
+ * slots_base.  A packet whose cooked form (up to 37 bytes longer, whole
+ * 16-byte pieces) does not fit its slot from RSMI_FEC_SLOT_PACKET gets
+ * out_len -1: size slot_stride for the tail (fec.py slot_stride_for).  ctx is
+ * an rsmi_cook.h context. */
+struct rsmi_cook_ctx;
+int rsmi_fenc_run_cooked_dev(rsmi_fenc *enc, uint8_t *slots_base, int64_t slot_stride,
+                             const struct rsmi_cook_ctx *ctx, uint64_t seed, uint8_t *out,
+                             int32_t *out_len, void *stream);
+
 /* ---- receive side: fec_decode_manager_t ------------------
  *
  * fec_decode_manager_t::input / output (fec_manager.cpp:469-797) take every

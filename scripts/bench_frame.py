@@ -13,7 +13,13 @@ The CPU baseline is the reference's own fec_encode_manager_t (oracle/_ref,
 fec_manager.cpp compiled unmodified) on one thread -- the reference runs it on
 its single libev thread -- over a bounded sample of the same events.
 
-    python scripts/bench_frame.py [--mode 0] [--groups 65536] [--reps 5]
+With --cook the run also cooks every emitted packet (do_cook, key set,
+device-drawn IVs): "dev" -- rsmi_fenc_run_cooked_dev into a device buffer;
+"host" -- the same into pinned host memory (the cook's stores are the D2H
+transfer, packets land where sendmmsg reads them); "sep" -- the unfused
+pipeline it replaces: run_dev, in-place rsmi_cook_dev, then a D2H copy.
+
+    python scripts/bench_frame.py [--mode 0] [--groups 65536] [--reps 5] [--cook dev|host|sep]
 """
 import argparse
 import json
@@ -52,6 +58,7 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--fec", default="20:10")
     ap.add_argument("--cpu-sample", type=int, default=100000, help="0 = no CPU baseline")
+    ap.add_argument("--cook", default="", choices=["", "dev", "host", "sep"])
     args = ap.parse_args()
     plen = args.len or (1200 if args.mode == 0 else 1250)
     npk = args.groups * 20
@@ -62,7 +69,11 @@ def main():
     s = torch.cuda.current_stream()
     res = []
     enc = FecEncoder(args.fec, args.mode, 1250, 200, seq0=1)  # steady state: one manager
-    slots = None
+    slots = out = None
+    ctx = None
+    if args.cook:
+        from udpspeeder_amd.cook import CookContext
+        ctx = CookContext(b"passwd123")
     for rep in range(args.reps + 1):
         t0 = time.perf_counter()
         p = enc.plan(lens, offs, inbuf)
@@ -70,10 +81,22 @@ def main():
         S = FecEncoder.slot_stride_for(int(p.groups["fec_len"].max()))
         if slots is None or slots.numel() < p.n_slots * S:
             slots = torch.empty(p.n_slots * S, dtype=torch.uint8, device=dev)
+            if args.cook:
+                out = torch.empty(p.n_slots * S, dtype=torch.uint8)
+                out = out.cuda() if args.cook == "dev" else out.pin_memory()
+        if args.cook == "sep":
+            offs_d = torch.from_numpy(p.packets["slot"].astype(np.int64) * S + 120).to(dev)
+            lens_d = torch.from_numpy(p.packets["len"].astype(np.int32)).to(dev)
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(s)
-        enc.run(slots, S)
+        if args.cook in ("dev", "host"):
+            enc.run_cooked(slots, S, ctx, rep + 1, out=out)
+        else:
+            enc.run(slots, S)
+            if args.cook == "sep":
+                ctx.cook(slots, lens_d, cap=S - 120, offsets=offs_d, seed=rep + 1)
+                out[:p.n_slots * S].copy_(slots[:p.n_slots * S], non_blocking=True)
         e1.record(s)
         torch.cuda.synchronize()
         if rep:
@@ -94,6 +117,12 @@ def main():
         "payload_GBps": round(payload / (t_run * 1e-3) / 1e9, 1),
         "frame_alg_bytes": frame_bytes, "encode_alg_bytes": enc_bytes,
         "run_alg_GBps": round((frame_bytes + enc_bytes) / (t_run * 1e-3) / 1e9, 1)}
+    if args.cook:
+        line["cook"] = {"dev": "fused, device out", "host": "fused, pinned host out (cook = D2H)",
+                        "sep": "run_dev + in-place cook + D2H copy"}[args.cook]
+        line["cooked_packets_per_s"] = round(len(p.packets) / (t_run * 1e-3), 1)
+        line["cooked_wire_GBps"] = round(int(p.packets["len"].sum() + 23 * len(p.packets)) /
+                                         (t_run * 1e-3) / 1e9, 1)
     if args.cpu_sample:
         line["cpu_baseline"] = cpu_baseline(args, plen, args.cpu_sample)
     print(json.dumps(line))

@@ -239,3 +239,67 @@ def test_gpu_per_call_interface(gpu):
         assert enc.input(d) == em.input(d)
         assert enc.output() == em.output()
     enc.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", NAMES)
+@pytest.mark.parametrize("nbatch,host", [(1, True), (3, False)])
+def test_gpu_frames_cooked_match_reference(fx, gpu, cook_oracle, name, nbatch, host):
+    """rsmi_fenc_run_cooked_dev: framing + encode + do_cook in one run, cooked
+    packets written straight into pinned host memory (or another device
+    buffer).  IVs are the device draw of (seed, packet index), so every cooked
+    packet is checked byte for byte against the oracle's do_cook of the
+    reference manager's packet (tests/golden/fec_encode.npz) where the fixture
+    holds full bytes, and through the oracle's de_cook against the fixture's
+    digest everywhere."""
+    import torch
+    from oracle.cpu import device_ivs
+    from udpspeeder_amd.cook import CookContext
+    from udpspeeder_amd.fec import FecEncoder
+    c = _case(fx, name)
+    key = b"secret key"
+    enc = FecEncoder(c["rs"], c["mode"], c["mtu"], c["ql"], seq0=c["seq0"])
+    ctx = CookContext(key)
+    lens, ev = c["lens"], c["ev"]
+    n = len(lens)
+    cuts = np.linspace(0, n, nbatch + 1).astype(int)
+    cooked, ivs = [], []
+    for bi, (a, b) in enumerate(zip(cuts[:-1], cuts[1:])):
+        offs = np.zeros(b - a, np.uint64)
+        o, chunks = 0, []
+        for i in range(a, b):
+            offs[i - a] = o
+            if ev[i] is not None:
+                chunks.append(ev[i])
+                o += len(ev[i])
+        inbuf = torch.from_numpy(np.frombuffer(b"".join(chunks) + bytes(32), np.uint8).copy()).cuda()
+        p = enc.plan(lens[a:b], offs, inbuf)
+        S = FecEncoder.slot_stride_for(max(p.slot_stride_min - 128, 0))
+        slots = torch.full((max(1, p.n_slots) * S,), 0xEE, dtype=torch.uint8, device="cuda")
+        out = torch.zeros(max(1, p.n_slots) * S, dtype=torch.uint8)
+        out = out.pin_memory() if host else out.cuda()
+        seed = 1000 + bi
+        ol = enc.run_cooked(slots, S, ctx, seed, out=out)
+        torch.cuda.synchronize()
+        ol = ol.cpu().numpy()[:len(p.packets)]
+        h = out.cpu().numpy()
+        iv, ivl = device_ivs(seed, 0, len(p.packets))
+        for i, (s, ln, _) in enumerate(p.packets):
+            assert ol[i] == ln + 4 + ivl[i] + 1, (bi, i)
+            cooked.append(h[s * S + 120:s * S + 120 + ol[i]].tobytes())
+            ivs.append(iv[i, :ivl[i]].tobytes())
+        del inbuf
+    assert len(cooked) == len(c["pk_len"])
+    plain = []
+    for ck in cooked:
+        rc, b, nl = cook_oracle.de_cook(ck, key)
+        assert rc == 0
+        plain.append(b[:nl])
+    assert [len(p) for p in plain] == list(c["pk_len"])
+    assert hashlib.sha256(b"".join(plain)).digest() == c["sha"]
+    exp = _expected_packets(c)
+    if exp is not None:
+        bad = [i for i, (ck, e, v) in enumerate(zip(cooked, exp, ivs))
+               if ck != cook_oracle.do_cook(e, v, key)]
+        assert not bad, (len(bad), bad[:5])
+    enc.close()

@@ -280,3 +280,44 @@ def test_full_size_round_trip(gpu):
     back = ctx.decook(base, out, cap=stride)
     assert bool((back == ln_).all())
     assert torch.equal(base[:, :ln_], orig[:, :ln_])
+
+
+@pytest.mark.parametrize("host", [False, True])
+def test_out_of_place_and_pinned_host(gpu, cook_oracle, host):
+    """rsmi_cook_to writes every cooked packet at the same offset of another
+    buffer -- device memory, or pinned host memory the kernel's stores reach
+    over PCIe (the send side's cook + D2H in one pass) -- and leaves the source
+    untouched; rsmi_decook_to reads a pinned host batch over PCIe (the receive
+    side's H2D + de_cook in one pass).  Bytes and lengths equal the oracle's
+    in-place transforms."""
+    import torch
+    from udpspeeder_amd.cook import CookContext
+    rng = np.random.default_rng(41 + host)
+    npk, stride, key = 300, 1344, b"passwd123"
+    lens = rng.integers(0, 1300, npk).astype(np.int32)
+    lens[:4] = [0, 1, 15, 16]
+    buf = rng.integers(0, 256, (npk, stride), dtype=np.uint8)
+    iv, ivl = cook_ivs(7, 0, npk)
+    ref, out_ref = _oracle_cook(cook_oracle, buf, lens, iv, ivl, key, 0)
+    t, ln, tiv, tivl = _tensors(gpu, buf, lens, iv, ivl)
+    ctx = CookContext(key)
+    dst = torch.zeros(npk * stride, dtype=torch.uint8)
+    dst = dst.pin_memory() if host else dst.to(gpu)
+    ol = ctx.cook_to(t, ln, dst, cap=stride, stride=stride, iv=tiv, iv_len=tivl)
+    torch.cuda.synchronize()
+    ol = ol.cpu().numpy()
+    assert (ol == out_ref).all()
+    got = dst.cpu().numpy().reshape(npk, stride)
+    for j in range(npk):
+        assert (got[j, :ol[j]] == ref[j, :ol[j]]).all(), j
+    assert (t.cpu().numpy() == buf).all()  # the source is read only
+    # de_cook from pinned host memory into the device
+    src = torch.from_numpy(ref.reshape(-1).copy()).pin_memory()
+    dec = torch.zeros(npk * stride, dtype=torch.uint8, device=gpu)
+    ln2 = torch.from_numpy(out_ref.astype(np.int32)).to(gpu)
+    ol2 = ctx.decook_to(src, ln2, dec, cap=stride, stride=stride)
+    torch.cuda.synchronize()
+    assert (ol2.cpu().numpy() == lens).all()
+    back = dec.cpu().numpy().reshape(npk, stride)
+    for j in range(npk):
+        assert (back[j, :lens[j]] == buf[j, :lens[j]]).all(), j

@@ -120,6 +120,8 @@ def _bind(lib: C.CDLL) -> C.CDLL:
         "rsmi_cook_ctx_destroy": ([vp], None),
         "rsmi_cook_dev": ([vp, vp, vp, vp, C.c_uint64, vp], i32),
         "rsmi_decook_dev": ([vp, vp, vp], i32),
+        "rsmi_cook_to": ([vp, vp, vp, vp, vp, C.c_uint64, vp], i32),
+        "rsmi_decook_to": ([vp, vp, vp, vp], i32),
         "rsmi_cook_host": ([vp, vp, i64, i64, C.c_int32, vp, vp, vp, vp, C.c_uint64], i32),
         "rsmi_decook_host": ([vp, vp, i64, i64, C.c_int32, vp, vp], i32),
         "rsmi_fec_config_init": ([vp, C.c_char_p, i32, i32, i32], i32),
@@ -130,6 +132,7 @@ def _bind(lib: C.CDLL) -> C.CDLL:
         "rsmi_fenc_packets": ([vp, vp], i32),
         "rsmi_fenc_groups": ([vp, vp, vp, vp, vp, vp, vp], i32),
         "rsmi_fenc_run_dev": ([vp, vp, i64, vp], i32),
+        "rsmi_fenc_run_cooked_dev": ([vp, vp, i64, vp, C.c_uint64, vp, vp, vp], i32),
         "rsmi_fdec_create": ([C.c_int32, vp], i32),
         "rsmi_fdec_destroy": ([vp], None),
         "rsmi_fdec_plan": ([vp, i64, vp, vp, vp, vp, i64, vp, vp], i32),

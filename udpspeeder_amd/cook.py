@@ -72,9 +72,9 @@ class CookContext:
         self.close()
 
     # ---- device batches -----------------------------------------------------------
-    def _batch(self, buf, lens, out_len, stride, offsets, cap):
+    def _batch(self, buf, lens, out_len, stride, offsets, cap, host_ok=False):
         import torch
-        if not (buf.is_cuda and buf.dtype == torch.uint8):
+        if not ((buf.is_cuda or (host_ok and buf.is_pinned())) and buf.dtype == torch.uint8):
             raise TypeError("buf must be a CUDA uint8 tensor")
         if lens.dtype != torch.int32 or not lens.is_cuda or not lens.is_contiguous():
             raise TypeError("lens must be a contiguous CUDA int32 tensor")
@@ -112,6 +112,48 @@ class CookContext:
         """de_cook every packet in place; returns out_len (-1 where de_cook fails)."""
         b, out_len = self._batch(buf, lens, out_len, stride, offsets, cap)
         check(lib().rsmi_decook_dev(self._h, C.byref(b), _stream_ptr(stream)), "rsmi_decook_dev")
+        return out_len
+
+    @staticmethod
+    def _out_ptr(out, need: int) -> int:
+        import torch
+        if not isinstance(out, torch.Tensor) or out.dtype != torch.uint8 or not out.is_contiguous():
+            raise TypeError("out must be a contiguous uint8 tensor")
+        if not out.is_cuda and not out.is_pinned():
+            raise TypeError("out must be a CUDA tensor or pinned host memory")
+        if out.numel() < need or out.data_ptr() % 16:
+            raise ValueError(f"out must be 16-aligned with >= {need} bytes")
+        return out.data_ptr()
+
+    def _extent(self, buf, b) -> int:
+        # packets sit at the same offsets in out as in buf: out spans buf
+        return buf.numel()
+
+    def cook_to(self, buf, lens, out, *, cap: int, stride: Optional[int] = None, offsets=None,
+                out_len=None, iv=None, iv_len=None, seed: int = 0, stream=None):
+        """do_cook every packet of buf into out at the same offset (rsmi_cook_to):
+        out may be a pinned host tensor, then the cooked packets cross PCIe in
+        the kernel's own stores.  Returns out_len."""
+        b, out_len = self._batch(buf, lens, out_len, stride, offsets, cap)
+        if (iv is None) != (iv_len is None):
+            raise ValueError("give both iv and iv_len or neither")
+        check(lib().rsmi_cook_to(self._h, C.byref(b), self._out_ptr(out, self._extent(buf, b)),
+                                 iv.data_ptr() if iv is not None else None,
+                                 iv_len.data_ptr() if iv_len is not None else None,
+                                 C.c_uint64(seed & (2**64 - 1)), _stream_ptr(stream)), "rsmi_cook_to")
+        return out_len
+
+    def decook_to(self, buf, lens, out, *, cap: int, stride: Optional[int] = None, offsets=None,
+                  out_len=None, stream=None):
+        """de_cook every packet of buf into out at the same offset (rsmi_decook_to);
+        buf may be a pinned host tensor read over PCIe in the kernel's loads."""
+        import torch
+        if isinstance(buf, torch.Tensor) and not buf.is_cuda:
+            if not buf.is_pinned():
+                raise TypeError("a host buf must be pinned")
+        b, out_len = self._batch(buf, lens, out_len, stride, offsets, cap, host_ok=True)
+        check(lib().rsmi_decook_to(self._h, C.byref(b), self._out_ptr(out, self._extent(buf, b)),
+                                   _stream_ptr(stream)), "rsmi_decook_to")
         return out_len
 
     # ---- host batches -------------------------------------------------------------

@@ -257,8 +257,13 @@ __device__ __forceinline__ int wave_max(int v) {
     return m;
 }
 
-__device__ __forceinline__ uint8_t *packet_ptr(const CookArgs &a, int64_t pk) {
-    return a.base + (a.offset ? a.offset[pk] : (uint64_t)pk * (uint64_t)a.stride);
+__device__ __forceinline__ uint64_t packet_off(const CookArgs &a, int64_t pk) {
+    if (a.pk) return (uint64_t)a.pk[pk].slot * (uint64_t)a.stride + (uint64_t)a.pk_off;
+    return a.offset ? a.offset[pk] : (uint64_t)pk * (uint64_t)a.stride;
+}
+
+__device__ __forceinline__ int packet_len(const CookArgs &a, int64_t pk) {
+    return a.pk ? a.pk[pk].len : a.len[pk];
 }
 
 // The kPpl pieces of round r owned by lane hl: zeros past ext.
@@ -308,13 +313,15 @@ __global__ __launch_bounds__(kThreads, COOK_OCC) void k_cook(CookArgs a) {
         const int64_t pk = kPpw * pw + sub;
         const bool have = pk < a.count;
         int L = -1, ivl = 0;
-        uint8_t *pkt = have ? packet_ptr(a, pk) : nullptr;
+        const uint64_t po = have ? packet_off(a, pk) : 0u;
+        uint8_t *pkt = have ? a.base + po : nullptr;
+        uint8_t *opkt = have ? (a.dst ? a.dst : a.base) + po : nullptr;  // where the output goes
         // round 0 is read up to the packet's cap (every packet owns cap bytes), so
         // these loads fly together with the length load instead of after it
         u32x4 cur[kPpl];
         load_round(cur, pkt, 0, hl, cap_extent(a, pkt, have));
         if (have) {
-            L = a.len[pk];
+            L = packet_len(a, pk);
             if (obs) ivl = a.iv ? a.iv_len[pk] : 4 + (int)(splitmix(a.seed, (uint64_t)pk, 0) % 29u);
         }
         const int out = L + (ck ? 4 : 0) + (obs ? ivl + 1 : 0);
@@ -354,7 +361,7 @@ __global__ __launch_bounds__(kThreads, COOK_OCC) void k_cook(CookArgs a) {
                 if (P < ext && P + 16 <= L) {  // wholly payload: obscure + xor, store now
                     u32x4 m = ks_piece(a, P);
                     if (ivl) m ^= iv_window_at(iv2w, ivr);
-                    st_piece(pkt + P, cur[p] ^ m);
+                    st_piece(opkt + P, cur[p] ^ m);
                 } else if (P < ext && P >= P0) {
                     dt = cur[p];
                     Pt = P;
@@ -396,7 +403,7 @@ __global__ __launch_bounds__(kThreads, COOK_OCC) void k_cook(CookArgs a) {
             if (ivl) m ^= iv_window(iv2w, (uint32_t)Pt, (uint32_t)ivl, magic);
             const u32x4 o = *reinterpret_cast<const u32x4 *>(ovl + (Pt - P0));
             const u32x4 lo = piece_mask(L - Pt), hi = piece_mask(out - Pt);
-            st_piece(pkt + Pt, ((dt ^ m) & lo) | (o & hi & ~lo) | (dt & ~hi));
+            st_piece(opkt + Pt, ((dt ^ m) & lo) | (o & hi & ~lo) | (dt & ~hi));
         }
         if (have && hl == 0) a.out_len[pk] = ok ? out : -1;
         wave_sync();  // the scratch slice is rewritten by the next packet
@@ -422,10 +429,12 @@ __global__ __launch_bounds__(kThreads, COOK_OCC) void k_decook(CookArgs a) {
         // (de_cook keeps its round-0 loads behind the length: loading up to the
         // cap here spills registers and measured slower)
         int L = -1;
-        uint8_t *pkt = nullptr;
+        uint8_t *pkt = nullptr, *opkt = nullptr;
         if (have) {
-            L = a.len[pk];
-            pkt = packet_ptr(a, pk);
+            L = packet_len(a, pk);
+            const uint64_t po = packet_off(a, pk);
+            pkt = a.base + po;
+            opkt = (a.dst ? a.dst : a.base) + po;  // where the output goes
         }
         const bool ok = have && L >= 0 && L <= RSMI_COOK_MAX_LEN && round16(L) <= a.cap &&
                         ((uintptr_t)pkt & 3) == 0;
@@ -481,7 +490,7 @@ __global__ __launch_bounds__(kThreads, COOK_OCC) void k_decook(CookArgs a) {
                     const u32x4 mi = ivl ? iv_window_at(iv2w, ivr) : u32x4{0, 0, 0, 0};
                     if (P + 16 <= L1) o = cur[p] ^ mk ^ mi;
                     else o = cur[p] ^ (mk & piece_mask(L - P)) ^ (mi & piece_mask(L1 - P));
-                    st_piece(pkt + P, o);
+                    st_piece(opkt + P, o);
                 }
                 if (ck) rc.add(T, crc_in(o, P, Lc), kLpp * p + hl, qr);
                 if (ivl) ivr = iv_step(ivr, sstep, (uint32_t)ivl);

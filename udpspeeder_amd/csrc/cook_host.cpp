@@ -206,6 +206,51 @@ extern "C" int rsmi_decook_dev(const rsmi_cook_ctx *c, const rsmi_packet_batch *
     return launch(make_args(c, b), c, true, (hipStream_t)stream);
 }
 
+extern "C" int rsmi_cook_to(const rsmi_cook_ctx *c, const rsmi_packet_batch *b, uint8_t *out,
+                            const uint8_t *iv, const uint8_t *iv_len, uint64_t seed, void *stream) {
+    if (!c) return fail(RSMI_ERR_INVALID, "null cook context");
+    if (int rc = check_batch(b)) return rc;
+    if ((iv == nullptr) != (iv_len == nullptr))
+        return fail(RSMI_ERR_INVALID, "iv and iv_len must both be given or both be NULL");
+    if (!out || ((uintptr_t)out & 15)) return fail(RSMI_ERR_INVALID, "out must be a 16-aligned pointer");
+    rsmi::CookArgs a = make_args(c, b);
+    a.dst = out;
+    a.iv = iv;
+    a.iv_len = iv_len;
+    a.seed = seed;
+    return launch(a, c, false, (hipStream_t)stream);
+}
+
+extern "C" int rsmi_decook_to(const rsmi_cook_ctx *c, const rsmi_packet_batch *b, uint8_t *out,
+                              void *stream) {
+    if (!c) return fail(RSMI_ERR_INVALID, "null cook context");
+    if (int rc = check_batch(b)) return rc;
+    if (!out || ((uintptr_t)out & 15)) return fail(RSMI_ERR_INVALID, "out must be a 16-aligned pointer");
+    rsmi::CookArgs a = make_args(c, b);
+    a.dst = out;
+    return launch(a, c, true, (hipStream_t)stream);
+}
+
+namespace rsmi {
+int cook_packets(const rsmi_cook_ctx *c, uint8_t *slots, int64_t S, const rsmi_fenc_packet *pk,
+                 int64_t npk, int32_t *out_len, uint8_t *dst, uint64_t seed, hipStream_t s) {
+    CookArgs a{};
+    a.base = slots;
+    a.dst = dst;
+    a.pk = pk;
+    a.pk_off = kSlotHeader;
+    a.stride = S;
+    a.count = npk;
+    a.cap = (int32_t)(S - kSlotHeader);
+    a.flags = c->flags;
+    a.out_len = out_len;
+    a.seed = seed;
+    a.tabs = c->tabs;
+    a.ks = c->ks;
+    return launch(a, c, false, s);
+}
+}  // namespace rsmi
+
 namespace {
 
 // Host batch: packets [count][stride] then len, out_len, iv, iv_len in one

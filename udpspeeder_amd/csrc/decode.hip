@@ -85,6 +85,18 @@ constexpr int kTile = 1280;    // bytes per lane-tile pass (64 x 16 + 64 x 4)
 #define DEC_PAIR 0             // uniform kernel: fold survivors in pairs (fewer XORs, more VGPRs)
 #endif
 constexpr int kDefer = 0x100;  // internal status: left for k_decode_ragged_big
+#ifndef DEC_TRACE
+#define DEC_TRACE 0            // measurement only: per-group phase timestamps of the class kernels
+#endif
+#if DEC_TRACE
+__device__ uint64_t *g_dec_trace;  // [group][8]: t0 t1 t2 t3 info wave tk0 tk1 (rsmi_debug_dec_trace)
+__device__ __forceinline__ uint64_t trace_now() {
+    asm volatile("" ::: "memory");
+    const uint64_t t = __builtin_amdgcn_s_memtime();
+    asm volatile("" ::: "memory");
+    return t;
+}
+#endif
 
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
     return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
@@ -196,27 +208,29 @@ __device__ __forceinline__ int select_survivors(int k, int n, Flag flag, const W
 }
 
 // ---- 3. Gauss-Jordan ------------------------------------------------------------
-// prow(R) points at the code's parity row R (R >= k: row R - k of the parity
-// rows).  Register form: lane c holds column c of [A | M], W = e + k <= 64.
+// Register form: lane c holds column c of [A | M], W = e + k <= 64: a missing
+// data index (c < e) or survivor c - e.  cv[r] is the code's parity row R_r
+// (survivor k - e + r) at column col, loaded by the caller before the first
+// survivor loads; rows >= e are don't-care.
+// Fraction-free elimination: pivot step p sets a[r] = piv * a[r] ^ f_r * a[p]
+// for every other row (f_r = a[r] at column p), with two split tables, both
+// one LDS level deep: the pivot's (uniform) and lane c's own a[p] (per lane,
+// multiplied by the scalar f_r as selector).  Every row is divided by its
+// diagonal at the end through log/exp (two per-lane levels for all rows).  The
+// dividing form chained pivot -> inverse -> table -> one row at a time.
 // Leaves coef[r][j] expanded into its split table at (t01, t2)[j * rows + r];
 // NR >= e is the number of row registers.
-template <int NR, class Row>
-__device__ __forceinline__ int gauss_jordan_regs(int k, int e, uint32_t sel_lane, const WaveLds &L,
-                                                 const Tables &T, Row prow, int lane) {
+template <int NR>
+__device__ __forceinline__ int gauss_jordan_regs(int k, int e, uint32_t col, const uint32_t (&cv)[NR],
+                                                 const uint32_t (&R)[NR], const WaveLds &L,
+                                                 const Tables &T, int lane) {
     int st = RSMI_DEC_OK;
     const int W = e + k;
-    // lane c holds column c: a missing data index (c < e) or survivor c - e
-    const uint32_t col = lane < e ? (uint32_t)L.miss[lane]
-                                  : (lane < W ? (uint32_t)L.sel[lane - e] : 0u);
     uint32_t a[NR];
 #pragma unroll
     for (int r = 0; r < NR; ++r) {
-        a[r] = 0;
-        if (r < e) {
-            const uint32_t R = __builtin_amdgcn_readlane(sel_lane, k - e + r);
-            const uint32_t v = prow(R)[col < (uint32_t)k ? col : 0u];
-            a[r] = (lane >= e && col >= (uint32_t)k) ? (uint32_t)(col == R) : v;
-        }
+        const uint32_t v = (lane >= e && col >= (uint32_t)k) ? (uint32_t)(col == R[r]) : cv[r];
+        a[r] = r < e ? v : 0u;
     }
 #pragma unroll
     for (int p = 0; p < NR; ++p) {
@@ -226,20 +240,30 @@ __device__ __forceinline__ int gauss_jordan_regs(int k, int e, uint32_t sel_lane
                 st = RSMI_DEC_SINGULAR;
                 break;
             }
-            const uint32_t ip = __builtin_amdgcn_readfirstlane(T.linv[piv]);
-            a[p] = gmul_t(T.s01[ip], T.s2[ip], a[p]);
+            const uint32_t ap = a[p];
+            const uint4 tp = T.s01[piv], tl = T.s01[ap];
+            const uint32_t tp2 = T.s2[piv], tl2 = T.s2[ap];
 #pragma unroll
             for (int r = 0; r < NR; ++r) {
                 if (r < e && r != p) {
                     const uint32_t f = __builtin_amdgcn_readlane(a[r], p);
-                    a[r] ^= gmul_t(T.s01[f], T.s2[f], a[p]);
+                    a[r] = gmul_t(tp, tp2, a[r]) ^ gmul_t(tl, tl2, f);
                 }
-                __builtin_amdgcn_sched_barrier(0);
             }
         }
     }
     st = __builtin_amdgcn_readfirstlane(st);
     if (st != RSMI_DEC_OK) return st;
+    // [D | D coef] -> [I | coef]: a[r] *= d_r^-1 as exp[log a + 255 - log d_r]
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+        if (r < e) {
+            const uint32_t d = __builtin_amdgcn_readlane(a[r], r);
+            const uint32_t li = 255u - (uint32_t)__builtin_amdgcn_readfirstlane(T.llog[d]);
+            const uint32_t x = a[r];
+            a[r] = x ? (uint32_t)T.lexp[T.llog[x] + li] : 0u;
+        }
+    }
     // coef[r][j] sits in lane e + j: expand into its split table
     if (lane >= e && lane < W) {
         const int base = (lane - e) * L.rows;
@@ -767,23 +791,38 @@ struct DeferMark {
     uint32_t epoch;
 };
 
-template <int WC, int NR, class Flag>
+struct NoHook {
+    __device__ void operator()() const {}
+};
+
+// after_select() runs once, right after the survivor selection (the class
+// kernels fetch the next group's present words there).
+template <int WC, int NR, class Flag, class Hook = NoHook>
 __device__ __forceinline__ void ragged_group_run(const GroupDesc &D, Flag flag, uint8_t *base,
                                                  int32_t *status_out, const Tables &T,
                                                  const WaveLds &L, int kmax, int lane,
-                                                 DeferMark dm = DeferMark{nullptr, 0}) {
+                                                 DeferMark dm = DeferMark{nullptr, 0},
+                                                 Hook after_select = Hook{}) {
     const int64_t g = D.g;
     const int k = D.k, n = D.n, len = D.len;
     const uint32_t ss = D.ss;
     const uint64_t off = D.off;
     const uint8_t *rows = D.rows;
     if (k < 1 || n < k || n > 256 || (n > k && !rows)) {
+        after_select();
         if (lane == 0) status_out[g] = RSMI_DEC_UNSUPPORTED;
         return;
     }
+#if DEC_TRACE
+    const uint64_t tr0 = trace_now();
+#endif
     int e;
     const int cnt = select_survivors(k, n, flag, L, lane, e);
     wave_sync();
+    after_select();
+#if DEC_TRACE
+    const uint64_t tr1 = trace_now();
+#endif
     if (cnt < k || e == 0) {
         if (lane == 0) status_out[g] = cnt < k ? RSMI_DEC_TOO_FEW : RSMI_DEC_OK;
         return;
@@ -795,9 +834,27 @@ __device__ __forceinline__ void ragged_group_run(const GroupDesc &D, Flag flag, 
         }
         return;
     }
-    auto prow = [&](uint32_t R) { return rows + (R - k) * k; };
     const int lpad = rag_lpad((uint32_t)len, ss);
     const uint32_t sel_lane = lane < k ? (uint32_t)L.sel[lane] : 0u;
+    // The system's code-row bytes (lane c: column c of rows R_0..R_{NR-1}, R_r
+    // = survivor k - e + r, clamped for r >= e), as buffer loads issued before
+    // the first survivor loads: waiting for them is vmcnt(survivor loads), not
+    // 0.  (Through a generic pointer they were flat loads, each followed by a
+    // full vmcnt(0) lgkmcnt(0) wait that also waited for the survivor ring.)
+    const uint32_t col = lane < e ? (uint32_t)L.miss[lane]
+                                  : (lane < e + k ? (uint32_t)L.sel[lane - e] : 0u);
+    uint32_t cv[NR], Rr[NR];
+    {
+        const __amdgpu_buffer_rsrc_t rr = group_rsrc(rows, (uint32_t)((n - k) * k));
+        const uint32_t cc = col < (uint32_t)k ? col : 0u;
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+            const int ri = k - e + r < k ? k - e + r : k - 1;
+            Rr[r] = __builtin_amdgcn_readlane(sel_lane, ri);
+            const uint32_t ro = Rr[r] >= (uint32_t)k ? (Rr[r] - (uint32_t)k) * (uint32_t)k : 0u;
+            cv[r] = __builtin_amdgcn_raw_buffer_load_b8(rr, ro + cc, 0, 0);
+        }
+    }
     auto rebuild = [&](auto wc) {
         constexpr int W = decltype(wc)::value;
         Rebuild<W> B;
@@ -809,8 +866,19 @@ __device__ __forceinline__ void ragged_group_run(const GroupDesc &D, Flag flag, 
         B.so_lane = sel_lane * ss;
         B.mo_lane = (lane < e ? (uint32_t)L.miss[lane] : 0u) * ss;
         if (len > 0) B.start_tile(0, lane);
-        const int st = gauss_jordan_regs<NR>(k, e, sel_lane, L, T, prow, lane);
+        const int st = gauss_jordan_regs<NR>(k, e, col, cv, Rr, L, T, lane);
+#if DEC_TRACE
+        const uint64_t tr2 = trace_now();
+#endif
         if (st == RSMI_DEC_OK && len > 0) B.run(L, lane);
+#if DEC_TRACE
+        const uint64_t tr3 = trace_now();
+        if (lane == 0 && g_dec_trace) {
+            uint64_t *t = g_dec_trace + g * 8;
+            t[0] = tr0; t[1] = tr1; t[2] = tr2; t[3] = tr3;
+            t[4] = (uint64_t)W | ((uint64_t)k << 8) | ((uint64_t)e << 16) | ((uint64_t)len << 32);
+        }
+#endif
         return st;
     };
     int st;
@@ -882,61 +950,78 @@ __global__ __launch_bounds__(256, DEC_RAG_OCC) void k_decode_ragged(
 
 // Plans: the groups of one tile-width class, registers cut for that width so
 // short groups run at up to 8 waves per SIMD: C3's groups are latency-bound
-// (a chain of dependent round trips per group).  Wave w takes the groups the
-// plan dealt it (ragged.cpp: balanced so that the one resident round of waves
-// ends together), as 8-dword records {offset lo, hi, stride, len, k | n << 16,
-// status index, parity-rows pointer lo, hi} at rec[wst[w] .. wst[w+1]): eight
-// records and their present masks come in with two wave-wide loads, and each
-// group's fields are read out of registers -- no descriptor, index or code
-// directory round trip per group.
+// (a chain of dependent round trips per group).  Workgroup b takes the groups
+// the plan dealt it (ragged.cpp: longest first onto the least-loaded
+// workgroup) as 8-dword records {offset lo, hi, stride, len, k | n << 16,
+// status index, parity-rows pointer lo, hi} at rec[wst[b] .. wst[b+1]): the
+// records and their 8 present words come into LDS with two block-wide loads,
+// and the block's waves take groups from an LDS counter, so a wave whose
+// groups lost many data shards (long eliminations and multiplies: costs the
+// plan cannot see) does not hold the round up while its neighbours idle.
 template <int W, int OCC>
-__global__ __launch_bounds__(256, OCC) void k_decode_ragged_cls(
-    const uint32_t *__restrict__ rec, const uint32_t *__restrict__ wst, int nw, uint8_t *base,
+__global__ __launch_bounds__(64 * kClsWaves, OCC) void k_decode_ragged_cls(
+    const uint32_t *__restrict__ rec, const uint32_t *__restrict__ wst, int nb, int maxb, uint8_t *base,
     const uint32_t *__restrict__ present, int32_t *status_out, const uint32_t *ptab,
     const uint8_t *gftab, int kmax, DeferMark dm) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+#if DEC_TRACE
+    const uint64_t tk0 = trace_now();
+#endif
+    const int b = blockIdx.x;
+    if (b >= nb) return;  // (whole block: before any barrier)
+    const uint32_t i0 = wst[b], cnt = wst[b + 1] - i0;
+    uint32_t *srec = reinterpret_cast<uint32_t *>(smem + kTabBytes + kClsWaves * rag_lds_bytes(kmax, kClsRows));
+    uint32_t *spw = srec + (size_t)maxb * 8;
+    uint32_t *next = spw + (size_t)maxb * 8;
+    for (uint32_t t = threadIdx.x; t < cnt * 8; t += blockDim.x) srec[t] = rec[(size_t)i0 * 8 + t];
+    if (threadIdx.x == 0) *next = 0;
     const Tables T = load_tables(smem, ptab, gftab);
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     const WaveLds L = rag_slice(smem + kTabBytes + wid * rag_lds_bytes(kmax, kClsRows), kmax, kClsRows);
     __syncthreads();
-    const int w = blockIdx.x * kWaves + wid;
-    if (w >= nw) return;
-    const uint32_t i0 = wst[w], i1 = wst[w + 1];
-    for (uint32_t b0 = i0; b0 < i1; b0 += 8) {
-        const uint32_t nb = i1 - b0 < 8u ? i1 - b0 : 8u;
-        // lane l: dword (l & 7) of record (l >> 3), then present word (l & 7)
-        // of that record's group
-        uint32_t r = 0, pw = 0;
-        if ((uint32_t)(lane >> 3) < nb) r = rec[(size_t)(b0 + (lane >> 3)) * 8 + (lane & 7)];
-        const uint32_t gl = (uint32_t)__shfl(r, (lane & ~7) | 5);
-        if ((uint32_t)(lane >> 3) < nb) pw = present[(size_t)gl * 8 + (lane & 7)];
-        for (uint32_t i = 0; i < nb; ++i) {
-            int q = (int)i * 8;
-            asm volatile("" : "+s"(q));  // the record's lane base, a scalar
-            GroupDesc D;
-            // (readlane returns int: every dword goes through uint32_t before it
-            // is widened, or a low half with bit 31 set sign-extends into the
-            // high half of a 64-bit offset or pointer)
-            auto dw = [&](int f) { return (uint32_t)__builtin_amdgcn_readlane(r, q + f); };
-            const uint32_t kn = dw(4);
-            D.g = (int64_t)dw(5);
-            D.k = (int)(kn & 0xFFFFu);
-            D.n = (int)(kn >> 16);
-            D.len = (int)dw(3);
-            D.ss = dw(2);
-            D.off = ((uint64_t)dw(1) << 32) | (uint64_t)dw(0);
-            D.rows = reinterpret_cast<const uint8_t *>((uintptr_t)(((uint64_t)dw(7) << 32) | (uint64_t)dw(6)));
-            ragged_group_run<W, kClsRows>(
-                D,
-                [&](int b, int idx) {
-                    const uint32_t lo = __builtin_amdgcn_readlane(pw, q + ((b >> 5) & 7));
-                    const uint32_t hi = __builtin_amdgcn_readlane(pw, q + (((b >> 5) + 1) & 7));
-                    return ((((idx & 32) ? hi : lo) >> (idx & 31)) & 1u) != 0;
-                },
-                base, status_out, T, L, kmax, lane, dm);
-            wave_sync();  // the LDS slice is rewritten by the next group
+    for (uint32_t t = threadIdx.x; t < cnt * 8; t += blockDim.x)
+        spw[t] = present[(size_t)srec[(t & ~7u) + 5] * 8 + (t & 7u)];
+    __syncthreads();
+#if DEC_TRACE
+    const uint64_t tk1 = trace_now();
+    const int w = b * kClsWaves + wid;
+#endif
+    for (;;) {
+        uint32_t i = 0;
+        if (lane == 0) i = __hip_atomic_fetch_add(next, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        i = (uint32_t)__builtin_amdgcn_readfirstlane(i);
+        if (i >= cnt) break;
+        const uint32_t r = srec[i * 8 + (lane & 7)];
+        const uint32_t pw = spw[i * 8 + (lane & 7)];
+        GroupDesc D;
+        // (readlane returns int: every dword goes through uint32_t before it
+        // is widened, or a low half with bit 31 set sign-extends into the
+        // high half of a 64-bit offset or pointer)
+        auto dw = [&](int f) { return (uint32_t)__builtin_amdgcn_readlane(r, f); };
+        const uint32_t kn = dw(4);
+        D.g = (int64_t)dw(5);
+        D.k = (int)(kn & 0xFFFFu);
+        D.n = (int)(kn >> 16);
+        D.len = (int)dw(3);
+        D.ss = dw(2);
+        D.off = ((uint64_t)dw(1) << 32) | (uint64_t)dw(0);
+        D.rows = reinterpret_cast<const uint8_t *>((uintptr_t)(((uint64_t)dw(7) << 32) | (uint64_t)dw(6)));
+#if DEC_TRACE
+        if (lane == 0 && g_dec_trace) {
+            uint64_t *tt = g_dec_trace + D.g * 8;
+            tt[5] = (uint64_t)w; tt[6] = tk0; tt[7] = tk1;
         }
+#endif
+        ragged_group_run<W, kClsRows>(
+            D,
+            [&](int bb, int idx) {
+                const uint32_t lo = __builtin_amdgcn_readlane(pw, (bb >> 5) & 7);
+                const uint32_t hi = __builtin_amdgcn_readlane(pw, ((bb >> 5) + 1) & 7);
+                return ((((idx & 32) ? hi : lo) >> (idx & 31)) & 1u) != 0;
+            },
+            base, status_out, T, L, kmax, lane, dm);
+        wave_sync();  // the LDS slice is rewritten by the next group
     }
 }
 
@@ -1134,13 +1219,15 @@ hipError_t launch_decode_ragged_cls(const rsmi_group *groups, const ClsLaunch &C
                                     const uint64_t *code_dir, const uint32_t *ptab,
                                     const uint8_t *gftab, hipStream_t s, const hipStream_t cs[4]) {
     kmax = kmax < 1 ? 1 : (kmax > 32 ? 32 : kmax);  // larger k: the workgroup kernel
-    const size_t lds = kTabBytes + (size_t)kWaves * rag_lds_bytes(kmax, kClsRows);
     auto launch = [&](auto kern, int c) {
-        const int nw = C.nw[c];
-        if (nw <= 0) return hipSuccess;
-        kern<<<(unsigned)((nw + kWaves - 1) / kWaves), 64 * kWaves, lds, cs[c]>>>(
-            C.rec, C.wst[c], nw, base, present_bits, status, ptab, gftab, kmax,
-            DeferMark{C.defer, C.epoch});
+        const int nb = C.nw[c];
+        if (nb <= 0) return hipSuccess;
+        // tables | wave slices | records | present words | counter
+        const size_t lds = kTabBytes + (size_t)kClsWaves * rag_lds_bytes(kmax, kClsRows) +
+                           (size_t)C.maxb[c] * 64 + 16;
+        kern<<<(unsigned)nb, 64 * kClsWaves, lds, cs[c]>>>(C.rec, C.wst[c], nb, C.maxb[c], base,
+                                                        present_bits, status, ptab, gftab, kmax,
+                                                        DeferMark{C.defer, C.epoch});
         return hipGetLastError();
     };
     hipError_t e = launch(k_decode_ragged_cls<5, DEC_CLS_OCC5>, 3);
@@ -1163,3 +1250,9 @@ hipError_t launch_decode_ragged_big(const rsmi_group *groups, int64_t ngroups, u
 }
 
 }  // namespace rsmi
+
+#if DEC_TRACE
+extern "C" int rsmi_debug_dec_trace(void *dev_ptr) {  // measurement builds only
+    return hipMemcpyToSymbol(HIP_SYMBOL(rsmi::g_dec_trace), &dev_ptr, sizeof(dev_ptr)) == hipSuccess ? 0 : -1;
+}
+#endif

@@ -84,6 +84,8 @@ struct HostArr {
     }
     void clear() { n = 0; }
     size_t size() const { return n; }
+    bool empty() const { return n == 0; }
+    T *data() const { return p; }
     T *begin() { return p; }
     T *end() { return p + n; }
     T &operator[](size_t i) { return p[i]; }
@@ -112,6 +114,7 @@ struct PlanSet {
     HostArr<CarryCopy> carry;
     HostArr<rsmi::ByteRun> stale;       // stale bytes of this batch's groups
     HostArr<rsmi::ByteRun> shadow_upd;  // the buffer at the batch end -> dshadow
+    HostArr<rsmi_fenc_packet> packets;  // what output() returns, in order (pinned: cooked runs upload it)
     hipEvent_t done = nullptr;
     bool in_flight = false;
 };
@@ -130,7 +133,6 @@ struct rsmi_fenc {
     PlanSet ps[2];
     int pcur = 1;              // ps[pcur] holds the last plan
     PlanSet *P = &ps[1];
-    std::vector<rsmi_fenc_packet> packets;
     std::vector<int64_t> g_slot0;
     std::vector<int32_t> g_k, g_m, g_len;
     std::vector<uint32_t> g_seq;
@@ -277,7 +279,7 @@ void close_group(rsmi_fenc *E, int k, int m, int fec_len) {
         const Pending &p = E->pend[j];
         E->P->srcs.push_back(FrameSrc{p.addr, p.len, E->cfg.mode == 0 ? off : 0u});
         off += 2 + p.len;
-        if (p.emitted >= 0) E->packets[(size_t)p.emitted].slot = slot0 + (int64_t)j;
+        if (p.emitted >= 0) E->P->packets[(size_t)p.emitted].slot = slot0 + (int64_t)j;
     }
     E->P->jobs.push_back(G);
     if (E->cfg.mode == 0) stale_runs(E, slot0, k, fec_len, E->blob_len);
@@ -357,38 +359,48 @@ int input_event(rsmi_fenc *E, int32_t event, bool has, int len, uint64_t addr) {
             fec_len = -1;
             for (const Pending &p : E->pend) fec_len = std::max(fec_len, (int)p.len + 2);
         }
-        const int64_t first_pk = (int64_t)E->packets.size();
+        const int64_t first_pk = (int64_t)E->P->packets.size();
         // the packets output() returns (:318-346, fast send :376-393)
         if (mode == 0) {
             for (int i = 0; i < k + m; ++i)
-                E->packets.push_back(rsmi_fenc_packet{-1, 8 + fec_len, event});
+                E->P->packets.push_back(rsmi_fenc_packet{-1, 8 + fec_len, event});
         } else {
             if (has) {  // the packet that completed the group goes with the parity (:376-381)
-                E->pend.back().emitted = (int64_t)E->packets.size();
-                E->packets.push_back(rsmi_fenc_packet{-1, 8 + (int)E->pend.back().len + 2, event});
+                E->pend.back().emitted = (int64_t)E->P->packets.size();
+                E->P->packets.push_back(rsmi_fenc_packet{-1, 8 + (int)E->pend.back().len + 2, event});
             }
             for (int i = k; i < k + m; ++i)
-                E->packets.push_back(rsmi_fenc_packet{-1, 8 + fec_len, event});
+                E->P->packets.push_back(rsmi_fenc_packet{-1, 8 + fec_len, event});
         }
         const int64_t slot0 = E->n_slots;
         close_group(E, k, m, fec_len);
         if (mode == 0) {
-            for (int i = 0; i < k + m; ++i) E->packets[(size_t)(first_pk + i)].slot = slot0 + i;
+            for (int i = 0; i < k + m; ++i) E->P->packets[(size_t)(first_pk + i)].slot = slot0 + i;
         } else {
             int64_t q = first_pk + (has ? 1 : 0);
-            for (int i = k; i < k + m; ++i) E->packets[(size_t)q++].slot = slot0 + i;
+            for (int i = k; i < k + m; ++i) E->P->packets[(size_t)q++].slot = slot0 + i;
         }
         E->seq++;
         E->pend.clear();
         E->blob_len = 4;
     } else if (has && mode == 1) {  // encode_fast_send (:394-429): the data packet goes now
-        E->pend.back().emitted = (int64_t)E->packets.size();
-        E->packets.push_back(rsmi_fenc_packet{-1, 8 + len + 2, event});
+        E->pend.back().emitted = (int64_t)E->P->packets.size();
+        E->P->packets.push_back(rsmi_fenc_packet{-1, 8 + len + 2, event});
     }
     if (has && delayed) append();  // :436-439
     return 0;
 }
 
+}  // namespace
+
+namespace {
+struct CookSpec {  // rsmi_fenc_run_cooked_dev: do_cook on the batch's packets after the encode
+    const rsmi_cook_ctx *ctx;
+    uint64_t seed;
+    uint8_t *out;
+    int32_t *out_len;
+};
+int run_dev(rsmi_fenc *E, uint8_t *slots, int64_t S, void *stream, const CookSpec *ck);
 }  // namespace
 
 extern "C" {
@@ -500,7 +512,7 @@ int rsmi_fenc_plan(rsmi_fenc *E, int64_t n_events, const int32_t *len, const uin
     E->P->jobs.clear();
     E->P->srcs.clear();
     E->P->carry.clear();
-    E->packets.clear();
+    E->P->packets.clear();
     E->g_slot0.clear();
     E->g_k.clear();
     E->g_m.clear();
@@ -537,7 +549,7 @@ int rsmi_fenc_plan(rsmi_fenc *E, int64_t n_events, const int32_t *len, const uin
         G.idx0 = (uint8_t)j;
         E->P->srcs.push_back(FrameSrc{p.addr, p.len, 0});
         E->P->jobs.push_back(G);
-        E->packets[(size_t)p.emitted].slot = slot;
+        E->P->packets[(size_t)p.emitted].slot = slot;
         E->stride_min = std::max(E->stride_min, (int32_t)((rsmi::kSlotShard + p.len + 2 + 15) & ~15u));
     }
     shadow_update(E);
@@ -556,14 +568,14 @@ int rsmi_fenc_plan(rsmi_fenc *E, int64_t n_events, const int32_t *len, const uin
     E->carry_cur = nxt;
     E->planned = true;
     if (n_slots) *n_slots = E->n_slots;
-    if (n_packets) *n_packets = (int64_t)E->packets.size();
+    if (n_packets) *n_packets = (int64_t)E->P->packets.size();
     if (slot_stride_min) *slot_stride_min = E->stride_min;
     return RSMI_OK;
 }
 
 int rsmi_fenc_packets(const rsmi_fenc *E, rsmi_fenc_packet *out) {
-    if (!E || (!out && !E->packets.empty())) return fail(RSMI_ERR_INVALID, "bad fenc_packets args");
-    if (!E->packets.empty()) std::memcpy(out, E->packets.data(), E->packets.size() * sizeof(rsmi_fenc_packet));
+    if (!E || (!out && !E->P->packets.empty())) return fail(RSMI_ERR_INVALID, "bad fenc_packets args");
+    if (!E->P->packets.empty()) std::memcpy(out, E->P->packets.data(), E->P->packets.size() * sizeof(rsmi_fenc_packet));
     return RSMI_OK;
 }
 
@@ -581,6 +593,24 @@ int rsmi_fenc_groups(const rsmi_fenc *E, int64_t *n, int64_t *slot0, int32_t *k,
 }
 
 int rsmi_fenc_run_dev(rsmi_fenc *E, uint8_t *slots, int64_t S, void *stream) {
+    return run_dev(E, slots, S, stream, nullptr);
+}
+
+int rsmi_fenc_run_cooked_dev(rsmi_fenc *E, uint8_t *slots, int64_t S, const rsmi_cook_ctx *ctx,
+                             uint64_t seed, uint8_t *out, int32_t *out_len, void *stream) {
+    if (!ctx) return fail(RSMI_ERR_INVALID, "rsmi_fenc_run_cooked_dev: null cook context");
+    if (E && E->planned && !E->P->packets.empty() && !out_len)
+        return fail(RSMI_ERR_INVALID, "rsmi_fenc_run_cooked_dev: null out_len");
+    if (out && ((uintptr_t)out & 15)) return fail(RSMI_ERR_INVALID, "cooked out must be 16-aligned");
+    const CookSpec ck{ctx, seed, out, out_len};
+    return run_dev(E, slots, S, stream, &ck);
+}
+
+}  // extern "C"
+
+namespace {
+
+int run_dev(rsmi_fenc *E, uint8_t *slots, int64_t S, void *stream, const CookSpec *ck) {
     if (!E || !E->planned) return fail(RSMI_ERR_INVALID, "rsmi_fenc_run_dev without a plan");
     if (E->plan_only) return fail(RSMI_ERR_INVALID, "rsmi_fenc_run_dev on a plan-only encoder");
     if (E->n_slots && (!slots || ((uintptr_t)slots & 15)))
@@ -626,13 +656,18 @@ int rsmi_fenc_run_dev(rsmi_fenc *E, uint8_t *slots, int64_t S, void *stream) {
         if (hipMemsetAsync(E->dshadow, 0, rsmi::kBlobBufBytes, s) != hipSuccess)
             return fail(RSMI_ERR_HIP, "fenc: clear blob buffer");
     }
+    // cooked runs: the packet list goes up with the plan (the cook kernel reads
+    // each packet's slot and length from it)
+    const size_t npk = ck ? E->P->packets.size() : 0;
     const size_t gb = E->P->jobs.size() * sizeof(FrameGroup), sb = E->P->srcs.size() * sizeof(FrameSrc),
                  cb = E->P->carry.size() * sizeof(CarryCopy),
                  rb = E->P->stale.size() * sizeof(rsmi::ByteRun),
-                 ub = E->P->shadow_upd.size() * sizeof(rsmi::ByteRun);
+                 ub = E->P->shadow_upd.size() * sizeof(rsmi::ByteRun),
+                 pb = npk * sizeof(rsmi_fenc_packet);
     const size_t go = 0, so = (gb + 255) & ~size_t(255), co = (so + sb + 255) & ~size_t(255),
-                 ro = (co + cb + 255) & ~size_t(255), uo = (ro + rb + 255) & ~size_t(255);
-    const size_t all = uo + ub + 16;
+                 ro = (co + cb + 255) & ~size_t(255), uo = (ro + rb + 255) & ~size_t(255),
+                 po = (uo + ub + 255) & ~size_t(255);
+    const size_t all = po + pb + 16;
     if (all > E->plan_cap) {
         int rcw = wait_set(prev);
         if (rcw) return rcw;
@@ -646,6 +681,7 @@ int rsmi_fenc_run_dev(rsmi_fenc *E, uint8_t *slots, int64_t S, void *stream) {
     if (e == hipSuccess && rb) e = hipMemcpyAsync(E->dplan + ro, E->P->stale.p, rb, hipMemcpyHostToDevice, s);
     if (e == hipSuccess && ub)
         e = hipMemcpyAsync(E->dplan + uo, E->P->shadow_upd.p, ub, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess && pb) e = hipMemcpyAsync(E->dplan + po, E->P->packets.p, pb, hipMemcpyHostToDevice, s);
     if (e == hipSuccess)
         e = rsmi::launch_frame(reinterpret_cast<const FrameGroup *>(E->dplan + go), (int64_t)E->P->jobs.size(),
                                reinterpret_cast<const FrameSrc *>(E->dplan + so), carry, slots, S, s);
@@ -666,11 +702,19 @@ int rsmi_fenc_run_dev(rsmi_fenc *E, uint8_t *slots, int64_t S, void *stream) {
     if (e == hipSuccess)
         e = rsmi::launch_carry(reinterpret_cast<const CarryCopy *>(E->dplan + co),
                                (int64_t)E->P->carry.size(), carry, s);
-    if (e == hipSuccess) e = hipEventRecord(E->P->done, s);
     if (e != hipSuccess) return fail(RSMI_ERR_HIP, std::string("fenc carry: ") + hipGetErrorString(e));
+    // do_cook on every packet output() returned (my_send, packet.cpp:165-168),
+    // after the blob buffer update above has read the plain shards
+    if (npk) {
+        rc = rsmi::cook_packets(ck->ctx, slots, S, reinterpret_cast<const rsmi_fenc_packet *>(E->dplan + po),
+                                (int64_t)npk, ck->out_len, ck->out, ck->seed, s);
+        if (rc) return rc;
+    }
+    e = hipEventRecord(E->P->done, s);
+    if (e != hipSuccess) return fail(RSMI_ERR_HIP, std::string("fenc event: ") + hipGetErrorString(e));
     E->P->in_flight = true;
     E->planned = false;
     return RSMI_OK;
 }
 
-}  // extern "C"
+}  // namespace

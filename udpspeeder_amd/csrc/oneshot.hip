@@ -59,7 +59,7 @@ __global__ __launch_bounds__(kOneThreads) void k_one_group(OneArgs a) {
     __shared__ uint32_t ct2[kCoefMax];
     __shared__ uint8_t aug[kAugMax];
     __shared__ __attribute__((aligned(16))) uint8_t xs[kSurvLds];  // survivor j at j * lpad
-    __shared__ int s_e, s_cnt, s_st;
+    __shared__ int s_e, s_st;
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int k = a.k, n = a.n, len = a.len;
@@ -99,7 +99,6 @@ __global__ __launch_bounds__(kOneThreads) void k_one_group(OneArgs a) {
         }
         if (lane == 0) {
             s_e = e;
-            s_cnt = cnt;
             s_st = cnt < k ? RSMI_DEC_TOO_FEW : RSMI_DEC_OK;
         }
     }

@@ -173,10 +173,12 @@ extern "C" int rsmi_ragged_plan_create(const rsmi_group *g, int64_t ngroups,
         if (nb <= nbuiltin) P->nwaves_builtin = P->nwaves;
     }
     // decode classes: the width each group's tiles take (decode.hip).  Each
-    // class kernel runs one resident round of waves; the class's groups are
-    // dealt to those waves longest-first onto the least-loaded wave, on an
-    // estimated cost, so the round ends together (a strided deal left the
-    // average wave alive for 53-67 % of its kernel: profiles/r03).
+    // class kernel runs one resident round of workgroups; the class's groups
+    // are dealt to the workgroups longest-first onto the least-loaded one, on
+    // an estimated cost, and a workgroup's waves take its groups one at a time
+    // (decode.hip k_decode_ragged_cls).  A deal straight to waves could not see
+    // the erasures, which set a group's elimination and multiply cost: the
+    // slowest wave of a round ran 44 % past the median (profiles/r03 c3_trace).
     std::vector<uint32_t> cls, wst;
     int64_t wst_first[4] = {0, 0, 0, 0};
     {
@@ -194,10 +196,13 @@ extern "C" int rsmi_ragged_plan_create(const rsmi_group *g, int64_t ngroups,
             auto &v = by[(size_t)c];
             const int W = c == 0 ? 1 : (c == 1 ? 2 : (c == 2 ? 4 : 5));
             const int64_t slots = (int64_t)ncu * 4 * rsmi::decode_cls_occupancy(c);
-            const int nw = (int)std::min<int64_t>((int64_t)v.size(), slots);
-            P->cls.nw[c] = nw;
+            // one wave per group at least: blocks of kClsWaves waves
+            const int nb = (int)((std::min<int64_t>((int64_t)v.size(), slots) + rsmi::kClsWaves - 1) /
+                                 rsmi::kClsWaves);
+            P->cls.nw[c] = nb;  // workgroups
+            P->cls.maxb[c] = 0;
             wst_first[c] = (int64_t)wst.size();
-            if (nw == 0) {
+            if (nb == 0) {
                 wst.push_back((uint32_t)(cls.size() / 8));
                 continue;
             }
@@ -205,10 +210,10 @@ extern "C" int rsmi_ragged_plan_create(const rsmi_group *g, int64_t ngroups,
             // plus per survivor a load and a W-dword multiply
             auto cost = [&](uint32_t i) { return 24.0 + g[i].k * (2.0 + W); };
             std::stable_sort(v.begin(), v.end(), [&](uint32_t a, uint32_t b) { return cost(a) > cost(b); });
-            std::vector<std::vector<uint32_t>> lists((size_t)nw);
-            std::vector<std::pair<double, int>> heap;  // (load, wave), min-heap
-            heap.reserve((size_t)nw);
-            for (int w = 0; w < nw; ++w) heap.push_back({0.0, w});
+            std::vector<std::vector<uint32_t>> lists((size_t)nb);
+            std::vector<std::pair<double, int>> heap;  // (load, block), min-heap
+            heap.reserve((size_t)nb);
+            for (int b = 0; b < nb; ++b) heap.push_back({0.0, b});
             auto gt = [](const std::pair<double, int> &a, const std::pair<double, int> &b) {
                 return a.first > b.first || (a.first == b.first && a.second > b.second);
             };
@@ -218,9 +223,10 @@ extern "C" int rsmi_ragged_plan_create(const rsmi_group *g, int64_t ngroups,
                 lists[(size_t)heap.back().second].push_back(i);
                 std::push_heap(heap.begin(), heap.end(), gt);
             }
-            for (int w = 0; w < nw; ++w) {
+            for (int b = 0; b < nb; ++b) {
                 wst.push_back((uint32_t)(cls.size() / 8));
-                for (uint32_t i : lists[(size_t)w]) {  // the group's 8-dword record (decode.hip)
+                P->cls.maxb[c] = std::max<int>(P->cls.maxb[c], (int)lists[(size_t)b].size());
+                for (uint32_t i : lists[(size_t)b]) {  // the group's 8-dword record (decode.hip)
                     const rsmi_group &d = g[i];
                     const uint64_t rows = (uint64_t)(uintptr_t)rsmi::device_code_rows(d.k, d.n);
                     const uint32_t r8[8] = {(uint32_t)d.offset, (uint32_t)(d.offset >> 32), d.shard_stride,

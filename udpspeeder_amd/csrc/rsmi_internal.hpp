@@ -10,6 +10,7 @@
 
 #include "../../include/rsmi.h"
 #include "../../include/rsmi_fec.h"
+#include "../../include/rsmi_cook.h"
 
 namespace rsmi {
 
@@ -80,14 +81,20 @@ __host__ __device__ inline int rag_width(int lpad) {
 }
 __host__ __device__ inline int rag_width_class(int w) { return w == 1 ? 0 : (w == 2 ? 1 : (w == 4 ? 2 : 3)); }
 // Plans: the groups sorted into the four width classes, one register-cut
-// kernel per class.  Within class c the groups are dealt to nw[c] waves
-// (about one resident round: decode_cls_occupancy) by longest-processing-time
-// first on an estimated cost, so the waves of the one round finish together;
-// wave w of class c takes records rec[wst[c][w] .. wst[c][w+1]).
+// kernel per class.  Within class c the groups are dealt to nw[c] workgroups
+// of kClsWaves waves (about one resident round: decode_cls_occupancy) by
+// longest-processing-time first on an estimated cost; workgroup b holds
+// records rec[wst[c][b] .. wst[c][b+1]) (at most maxb[c]) and its waves take
+// them one at a time.
+#ifndef DEC_CLS_WAVES
+#define DEC_CLS_WAVES 4
+#endif
+constexpr int kClsWaves = DEC_CLS_WAVES;  // waves per class workgroup (they share its groups)
 struct ClsLaunch {
-    const uint32_t *rec;     // device: 8-dword group records (decode.hip), wave-major per class
+    const uint32_t *rec;     // device: 8-dword group records (decode.hip), workgroup-major per class
     const uint32_t *wst[4];  // device: per class, nw[c] + 1 offsets into rec (in records)
-    int nw[4];
+    int nw[4];               // workgroups of class c
+    int maxb[4];             // most records one workgroup of class c holds
     uint32_t *defer;         // device word: set to epoch when a group is left for the big kernel
     uint32_t epoch;          // this call's mark (plans count calls)
 };
@@ -187,7 +194,11 @@ constexpr int kCookKsBytes = 65536 + 128;  // key stream covers every byte posit
 
 struct CookArgs {
     uint8_t *base;
+    uint8_t *dst;                // out of place: packet i's output at dst + its offset (NULL: in place);
+                                 // may be pinned host memory (the transfer is fused into the kernel)
     const uint64_t *offset;
+    const rsmi_fenc_packet *pk;  // or an FEC packet list: packet i at pk[i].slot * stride + pk_off,
+    int32_t pk_off;              // pk[i].len bytes (len unused)
     int64_t stride, count;
     int32_t cap, flags;
     const int32_t *len;
@@ -198,6 +209,12 @@ struct CookArgs {
     const uint8_t *ks;           // device key stream, NULL when there is no XOR stage
 };
 size_t cook_lds_bytes(bool decook);
+// do_cook over an FEC packet list (rsmi_fenc_run_cooked_dev): packet p at
+// slots + pk[p].slot * S + RSMI_FEC_SLOT_PACKET, pk[p].len bytes (device
+// list); output at the same offset of dst (NULL: in place), IVs drawn on the
+// device from seed (cook_host.cpp).
+int cook_packets(const rsmi_cook_ctx *ctx, uint8_t *slots, int64_t S, const rsmi_fenc_packet *pk,
+                 int64_t npk, int32_t *out_len, uint8_t *dst, uint64_t seed, hipStream_t s);
 hipError_t launch_cook(const CookArgs &a, bool decook, int max_blocks, hipStream_t s);
 
 

@@ -115,6 +115,7 @@ class FecEncoder:
                                          g["seq"].ctypes.data), "rsmi_fenc_groups")
         # the input must outlive the run, which may overlap the next plan
         self._keep = (in_buf, (self._keep or (None,))[0])
+        self._last_packets = packets
         return FencPlan(ns.value, smin.value, ret, packets, g)
 
     def plan_host(self, lens, offsets) -> FencPlan:
@@ -129,6 +130,29 @@ class FecEncoder:
         s = stream if stream is not None else torch.cuda.current_stream()
         check(lib().rsmi_fenc_run_dev(self._h, slots.data_ptr() if slots.numel() else None,
                                       int(slot_stride), s.cuda_stream), "rsmi_fenc_run_dev")
+
+    def run_cooked(self, slots, slot_stride: int, cook, seed: int, out=None, out_len=None,
+                   stream=None):
+        """Frame + encode + carry the planned batch into `slots`, then do_cook
+        every packet it emits into `out` at the same slot layout (None: in place
+        in slots) -- rsmi_fenc_run_cooked_dev.  out may be pinned host memory:
+        the cooked packets then reach the host in the cook kernel's own stores.
+        cook: a cook.CookContext.  Returns the int32 CUDA tensor of cooked
+        lengths, one per planned packet (-1: did not fit)."""
+        import torch
+        s = stream if stream is not None else torch.cuda.current_stream()
+        npk = len(self._last_packets) if getattr(self, "_last_packets", None) is not None else None
+        if out_len is None:
+            out_len = torch.empty(max(npk or 0, 1), dtype=torch.int32, device="cuda")
+        if out is not None:
+            if out.dtype != torch.uint8 or not (out.is_cuda or out.is_pinned()) or out.data_ptr() % 16:
+                raise TypeError("out must be a 16-aligned CUDA or pinned uint8 tensor")
+        check(lib().rsmi_fenc_run_cooked_dev(self._h, slots.data_ptr() if slots.numel() else None,
+                                             int(slot_stride), cook._h, C.c_uint64(seed & (2**64 - 1)),
+                                             out.data_ptr() if out is not None else None,
+                                             out_len.data_ptr(), s.cuda_stream),
+              "rsmi_fenc_run_cooked_dev")
+        return out_len
 
     @staticmethod
     def slot_stride_for(fec_len_max: int) -> int:
