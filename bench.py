@@ -336,6 +336,7 @@ def extra_configs(u, synth, torch, dev, buf, G):
     out["c4_one_gpu"] = c4_one_gpu(u, synth, torch, dev)
     out["rtc_f10_5_encode"] = rtc_config(u, synth, torch, dev)
     out["f2_cook_decook"] = cook_config(torch, dev, buf, G)
+    out["f1_f2_frame_encode_cook"] = frame_cook_config(torch, dev)
     out["dropin_latency_us"] = dropin_latency_both(u)
     return out
 
@@ -469,6 +470,51 @@ def cook_config(torch, dev, buf, G):
             "cook_frac": round(alg / (tc * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             "decook_frac": round(alg / (td * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             "roundtrip_ok": ok}
+
+
+def frame_cook_config(torch, dev, groups=65536, reps=4):
+    """f1 + f2 fused: one connection's 1200-B datagrams (mode 0, -f 20:10, mtu
+    1250: 65,536 RS(20,10) groups) through rsmi_fenc_run_cooked_dev -- framing,
+    bit-sliced encode and do_cook of every emitted packet in one run into a
+    device buffer.  Planning is host work outside the timed region (bench_frame.py
+    times it); each rep plans the next batch of the same stream."""
+    import numpy as np
+    from udpspeeder_amd.cook import CookContext
+    from udpspeeder_amd.fec import FecEncoder
+    plen = 1200
+    npk = groups * 20
+    lens = np.full(npk, plen, np.int32)
+    offs = np.arange(npk, dtype=np.uint64) * np.uint64(1216)
+    inbuf = torch.randint(0, 256, (npk * 1216 + 64,), dtype=torch.uint8, device=dev)
+    enc = FecEncoder("20:10", 0, 1250, 200, seq0=1)
+    ctx = CookContext(b"bench-key")
+    slots = out = None
+    ts, nout, ok = [], 0, True
+    for i in range(reps + 1):
+        p = enc.plan(lens, offs, inbuf)
+        S = FecEncoder.slot_stride_for(int(p.groups["fec_len"].max()))
+        if slots is None:
+            slots = torch.empty(p.n_slots * S, dtype=torch.uint8, device=dev)
+            out = torch.empty_like(slots)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        ol = enc.run_cooked(slots, S, ctx, 11 + i, out=out)
+        e1.record()
+        torch.cuda.synchronize()
+        nout = len(p.packets)
+        ok = ok and bool((ol[:nout] > torch.from_numpy(p.packets["len"]).to(dev)).all())
+        if i:
+            ts.append(e0.elapsed_time(e1))
+    t = statistics.median(ts)
+    enc.close()
+    ctx.close()
+    del slots, out, inbuf
+    return {"datagrams_in": npk, "datagram_len": plen, "groups": groups, "packets_out": nout,
+            "run_ms": round(t, 4), "datagrams_in_per_s": round(npk / (t * 1e-3), 1),
+            "cooked_packets_per_s": round(nout / (t * 1e-3), 1),
+            "what": "rsmi_fenc_run_cooked_dev: plan upload + k_frame + k_bs_20_30 + carry + k_cook, "
+                    "device-resident, key on, device-drawn IVs", "lengths_ok": ok}
 
 
 def dropin_latency(u, calls=300):
