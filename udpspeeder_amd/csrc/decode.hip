@@ -69,8 +69,11 @@ constexpr int kTile = 1280;    // bytes per lane-tile pass (64 x 16 + 64 x 4)
 #ifndef DEC_NOMEM
 #define DEC_NOMEM 0            // measurement only: survivor loads all hit one cached slot
 #endif
-#ifndef DEC_RAG_RING45
-#define DEC_RAG_RING45 DEC_RING  // ragged kernels: survivors in flight for 16- and 20-byte lane pieces
+#ifndef DEC_RAG_RING4
+#define DEC_RAG_RING4 2  // ragged kernels: survivors in flight for 16-byte lane pieces
+#endif
+#ifndef DEC_RAG_RING5
+#define DEC_RAG_RING5 3  // ... and for 20-byte pieces (W = 4: ring 2 at 8 waves/SIMD, W = 5: 3 at 6, beat 4 at 6 / 5: profiles/r03/c3)
 #endif
 #ifndef DEC_RAG_DEEP
 #define DEC_RAG_DEEP 1  // ragged kernel: 16 / W survivors in flight for 4- and 8-byte lane pieces
@@ -330,7 +333,7 @@ template <int W>
 struct Rebuild {
     // narrow tiles keep more survivors in flight in the same registers (16
     // dwords of ring): short groups are latency-bound, not VGPR-bound
-    static constexpr int R = DEC_RAG_DEEP && W <= 2 ? 16 / W : DEC_RAG_RING45;
+    static constexpr int R = DEC_RAG_DEEP && W <= 2 ? 16 / W : (W == 4 ? DEC_RAG_RING4 : DEC_RAG_RING5);
     __amdgpu_buffer_rsrc_t rsrc;
     uint32_t so_lane, mo_lane;
     int k, e, len, lpad;
@@ -764,10 +767,10 @@ __global__ __launch_bounds__(256, DEC_OCC) void k_decode_fused(UniformArgs a, co
 #define DEC_CLS_OCC2 8
 #endif
 #ifndef DEC_CLS_OCC4
-#define DEC_CLS_OCC4 6
+#define DEC_CLS_OCC4 8
 #endif
 #ifndef DEC_CLS_OCC5
-#define DEC_CLS_OCC5 5
+#define DEC_CLS_OCC5 6
 #endif
 constexpr int kClsRows = 5;  // class kernels: e <= 5 in registers, more is deferred
 
