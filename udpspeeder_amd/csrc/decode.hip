@@ -39,7 +39,8 @@ namespace {
 
 constexpr int kWaves = 4;      // waves per block (one group each)
 #ifndef DEC_RING
-#define DEC_RING 4
+#define DEC_RING 2             // fused kernel: survivors in flight (2 at 5 waves/SIMD: decode -1 %,
+                               // C2 worst -1.5 % against 4 at 4 waves/SIMD, profiles/r03/dec_occ5_ab.txt)
 #endif
 #ifndef DEC_LD_AUX
 #define DEC_LD_AUX 2           // cache policy of the survivor loads: nt (bench step: decode
@@ -61,7 +62,7 @@ constexpr int kTile = 1280;    // bytes per lane-tile pass (64 x 16 + 64 x 4)
                                // DevIO::store: no hazard wait state is inserted for that form)
 #endif
 #ifndef DEC_OCC
-#define DEC_OCC 4              // waves per SIMD the register budget is cut for
+#define DEC_OCC 5              // waves per SIMD the fused kernel's register budget is cut for
 #endif
 #ifndef DEC_FAKE
 #define DEC_FAKE 0             // measurement only: rows computed per survivor (0 = e, the real decode)
@@ -757,7 +758,7 @@ __global__ __launch_bounds__(256, DEC_OCC) void k_decode_fused(UniformArgs a, co
 #define DEC_RAG_W 1  // ragged kernel: tile width per group (0: always 1280-byte tiles)
 #endif
 #ifndef DEC_RAG_OCC
-#define DEC_RAG_OCC DEC_OCC  // waves per SIMD the ragged kernel's registers are cut for
+#define DEC_RAG_OCC 4  // waves per SIMD the ragged (single-kernel) form's registers are cut for
 #endif
 // class kernels (plans): waves per SIMD per tile width
 #ifndef DEC_CLS_OCC1
