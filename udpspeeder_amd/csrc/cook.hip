@@ -36,6 +36,21 @@
 namespace rsmi {
 namespace {
 
+#ifndef COOK_TRACE
+#define COOK_TRACE 0  // measurement only: per wave-step phase timestamps of k_cook
+#endif
+#if COOK_TRACE
+__device__ uint64_t *g_cook_trace;  // [wave step][8]: t0..t4 (rsmi_debug_cook_trace)
+__device__ __forceinline__ uint64_t ctrace_now() {
+    asm volatile("" ::: "memory");
+    const uint64_t t = __builtin_amdgcn_s_memtime();
+    asm volatile("" ::: "memory");
+    return t;
+}
+#define CT(i) const uint64_t ct##i = ctrace_now()
+#else
+#define CT(i)
+#endif
 constexpr int kLpp = kCookLpp;          // lanes per packet
 constexpr int kPpw = 64 / kLpp;         // packets per wave
 constexpr int kPpl = 96 / kLpp;         // pieces per lane per round
@@ -44,6 +59,9 @@ constexpr int kPpl = 96 / kLpp;         // pieces per lane per round
 #endif
 #ifndef COOK_ABS_LDS
 #define COOK_ABS_LDS 1  // CRC tables addressed from LDS address 0 (see tab_byte)
+#endif
+#ifndef COOK_SKIP
+#define COOK_SKIP 1  // skip the CRC of piece slots past every packet's last crc piece of the wave
 #endif
 #ifndef COOK_SB
 #define COOK_SB 1  // scheduling fence every COOK_SB pieces (0: none), bounds registers
@@ -310,6 +328,7 @@ __global__ __launch_bounds__(kThreads, COOK_OCC) void k_cook(CookArgs a) {
 
     for (int64_t pw = (int64_t)blockIdx.x * (kThreads / 64) + wid; pw < nunits;
          pw += (int64_t)gridDim.x * (kThreads / 64)) {
+        CT(0);
         const int64_t pk = kPpw * pw + sub;
         const bool have = pk < a.count;
         int L = -1, ivl = 0;
@@ -342,6 +361,7 @@ __global__ __launch_bounds__(kThreads, COOK_OCC) void k_cook(CookArgs a) {
             }
         }
         wave_sync();
+        CT(1);
         const uint32_t sstep = ivl ? mod_ivl(16u * kLpp, (uint32_t)ivl, magic) : 0u;
         const int Q = (L + 15) >> 4;            // pieces holding payload (crc input)
         const int P0 = L & ~15;                 // first piece that holds tail bytes
@@ -352,12 +372,15 @@ __global__ __launch_bounds__(kThreads, COOK_OCC) void k_cook(CookArgs a) {
         for (int r = 0; r < nrm; ++r) {
             if (r) load_round(cur, pkt, r, hl, ext);   // rounds past the first (long packets)
             const int qr = min(max(Q - 96 * r, 0), 96);
+            // pieces at or past every packet's last crc piece in this round:
+            // skip their CRC (a wave-uniform branch per piece slot)
+            const int qr_max = COOK_SKIP ? wave_max(qr) : 96;
             RoundCrc rc;
             uint32_t ivr = ivl ? mod_ivl((uint32_t)(r * kRound + 16 * hl), (uint32_t)ivl, magic) : 0u;
 #pragma unroll
             for (int p = 0; p < kPpl; ++p) {
                 const int P = r * kRound + 16 * (kLpp * p + hl);
-                if (ck) rc.add(T, crc_in(cur[p], P, L), kLpp * p + hl, qr);
+                if (ck && kLpp * p < qr_max) rc.add(T, crc_in(cur[p], P, L), kLpp * p + hl, qr);
                 if (P < ext && P + 16 <= L) {  // wholly payload: obscure + xor, store now
                     u32x4 m = ks_piece(a, P);
                     if (ivl) m ^= iv_window_at(iv2w, ivr);
@@ -376,6 +399,7 @@ __global__ __launch_bounds__(kThreads, COOK_OCC) void k_cook(CookArgs a) {
                 acc = qr > 0 ? nacc : acc;
             }
         }
+        CT(2);
         uint32_t crc = 0;
         if (ck && L > 0) crc = ~unshift(T, acc, (uint32_t)(16 * Q - L));
         // ---- tail: crc (BE), iv, iv_len appended after the payload -------------
@@ -392,21 +416,32 @@ __global__ __launch_bounds__(kThreads, COOK_OCC) void k_cook(CookArgs a) {
                         const int w = u - (ck ? 4 : 0);
                         v = w < ivl ? scr[w] : (uint32_t)ivl;
                     }
-                    if (a.ks) v ^= a.ks[pos];
                 }
-                ovl[t] = (uint8_t)v;
+                ovl[t] = (uint8_t)v;  // the key stream goes on with the tail piece below
             }
         }
         wave_sync();
+        CT(3);
         if (Pt >= 0) {
-            u32x4 m = ks_piece(a, Pt);
+            // the overlay holds the tail bytes before encrypt_0: the piece's key
+            // stream covers payload and tail alike (one 16-B load, where a byte
+            // load per tail byte stood in the overlay loop's dependent chain)
+            const u32x4 k = ks_piece(a, Pt);
+            u32x4 m = k;
             if (ivl) m ^= iv_window(iv2w, (uint32_t)Pt, (uint32_t)ivl, magic);
             const u32x4 o = *reinterpret_cast<const u32x4 *>(ovl + (Pt - P0));
             const u32x4 lo = piece_mask(L - Pt), hi = piece_mask(out - Pt);
-            st_piece(opkt + Pt, ((dt ^ m) & lo) | (o & hi & ~lo) | (dt & ~hi));
+            st_piece(opkt + Pt, ((dt ^ m) & lo) | ((o ^ k) & hi & ~lo) | (dt & ~hi));
         }
         if (have && hl == 0) a.out_len[pk] = ok ? out : -1;
         wave_sync();  // the scratch slice is rewritten by the next packet
+#if COOK_TRACE
+        CT(4);
+        if (lane == 0 && g_cook_trace) {
+            uint64_t *t = g_cook_trace + pw * 8;
+            t[0] = ct0; t[1] = ct1; t[2] = ct2; t[3] = ct3; t[4] = ct4; t[5] = (uint64_t)nrm;
+        }
+#endif
     }
 }
 
@@ -455,7 +490,25 @@ __global__ __launch_bounds__(kThreads, COOK_OCC) void k_decook(CookArgs a) {
         const uint32_t magic = ivl ? 0xFFFFFFFFu / (uint32_t)ivl : 0u;
         const uint32_t sstep = ivl ? mod_ivl(16u * kLpp, (uint32_t)ivl, magic) : 0u;
         if (ok && ivl) {
-            for (int t = hl; t < ivl + 20; t += kLpp) {
+            // the IV repeated (iv2[t] = iv[t % ivl], t < ivl + 20): the first
+            // kIvPre steps' byte loads are issued together before any store
+            // (iv_len <= 32 + ... as the reference sends it needs no more),
+            // then the rest (iv_len up to 255 is accepted on the wire)
+            constexpr int kIvPre = (52 + kLpp - 1) / kLpp;
+            uint32_t bv[kIvPre];
+#pragma unroll
+            for (int i = 0; i < kIvPre; ++i) {
+                const int t = hl + kLpp * i;
+                bv[i] = 0;
+                if (t < ivl + 20) {
+                    const int pos = L1 + (int)mod_ivl((uint32_t)t, (uint32_t)ivl, magic);
+                    bv[i] = pkt[pos] ^ (a.ks ? a.ks[pos] : 0);
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < kIvPre; ++i)
+                if (hl + kLpp * i < ivl + 20) scr[hl + kLpp * i] = (uint8_t)bv[i];
+            for (int t = hl + kLpp * kIvPre; t < ivl + 20; t += kLpp) {
                 const int pos = L1 + (int)mod_ivl((uint32_t)t, (uint32_t)ivl, magic);
                 scr[t] = pkt[pos] ^ (a.ks ? a.ks[pos] : 0);
             }
@@ -479,6 +532,7 @@ __global__ __launch_bounds__(kThreads, COOK_OCC) void k_decook(CookArgs a) {
         for (int r = 0; r < nrm; ++r) {
             if (r) load_round(cur, pkt, r, hl, ext);   // rounds past the first (long packets)
             const int qr = crc_on ? min(max(Q - 96 * r, 0), 96) : 0;
+            const int qr_max = COOK_SKIP ? wave_max(qr) : 96;
             RoundCrc rc;
             uint32_t ivr = ivl ? mod_ivl((uint32_t)(r * kRound + 16 * hl), (uint32_t)ivl, magic) : 0u;
 #pragma unroll
@@ -492,7 +546,7 @@ __global__ __launch_bounds__(kThreads, COOK_OCC) void k_decook(CookArgs a) {
                     else o = cur[p] ^ (mk & piece_mask(L - P)) ^ (mi & piece_mask(L1 - P));
                     st_piece(opkt + P, o);
                 }
-                if (ck) rc.add(T, crc_in(o, P, Lc), kLpp * p + hl, qr);
+                if (ck && kLpp * p < qr_max) rc.add(T, crc_in(o, P, Lc), kLpp * p + hl, qr);
                 if (ivl) ivr = iv_step(ivr, sstep, (uint32_t)ivl);
                 if (COOK_SB && p % COOK_SB == COOK_SB - 1) __builtin_amdgcn_sched_barrier(0);
             }
@@ -531,3 +585,9 @@ hipError_t launch_cook(const CookArgs &a, bool decook, int max_blocks, hipStream
 }
 
 }  // namespace rsmi
+
+#if COOK_TRACE
+extern "C" int rsmi_debug_cook_trace(void *dev_ptr) {  // measurement builds only
+    return hipMemcpyToSymbol(HIP_SYMBOL(rsmi::g_cook_trace), &dev_ptr, sizeof(dev_ptr)) == hipSuccess ? 0 : -1;
+}
+#endif
