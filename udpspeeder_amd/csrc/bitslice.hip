@@ -74,11 +74,32 @@ int bitslice_code_index(int k, int n) {
 
 int bitslice_builtin_count() { return BS_NUM_CODES; }
 
+int bitslice_code_k(int i) {
+    int idx = 0;
+#define BS_K(K, N)                   \
+    if (i == idx) return K;          \
+    ++idx;
+    BS_FOR_EACH_CODE(BS_K)
+#undef BS_K
+    return 0;
+}
+
+int bitslice_code_n(int i) {
+    int idx = 0;
+#define BS_N(K, N)                   \
+    if (i == idx) return N;          \
+    ++idx;
+    BS_FOR_EACH_CODE(BS_N)
+#undef BS_N
+    return 0;
+}
+
 hipError_t launch_encode_bitslice_ragged(const rsmi_group *groups, const uint32_t *colmap,
                                          const uint32_t *waves, uint32_t nwaves, uint8_t *base,
                                          uint32_t bytes, hipStream_t s) {
     if (nwaves == 0) return hipSuccess;
-    const uint32_t blocks = (nwaves + 3) / 4;
+    uint32_t blocks = (nwaves + 3) / 4;
+    if (BS_RAG_XCD) blocks = (blocks + 7) & ~7u;  // whole rounds of 8 XCDs (the remap)
     k_bs_ragged<<<blocks, 256, 0, s>>>(reinterpret_cast<const BsGroup *>(groups), colmap, waves,
                                        nwaves, base, bytes);
     return hipGetLastError();
@@ -93,7 +114,9 @@ hipError_t launch_encode_bitslice_ragged_rtc(int k, int n, const rsmi_group *gro
     if (!f) return hipErrorNotSupported;
     const BsGroup *g = reinterpret_cast<const BsGroup *>(groups);
     void *args[] = {&g, &colmap, &waves, &nwaves, &base, &bytes};
-    return hipModuleLaunchKernel(f, (nwaves + 3) / 4, 1, 1, 256, 1, 1, 0, s, args, nullptr);
+    uint32_t blocks = (nwaves + 3) / 4;
+    if (BS_RAG_XCD) blocks = (blocks + 7) & ~7u;
+    return hipModuleLaunchKernel(f, blocks, 1, 1, 256, 1, 1, 0, s, args, nullptr);
 }
 
 bool has_bitslice(int k, int n) {

@@ -39,6 +39,13 @@
 #define BS_XCD 1  // blocks b, b+8, ... (dispatched to one XCD) take one contiguous range of
                   // chunks (measured 1.5 % faster than the plain order, scripts/gpu_bench_ab.sh)
 #endif
+#ifndef BS_RAG_XCD
+#define BS_RAG_XCD 0  // 1: the same remap for the ragged kernels, so the blocks one CU holds come
+                      // from one narrow window of the code-sorted wave list (one code's network
+                      // of the ~550 KB in k_bs_ragged).  Measured 10 % slower on C3: each XCD
+                      // then owns one slice of the codes and the slice of the largest ones
+                      // finishes last (scripts/gpu_c3enc_ab.sh)
+#endif
 #define BS_ACC3(acc, a, b) ((acc) = __builtin_amdgcn_bitop3_b32((acc), (a), (b), 0x96))
 #define BS_ACC2(acc, a) ((acc) ^= (a))
 // keep the generated shard blocks in order so the raw-load ring bounds the
@@ -171,7 +178,9 @@ __device__ __forceinline__ bool bs_rag_setup(const BsGroup *groups, const uint32
                                              const uint32_t *waves, uint32_t nwaves,
                                              uint8_t *base, uint32_t bytes, RagIO &io,
                                              uint32_t &code) {
-    const uint32_t w = blockIdx.x * 4u + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t bid = BS_RAG_XCD ? (blockIdx.x & 7u) * (gridDim.x >> 3) + (blockIdx.x >> 3)
+                                    : blockIdx.x;
+    const uint32_t w = bid * 4u + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (w >= nwaves) return false;
     code = __builtin_amdgcn_readfirstlane(waves[2 * w]);
     const uint32_t c0 = __builtin_amdgcn_readfirstlane(waves[2 * w + 1]) + (threadIdx.x & 63u);

@@ -350,10 +350,16 @@ void write_file_atomic(const std::string &p, const std::vector<char> &data) {
 
 const char *const kRtcOpts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17"};
 
+#ifndef BS_RAG_XCD
+#define BS_RAG_XCD 0  // bitslice_kern.hpp's default: the runtime-compiled ragged kernels must
+                      // remap blocks exactly as the launcher (bitslice.hip) sizes the grid
+#endif
+
 std::string unit_source(const Unit &U) {
     std::string s =
         "typedef unsigned char uint8_t; typedef unsigned short uint16_t;\n"
-        "typedef unsigned int uint32_t; typedef unsigned long uint64_t; typedef long int64_t;\n";
+        "typedef unsigned int uint32_t; typedef unsigned long uint64_t; typedef long int64_t;\n"
+        "#define BS_RAG_XCD " + S(BS_RAG_XCD) + "\n";
     s += kBsCoreText;
     s += kBsKernText;
     for (auto &c : U.codes) {

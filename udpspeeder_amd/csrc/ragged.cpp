@@ -24,6 +24,10 @@
 #ifndef RSMI_DEC_CLASSES
 #define RSMI_DEC_CLASSES 1  // plan decodes: one register-cut kernel per tile-width class
 #endif
+#ifndef RAG_LPT
+#define RAG_LPT 1  // bit-sliced ragged waves: costliest code first (0: code-list order)
+#endif
+static constexpr bool kRagLptOrder = RAG_LPT != 0;
 
 namespace rsmi {
 int prepare_code(int k, int n);
@@ -157,7 +161,18 @@ extern "C" int rsmi_ragged_plan_create(const rsmi_group *g, int64_t ngroups,
             fill[(size_t)b] += pcs;
         }
         const int nbuiltin = rsmi::bitslice_builtin_count();
-        for (int b = 0; b < nb; ++b) {
+        // wave order of the built-in buckets: costliest code first (most rows,
+        // then most data shards) so the grid's last dispatched waves are the
+        // cheap ones and no big-code wave starts at the tail
+        std::vector<int> order((size_t)nb);
+        for (int b = 0; b < nb; ++b) order[(size_t)b] = b;
+        if (kRagLptOrder)
+            std::stable_sort(order.begin(), order.begin() + std::min(nb, nbuiltin), [](int a, int b) {
+                const int ka = rsmi::bitslice_code_k(a), kb = rsmi::bitslice_code_k(b);
+                const int na = rsmi::bitslice_code_n(a), nb2 = rsmi::bitslice_code_n(b);
+                return na != nb2 ? na > nb2 : ka > kb;
+            });
+        for (int b : order) {
             if (b == nbuiltin) P->nwaves_builtin = (uint32_t)(waves.size() / 2);
             const uint32_t first = (uint32_t)(waves.size() / 2);
             for (uint64_t w = 0; w < (cols[(size_t)b] + 127) / 128; ++w) {

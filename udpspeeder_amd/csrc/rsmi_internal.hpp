@@ -122,6 +122,8 @@ hipError_t launch_decode_ragged_big(const rsmi_group *groups, int64_t ngroups, u
 hipError_t launch_encode_bitslice(const UniformArgs &a, hipStream_t s);
 bool has_bitslice(int k, int n);
 int bitslice_code_index(int k, int n);  // position in the generated code list, -1 if none
+int bitslice_code_k(int idx);  // (k, n) of generated code idx
+int bitslice_code_n(int idx);
 // Ragged bucketed launch over a host-built plan (ragged.cpp): colmap entries
 // (group << 12) | piece, waves = {code index, first column} pairs.
 hipError_t launch_encode_bitslice_ragged(const rsmi_group *groups, const uint32_t *colmap,
