@@ -7,7 +7,7 @@ libs="default"
 for l in udpspeeder_amd/ab/*.so; do libs="$libs $l"; done
 for lib in $libs; do
   [ $lib = default ] && unset RSMI_LIB || export RSMI_LIB=$PWD/$lib
-  timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q -k "ragged or plan or rtc" \
+  timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_bitslice_rtc.py -m gpu -x -q -k "ragged or plan or rtc" \
       --timeout 120 --timeout-method thread > gpurun_out/c3enc/tests_$(basename $lib).log 2>&1; rc=$?
   echo "$lib: $(tail -1 gpurun_out/c3enc/tests_$(basename $lib).log)"
   [ $rc -eq 0 ] || exit $rc
