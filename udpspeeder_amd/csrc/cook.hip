@@ -84,11 +84,22 @@ __device__ __forceinline__ void wave_sync() {
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef u32x4 u32x4_a4 __attribute__((aligned(4)));  // packet pieces: 4-byte aligned
 
+#ifndef COOK_NT
+#define COOK_NT 0  // 1: packet loads and stores non-temporal (read and written once)
+#endif
 __device__ __forceinline__ u32x4 ld_piece(const uint8_t *p) {
+#if COOK_NT
+    return __builtin_nontemporal_load(reinterpret_cast<const u32x4_a4 *>(p));
+#else
     return *reinterpret_cast<const u32x4_a4 *>(p);
+#endif
 }
 __device__ __forceinline__ void st_piece(uint8_t *p, u32x4 v) {
+#if COOK_NT
+    __builtin_nontemporal_store(v, reinterpret_cast<u32x4_a4 *>(p));
+#else
     *reinterpret_cast<u32x4_a4 *>(p) = v;
+#endif
 }
 
 // Table word at word index w + byte b of x (b = 0..3): the tables sit at LDS
@@ -108,6 +119,7 @@ __device__ __forceinline__ uint32_t tab_byte(const uint32_t *T, int w, uint32_t 
 }
 #endif
 
+#if !COOK_S16
 // CRC register after 8 bytes (dwords a, b little-endian) from register c.
 __device__ __forceinline__ uint32_t slice8(const uint32_t *T, uint32_t c, uint32_t a, uint32_t b) {
     const uint32_t x = c ^ a;
@@ -116,6 +128,7 @@ __device__ __forceinline__ uint32_t slice8(const uint32_t *T, uint32_t c, uint32
     r = xor3(r, tab_byte(T, 2 * 256, b, 1), tab_byte(T, 256, b, 2));
     return r ^ tab_byte(T, 0, b, 3);
 }
+#endif
 
 // A linear map of the CRC register held as 8 nibble tables of 16 words.
 __device__ __forceinline__ uint32_t nib_map(const uint32_t *M, uint32_t c) {
@@ -213,10 +226,30 @@ __device__ __forceinline__ uint32_t zh(const uint32_t *T, uint32_t c) {
            tab_byte(T, kCookZH + 768, c, 3);
 }
 
+#if COOK_S16
+// Table word of T_k (byte followed by k zero bytes), k = 0..15.
+__device__ __forceinline__ constexpr int tword(int k) { return k < 8 ? 256 * k : kCookS16 + 256 * (k - 8); }
+
+// Raw CRC of one 16-byte piece: byte j through T_{15-j}, all 16 lookups independent.
+__device__ __forceinline__ uint32_t crc16(const uint32_t *T, u32x4 v) {
+    const uint32_t a = xor3(tab_byte(T, tword(15), v.x, 0), tab_byte(T, tword(14), v.x, 1),
+                            tab_byte(T, tword(13), v.x, 2));
+    const uint32_t b = xor3(tab_byte(T, tword(12), v.x, 3), tab_byte(T, tword(11), v.y, 0),
+                            tab_byte(T, tword(10), v.y, 1));
+    const uint32_t c = xor3(tab_byte(T, tword(9), v.y, 2), tab_byte(T, tword(8), v.y, 3),
+                            tab_byte(T, tword(7), v.z, 0));
+    const uint32_t d = xor3(tab_byte(T, tword(6), v.z, 1), tab_byte(T, tword(5), v.z, 2),
+                            tab_byte(T, tword(4), v.z, 3));
+    const uint32_t e = xor3(tab_byte(T, tword(3), v.w, 0), tab_byte(T, tword(2), v.w, 1),
+                            tab_byte(T, tword(1), v.w, 2));
+    return xor3(a, b, c) ^ xor3(d, e, tab_byte(T, tword(0), v.w, 3));
+}
+#else
 // Raw CRC of one 16-byte piece.
 __device__ __forceinline__ uint32_t crc16(const uint32_t *T, u32x4 v) {
     return slice8(T, slice8(T, 0u, v.x, v.y), v.z, v.w);
 }
+#endif
 #endif
 
 // Remove z < 16 trailing zero bytes: Z_{-z} = Z_{-(z&3)} o Z_{-4(z>>2)}.

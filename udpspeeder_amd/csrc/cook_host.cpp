@@ -94,6 +94,11 @@ struct CrcTables {
             }
         for (int c = 1; c < 4; ++c) put_map(&blob[rsmi::kCookUns + 128 * (c - 1)], -c);
         for (int c = 1; c < 4; ++c) put_map(&blob[rsmi::kCookUns + 128 * (2 + c)], -4 * c);
+        if (COOK_S16)  // T_8..T_15, each one zero byte past the one before (T_7 first)
+            for (int k = 8; k < 16; ++k) {
+                const uint32_t *src = k == 8 ? &blob[256 * 7] : &blob[rsmi::kCookS16 + 256 * (k - 9)];
+                for (int v = 0; v < 256; ++v) blob[rsmi::kCookS16 + 256 * (k - 8) + v] = feed0(src[v]);
+            }
         if (!COOK_NIB) return;
         // nibble i of a piece is the low (i even) or high nibble of byte i / 2
         for (int i = 0; i < 32; ++i)

@@ -46,6 +46,9 @@ constexpr int kWaves = 4;      // waves per block (one group each)
 #define DEC_LD_AUX 2           // cache policy of the survivor loads: nt (bench step: decode
                                // 0.466 vs 0.475 ms with default-policy loads, encode unchanged)
 #endif
+#ifndef DEC_RAG_LD_AUX
+#define DEC_RAG_LD_AUX DEC_LD_AUX  // ... of the ragged kernels' survivor loads (TileIO)
+#endif
 #ifndef DEC_ST_AUX
 #define DEC_ST_AUX 0           // cache policy of the rebuilt-row stores
 #endif
@@ -297,15 +300,15 @@ struct TileIO {
     }
     __device__ __forceinline__ void load(__amdgpu_buffer_rsrc_t r, uint32_t so, uint32_t (&x)[W]) const {
         if constexpr (W == 1) {
-            x[0] = __builtin_amdgcn_raw_buffer_load_b32(r, v16, so, DEC_LD_AUX);
+            x[0] = __builtin_amdgcn_raw_buffer_load_b32(r, v16, so, DEC_RAG_LD_AUX);
         } else if constexpr (W == 2) {
             typedef uint32_t u2 __attribute__((ext_vector_type(2)));
-            const u2 v = __builtin_amdgcn_raw_buffer_load_b64(r, v16, so, DEC_LD_AUX);
+            const u2 v = __builtin_amdgcn_raw_buffer_load_b64(r, v16, so, DEC_RAG_LD_AUX);
             x[0] = v.x; x[1] = v.y;
         } else {
-            const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, v16, so, DEC_LD_AUX);
+            const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, v16, so, DEC_RAG_LD_AUX);
             x[0] = v.x; x[1] = v.y; x[2] = v.z; x[3] = v.w;
-            if constexpr (W == 5) x[4] = __builtin_amdgcn_raw_buffer_load_b32(r, v4, so, DEC_LD_AUX);
+            if constexpr (W == 5) x[4] = __builtin_amdgcn_raw_buffer_load_b32(r, v4, so, DEC_RAG_LD_AUX);
         }
     }
     // offsets in the VGPR, soffset 0 (see bitslice_kern.hpp DevIO::store)

@@ -181,17 +181,25 @@ constexpr int kCookLpp = COOK_LPP;
 //   kCookUns + 128i  nibble maps of Z_{-c}, c = 1..3, then Z_{-4c}, c = 1..3
 //   kCookNib + 16i   raw CRC of a 16-byte piece holding nibble i alone, i = 0..31
 //   kCookZN          nibble map of Z_{16 kCookLpp}
+//   kCookS16 + 256k  (COOK_S16) T_{8+k}, k = 0..7: slicing-by-16 with T_0..T_7
 // COOK_NIB selects the nibble forms for the per-piece work: 16-entry tables sit in
 // distinct LDS banks, so a wave's lookups into one never conflict.
+// COOK_S16: a piece's raw CRC as 16 independent byte lookups (one level)
+// instead of two chained slicing-by-8 steps.
 #ifndef COOK_NIB
 #define COOK_NIB 0
+#endif
+#ifndef COOK_S16
+#define COOK_S16 1
 #endif
 constexpr int kCookLane = 2048;
 constexpr int kCookZH = kCookLane + kCookLpp * 128;
 constexpr int kCookUns = kCookZH + 1024;
 constexpr int kCookNib = kCookUns + 6 * 128;
 constexpr int kCookZN = kCookNib + 512;
-constexpr int kCookTabWords = COOK_NIB ? kCookZN + 128 : kCookNib;
+constexpr int kCookS16 = kCookNib;  // COOK_S16 and COOK_NIB exclude each other
+constexpr int kCookTabWords = COOK_NIB ? kCookZN + 128 : (COOK_S16 ? kCookS16 + 2048 : kCookNib);
+static_assert(!(COOK_NIB && COOK_S16), "COOK_NIB and COOK_S16 are alternatives");
 constexpr int kCookKsBytes = 65536 + 128;  // key stream covers every byte position used
 
 struct CookArgs {
