@@ -262,21 +262,38 @@ __device__ __forceinline__ uint32_t unshift(const uint32_t *T, uint32_t c, uint3
     return hi ? c2 : c;
 }
 
-// CRC of a round, folded one piece at a time: piece q (= kLpp p + lane) of the
-// round, crc input v; qr = data pieces of the packet in this round (0..96).
+// Z_{32 kLpp}: two piece slots of a lane (the two-chain fold's step).
+__device__ __forceinline__ uint32_t zh2(const uint32_t *T, uint32_t c) {
+    return xor3(tab_byte(T, kCookZH2, c, 0), tab_byte(T, kCookZH2 + 256, c, 1),
+                tab_byte(T, kCookZH2 + 512, c, 2)) ^
+           tab_byte(T, kCookZH2 + 768, c, 3);
+}
+
+// CRC of a round, folded one piece at a time: piece q (= kLpp p + lane, slot
+// p) of the round, crc input v; qr = data pieces of the packet in this round
+// (0..96).  TWO: even and odd slots fold as two Horner chains with step
+// Z_{32 kLpp}; the data pieces are a prefix of the slots, so the other chain's
+// last piece is one slot before the lane's last and joins it through Z_{16 kLpp}.
+template <bool TWO>
 struct RoundCrc {
-    uint32_t h = 0;
+    uint32_t h[2] = {0, 0};
     int last = -1;
-    __device__ __forceinline__ void add(const uint32_t *T, u32x4 v, int q, int qr) {
-        const uint32_t hn = zh(T, h) ^ crc16(T, v);
-        h = q < qr ? hn : h;
+    __device__ __forceinline__ void add(const uint32_t *T, u32x4 v, int p, int q, int qr) {
+        const int c = TWO ? (p & 1) : 0;
+        const uint32_t hn = (TWO ? zh2(T, h[c]) : zh(T, h[c])) ^ crc16(T, v);
+        h[c] = q < qr ? hn : h[c];
         last = q < qr ? q : last;
     }
     // The round's raw CRC relative to the end of its data, in all kLpp lanes.
     __device__ __forceinline__ uint32_t finish(const uint32_t *T, int qr) const {
+        uint32_t hh = h[0];
+        if (TWO) {  // Z(0) = 0: an empty chain adds nothing
+            const bool odd = last >= 0 && ((last / kLpp) & 1);
+            hh = zh(T, odd ? h[0] : h[1]) ^ (odd ? h[1] : h[0]);
+        }
         int k = qr - 1 - last;
         k = (last >= 0 && k >= 0 && k < kLpp) ? k : 0;
-        const uint32_t c = nib_map(T + kCookLane + 128 * k, h);
+        const uint32_t c = nib_map(T + kCookLane + 128 * k, hh);
         return group_xor(last >= 0 ? c : 0u);
     }
 };
@@ -294,8 +311,8 @@ __device__ __forceinline__ uint32_t shift_pieces(const uint32_t *T, uint32_t acc
 
 __device__ __forceinline__ int round16(int x) { return (x + 15) & ~15; }
 
-__device__ __forceinline__ void load_tables(uint32_t *lds, const uint32_t *tabs) {
-    for (int i = threadIdx.x; i < kCookTabWords / 4; i += kThreads)
+__device__ __forceinline__ void load_tables(uint32_t *lds, const uint32_t *tabs, int words) {
+    for (int i = threadIdx.x; i < words / 4; i += kThreads)
         reinterpret_cast<u32x4 *>(lds)[i] = reinterpret_cast<const u32x4 *>(tabs)[i];
     __syncthreads();
 }
@@ -351,7 +368,7 @@ __global__ __launch_bounds__(kThreads, COOK_OCC) void k_cook(CookArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const bool ck = !(a.flags & RSMI_COOK_NO_CHECKSUM);
     const bool obs = !(a.flags & RSMI_COOK_NO_OBSCURE);
-    if (ck) load_tables(lds, a.tabs);
+    if (ck) load_tables(lds, a.tabs, kCookTabWords);
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63, sub = lane / kLpp, hl = lane % kLpp;
     uint8_t *scr = reinterpret_cast<uint8_t *>(lds + kCookTabWords) + (wid * kPpw + sub) * kScrCook;
     uint32_t *iv2w = reinterpret_cast<uint32_t *>(scr);
@@ -408,12 +425,12 @@ __global__ __launch_bounds__(kThreads, COOK_OCC) void k_cook(CookArgs a) {
             // pieces at or past every packet's last crc piece in this round:
             // skip their CRC (a wave-uniform branch per piece slot)
             const int qr_max = COOK_SKIP ? wave_max(qr) : 96;
-            RoundCrc rc;
+            RoundCrc<COOK_2CH != 0> rc;
             uint32_t ivr = ivl ? mod_ivl((uint32_t)(r * kRound + 16 * hl), (uint32_t)ivl, magic) : 0u;
 #pragma unroll
             for (int p = 0; p < kPpl; ++p) {
                 const int P = r * kRound + 16 * (kLpp * p + hl);
-                if (ck && kLpp * p < qr_max) rc.add(T, crc_in(cur[p], P, L), kLpp * p + hl, qr);
+                if (ck && kLpp * p < qr_max) rc.add(T, crc_in(cur[p], P, L), p, kLpp * p + hl, qr);
                 if (P < ext && P + 16 <= L) {  // wholly payload: obscure + xor, store now
                     u32x4 m = ks_piece(a, P);
                     if (ivl) m ^= iv_window_at(iv2w, ivr);
@@ -482,9 +499,9 @@ __global__ __launch_bounds__(kThreads, COOK_OCC) void k_decook(CookArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const bool ck = !(a.flags & RSMI_COOK_NO_CHECKSUM);
     const bool obs = !(a.flags & RSMI_COOK_NO_OBSCURE);
-    if (ck) load_tables(lds, a.tabs);
+    if (ck) load_tables(lds, a.tabs, kCookTabDecook);
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63, sub = lane / kLpp, hl = lane % kLpp;
-    uint8_t *scr = reinterpret_cast<uint8_t *>(lds + kCookTabWords) + (wid * kPpw + sub) * kScrDecook;
+    uint8_t *scr = reinterpret_cast<uint8_t *>(lds + kCookTabDecook) + (wid * kPpw + sub) * kScrDecook;
     uint32_t *iv2w = reinterpret_cast<uint32_t *>(scr);
     uint8_t *misc = scr + 288;
     const uint32_t *T = lds;
@@ -566,7 +583,7 @@ __global__ __launch_bounds__(kThreads, COOK_OCC) void k_decook(CookArgs a) {
             if (r) load_round(cur, pkt, r, hl, ext);   // rounds past the first (long packets)
             const int qr = crc_on ? min(max(Q - 96 * r, 0), 96) : 0;
             const int qr_max = COOK_SKIP ? wave_max(qr) : 96;
-            RoundCrc rc;
+            RoundCrc<false> rc;
             uint32_t ivr = ivl ? mod_ivl((uint32_t)(r * kRound + 16 * hl), (uint32_t)ivl, magic) : 0u;
 #pragma unroll
             for (int p = 0; p < kPpl; ++p) {
@@ -579,7 +596,7 @@ __global__ __launch_bounds__(kThreads, COOK_OCC) void k_decook(CookArgs a) {
                     else o = cur[p] ^ (mk & piece_mask(L - P)) ^ (mi & piece_mask(L1 - P));
                     st_piece(opkt + P, o);
                 }
-                if (ck && kLpp * p < qr_max) rc.add(T, crc_in(o, P, Lc), kLpp * p + hl, qr);
+                if (ck && kLpp * p < qr_max) rc.add(T, crc_in(o, P, Lc), p, kLpp * p + hl, qr);
                 if (ivl) ivr = iv_step(ivr, sstep, (uint32_t)ivl);
                 if (COOK_SB && p % COOK_SB == COOK_SB - 1) __builtin_amdgcn_sched_barrier(0);
             }
@@ -601,7 +618,8 @@ __global__ __launch_bounds__(kThreads, COOK_OCC) void k_decook(CookArgs a) {
 }  // namespace
 
 size_t cook_lds_bytes(bool decook) {
-    return (size_t)kCookTabWords * 4 + (size_t)(kThreads / kLpp) * (decook ? kScrDecook : kScrCook);
+    return (size_t)(decook ? kCookTabDecook : kCookTabWords) * 4 +
+           (size_t)(kThreads / kLpp) * (decook ? kScrDecook : kScrCook);
 }
 
 hipError_t launch_cook(const CookArgs &a, bool decook, int max_blocks, hipStream_t s) {

@@ -65,6 +65,23 @@ struct CrcTables {
             }
     }
 
+    // Z_d (d > 0) as four byte tables: Z(c) = B0[c & 255] ^ B1[c >> 8 & 255] ^ ...
+    void put_bytemap(uint32_t *dst, int d) const {
+        uint32_t basis[32];
+        for (int b = 0; b < 32; ++b) {
+            uint32_t c = 1u << b;
+            for (int i = 0; i < d; ++i) c = feed0(c);
+            basis[b] = c;
+        }
+        for (int t = 0; t < 4; ++t)
+            for (int v = 0; v < 256; ++v) {
+                uint32_t r = 0;
+                for (int b = 0; b < 8; ++b)
+                    if (v >> b & 1) r ^= basis[8 * t + b];
+                dst[256 * t + v] = r;
+            }
+    }
+
     CrcTables() {
         for (uint32_t v = 0; v < 256; ++v) {
             uint32_t c = v;
@@ -79,19 +96,8 @@ struct CrcTables {
         for (int k = 0; k < rsmi::kCookLpp; ++k) put_map(&blob[rsmi::kCookLane + 128 * k], 16 * k);
         // Z_{16 kCookLpp} (a lane's step to its next piece) as four byte tables:
         // Z(c) = B0[c & 255] ^ B1[c >> 8 & 255] ^ ...
-        uint32_t basis[32];
-        for (int b = 0; b < 32; ++b) {
-            uint32_t c = 1u << b;
-            for (int i = 0; i < 16 * rsmi::kCookLpp; ++i) c = feed0(c);
-            basis[b] = c;
-        }
-        for (int t = 0; t < 4; ++t)
-            for (int v = 0; v < 256; ++v) {
-                uint32_t r = 0;
-                for (int b = 0; b < 8; ++b)
-                    if (v >> b & 1) r ^= basis[8 * t + b];
-                blob[rsmi::kCookZH + 256 * t + v] = r;
-            }
+        put_bytemap(&blob[rsmi::kCookZH], 16 * rsmi::kCookLpp);
+        if (COOK_2CH) put_bytemap(&blob[rsmi::kCookZH2], 32 * rsmi::kCookLpp);
         for (int c = 1; c < 4; ++c) put_map(&blob[rsmi::kCookUns + 128 * (c - 1)], -c);
         for (int c = 1; c < 4; ++c) put_map(&blob[rsmi::kCookUns + 128 * (2 + c)], -4 * c);
         if (COOK_S16)  // T_8..T_15, each one zero byte past the one before (T_7 first)

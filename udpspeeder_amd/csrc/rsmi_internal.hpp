@@ -182,6 +182,7 @@ constexpr int kCookLpp = COOK_LPP;
 //   kCookNib + 16i   raw CRC of a 16-byte piece holding nibble i alone, i = 0..31
 //   kCookZN          nibble map of Z_{16 kCookLpp}
 //   kCookS16 + 256k  (COOK_S16) T_{8+k}, k = 0..7: slicing-by-16 with T_0..T_7
+//   kCookZH2         (COOK_2CH) byte map of Z_{32 kCookLpp}, the two-chain step (4 x 256)
 // COOK_NIB selects the nibble forms for the per-piece work: 16-entry tables sit in
 // distinct LDS banks, so a wave's lookups into one never conflict.
 // COOK_S16: a piece's raw CRC as 16 independent byte lookups (one level)
@@ -198,7 +199,16 @@ constexpr int kCookUns = kCookZH + 1024;
 constexpr int kCookNib = kCookUns + 6 * 128;
 constexpr int kCookZN = kCookNib + 512;
 constexpr int kCookS16 = kCookNib;  // COOK_S16 and COOK_NIB exclude each other
-constexpr int kCookTabWords = COOK_NIB ? kCookZN + 128 : (COOK_S16 ? kCookS16 + 2048 : kCookNib);
+// COOK_2CH: k_cook folds a lane's pieces as two interleaved Horner chains
+// (even and odd piece slots, step Z_{32 kCookLpp}: byte tables at kCookZH2),
+// half the dependent LDS round trips per round.  k_decook keeps one chain and
+// copies only the tables before kCookZH2 (its per-packet scratch is larger).
+#ifndef COOK_2CH
+#define COOK_2CH 1
+#endif
+constexpr int kCookZH2 = COOK_NIB ? kCookZN + 128 : (COOK_S16 ? kCookS16 + 2048 : kCookNib);
+constexpr int kCookTabDecook = kCookZH2;                            // k_decook's LDS tables
+constexpr int kCookTabWords = kCookZH2 + (COOK_2CH ? 1024 : 0);     // the blob, k_cook's tables
 static_assert(!(COOK_NIB && COOK_S16), "COOK_NIB and COOK_S16 are alternatives");
 constexpr int kCookKsBytes = 65536 + 128;  // key stream covers every byte position used
 
