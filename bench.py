@@ -20,7 +20,9 @@ bytes per group per operation, encode + decode), timed between barriers and
 taken as the max over ranks.  ``roofline`` is for whichever kernel takes
 longer per step, measured with HIP events on the launch stream;
 ``cpu_baseline`` times the reference codec (oracle/_ref) on this host, 1
-thread and the CPU share (16 threads).
+thread and one thread per CPU of the process's affinity set (16 beside it).
+After the timed region every rank checks its own slice's bytes against the
+reference's digests (``parity_ok``, one entry per rank).
 """
 from __future__ import annotations
 
@@ -57,7 +59,11 @@ def parse(argv=None):
     p.add_argument("--scaling", choices=["weak", "strong"], default=None,
                    help="default: weak at N=1 (C1+C2), strong over --total-groups at N>1 (C4)")
     p.add_argument("--total-groups", type=int, default=C4_GROUPS, help="strong scaling total")
-    p.add_argument("--cpu-threads", type=int, default=16, help="threads of the all-cores CPU leg")
+    p.add_argument("--cpu-threads", type=int, default=None,
+                   help="threads of the all-cores CPU leg (default: len(os.sched_getaffinity(0)), "
+                        "the CPUs this process may run on; a 16-thread leg is reported beside it)")
+    p.add_argument("--no-verify", action="store_true",
+                   help="skip the after-the-timed-region check of every rank's bytes")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-extras", action="store_true", help="skip the other_configs lines")
     p.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL)")
@@ -165,12 +171,26 @@ def main():
     enc_ms = statistics.mean(a.elapsed_time(b) for a, b, _ in ev)
     dec_ms = statistics.mean(b.elapsed_time(c) for _, b, c in ev)
     bad = int((status != 0).sum().item())
+    extras = None
+    if rank == 0 and world == 1 and not args.no_extras:
+        extras = extra_configs(u, synth, torch, dev, buf, G)
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(buf, present, G, args.cpu_threads)
+    # after the timed region (and after the lines above, which read buf's
+    # parity): this rank's bytes against the reference's digests
+    check = None if args.no_verify else verify_slice(u, synth, torch, buf, present, g0, G)
+    ok_flags = [-1.0] * world
+    ok_flags[rank] = -1.0 if check is None or check.get("ok") is None else float(check["ok"])
+    parity_ok = [None if f < 0 else bool(f) for f in ok_flags]
     if world > 1:
-        # max over ranks: the job is as slow as its slowest GPU
-        t = torch.tensor([elapsed, enc_ms, dec_ms, float(bad)], dtype=torch.float64,
+        # max over ranks: the job is as slow as its slowest GPU; every rank's
+        # parity flag rides along in its own slot (-1 elsewhere)
+        t = torch.tensor([elapsed, enc_ms, dec_ms, float(bad)] + ok_flags, dtype=torch.float64,
                          device=dev if args.backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, enc_ms, dec_ms, bad = float(t[0]), float(t[1]), float(t[2]), int(t[3])
+        parity_ok = [None if float(f) < 0 else bool(f > 0.5) for f in t[4:]]
 
     payload_op = float(total_groups) * K * LEN  # one operation over the whole job
     value = 2.0 * payload_op * args.steps / elapsed / 2**30
@@ -188,13 +208,6 @@ def main():
     }
     dominant = "decode" if dec_ms >= enc_ms else "encode"
     other = "encode" if dominant == "decode" else "decode"
-
-    extras = None
-    if rank == 0 and world == 1 and not args.no_extras:
-        extras = extra_configs(u, synth, torch, dev, buf, G)
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(buf, present, G, args.cpu_threads)
 
     if rank == 0:
         if scaling == "weak":
@@ -219,6 +232,9 @@ def main():
             "encode_GiBps": round(payload_op / (enc_ms * 1e-3) / 2**30, 2),
             "decode_GiBps": round(payload_op / (dec_ms * 1e-3) / 2**30, 2),
             "decode_failures": bad,
+            "parity_ok": parity_ok,
+            "parity_check": None if check is None else {
+                k_: v for k_, v in check.items() if k_ != "ok"},
             "roofline": roof[dominant],
             f"roofline_{other}": roof[other],
             "cpu_baseline": cpu,
@@ -227,6 +243,42 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def verify_slice(u, synth, torch, buf, present, g0, G):
+    """This rank's bytes, checked after the timed region against digests the
+    real reference produced (tests/golden/full_hashes.json, c4_rank_slices
+    ranges, made by oracle/gen_golden.py --c4) for exactly this group range:
+    * parity: the timed loop's encode output (the parity rows now in buf);
+    * decode: the rank's slice refilled as the non-codeword input (data from
+      DATA_SEED, parity from DATA_SEED ^ 0xFFFF), every erased slot poisoned,
+      one decode through the same call as the step, the k data rows compared
+      (pins which survivors rs_decode uses, lib/rs.cpp:24-39).
+    Digests are sha256 over per-group checksums (synth.group_hashes_dev), so
+    8 B per group leave the device.  ``ok`` is None when no fixture covers the
+    range (e.g. a --groups the fixtures were not made for)."""
+    t0 = time.perf_counter()
+    path = os.path.join(ROOT, "tests", "golden", "full_hashes.json")
+    try:
+        F = json.load(open(path))["c4_rank_slices"]
+        R = F["ranges"].get(f"{g0}-{g0 + G}")
+    except (OSError, ValueError, KeyError):
+        F, R = None, None
+    if R is None:
+        return {"ok": None, "range": [g0, g0 + G], "why": "no reference digest for this range"}
+    n = K + M
+    par = synth.hashes_digest(synth.group_hashes_dev(buf[:, K:, :LEN]))
+    u.fill_data(buf, K, LEN, F["seed"], g0=g0)
+    u.fill_data(buf[:, K:], M, LEN, F["parity_seed"], g0=g0)
+    buf.masked_fill_((present == 0).unsqueeze(-1), 0xA5)  # erased slots hold junk
+    st = u.decode(buf, present, K, n, LEN)
+    fails = int((st != 0).sum().item())
+    dat = synth.hashes_digest(synth.group_hashes_dev(buf[:, :K, :LEN]))
+    ok = par == R["parity_gsum"] and dat == R["data_out_gsum"] and fails == 0
+    return {"ok": ok, "range": [g0, g0 + G], "parity_match": par == R["parity_gsum"],
+            "decode_match": dat == R["data_out_gsum"], "decode_failures": fails,
+            "check_s": round(time.perf_counter() - t0, 2),
+            "what": "reference digests of this rank's encode parity and non-codeword decode"}
 
 
 def roofline(which, kernel, alg_bytes, ms, G):
@@ -493,8 +545,9 @@ def frame_cook_config(torch, dev, groups=65536, reps=4):
     for i in range(reps + 1):
         p = enc.plan(lens, offs, inbuf)
         S = FecEncoder.slot_stride_for(int(p.groups["fec_len"].max()))
-        if slots is None:
-            slots = torch.empty(p.n_slots * S, dtype=torch.uint8, device=dev)
+        if slots is None or slots.numel() < p.n_slots * S:  # a batch may open more slots (carry)
+            slots = out = None
+            slots = torch.empty(p.n_slots * S + 64 * S, dtype=torch.uint8, device=dev)
             out = torch.empty_like(slots)
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -617,9 +670,25 @@ def cpu_baseline(buf, present, G, threads):
 
     one_sample = min(4096, host.shape[0])
     gib1, enc1, dec1 = run(one_sample, 1)
-    nthreads = threads if ref else 1
+    # the box's CPU share: the CPUs this process may run on, bounded by its
+    # cgroup's CPU quota (a 16-CPU quota over 256 affine CPUs throttles 256
+    # threads to 16 CPUs' time, and their contention then costs more than it
+    # gains -- both runs are reported)
+    affinity = len(os.sched_getaffinity(0))
+    quota = None
+    try:  # cgroup v2: "max 100000" or "<quota> <period>"
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        quota = None if q == "max" else int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    share = min(affinity, max(1, int(quota + 0.5))) if quota else affinity
+    nthreads = (threads or share) if ref else 1
     many_sample = host.shape[0]
     gibn, _, _ = run(many_sample, nthreads) if nthreads > 1 else (gib1, enc1, dec1)
+    side = {}
+    for t in sorted({16, affinity} - {nthreads}):
+        if ref:
+            side[t] = run(many_sample, t, reps=3)[0]
     try:
         model = [l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo")
                  if l.startswith("model name")][0]
@@ -627,8 +696,12 @@ def cpu_baseline(buf, present, G, threads):
         model = platform.processor()
     return {"value": round(gibn, 3), "unit": "GiB/s", "cores": nthreads, "kind": kind,
             "sample": f"{many_sample} groups RS(20,10)x1250B encode + decode (5 erasures), "
-                      f"median of 5 reps, {nthreads} threads on {model} "
-                      f"(the GPU box's CPU share; os.cpu_count()={os.cpu_count()})",
+                      f"median of 5 reps, {nthreads} threads (= the box's CPU share: "
+                      f"min(sched_getaffinity, cgroup quota)) on {model}",
+            "cpu_model": model, "affinity_cpus": affinity, "cgroup_cpu_quota": quota,
+            "os_cpu_count": os.cpu_count(),
+            "other_thread_counts": {str(t): {"value": round(v, 3), "unit": "GiB/s", "reps": 3}
+                                    for t, v in side.items()},
             "single_thread": {"value": round(gib1, 3), "unit": "GiB/s", "cores": 1,
                               "sample": f"{one_sample} groups, median of 5 reps",
                               "rs_encode2_us_per_call": round(enc1 * 1e6, 1),

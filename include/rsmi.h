@@ -74,6 +74,11 @@ const char *rsmi_last_error(void);
  * staging over PCIe and raises a completion flag (oneshot.hip); 0 takes the
  * staged copy path (H2D, kernel, D2H). */
 #define RSMI_OPT_ONE_GROUP 3
+/* RSMI_OPT_CLS_REC_CAP: 0 (default) sizes each ragged plan's decode workgroups
+ * to the LDS budget of the class kernels' occupancy; n > 0 caps the group
+ * records one workgroup stages at n (tests force small caps to exercise plans
+ * of many workgroup rounds).  Read when a plan is created. */
+#define RSMI_OPT_CLS_REC_CAP 4
 int rsmi_set_option(int option, int value);
 
 /* Host copy of fec_new(k,n)'s n x k systematic encoding matrix (row-major),

@@ -107,6 +107,21 @@ def ragged_draw(seed: int, g0: int, ng: int, table_y: np.ndarray,
     return k, m, ln
 
 
+HASH_SEED = 0xC4C4D16E57
+
+
+def group_hashes(rows: np.ndarray) -> np.ndarray:
+    """Per-group checksum of [G, R, L] uint8 rows (the checker's restatement of
+    udpspeeder_amd.synth.group_hashes_dev): h_g = sum_j w_j * byte_j mod 2^64,
+    w_j = mix(HASH_SEED + (j + 1) * GAMMA) | 1, j the byte's row-major index."""
+    G = rows.shape[0]
+    flat = np.ascontiguousarray(rows).reshape(G, -1)
+    with np.errstate(over="ignore"):
+        w = _mix(np.uint64(HASH_SEED) + np.arange(1, flat.shape[1] + 1, dtype=np.uint64) * GAMMA)
+        w |= np.uint64(1)
+        return flat.astype(np.uint64) @ w
+
+
 def _p(a: np.ndarray):
     return a.ctypes.data_as(C.c_void_p)
 

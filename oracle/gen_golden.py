@@ -15,8 +15,10 @@ compiled by oracle/Makefile) and writes small data fixtures:
                         extra survivors, too-few survivors, and the pointer permutation
   full_hashes.json      sha256 over full-size C1 encode parity, C3 ragged parity, a
                         C2 non-codeword decode (pins the PRNG definitions too), and
-                        the C4 rank slices 3/8 and 7/8 of 2^20 groups (encode parity
-                        + non-codeword decode), python -m oracle.gen_golden --c4
+                        the C4 rank slices 0, 3, 5, 7 of 8 over 2^20 groups (encode
+                        parity + non-codeword decode), and per-group-checksum digests
+                        of every range a bench.py rank owns at N = 1, 2, 4, 8
+                        (python -m oracle.gen_golden --c4)
 
 Inputs are regenerated from the PRNG definitions in oracle/cpu.py, so the fixtures
 hold outputs (plus sha256 of inputs to pin the generator).
@@ -238,40 +240,78 @@ def c3_ragged_decode(ref: Reference, ora: Oracle):
 
 C4_GROUPS = 1 << 20
 C4_WORLD = 8
-C4_RANKS = (3, 7)
+C4_RANKS = (0, 3, 5, 7)
+C4_WORLDS = (1, 2, 4, 8)
+C4_WEAK = 65536  # bench.py --scaling weak / N = 1: groups per rank
+
+
+def c4_ranges():
+    """Every group range a bench.py rank can own over the C4 stream: the
+    strong splits of 2^20 groups over 1/2/4/8 ranks and the weak 65,536-group
+    blocks of ranks 0..7 (block 0 is the N = 1 C1+C2 batch)."""
+    rs = set()
+    for w in C4_WORLDS:
+        for r in range(w):
+            rs.add((C4_GROUPS * r // w, C4_GROUPS * (r + 1) // w))
+    for r in range(8):
+        rs.add((r * C4_WEAK, (r + 1) * C4_WEAK))
+    return sorted(rs)
 
 
 def c4_rank_slices(ref: Reference, nthreads: int):
-    """C4 (RS(20,10), 1250 B, 2^20 groups over 8 ranks): for ranks 3 and 7 of
-    8, the slice [g0, g1) = shard.strong_range(r, 8, 2^20) as one rank encodes
-    and decodes it (global group ids g0.. drive the PRNG streams):
-      parity_sha256   rs_encode2 parity of the slice's DATA_SEED data;
-      data_out_sha256 rs_decode2 of the non-codeword slice (DATA_SEED data,
-                      DATA_SEED ^ 0xFFFF parity, 5 erasures per group from
-                      ERASE_SEED), digest of the k data rows (len bytes each).
+    """C4 (RS(20,10), 1250 B, 2^20 groups; global group ids drive the PRNG
+    streams), run through the reference in one pass over all groups:
+      ranks[r]        for ranks 0, 3, 5, 7 of 8, the slice [g0, g1) =
+                      shard.strong_range(r, 8, 2^20) as one rank encodes and
+                      decodes it:
+        parity_sha256   rs_encode2 parity of the slice's DATA_SEED data;
+        data_out_sha256 rs_decode2 of the non-codeword slice (DATA_SEED data,
+                        DATA_SEED ^ 0xFFFF parity, 5 erasures per group from
+                        ERASE_SEED), digest of the k data rows (len bytes each);
+      ranges["g0-g1"] for every range of c4_ranges(): sha256 over the per-group
+                      checksums (oracle.cpu.group_hashes) of the same parity
+                      rows ("parity_gsum") and decoded data rows
+                      ("data_out_gsum") -- what bench.py's ranks check their
+                      slices against after the timed region.
     Groups are independent (connection.h:244-245), so each slice's digest is
-    what the 8-GPU job's rank r must produce."""
+    what rank r of an N-GPU job must produce."""
+    from oracle.cpu import group_hashes
     k, n, ln = 20, 30, 1250
     chunk = 8192
     out = {"k": k, "n": n, "len": ln, "groups": C4_GROUPS, "world": C4_WORLD,
            "seed": DATA_SEED, "parity_seed": DATA_SEED ^ 0xFFFF, "erase_seed": ERASE_SEED,
-           "erasures": 5, "ranks": {}}
+           "erasures": 5, "checksum": "oracle.cpu.group_hashes / udpspeeder_amd.synth.group_hashes_dev",
+           "ranks": {}, "ranges": {}}
+    bounds = {r: (C4_GROUPS * r // C4_WORLD, C4_GROUPS * (r + 1) // C4_WORLD) for r in C4_RANKS}
+    sh = {r: (hashlib.sha256(), hashlib.sha256()) for r in C4_RANKS}
+    hpar = np.empty(C4_GROUPS, np.uint64)
+    hdat = np.empty(C4_GROUPS, np.uint64)
+    for c0 in range(0, C4_GROUPS, chunk):
+        m = min(chunk, C4_GROUPS - c0)
+        buf = np.zeros((m, n, ln), np.uint8)
+        buf[:, :k] = group_data(DATA_SEED, c0, m, k, ln)
+        ref.encode_batch(k, n, buf.reshape(-1), n * ln, ln, ln, m, nthreads)
+        hpar[c0:c0 + m] = group_hashes(buf[:, k:])
+        owner = [r for r, (a, b) in bounds.items() if a <= c0 < b]
+        if owner:
+            sh[owner[0]][0].update(buf[:, k:].tobytes())
+        buf[:, k:] = group_data(DATA_SEED ^ 0xFFFF, c0, m, n - k, ln)
+        pres = present_from_erasures(erasures(ERASE_SEED, c0, m, n, 5), n)
+        st = ref.decode_batch(k, n, buf.reshape(-1), n * ln, ln, ln, m, pres, True, nthreads)
+        assert (st == 0).all()
+        hdat[c0:c0 + m] = group_hashes(buf[:, :k])
+        if owner:
+            sh[owner[0]][1].update(buf[:, :k].tobytes())
+        if c0 % (chunk * 16) == 0:
+            print("c4", c0, flush=True)
     for r in C4_RANKS:
-        g0, g1 = C4_GROUPS * r // C4_WORLD, C4_GROUPS * (r + 1) // C4_WORLD
-        hp = hashlib.sha256(); hx = hashlib.sha256()
-        for c0 in range(g0, g1, chunk):
-            m = min(chunk, g1 - c0)
-            buf = np.zeros((m, n, ln), np.uint8)
-            buf[:, :k] = group_data(DATA_SEED, c0, m, k, ln)
-            ref.encode_batch(k, n, buf.reshape(-1), n * ln, ln, ln, m, nthreads)
-            hp.update(buf[:, k:].tobytes())
-            buf[:, k:] = group_data(DATA_SEED ^ 0xFFFF, c0, m, n - k, ln)
-            pres = present_from_erasures(erasures(ERASE_SEED, c0, m, n, 5), n)
-            st = ref.decode_batch(k, n, buf.reshape(-1), n * ln, ln, ln, m, pres, True, nthreads)
-            assert (st == 0).all()
-            hx.update(buf[:, :k].tobytes())
-        out["ranks"][str(r)] = {"g0": g0, "g1": g1, "parity_sha256": hp.hexdigest(),
-                                "data_out_sha256": hx.hexdigest()}
+        g0, g1 = bounds[r]
+        out["ranks"][str(r)] = {"g0": g0, "g1": g1, "parity_sha256": sh[r][0].hexdigest(),
+                                "data_out_sha256": sh[r][1].hexdigest()}
+    dig = lambda h: hashlib.sha256(np.ascontiguousarray(h, dtype="<u8").tobytes()).hexdigest()
+    for g0, g1 in c4_ranges():
+        out["ranges"][f"{g0}-{g1}"] = {"parity_gsum": dig(hpar[g0:g1]),
+                                       "data_out_gsum": dig(hdat[g0:g1])}
     return out
 
 

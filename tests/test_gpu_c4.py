@@ -4,7 +4,7 @@ C4 is RS(20,10) encode + decode of 1250-B shards over 2^20 groups split across
 8 GPUs.  FEC groups are independent (connection.h:244-245), so a
 rank's work is exactly its contiguous slice shard.strong_range(r, 8, 2^20),
 with the PRNG streams keyed by the GLOBAL group id.  These tests run two
-ranks' slices (3/8 at g0 = 393,216 and 7/8 at g0 = 917,504) through the same
+ranks' slices (0/8, 3/8 at g0 = 393,216, 5/8 and 7/8 at g0 = 917,504) through the same
 calls bench.py's ranks make, and check the bytes against sha256 digests the
 real reference (lib/rs.cpp + lib/fec.cpp, oracle/_ref) produced for exactly
 those slices (tests/golden/full_hashes.json "c4_rank_slices", made by
@@ -21,7 +21,7 @@ pytestmark = pytest.mark.gpu
 STRIDE = 1280
 
 
-@pytest.mark.parametrize("rank", [3, 7])
+@pytest.mark.parametrize("rank", [0, 3, 5, 7])
 def test_c4_rank_slice_encode_decode(gpu, golden, rank):
     import torch
     import udpspeeder_amd as u
@@ -79,3 +79,30 @@ def test_c4_all_groups_one_gpu_roundtrip(gpu, golden):
     assert torch.equal(t[:, :k, :ln], orig)
     del orig
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("world,rank", [(1, 0), (4, 2), (8, 5)])
+def test_bench_verify_slice(gpu, world, rank):
+    """bench.py's after-the-timed-region check (verify_slice): a rank's C4
+    slice, encoded and decoded through the bench's own calls, matches the
+    reference's per-group-checksum digests for its range (N = 1's 65,536
+    groups, rank 2 of 4, rank 5 of 8); a corrupted parity byte is caught."""
+    import torch
+    import bench
+    import udpspeeder_amd as u
+    from udpspeeder_amd import shard, synth
+    k, n, ln = 20, 30, 1250
+    g0, g1 = (0, 65536) if world == 1 else shard.strong_range(rank, world, 1 << 20)
+    G = g1 - g0
+    t = torch.empty((G, n, STRIDE), dtype=torch.uint8, device=gpu)
+    u.fill_data(t, k, ln, synth.DATA_SEED, g0=g0)
+    pres = torch.from_numpy(synth.erasure_present(synth.ERASE_SEED, g0, G, n, 5)).to(gpu)
+    u.encode(t, k, n, ln)
+    u.decode(t, pres, k, n, ln)
+    r = bench.verify_slice(u, synth, torch, t, pres, g0, G)
+    assert r["ok"] is True, r
+    u.fill_data(t, k, ln, synth.DATA_SEED, g0=g0)
+    u.encode(t, k, n, ln)
+    t[G // 2, k + 3, 100] ^= 1
+    r = bench.verify_slice(u, synth, torch, t, pres, g0, G)
+    assert r["ok"] is False and not r["parity_match"] and r["decode_match"], r

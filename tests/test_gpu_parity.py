@@ -550,6 +550,112 @@ def test_ragged_plan_decode_many_codes_vs_oracle(gpu, oracle):
         assert (got[:k, :d.len] == seg.reshape(n, d.shard_stride)[:k, :d.len]).all(), (i, k, n)
 
 
+def test_ragged_decode_offsets_bit31(gpu, oracle):
+    """Round-3 fault, pinned on purpose: the class kernels rebuild a group's
+    64-bit offset from two record dwords read with v_readlane, and a low dword
+    with bit 31 set once sign-extended into the high half (commit 83459b6).
+    Here every group of the batch sits past 2 GiB inside one tensor (offsets
+    0x8000_0000 + ..., low dword bit 31 set), and the batch decodes through a
+    plan (k_decode_ragged_cls, plus the workgroup kernel for e > 5) and
+    through the device-descriptor form (k_decode_ragged), both against the
+    oracle.  Before the fix this faulted the GPU; now it must be bit-exact."""
+    import torch
+    import udpspeeder_amd as u
+    from udpspeeder_amd import synth
+    rng = np.random.default_rng(31)
+    G = 400
+    ks = rng.integers(1, 21, G)
+    ms = rng.integers(1, 11, G)
+    ls = rng.integers(1, 1300, G)  # every tile-width class
+    groups, total = u.make_groups(ks, ks + ms, ls)
+    shift = 0x80000000 + 4096
+    for i in range(G):
+        groups[i].offset += shift
+        assert (groups[i].offset & 0xFFFFFFFF) >> 31 == 1
+    host = rng.integers(0, 256, total, dtype=np.uint8)
+    flags = np.zeros((G, 256), np.uint8)
+    for i in range(G):
+        n = int(ks[i] + ms[i])
+        flags[i, :n] = 1
+        ne = min(int(rng.integers(1, 8)), int(ms[i]))  # some e > 5: deferred groups too
+        flags[i, rng.choice(n, ne, replace=False)] = 0
+    for c in set(zip(ks.tolist(), (ks + ms).tolist())):
+        u.prepare_code(*c)
+    base = torch.zeros(shift + total, dtype=torch.uint8, device=gpu)
+    bits = torch.from_numpy(synth.present_bits(flags).view(np.int32)).to(gpu)
+    exp, ost = host.copy(), np.zeros(G, np.int32)
+    for i in range(G):
+        d = groups[i]
+        o = d.offset - shift
+        seg = exp[o:o + d.n * d.shard_stride]
+        ost[i] = oracle.decode_batch(d.k, d.n, seg, 0, d.shard_stride, d.len, 1,
+                                     flags[i:i + 1, :d.n])[0]
+        exp[o:o + d.n * d.shard_stride] = seg
+    plan = u.rs.RaggedPlan(groups, wait_codes=False)
+    dgroups = u.rs.groups_to_device(groups, gpu)
+    for form in ("plan", "dev"):
+        base[shift:].copy_(torch.from_numpy(host).to(gpu))
+        if form == "plan":
+            st = plan.decode(base, bits)
+        else:
+            st = u.rs.decode_ragged_dev(base, dgroups, G, bits, kmax=20)
+        st = st.cpu().numpy()
+        out = base[shift:].cpu().numpy()
+        assert (base[:shift].count_nonzero().item()) == 0, form  # nothing written below the groups
+        assert (st == ost).all(), form
+        for i in range(G):
+            d = groups[i]
+            o = d.offset - shift
+            got = out[o:o + d.n * d.shard_stride].reshape(d.n, d.shard_stride)
+            ref = exp[o:o + d.n * d.shard_stride].reshape(d.n, d.shard_stride)
+            assert (got[:d.k, :d.len] == ref[:d.k, :d.len]).all(), (form, i)
+    plan.close()
+
+
+@pytest.mark.parametrize("cap", [1, 3])
+def test_ragged_plan_decode_record_cap(gpu, oracle, cap):
+    """A plan's decode workgroups stage their group records in LDS, capped to
+    the class kernels' LDS budget (ragged.cpp); past the cap the plan deals
+    the groups to more workgroups than one resident round.  Forcing a cap of
+    1 or 3 records (RSMI_OPT_CLS_REC_CAP) makes a 6,000-group plan run every
+    width class over many rounds of workgroups: bit-exact with the oracle."""
+    import torch
+    import udpspeeder_amd as u
+    from udpspeeder_amd import synth
+    from udpspeeder_amd._lib import RSMI_OPT_CLS_REC_CAP
+    rng = np.random.default_rng(50 + cap)
+    G = 6000
+    ks = rng.integers(1, 21, G)
+    ms = rng.integers(1, 11, G)
+    ls = rng.integers(1, 1300, G)
+    groups, total = u.make_groups(ks, ks + ms, ls)
+    host = rng.integers(0, 256, total, dtype=np.uint8)
+    flags = np.zeros((G, 256), np.uint8)
+    for i in range(G):
+        n = int(ks[i] + ms[i])
+        flags[i, :n] = 1
+        flags[i, rng.choice(n, min(5, int(ms[i])), replace=False)] = 0
+    L = u.lib()
+    prev = L.rsmi_set_option(RSMI_OPT_CLS_REC_CAP, cap)
+    try:
+        plan = u.rs.RaggedPlan(groups, wait_codes=False)
+    finally:
+        L.rsmi_set_option(RSMI_OPT_CLS_REC_CAP, prev)
+    base = upload(host, gpu)
+    bits = torch.from_numpy(synth.present_bits(flags).view(np.int32)).to(gpu)
+    st = plan.decode(base, bits).cpu().numpy()
+    plan.close()
+    out = base.cpu().numpy()
+    for i in range(G):
+        d = groups[i]
+        n, k = d.n, d.k
+        seg = host[d.offset:d.offset + n * d.shard_stride].copy()
+        ost = oracle.decode_batch(k, n, seg, 0, d.shard_stride, d.len, 1, flags[i:i + 1, :n])
+        assert st[i] == ost[0], (i, k, n)
+        got = out[d.offset:d.offset + n * d.shard_stride].reshape(n, d.shard_stride)
+        assert (got[:k, :d.len] == seg.reshape(n, d.shard_stride)[:k, :d.len]).all(), (i, k, n)
+
+
 def test_ragged_plan_decode_graph_capture(gpu, oracle):
     """A ragged plan decode forks its width classes over extra streams and joins
     them back (event fork/join): it captures into a graph, and every replay
@@ -675,21 +781,25 @@ def test_compat_pointer_permutation(gpu, golden, name):
 
 @pytest.mark.parametrize("one_group", [True, False])
 @pytest.mark.parametrize("k,n,ln", [(20, 30, 1250), (3, 6, 3), (1, 2, 1), (40, 60, 700),
-                                    (10, 16, 5000), (128, 255, 64), (7, 13, 100), (20, 30, 17)])
+                                    (10, 16, 5000), (128, 255, 64), (7, 13, 100), (20, 30, 17),
+                                    (60, 70, 300), (20, 52, 200)])
 def test_dropin_one_group_vs_oracle(gpu, oracle, one_group, k, n, ln):
     """rs_encode2 / rs_decode2 of one group on non-codeword inputs, through
     the one-kernel latency path (RSMI_OPT_ONE_GROUP, oneshot.hip: pinned
     staging read over PCIe, completion flag) and through the staged copy path:
     both bit-exact with the oracle.  Covers survivors beyond one register
     chunk (k = 40), shards longer than 4 KiB (several column blocks), e > 8
-    (several row blocks) and a code outside the kernel's LDS budget
-    (k = 128, n = 255: it falls back)."""
+    (several row blocks), a code outside the kernel's LDS budget (k = 128,
+    n = 255: it falls back), and the whole-workgroup LDS elimination of
+    oneshot.hip: (60, 70) with e = 5 and 9 has e + k > 64 columns, (20, 52)
+    with e = 13 and 20 has more than 10 rows."""
     import udpspeeder_amd as u
     L = u.lib()
     prev = L.rsmi_set_option(3, int(one_group))
     try:
         rng = np.random.default_rng(k * 31 + n + ln)
-        for trial in range(3):
+        es = [1, 5, 9] + ([13, 20] if min(k, n - k) > 10 else [])
+        for trial, e_want in enumerate(es):
             rows = rng.integers(0, 256, (n, ln), dtype=np.uint8)
             # encode
             data = [bytearray(rows[j].tobytes()) for j in range(n)]
@@ -701,7 +811,7 @@ def test_dropin_one_group_vs_oracle(gpu, oracle, one_group, k, n, ln):
                 assert bytes(data[j]) == ref[j].tobytes(), ("encode", trial, j)
             # decode a non-codeword: up to min(k, m) erasures, data first
             m = n - k
-            e = min(k, m, 1 + trial * 4)
+            e = min(k, m, e_want)
             er = [int(x) for x in rng.choice(k, e, replace=False)]
             if m > e:  # and one parity shard, so the survivors skip it
                 er.append(k + int(rng.integers(0, m)))

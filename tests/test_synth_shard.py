@@ -82,3 +82,38 @@ def test_ragged_erasures_match_oracle():
     assert bits.dtype == np.uint32 and bits.shape == (3000, 8)
     back = np.unpackbits(bits.view(np.uint8), axis=1, bitorder="little")
     assert (back == a).all()
+
+
+def test_group_hashes_restatement_agrees():
+    """bench.py's per-group checksum (synth.group_hashes_dev, torch) and the
+    checker's numpy restatement (oracle.cpu.group_hashes) agree bit for bit on
+    strided slices of a [G, n, stride] batch, and a one-byte change moves the
+    group's checksum."""
+    import torch
+    from oracle.cpu import group_hashes
+    from udpspeeder_amd import synth
+    b = np.random.default_rng(9).integers(0, 256, (300, 30, 1280), dtype=np.uint8)
+    t = torch.from_numpy(b)
+    for sl in ((slice(None), slice(20, None), slice(0, 1250)),
+               (slice(None), slice(0, 20), slice(0, 1250)), (slice(5, 77), slice(3, 4), slice(0, 17))):
+        assert (synth.group_hashes_dev(t[sl], chunk=64) == group_hashes(b[sl])).all()
+    h0 = group_hashes(b[:, 20:, :1250])
+    b[7, 25, 1000] ^= 0x80
+    h1 = group_hashes(b[:, 20:, :1250])
+    assert (h0 != h1).sum() == 1 and h0[7] != h1[7]
+    assert synth.hashes_digest(h0) != synth.hashes_digest(h1)
+
+
+def test_c4_fixture_covers_every_bench_range(golden):
+    """tests/golden/full_hashes.json holds reference digests for every group
+    range a bench.py rank owns: strong splits of 2^20 over 1/2/4/8 ranks and
+    the weak 65,536-group blocks (so a driver N-GPU run checks all its ranks)."""
+    from udpspeeder_amd import shard
+    R = golden.full["c4_rank_slices"]["ranges"]
+    for w in (1, 2, 4, 8):
+        for r in range(w):
+            g0, g1 = shard.strong_range(r, w, 1 << 20)
+            assert f"{g0}-{g1}" in R
+        for r in range(w):
+            g0, g1 = shard.weak_range(r, 65536)
+            assert f"{g0}-{g1}" in R

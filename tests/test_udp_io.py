@@ -147,3 +147,22 @@ def test_connection_refused_mid_batch():
         assert 0 < n <= 64
         total += n
     assert total < 4 * 64  # at least one refused datagram was skipped, not fatal
+
+
+def test_socket_error_stops_the_batch():
+    """A failure of the socket itself (here EDESTADDRREQ: an unconnected socket
+    and no destination) is not a per-datagram drop: every later datagram would
+    fail the same way, so the call reports an I/O error at once instead of
+    spending one syscall per datagram."""
+    import socket
+    import time
+    from udpspeeder_amd._lib import RsmiError
+    tx = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+    try:
+        src = io.Slab(4096, 64)
+        t0 = time.perf_counter()
+        with pytest.raises(RsmiError, match="sendmmsg"):
+            io.send_batch(tx, src, 0, np.full(4096, 16, np.int32))
+        assert time.perf_counter() - t0 < 0.5
+    finally:
+        tx.close()

@@ -20,6 +20,8 @@ RSMI_ERR_HIP = -3
 RSMI_ERR_NOMEM = -4
 RSMI_OPT_BITSLICE = 1
 RSMI_OPT_FUSED_DECODE = 2
+RSMI_OPT_ONE_GROUP = 3
+RSMI_OPT_CLS_REC_CAP = 4
 RSMI_DEC_OK = 0
 RSMI_DEC_TOO_FEW = -1
 RSMI_DEC_SINGULAR = 1

@@ -20,6 +20,7 @@
 #include "rsmi_internal.hpp"
 
 namespace rsmi {
+std::atomic<int> g_opt_cls_cap{0};  // RSMI_OPT_CLS_REC_CAP (read by ragged.cpp)
 namespace {
 
 thread_local std::string g_err;
@@ -105,9 +106,23 @@ int init_device(Device &D) {
     std::vector<uint32_t> pt(256 * kPtabDwords, 0);
     for (int c = 0; c < 256; ++c) perm_tables((uint8_t)c, &pt[(size_t)c * kPtabDwords]);
     const GF &F = gf();
-    std::vector<uint8_t> gt(768);
+    // exp[512] | log[256] | pad | the ragged decode's Lagrange tables at
+    // kGfLtabOff (decode.hip LTables: the split table of alpha^v by v, the
+    // evaluation point of each shard index, log with log 0 = 0), copied into
+    // LDS by each workgroup with one 16-byte load per piece
+    std::vector<uint8_t> gt(kGfLtabOff + kGfLtabBytes, 0);
     std::memcpy(gt.data(), F.exp, 512);
     for (int i = 0; i < 256; ++i) gt[512 + i] = (uint8_t)F.log[i];
+    {
+        uint8_t *lt = gt.data() + kGfLtabOff;
+        for (int v = 0; v < 256; ++v) {
+            const uint32_t c = F.exp[v < 255 ? v : 0];
+            std::memcpy(lt + 16 * v, &pt[(size_t)c * kPtabDwords], 16);
+            std::memcpy(lt + 4096 + 4 * v, &pt[(size_t)c * kPtabDwords + 4], 4);
+            lt[5120 + v] = v ? F.exp[v - 1] : 0;
+            lt[5376 + v] = v ? (uint8_t)F.log[v] : 0;
+        }
+    }
     RSMI_HIP(hipMalloc(&D.ptab, pt.size() * 4), "hipMalloc(ptab)");
     RSMI_HIP(hipMalloc(&D.gftab, gt.size()), "hipMalloc(gftab)");
     RSMI_HIP(hipMalloc(&D.code_dir, sizeof(uint64_t) * 257 * 257), "hipMalloc(code_dir)");
@@ -847,6 +862,7 @@ int rsmi_set_option(int option, int value) {
     if (option == RSMI_OPT_BITSLICE) return rsmi::g_opt_bitslice.exchange(value ? 1 : 0);
     if (option == RSMI_OPT_FUSED_DECODE) return rsmi::g_opt_fused.exchange(value ? 1 : 0);
     if (option == RSMI_OPT_ONE_GROUP) return rsmi::g_opt_oneshot.exchange(value ? 1 : 0);
+    if (option == RSMI_OPT_CLS_REC_CAP) return rsmi::g_opt_cls_cap.exchange(value > 0 ? value : 0);
     rsmi::set_error("unknown option");
     return RSMI_ERR_INVALID;
 }

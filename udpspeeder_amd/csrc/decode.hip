@@ -79,6 +79,9 @@ constexpr int kTile = 1280;    // bytes per lane-tile pass (64 x 16 + 64 x 4)
 #ifndef DEC_RAG_RING5
 #define DEC_RAG_RING5 3  // ... and for 20-byte pieces (W = 4: ring 2 at 8 waves/SIMD, W = 5: 3 at 6, beat 4 at 6 / 5: profiles/r03/c3)
 #endif
+#ifndef DEC_RAG_UNCOND_W
+#define DEC_RAG_UNCOND_W 4  // ragged kernels: unconditional ring refills for tile widths >= this
+#endif
 #ifndef DEC_RAG_DEEP
 #define DEC_RAG_DEEP 1  // ragged kernel: 16 / W survivors in flight for 4- and 8-byte lane pieces
 #endif
@@ -153,6 +156,62 @@ __device__ __forceinline__ uint32_t gmul_t(uint4 t, uint32_t t2, uint32_t x) {
 __device__ __forceinline__ uint32_t gmul(const uint8_t *lexp, const uint8_t *llog, uint32_t a,
                                          uint32_t b) {
     return (a && b) ? lexp[llog[a] + llog[b]] : 0u;
+}
+
+// ---- Lagrange form of the decode coefficients ------------------------------------
+// fec_new's code is systematic Vandermonde (lib/fec.cpp:665-720): shard i is
+// the value at the point x_i = (i ? alpha^(i-1) : 0) of the polynomial P of
+// degree < k whose values at x_0..x_{k-1} are the data shards.  Any k
+// survivors S fix P, so a missing data row d is
+//     d = sum_{s in S} L_s(x_d) * shard_s,
+//     L_s(x_d) = prod_{t in S, t != s} (x_d ^ x_t) / (x_s ^ x_t),
+// and the matrix [L_s(x_d)] is the inverse fec_decode's Gauss-Jordan builds
+// (lib/fec.cpp:795-825, 425-549): both are the unique left inverse of the
+// survivors' rows of the encoding matrix, so the bytes are the same for any
+// input, codeword or not.  In logs (lz: log with lz[0] = 0, so t = s drops out
+// of every sum by itself):
+//     log L_s(x_d) = A_d - lz[x_d ^ x_s] - B_s   (mod 255),
+//     A_d = sum_{t in S} lz[x_d ^ x_t],   B_s = sum_{t in S} lz[x_s ^ x_t].
+// Lane s computes B_s (k independent LDS byte lookups) and lz[x_d ^ x_s] for
+// every missing row d; A_d is a wave sum of the latter (DPP, two rows packed
+// per 32-bit sum).  The coefficient's v_perm split table is read straight by
+// its log (tl01 / tl2 below), so no exp step and no pivot chain: a handful of
+// independent lookups in place of e dependent elimination steps.  Every
+// coefficient is nonzero (distinct points), so every one has a log.
+#ifndef DEC_LAGRANGE
+#define DEC_LAGRANGE 1         // ragged kernels: Lagrange coefficients (0: Gauss-Jordan)
+#endif
+constexpr int kLTabBytes = 5632;  // tl01[255] (4096) | tl2[255] (1024) | px[256] | lz[256]
+
+struct LTables {
+    const uint4 *t01;      // split table of alpha^v, v = 0..254 (T0lo T0hi T1lo T1hi)
+    const uint32_t *t2;    // ... its T2
+    const uint8_t *px;     // px[i] = x_i, the evaluation point of shard i
+    const uint8_t *lz;     // lz[v] = log v, lz[0] = 0
+};
+
+// The image sits in gftab at kGfLtabOff (api.cpp init_device builds it):
+// one independent 16-byte load per piece, no gftab -> ptab chain.
+static_assert(kGfLtabBytes == kLTabBytes, "LTables image size");
+__device__ __forceinline__ LTables load_ltables(uint8_t *smem, const uint32_t *,
+                                                const uint8_t *gftab) {
+    const uint4 *src = reinterpret_cast<const uint4 *>(gftab + kGfLtabOff);
+    uint4 *dst = reinterpret_cast<uint4 *>(smem);
+    for (int i = threadIdx.x; i < kLTabBytes / 16; i += blockDim.x) dst[i] = src[i];
+    return LTables{reinterpret_cast<const uint4 *>(smem), reinterpret_cast<const uint32_t *>(smem + 4096),
+                   smem + 5120, smem + 5376};
+}
+
+// Sum of x over the wave, in every lane's result (Kogge-Stone within each row
+// of 16 lanes, then the row sums through row_bcast:15 / row_bcast:31).
+__device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, true);  // row_shr:1
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, true);  // row_shr:2
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, true);  // row_shr:4
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, true);  // row_shr:8
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false); // row_bcast:15
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false); // row_bcast:31
+    return (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
 }
 
 struct WaveLds {  // per-wave LDS slice
@@ -286,6 +345,66 @@ __device__ __forceinline__ int gauss_jordan_regs(int k, int e, uint32_t col, con
     return RSMI_DEC_OK;
 }
 
+// Lagrange coefficients (see LTables above) for k <= 64 survivors, e <= NR
+// missing data rows: lane s < k holds survivor s's shard index in sel_lane,
+// lane d < e missing row d's in miss_lane.  Leaves coef[r][j]'s split table at
+// (t01, t2)[j * rows + r], as gauss_jordan_regs does.
+template <int NR>
+__device__ __forceinline__ void lagrange_coefs(int k, int e, uint32_t sel_lane, uint32_t miss_lane,
+                                               const WaveLds &L, const LTables &T, int lane) {
+    const bool act = lane < k;
+    const uint32_t xs = T.px[sel_lane & 255u];
+    const uint32_t xm = T.px[miss_lane & 255u];
+    // B_s: two chains of independent lookups
+    uint32_t b0 = 0, b1 = 0;
+    int t = 0;
+    for (; t + 1 < k; t += 2) {
+        const uint32_t x0 = (uint32_t)__builtin_amdgcn_readlane((int)xs, t);
+        const uint32_t x1 = (uint32_t)__builtin_amdgcn_readlane((int)xs, t + 1);
+        b0 += T.lz[xs ^ x0];
+        b1 += T.lz[xs ^ x1];
+    }
+    if (t < k) b0 += T.lz[xs ^ (uint32_t)__builtin_amdgcn_readlane((int)xs, t)];
+    const uint32_t B = b0 + b1;
+    // lz[x_d ^ x_s] of rows 2i and 2i + 1 packed in q[i] (each half <= 254,
+    // and a wave sum of halves <= 64 * 254 < 2^16): A_d for two rows per sum
+    constexpr int NQ = (NR + 1) / 2;
+    uint32_t q[NQ], A[NQ];
+#pragma unroll
+    for (int i = 0; i < NQ; ++i) {
+        q[i] = 0;
+        A[i] = 0;
+        if (2 * i < e) {
+            const uint32_t x0 = (uint32_t)__builtin_amdgcn_readlane((int)xm, 2 * i);
+            uint32_t v = T.lz[x0 ^ xs];
+            if (2 * i + 1 < e) {
+                const uint32_t x1 = (uint32_t)__builtin_amdgcn_readlane((int)xm, 2 * i + 1);
+                v |= (uint32_t)T.lz[x1 ^ xs] << 16;
+            }
+            q[i] = act ? v : 0u;
+            A[i] = wave_sum(q[i]);
+        }
+    }
+    if (act) {
+        const int base = lane * L.rows;
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+            if (r < e) {
+                const uint32_t sh = (r & 1) * 16;
+                const uint32_t a = (A[r >> 1] >> sh) & 0xFFFFu, l = (q[r >> 1] >> sh) & 0xFFFFu;
+                // A + 255 * 64 - l - B > 0 (l + B <= 64 * 254), then mod 255
+                uint32_t v = a + 255u * 64u - l - B;
+                v = (v & 255u) + (v >> 8);       // <= 255 + 127
+                v = (v & 255u) + (v >> 8);       // <= 255
+                v = min(v, v - 255u);            // 255 -> 0
+                L.t01[base + r] = T.t01[v];
+                L.t2[base + r] = T.t2[v];
+            }
+        }
+    }
+    wave_sync();
+}
+
 // Tile geometry for W dwords per lane: W = 1, 2, 4 is one 4W-byte load per
 // lane (a 256W-byte tile); W = 5 is a 16-byte load plus a dword load (1280 B).
 template <int W>
@@ -338,24 +457,38 @@ struct Rebuild {
     // narrow tiles keep more survivors in flight in the same registers (16
     // dwords of ring): short groups are latency-bound, not VGPR-bound
     static constexpr int R = DEC_RAG_DEEP && W <= 2 ? 16 / W : (W == 4 ? DEC_RAG_RING4 : DEC_RAG_RING5);
-    __amdgpu_buffer_rsrc_t rsrc;
+    __amdgpu_buffer_rsrc_t rsrc, rnull;  // rnull: num_records 0, every load reads 0
     uint32_t so_lane, mo_lane;
     int k, e, len, lpad;
     TileIO<W> io;
     uint32_t rq[R][W];
 
+    // Ring slot q <- survivor j.  For the wide tiles (W >= 4, rings of 2-3)
+    // the refills are unconditional: past the last survivor they go through
+    // rnull (no memory access, zeros).  A refill under "if (j < k)" makes
+    // rq[q] a loop-carried phi of old and new values, and the compiler then
+    // loads into spare registers and copies them back at the bottom of the
+    // loop behind an s_waitcnt vmcnt(0): every iteration waited for the loads
+    // it had just issued.  The narrow tiles keep the guard: their deep rings
+    // (8-16 slots) would issue that many dead loads per group, and the depth
+    // hides the wait anyway.
+    static constexpr bool kUncond = W >= DEC_RAG_UNCOND_W;
     __device__ __forceinline__ void load(int q, int j) {
-        io.load(rsrc, __builtin_amdgcn_readlane(so_lane, j), rq[q]);
+        if (kUncond) {
+            const bool ok = j < k;
+            io.load(ok ? rsrc : rnull, (uint32_t)__builtin_amdgcn_readlane(so_lane, ok ? j : 0), rq[q]);
+        } else if (j < k) {
+            io.load(rsrc, (uint32_t)__builtin_amdgcn_readlane(so_lane, j), rq[q]);
+        }
     }
     // whole cache lines where the slot has room (rsmi.h padding rule)
     __device__ __forceinline__ void start_tile(int toff, int lane) {
         io.set(toff, lpad - toff, lane);
 #pragma unroll
-        for (int q = 0; q < R; ++q)
-            if (q < k) load(q, q);
+        for (int q = 0; q < R; ++q) load(q, q);
     }
     // passes over (tile, block of kPass rows); tile 0's first loads were
-    // issued by start_tile(0) before the Gauss-Jordan
+    // issued by start_tile(0) before the coefficients
     __device__ __forceinline__ void run(const WaveLds &L, int lane) {
         for (int toff = 0; toff < len; toff += TileIO<W>::kBytes) {
             for (int rb = 0; rb < e; rb += kPass) {
@@ -365,23 +498,30 @@ struct Rebuild {
                 for (int r = 0; r < kPass; ++r)
 #pragma unroll
                     for (int w = 0; w < W; ++w) acc[r][w] = 0;
+                // a VGPR zero the compiler cannot see through: the per-survivor
+                // table addresses become one VALU add each (rows at immediate
+                // offsets) instead of a v_mov of an SGPR address per row
+                int z = 0;
+                asm volatile("" : "+v"(z));
                 for (int jb = 0; jb < k; jb += R) {
 #pragma unroll
                     for (int q = 0; q < R; ++q) {
                         const int j = jb + q;
+                        // the 3-bit split selectors of the survivor's W dwords
+                        uint32_t a0[W], a1[W], a2[W];
                         if (j < k) {
-                            // the 3-bit split selectors of the survivor's W dwords
-                            uint32_t a0[W], a1[W], a2[W];
 #pragma unroll
                             for (int w = 0; w < W; ++w) {
                                 a0[w] = rq[q][w] & 0x07070707u;
                                 a1[w] = (rq[q][w] >> 3) & 0x07070707u;
                                 a2[w] = (rq[q][w] >> 6) & 0x03030303u;
                             }
-                            // ring slot q took survivor j: load survivor j + R into it
-                            if (j + R < k) load(q, j + R);
-                            const uint4 *ta = L.t01 + j * L.rows + rb;
-                            const uint32_t *ta2 = L.t2 + j * L.rows + rb;
+                        }
+                        // ring slot q took survivor j: load survivor j + R into it
+                        load(q, j + R);
+                        if (j < k) {
+                            const uint4 *ta = L.t01 + (z + j * L.rows + rb);
+                            const uint32_t *ta2 = L.t2 + (z + j * L.rows + rb);
                             int nr = e - rb;  // opaque SGPR: see k_decode_fused's row guards
                             asm volatile("" : "+s"(nr));
 #pragma unroll
@@ -510,6 +650,11 @@ __global__ __launch_bounds__(256, DEC_OCC) void k_decode_fused(UniformArgs a, co
                              (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)gb);
         const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
             reinterpret_cast<uint8_t *>(gbu), 0, (int)(a.n * a.shard_stride), 0x00020000);
+        // num_records 0: the ring's loads past the last survivor read zeros
+        // without touching memory (see Rebuild::load for why they are not
+        // skipped instead)
+        const __amdgpu_buffer_rsrc_t rnull = __builtin_amdgcn_make_buffer_rsrc(
+            reinterpret_cast<uint8_t *>(gbu), 0, 0, 0x00020000);
         const uint32_t ss = (uint32_t)a.shard_stride;
         // survivor j's shard offset lives in lane j (k <= 64 on this path):
         // v_readlane gives the scalar soffset without an LDS round trip
@@ -529,11 +674,11 @@ __global__ __launch_bounds__(256, DEC_OCC) void k_decode_fused(UniformArgs a, co
             v4 = (1024 + 4 * lane < tlen) ? (uint32_t)(toff + 1024 + 4 * lane) : 0x80000000u;
 #pragma unroll
             for (int q = 0; q < kRing; ++q) {
-                if (q < k) {
-                    const uint32_t so = __builtin_amdgcn_readlane(so_lane, q);
-                    rq[q] = __builtin_amdgcn_raw_buffer_load_b128(DEC_NOMEM ? rsrc0 : rsrc, v16, DEC_NOMEM ? 0u : so, LDAUX);
-                    rd[q] = __builtin_amdgcn_raw_buffer_load_b32(DEC_NOMEM ? rsrc0 : rsrc, v4, DEC_NOMEM ? 0u : so, LDAUX);
-                }
+                const bool ok = q < k;
+                const uint32_t so = __builtin_amdgcn_readlane(so_lane, ok ? q : 0);
+                const __amdgpu_buffer_rsrc_t r = DEC_NOMEM ? rsrc0 : (ok ? rsrc : rnull);
+                rq[q] = __builtin_amdgcn_raw_buffer_load_b128(r, v16, DEC_NOMEM ? 0u : so, LDAUX);
+                rd[q] = __builtin_amdgcn_raw_buffer_load_b32(r, v4, DEC_NOMEM ? 0u : so, LDAUX);
             }
         };
         start_tile(0);  // the first survivors fly while the matrix is inverted
@@ -657,12 +802,13 @@ __global__ __launch_bounds__(256, DEC_OCC) void k_decode_fused(UniformArgs a, co
             }
         };
         // ring slot q took survivor j: load survivor j + kRing into it
+        // (unconditional: past the last survivor through rnull)
         auto refill = [&](int q, int j) {
-            if (j + kRing < k) {
-                const uint32_t so = __builtin_amdgcn_readlane(so_lane, j + kRing);
-                rq[q] = __builtin_amdgcn_raw_buffer_load_b128(DEC_NOMEM ? rsrc0 : rsrc, v16, DEC_NOMEM ? 0u : so, LDAUX);
-                rd[q] = __builtin_amdgcn_raw_buffer_load_b32(DEC_NOMEM ? rsrc0 : rsrc, v4, DEC_NOMEM ? 0u : so, LDAUX);
-            }
+            const bool ok = j + kRing < k;
+            const uint32_t so = __builtin_amdgcn_readlane(so_lane, ok ? j + kRing : 0);
+            const __amdgpu_buffer_rsrc_t r = DEC_NOMEM ? rsrc0 : (ok ? rsrc : rnull);
+            rq[q] = __builtin_amdgcn_raw_buffer_load_b128(r, v16, DEC_NOMEM ? 0u : so, LDAUX);
+            rd[q] = __builtin_amdgcn_raw_buffer_load_b32(r, v4, DEC_NOMEM ? 0u : so, LDAUX);
         };
         for (int toff = 0; toff < a.len; toff += kTile) {
             for (int rb = 0; rb < e; rb += kPass) {
@@ -672,6 +818,8 @@ __global__ __launch_bounds__(256, DEC_OCC) void k_decode_fused(UniformArgs a, co
                 for (int r = 0; r < kPass; ++r)
 #pragma unroll
                     for (int w = 0; w < 5; ++w) acc[r][w] = 0;
+                int z = 0;  // VGPR zero: one address add per survivor (see Rebuild::run)
+                asm volatile("" : "+v"(z));
                 for (int jb = 0; jb < k; jb += kRing) {
 #pragma unroll
                     for (int q = 0; q < kRing; q += DEC_PAIR ? 2 : 1) {
@@ -704,11 +852,12 @@ __global__ __launch_bounds__(256, DEC_OCC) void k_decode_fused(UniformArgs a, co
                                     }
                                 }
                             }
-                        } else if (j < k) {
+                        } else {
                             uint32_t a0[5], a1[5], a2[5];
-                            split(rq[q], rd[q], a0, a1, a2);
-                            refill(q, j);
-                            const uint32_t *ta = L.tab + (j * kRows + rb) * 8;
+                            if (j < k) split(rq[q], rd[q], a0, a1, a2);
+                            refill(q, j);  // every iteration: see Rebuild::run
+                            if (j >= k) continue;
+                            const uint32_t *ta = L.tab + (z + (j * kRows + rb) * 8);
                             // rows in this pass, as an opaque SGPR per survivor: a
                             // loop-invariant "rb + r < e" is hoisted as a lane-mask
                             // boolean and re-materialised with v_cndmask + v_cmp at
@@ -777,6 +926,19 @@ __global__ __launch_bounds__(256, DEC_OCC) void k_decode_fused(UniformArgs a, co
 #define DEC_CLS_OCC5 6
 #endif
 constexpr int kClsRows = 5;  // class kernels: e <= 5 in registers, more is deferred
+#if DEC_LAGRANGE
+using RagTables = LTables;
+constexpr int kRagTabBytes = kLTabBytes;
+__device__ __forceinline__ RagTables load_rag_tables(uint8_t *smem, const uint32_t *ptab, const uint8_t *gftab) {
+    return load_ltables(smem, ptab, gftab);
+}
+#else
+using RagTables = Tables;
+constexpr int kRagTabBytes = kTabBytes;
+__device__ __forceinline__ RagTables load_rag_tables(uint8_t *smem, const uint32_t *ptab, const uint8_t *gftab) {
+    return load_tables(smem, ptab, gftab);
+}
+#endif
 
 // One group's wave-uniform description.
 struct GroupDesc {
@@ -806,7 +968,7 @@ struct NoHook {
 // kernels fetch the next group's present words there).
 template <int WC, int NR, class Flag, class Hook = NoHook>
 __device__ __forceinline__ void ragged_group_run(const GroupDesc &D, Flag flag, uint8_t *base,
-                                                 int32_t *status_out, const Tables &T,
+                                                 int32_t *status_out, const RagTables &T,
                                                  const WaveLds &L, int kmax, int lane,
                                                  DeferMark dm = DeferMark{nullptr, 0},
                                                  Hook after_select = Hook{}) {
@@ -843,6 +1005,9 @@ __device__ __forceinline__ void ragged_group_run(const GroupDesc &D, Flag flag, 
     }
     const int lpad = rag_lpad((uint32_t)len, ss);
     const uint32_t sel_lane = lane < k ? (uint32_t)L.sel[lane] : 0u;
+#if DEC_LAGRANGE
+    const uint32_t miss_lane = lane < e ? (uint32_t)L.miss[lane] : 0u;
+#else
     // The system's code-row bytes (lane c: column c of rows R_0..R_{NR-1}, R_r
     // = survivor k - e + r, clamped for r >= e), as buffer loads issued before
     // the first survivor loads: waiting for them is vmcnt(survivor loads), not
@@ -862,18 +1027,25 @@ __device__ __forceinline__ void ragged_group_run(const GroupDesc &D, Flag flag, 
             cv[r] = __builtin_amdgcn_raw_buffer_load_b8(rr, ro + cc, 0, 0);
         }
     }
+#endif
     auto rebuild = [&](auto wc) {
         constexpr int W = decltype(wc)::value;
         Rebuild<W> B;
         B.rsrc = group_rsrc(base + off, (uint32_t)(n * ss));
+        B.rnull = group_rsrc(base + off, 0u);
         B.k = k;
         B.e = e;
         B.len = len;
         B.lpad = lpad;
         B.so_lane = sel_lane * ss;
         B.mo_lane = (lane < e ? (uint32_t)L.miss[lane] : 0u) * ss;
-        if (len > 0) B.start_tile(0, lane);
+        if (len > 0) B.start_tile(0, lane);  // the first survivors fly while the coefficients form
+#if DEC_LAGRANGE
+        lagrange_coefs<NR>(k, e, sel_lane, miss_lane, L, T, lane);
+        const int st = RSMI_DEC_OK;  // distinct points: never singular
+#else
         const int st = gauss_jordan_regs<NR>(k, e, col, cv, Rr, L, T, lane);
+#endif
 #if DEC_TRACE
         const uint64_t tr2 = trace_now();
 #endif
@@ -906,7 +1078,7 @@ __device__ __forceinline__ void ragged_group_run(const GroupDesc &D, Flag flag, 
 template <int WC, int NR>
 __device__ __forceinline__ void ragged_group(int64_t g, const rsmi_group &d, uint32_t w8,
                                              uint8_t *base, int32_t *status_out,
-                                             const uint64_t *code_dir, const Tables &T,
+                                             const uint64_t *code_dir, const RagTables &T,
                                              const WaveLds &L, int kmax, int lane) {
     GroupDesc D;
     D.g = g;
@@ -937,10 +1109,10 @@ __global__ __launch_bounds__(256, DEC_RAG_OCC) void k_decode_ragged(
     const uint32_t *__restrict__ present, int32_t *status_out, const uint64_t *__restrict__ code_dir,
     const uint32_t *ptab, const uint8_t *gftab, int kmax) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const Tables T = load_tables(smem, ptab, gftab);
+    const RagTables T = load_rag_tables(smem, ptab, gftab);
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane0 = threadIdx.x & 63;
-    const WaveLds L = rag_slice(smem + kTabBytes + wid * rag_lds_bytes(kmax, kRows), kmax, kRows);
+    const WaveLds L = rag_slice(smem + kRagTabBytes + wid * rag_lds_bytes(kmax, kRows), kmax, kRows);
     __syncthreads();
     const int64_t nwaves = (int64_t)gridDim.x * kWaves;
     for (int64_t g = (int64_t)blockIdx.x * kWaves + wid; g < ngroups; g += nwaves) {
@@ -977,15 +1149,15 @@ __global__ __launch_bounds__(64 * kClsWaves, OCC) void k_decode_ragged_cls(
     const int b = blockIdx.x;
     if (b >= nb) return;  // (whole block: before any barrier)
     const uint32_t i0 = wst[b], cnt = wst[b + 1] - i0;
-    uint32_t *srec = reinterpret_cast<uint32_t *>(smem + kTabBytes + kClsWaves * rag_lds_bytes(kmax, kClsRows));
+    uint32_t *srec = reinterpret_cast<uint32_t *>(smem + kRagTabBytes + kClsWaves * rag_lds_bytes(kmax, kClsRows));
     uint32_t *spw = srec + (size_t)maxb * 8;
     uint32_t *next = spw + (size_t)maxb * 8;
     for (uint32_t t = threadIdx.x; t < cnt * 8; t += blockDim.x) srec[t] = rec[(size_t)i0 * 8 + t];
     if (threadIdx.x == 0) *next = 0;
-    const Tables T = load_tables(smem, ptab, gftab);
+    const RagTables T = load_rag_tables(smem, ptab, gftab);
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
-    const WaveLds L = rag_slice(smem + kTabBytes + wid * rag_lds_bytes(kmax, kClsRows), kmax, kClsRows);
+    const WaveLds L = rag_slice(smem + kRagTabBytes + wid * rag_lds_bytes(kmax, kClsRows), kmax, kClsRows);
     __syncthreads();
     for (uint32_t t = threadIdx.x; t < cnt * 8; t += blockDim.x)
         spw[t] = present[(size_t)srec[(t & ~7u) + 5] * 8 + (t & 7u)];
@@ -1020,6 +1192,10 @@ __global__ __launch_bounds__(64 * kClsWaves, OCC) void k_decode_ragged_cls(
             tt[5] = (uint64_t)w; tt[6] = tk0; tt[7] = tk1;
         }
 #endif
+        // lane-derived values (LDS row addresses) are recomputed per group:
+        // hoisted out of the loop they stay live across it and spill
+        int lane_g = lane;
+        asm volatile("" : "+v"(lane_g));
         ragged_group_run<W, kClsRows>(
             D,
             [&](int bb, int idx) {
@@ -1027,7 +1203,7 @@ __global__ __launch_bounds__(64 * kClsWaves, OCC) void k_decode_ragged_cls(
                 const uint32_t hi = __builtin_amdgcn_readlane(pw, ((bb >> 5) + 1) & 7);
                 return ((((idx & 32) ? hi : lo) >> (idx & 31)) & 1u) != 0;
             },
-            base, status_out, T, L, kmax, lane, dm);
+            base, status_out, T, L, kmax, lane_g, dm);
         wave_sync();  // the LDS slice is rewritten by the next group
     }
 }
@@ -1205,7 +1381,7 @@ hipError_t launch_decode_ragged(const rsmi_group *groups, int64_t ngroups, uint8
                                 const uint8_t *gftab, hipStream_t s) {
     if (ngroups <= 0) return hipSuccess;
     kmax = kmax < 1 ? 1 : (kmax > 32 ? 32 : kmax);  // larger k: the workgroup kernel
-    const size_t lds = kTabBytes + (size_t)kWaves * rag_lds_bytes(kmax, kRows);
+    const size_t lds = kRagTabBytes + (size_t)kWaves * rag_lds_bytes(kmax, kRows);
     int64_t blocks = (ngroups + kWaves - 1) / kWaves;
     if (blocks > 256 * 8) blocks = 256 * 8;
     k_decode_ragged<<<(unsigned)blocks, 64 * kWaves, lds, s>>>(groups, ngroups, base, present_bits,
@@ -1214,6 +1390,12 @@ hipError_t launch_decode_ragged(const rsmi_group *groups, int64_t ngroups, uint8
     if (e != hipSuccess) return e;
     return launch_decode_ragged_big(groups, ngroups, base, present_bits, status, code_dir, ptab,
                                     gftab, s);
+}
+
+// tables | wave slices | records | present words | counter
+size_t cls_lds_bytes(int kmax, int maxb) {
+    kmax = kmax < 1 ? 1 : (kmax > 32 ? 32 : kmax);
+    return kRagTabBytes + (size_t)kClsWaves * rag_lds_bytes(kmax, kClsRows) + (size_t)maxb * 64 + 16;
 }
 
 int decode_cls_occupancy(int c) {
@@ -1230,8 +1412,7 @@ hipError_t launch_decode_ragged_cls(const rsmi_group *groups, const ClsLaunch &C
         const int nb = C.nw[c];
         if (nb <= 0) return hipSuccess;
         // tables | wave slices | records | present words | counter
-        const size_t lds = kTabBytes + (size_t)kClsWaves * rag_lds_bytes(kmax, kClsRows) +
-                           (size_t)C.maxb[c] * 64 + 16;
+        const size_t lds = cls_lds_bytes(kmax, C.maxb[c]);
         kern<<<(unsigned)nb, 64 * kClsWaves, lds, cs[c]>>>(C.rec, C.wst[c], nb, C.maxb[c], base,
                                                         present_bits, status, ptab, gftab, kmax,
                                                         DeferMark{C.defer, C.epoch});
@@ -1249,8 +1430,11 @@ hipError_t launch_decode_ragged_big(const rsmi_group *groups, int64_t ngroups, u
                                     const uint64_t *code_dir, const uint32_t *ptab,
                                     const uint8_t *gftab, hipStream_t s, const uint32_t *defer_word,
                                     uint32_t epoch) {
+    // one block per CU at most: when nothing was deferred (the usual case
+    // for plans) every block only reads the mark and leaves, and 1,024 of
+    // them cost 5 us of launch and drain per decode call (C3, rocprofv3)
     int64_t bb = (ngroups + 255) / 256;
-    if (bb > 256 * 4) bb = 256 * 4;
+    if (bb > 256) bb = 256;
     k_decode_ragged_big<<<(unsigned)bb, 256, kTabBytes + 512 + kBigAug, s>>>(
         groups, ngroups, base, present_bits, status, code_dir, ptab, gftab, defer_word, epoch);
     return hipGetLastError();

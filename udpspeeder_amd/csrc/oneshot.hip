@@ -118,7 +118,11 @@ __global__ __launch_bounds__(kOneThreads) void k_one_group(OneArgs a) {
             const int p = tid + q * kOneThreads;
             if (p < k * np) {
                 const int j = p / np, c = p - j * np;
-                v[q] = __builtin_amdgcn_raw_buffer_load_b128(in, (uint32_t)c * 16u, (uint32_t)sel[j] * ss, kAux);
+                // the shard offset differs per lane: it belongs in voffset
+                // (soffset must be wave-uniform, or the compiler wraps the
+                // load in a waterfall loop, one pass per distinct value)
+                v[q] = __builtin_amdgcn_raw_buffer_load_b128(in, (uint32_t)c * 16u + (uint32_t)sel[j] * ss, 0u,
+                                                             kAux);
             }
         }
         // coefficients while the loads fly

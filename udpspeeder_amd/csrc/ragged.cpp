@@ -39,6 +39,7 @@ int decode_ragged_dev(const rsmi_group *dg, int64_t ngroups, uint8_t *base,
 int decode_ragged_cls_dev(const rsmi_group *dg, int64_t ngroups, const ClsLaunch &C, uint8_t *base,
                           const uint32_t *present_bits, int32_t *status, int kmax, hipStream_t s);
 const uint32_t *device_ptab(int *rc);
+extern std::atomic<int> g_opt_cls_cap;  // RSMI_OPT_CLS_REC_CAP (api.cpp)
 }  // namespace rsmi
 
 struct rsmi_ragged_plan {
@@ -210,10 +211,26 @@ extern "C" int rsmi_ragged_plan_create(const rsmi_group *g, int64_t ngroups,
         for (int c = 0; c < 4; ++c) {
             auto &v = by[(size_t)c];
             const int W = c == 0 ? 1 : (c == 1 ? 2 : (c == 2 ? 4 : 5));
-            const int64_t slots = (int64_t)ncu * 4 * rsmi::decode_cls_occupancy(c);
+            const int occ = rsmi::decode_cls_occupancy(c);
+            const int64_t slots = (int64_t)ncu * 4 * occ;
             // one wave per group at least: blocks of kClsWaves waves
-            const int nb = (int)((std::min<int64_t>((int64_t)v.size(), slots) + rsmi::kClsWaves - 1) /
-                                 rsmi::kClsWaves);
+            int64_t nb64 = (std::min<int64_t>((int64_t)v.size(), slots) + rsmi::kClsWaves - 1) /
+                           rsmi::kClsWaves;
+            // A workgroup stages its records in LDS (64 B each): cap them so
+            // the class's occupancy holds (160 KiB of LDS per CU over occ
+            // workgroups of kClsWaves waves, never past the 64 KiB a workgroup
+            // may take).  Past the cap, more workgroups: the extra ones run
+            // in later rounds as earlier ones retire.
+            const size_t fixed = rsmi::cls_lds_bytes(kmax, 0);
+            const size_t budget = std::min<size_t>(163840 / (size_t)occ, 65536);
+            int64_t cap = budget > fixed + 64 * 16 ? (int64_t)((budget - fixed) / 64) : 16;
+            if (rsmi::g_opt_cls_cap.load() > 0) cap = rsmi::g_opt_cls_cap.load();
+            nb64 = std::max<int64_t>(nb64, ((int64_t)v.size() + cap - 1) / cap);
+            if (nb64 > 0x7FFFFFFF) {
+                delete P;
+                return fail(RSMI_ERR_INVALID, "ragged plan: too many decode workgroups");
+            }
+            const int nb = (int)nb64;
             P->cls.nw[c] = nb;  // workgroups
             P->cls.maxb[c] = 0;
             wst_first[c] = (int64_t)wst.size();
@@ -232,11 +249,15 @@ extern "C" int rsmi_ragged_plan_create(const rsmi_group *g, int64_t ngroups,
             auto gt = [](const std::pair<double, int> &a, const std::pair<double, int> &b) {
                 return a.first > b.first || (a.first == b.first && a.second > b.second);
             };
-            for (uint32_t i : v) {
+            for (uint32_t i : v) {  // nb * cap >= |v|: the heap never runs dry
                 std::pop_heap(heap.begin(), heap.end(), gt);
                 heap.back().first += cost(i);
-                lists[(size_t)heap.back().second].push_back(i);
-                std::push_heap(heap.begin(), heap.end(), gt);
+                auto &lst = lists[(size_t)heap.back().second];
+                lst.push_back(i);
+                if ((int64_t)lst.size() < cap)
+                    std::push_heap(heap.begin(), heap.end(), gt);
+                else
+                    heap.pop_back();  // full: no more records for this workgroup
             }
             for (int b = 0; b < nb; ++b) {
                 wst.push_back((uint32_t)(cls.size() / 8));

@@ -101,6 +101,7 @@ struct ClsLaunch {
 // The (k,n) code's parity rows on the current device (nullptr: not resident).
 const uint8_t *device_code_rows(int k, int n);
 int decode_cls_occupancy(int c);  // waves per SIMD class c's kernel is cut for
+size_t cls_lds_bytes(int kmax, int maxb);  // LDS of a class workgroup holding maxb records
 // Class c runs on cs[c]; the caller orders cs[] against s and then runs
 // launch_decode_ragged_big on s.
 hipError_t launch_decode_ragged_cls(const rsmi_group *groups, const ClsLaunch &L, uint8_t *base,
@@ -148,6 +149,10 @@ hipError_t launch_encode_bitslice_ragged_rtc(int k, int n, const rsmi_group *gro
                                              hipStream_t s);
 
 constexpr int kPtabDwords = 8;  // per coefficient: T0lo T0hi T1lo T1hi | T2 pad pad pad
+// The device GF table blob (gftab): exp[512] | log[256] | pad, then at
+// kGfLtabOff the ragged decode's Lagrange tables (decode.hip LTables image).
+constexpr int kGfLtabOff = 1024;
+constexpr int kGfLtabBytes = 5632;
 
 // ---- one group per call, latency path (oneshot.hip) ------------------------------
 constexpr int kOneAug = 16384;  // LDS bytes for [A | M] (e * (e + k)) or the encode coefficients

@@ -32,6 +32,13 @@ int fail(int code, const std::string &m) {
 
 int io_fail(const char *what) { return fail(RSMI_ERR_IO, std::string(what) + ": " + std::strerror(errno)); }
 
+// sendmmsg errors that belong to one datagram (its destination or its size),
+// after which the next datagram may still go out
+bool per_datagram_error(int en) {
+    return en == ECONNREFUSED || en == EMSGSIZE || en == EHOSTUNREACH || en == ENETUNREACH ||
+           en == EPERM || en == EACCES || en == EHOSTDOWN || en == ENETDOWN;
+}
+
 }  // namespace
 
 extern "C" {
@@ -165,10 +172,18 @@ int send_all(int fd, int32_t n, const int32_t *len, Addr addr, const rsmi_udp_ad
                     continue;
                 }
                 // msgs[done] failed on its own (ECONNREFUSED after an ICMP
-                // port-unreachable, EMSGSIZE, ...): drop that one datagram and
-                // go on, as the reference's per-packet sendto/send does
-                // (packet.cpp:143-162 logs and carries on)
-                if (!failed) err = errno;
+                // port-unreachable, EMSGSIZE, an unreachable or filtered
+                // destination): drop that one datagram and go on, as the
+                // reference's per-packet sendto/send does (packet.cpp:143-162
+                // logs and carries on).  Anything else is the socket's own
+                // failure (EBADF, ENOTSOCK, EFAULT, EDESTADDRREQ, EPIPE, ...):
+                // every later datagram would fail the same way, so stop now.
+                const int en = errno;
+                if (!per_datagram_error(en)) {
+                    errno = en;
+                    return io_fail("sendmmsg");
+                }
+                if (!failed) err = en;
                 ++failed;
                 ++done;
                 continue;

@@ -116,7 +116,17 @@ class FecEncoder:
         # the input must outlive the run, which may overlap the next plan
         self._keep = (in_buf, (self._keep or (None,))[0])
         self._last_packets = packets
+        self._last_nslots = ns.value
         return FencPlan(ns.value, smin.value, ret, packets, g)
+
+    def _check_slots(self, buf, slot_stride: int, what: str):
+        """The kernels write at slot * slot_stride (+ the packet or shard
+        offset) with no bound of their own: a buffer shorter than the last
+        plan's n_slots * slot_stride would be written past its end."""
+        need = getattr(self, "_last_nslots", 0) * int(slot_stride)
+        if buf.numel() < need:
+            raise ValueError(f"{what} holds {buf.numel()} bytes; the last plan needs "
+                             f"n_slots * slot_stride = {need}")
 
     def plan_host(self, lens, offsets) -> FencPlan:
         """Plan only (no device): decisions, packet list and groups for a batch
@@ -128,6 +138,7 @@ class FecEncoder:
         >= n_slots * slot_stride bytes); asynchronous on `stream`."""
         import torch
         s = stream if stream is not None else torch.cuda.current_stream()
+        self._check_slots(slots, slot_stride, "slots")
         check(lib().rsmi_fenc_run_dev(self._h, slots.data_ptr() if slots.numel() else None,
                                       int(slot_stride), s.cuda_stream), "rsmi_fenc_run_dev")
 
@@ -144,9 +155,14 @@ class FecEncoder:
         npk = len(self._last_packets) if getattr(self, "_last_packets", None) is not None else None
         if out_len is None:
             out_len = torch.empty(max(npk or 0, 1), dtype=torch.int32, device="cuda")
+        elif out_len.dtype != torch.int32 or not out_len.is_cuda or out_len.numel() < (npk or 0):
+            raise ValueError(f"out_len must be an int32 CUDA tensor of >= {npk} entries "
+                             "(one per planned packet)")
+        self._check_slots(slots, slot_stride, "slots")
         if out is not None:
             if out.dtype != torch.uint8 or not (out.is_cuda or out.is_pinned()) or out.data_ptr() % 16:
                 raise TypeError("out must be a 16-aligned CUDA or pinned uint8 tensor")
+            self._check_slots(out, slot_stride, "out")
         check(lib().rsmi_fenc_run_cooked_dev(self._h, slots.data_ptr() if slots.numel() else None,
                                              int(slot_stride), cook._h, C.c_uint64(seed & (2**64 - 1)),
                                              out.data_ptr() if out is not None else None,

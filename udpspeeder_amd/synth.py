@@ -74,6 +74,40 @@ def ragged_erasures(seed: int, g0: int, ns, ms, emax: int = 5) -> np.ndarray:
     return pres
 
 
+HASH_SEED = 0xC4C4D16E57
+
+
+def hash_weights(nbytes: int) -> np.ndarray:
+    """Odd uint64 weights of the per-group checksum: w_j = mix(HASH_SEED +
+    (j + 1) * GAMMA) | 1 for byte j of a group's rows (row-major)."""
+    with np.errstate(over="ignore"):
+        j = np.arange(1, nbytes + 1, dtype=np.uint64) * GAMMA
+        return _mix(np.uint64(HASH_SEED) + j) | np.uint64(1)
+
+
+def group_hashes_dev(rows, chunk: int = 4096) -> np.ndarray:
+    """Per-group checksum of a [G, R, L] uint8 tensor (any device, any
+    strides): h_g = sum_j w_j * byte_j mod 2^64 over the group's R*L bytes.
+    Every single-byte change moves h_g (odd weights); the digest of a range is
+    sha256 over its h_g (``hashes_digest``).  The golden side restates it in
+    numpy (oracle/cpu.py ``group_hashes``) from the reference's own bytes, so a
+    rank checks its whole slice after the timed region by moving 8 B per group
+    off the device instead of the slice itself."""
+    import torch
+    G, R, L = rows.shape
+    w = torch.from_numpy(hash_weights(R * L).view(np.int64)).to(rows.device)
+    out = torch.empty(G, dtype=torch.int64, device=rows.device)
+    for c in range(0, G, chunk):
+        b = rows[c:c + chunk].reshape(-1, R * L).to(torch.int64)
+        out[c:c + chunk] = (b * w).sum(dim=1)  # int64 arithmetic wraps mod 2^64
+    return out.cpu().numpy().view(np.uint64)
+
+
+def hashes_digest(h) -> str:
+    import hashlib
+    return hashlib.sha256(np.ascontiguousarray(h, dtype="<u8").tobytes()).hexdigest()
+
+
 def present_bits(flags) -> np.ndarray:
     """[ng, <=256] present flags -> the ragged decode's [ng, 8] uint32 masks
     (bit j % 32 of word j / 32 = shard j received)."""
