@@ -371,7 +371,9 @@ int decode_ragged_cls_dev(const rsmi_group *dg, int64_t ngroups, const ClsLaunch
     const hipStream_t cs[4] = {s, s, s, s};
     hipError_t e = launch_decode_ragged_cls(dg, C, base, present_bits, status, kmax, D->code_dir,
                                             D->ptab, D->gftab, s, cs);
-    if (e == hipSuccess)
+    // the plan knows whether any group can be deferred (e never defers: the
+    // class kernels take any e in row blocks); without one, no big launch
+    if (e == hipSuccess && C.need_big)
         e = launch_decode_ragged_big(dg, ngroups, base, present_bits, status, D->code_dir, D->ptab,
                                      D->gftab, s, C.defer, C.epoch);
     if (e != hipSuccess) return hip_fail(e, "ragged decode launch");

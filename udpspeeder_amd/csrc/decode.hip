@@ -77,7 +77,7 @@ constexpr int kTile = 1280;    // bytes per lane-tile pass (64 x 16 + 64 x 4)
 #define DEC_RAG_RING4 2  // ragged kernels: survivors in flight for 16-byte lane pieces
 #endif
 #ifndef DEC_RAG_RING5
-#define DEC_RAG_RING5 3  // ... and for 20-byte pieces (W = 4: ring 2 at 8 waves/SIMD, W = 5: 3 at 6, beat 4 at 6 / 5: profiles/r03/c3)
+#define DEC_RAG_RING5 2  // ... and for 20-byte pieces (round 4: 2 at 7 waves/SIMD in the merged class launch, 0.139-0.142 vs 0.1425 ms for 3 at 6)
 #endif
 #ifndef DEC_RAG_UNCOND_W
 #define DEC_RAG_UNCOND_W 4  // ragged kernels: unconditional ring refills for tile widths >= this
@@ -178,9 +178,6 @@ __device__ __forceinline__ uint32_t gmul(const uint8_t *lexp, const uint8_t *llo
 // its log (tl01 / tl2 below), so no exp step and no pivot chain: a handful of
 // independent lookups in place of e dependent elimination steps.  Every
 // coefficient is nonzero (distinct points), so every one has a log.
-#ifndef DEC_LAGRANGE
-#define DEC_LAGRANGE 1         // ragged kernels: Lagrange coefficients (0: Gauss-Jordan)
-#endif
 constexpr int kLTabBytes = 5632;  // tl01[255] (4096) | tl2[255] (1024) | px[256] | lz[256]
 
 struct LTables {
@@ -231,8 +228,8 @@ __host__ __device__ inline int wave_lds_bytes(int k) {
     return 512 + aug_bytes(k) + k * kRows * 32;
 }
 
-// Ragged kernels' slice: sel[64] miss[64] t01[k*rows] t2[k*rows] (k <= 32,
-// e <= rows: the register Gauss-Jordan always applies, no aug matrix).
+// Ragged kernels' slice: sel[64] miss[64] t01[k*rows] t2[k*rows] (k <= 32;
+// the split tables of one block of `rows` missing rows at a time).
 __host__ __device__ inline int rag_lds_bytes(int k, int rows) { return 128 + k * rows * 20; }
 
 __device__ __forceinline__ WaveLds rag_slice(uint8_t *wl, int k, int rows) {
@@ -273,82 +270,10 @@ __device__ __forceinline__ int select_survivors(int k, int n, Flag flag, const W
     return __builtin_amdgcn_readfirstlane(cnt);
 }
 
-// ---- 3. Gauss-Jordan ------------------------------------------------------------
-// Register form: lane c holds column c of [A | M], W = e + k <= 64: a missing
-// data index (c < e) or survivor c - e.  cv[r] is the code's parity row R_r
-// (survivor k - e + r) at column col, loaded by the caller before the first
-// survivor loads; rows >= e are don't-care.
-// Fraction-free elimination: pivot step p sets a[r] = piv * a[r] ^ f_r * a[p]
-// for every other row (f_r = a[r] at column p), with two split tables, both
-// one LDS level deep: the pivot's (uniform) and lane c's own a[p] (per lane,
-// multiplied by the scalar f_r as selector).  Every row is divided by its
-// diagonal at the end through log/exp (two per-lane levels for all rows).  The
-// dividing form chained pivot -> inverse -> table -> one row at a time.
-// Leaves coef[r][j] expanded into its split table at (t01, t2)[j * rows + r];
-// NR >= e is the number of row registers.
-template <int NR>
-__device__ __forceinline__ int gauss_jordan_regs(int k, int e, uint32_t col, const uint32_t (&cv)[NR],
-                                                 const uint32_t (&R)[NR], const WaveLds &L,
-                                                 const Tables &T, int lane) {
-    int st = RSMI_DEC_OK;
-    const int W = e + k;
-    uint32_t a[NR];
-#pragma unroll
-    for (int r = 0; r < NR; ++r) {
-        const uint32_t v = (lane >= e && col >= (uint32_t)k) ? (uint32_t)(col == R[r]) : cv[r];
-        a[r] = r < e ? v : 0u;
-    }
-#pragma unroll
-    for (int p = 0; p < NR; ++p) {
-        if (p < e) {
-            const uint32_t piv = __builtin_amdgcn_readlane(a[p], p);
-            if (piv == 0) {
-                st = RSMI_DEC_SINGULAR;
-                break;
-            }
-            const uint32_t ap = a[p];
-            const uint4 tp = T.s01[piv], tl = T.s01[ap];
-            const uint32_t tp2 = T.s2[piv], tl2 = T.s2[ap];
-#pragma unroll
-            for (int r = 0; r < NR; ++r) {
-                if (r < e && r != p) {
-                    const uint32_t f = __builtin_amdgcn_readlane(a[r], p);
-                    a[r] = gmul_t(tp, tp2, a[r]) ^ gmul_t(tl, tl2, f);
-                }
-            }
-        }
-    }
-    st = __builtin_amdgcn_readfirstlane(st);
-    if (st != RSMI_DEC_OK) return st;
-    // [D | D coef] -> [I | coef]: a[r] *= d_r^-1 as exp[log a + 255 - log d_r]
-#pragma unroll
-    for (int r = 0; r < NR; ++r) {
-        if (r < e) {
-            const uint32_t d = __builtin_amdgcn_readlane(a[r], r);
-            const uint32_t li = 255u - (uint32_t)__builtin_amdgcn_readfirstlane(T.llog[d]);
-            const uint32_t x = a[r];
-            a[r] = x ? (uint32_t)T.lexp[T.llog[x] + li] : 0u;
-        }
-    }
-    // coef[r][j] sits in lane e + j: expand into its split table
-    if (lane >= e && lane < W) {
-        const int base = (lane - e) * L.rows;
-#pragma unroll
-        for (int r = 0; r < NR; ++r) {
-            if (r < e) {
-                L.t01[base + r] = T.s01[a[r]];
-                L.t2[base + r] = T.s2[a[r]];
-            }
-        }
-    }
-    wave_sync();
-    return RSMI_DEC_OK;
-}
-
 // Lagrange coefficients (see LTables above) for k <= 64 survivors, e <= NR
 // missing data rows: lane s < k holds survivor s's shard index in sel_lane,
 // lane d < e missing row d's in miss_lane.  Leaves coef[r][j]'s split table at
-// (t01, t2)[j * rows + r], as gauss_jordan_regs does.
+// (t01, t2)[j * rows + r], where Rebuild reads them.
 template <int NR>
 __device__ __forceinline__ void lagrange_coefs(int k, int e, uint32_t sel_lane, uint32_t miss_lane,
                                                const WaveLds &L, const LTables &T, int lane) {
@@ -487,12 +412,14 @@ struct Rebuild {
 #pragma unroll
         for (int q = 0; q < R; ++q) load(q, q);
     }
-    // passes over (tile, block of kPass rows); tile 0's first loads were
-    // issued by start_tile(0) before the coefficients
-    __device__ __forceinline__ void run(const WaveLds &L, int lane) {
+    // Rows [rb0, rb0 + nrows) (their coefficients at table rows 0..nrows-1),
+    // in passes over (tile, block of kPass rows); the first pass's loads were
+    // issued by start_tile(0) before the coefficients.
+    __device__ __forceinline__ void run(const WaveLds &L, int lane, int rb0, int nrows) {
+        const int rend = rb0 + nrows;
         for (int toff = 0; toff < len; toff += TileIO<W>::kBytes) {
-            for (int rb = 0; rb < e; rb += kPass) {
-                if (toff || rb) start_tile(toff, lane);
+            for (int rb = rb0; rb < rend; rb += kPass) {
+                if (toff || rb != rb0) start_tile(toff, lane);
                 uint32_t acc[kPass][W];
 #pragma unroll
                 for (int r = 0; r < kPass; ++r)
@@ -520,9 +447,9 @@ struct Rebuild {
                         // ring slot q took survivor j: load survivor j + R into it
                         load(q, j + R);
                         if (j < k) {
-                            const uint4 *ta = L.t01 + (z + j * L.rows + rb);
-                            const uint32_t *ta2 = L.t2 + (z + j * L.rows + rb);
-                            int nr = e - rb;  // opaque SGPR: see k_decode_fused's row guards
+                            const uint4 *ta = L.t01 + (z + j * L.rows + (rb - rb0));
+                            const uint32_t *ta2 = L.t2 + (z + j * L.rows + (rb - rb0));
+                            int nr = rend - rb;  // opaque SGPR: see k_decode_fused's row guards
                             asm volatile("" : "+s"(nr));
 #pragma unroll
                             for (int r = 0; r < kPass; ++r) {
@@ -541,7 +468,7 @@ struct Rebuild {
                 }
 #pragma unroll
                 for (int r = 0; r < kPass; ++r)
-                    if (rb + r < e) io.store(rsrc, __builtin_amdgcn_readlane(mo_lane, rb + r), acc[r]);
+                    if (rb + r < rend) io.store(rsrc, __builtin_amdgcn_readlane(mo_lane, rb + r), acc[r]);
             }
         }
     }
@@ -923,22 +850,17 @@ __global__ __launch_bounds__(256, DEC_OCC) void k_decode_fused(UniformArgs a, co
 #define DEC_CLS_OCC4 8
 #endif
 #ifndef DEC_CLS_OCC5
-#define DEC_CLS_OCC5 6
+#define DEC_CLS_OCC5 7
 #endif
 constexpr int kClsRows = 5;  // class kernels: e <= 5 in registers, more is deferred
-#if DEC_LAGRANGE
+#ifndef DEC_MIX
+#define DEC_MIX 2  // class launches: 0 one per class, 1 W = 5 alone + the others in one, 2 all in one
+#endif
 using RagTables = LTables;
 constexpr int kRagTabBytes = kLTabBytes;
 __device__ __forceinline__ RagTables load_rag_tables(uint8_t *smem, const uint32_t *ptab, const uint8_t *gftab) {
     return load_ltables(smem, ptab, gftab);
 }
-#else
-using RagTables = Tables;
-constexpr int kRagTabBytes = kTabBytes;
-__device__ __forceinline__ RagTables load_rag_tables(uint8_t *smem, const uint32_t *ptab, const uint8_t *gftab) {
-    return load_tables(smem, ptab, gftab);
-}
-#endif
 
 // One group's wave-uniform description.
 struct GroupDesc {
@@ -966,12 +888,16 @@ struct NoHook {
 
 // after_select() runs once, right after the survivor selection (the class
 // kernels fetch the next group's present words there).
+// Rows rb0 .. rb0 + NR - 1 of the group's missing data rows (the slice holds
+// split tables for NR rows; Lagrange coefficients need no elimination, so a
+// group with e > NR is never deferred: the caller runs it again with rb0 + NR
+// while this returns true, and the status is written by the last call).
 template <int WC, int NR, class Flag, class Hook = NoHook>
-__device__ __forceinline__ void ragged_group_run(const GroupDesc &D, Flag flag, uint8_t *base,
+__device__ __forceinline__ bool ragged_group_run(const GroupDesc &D, Flag flag, uint8_t *base,
                                                  int32_t *status_out, const RagTables &T,
                                                  const WaveLds &L, int kmax, int lane,
                                                  DeferMark dm = DeferMark{nullptr, 0},
-                                                 Hook after_select = Hook{}) {
+                                                 Hook after_select = Hook{}, int rb0 = 0) {
     const int64_t g = D.g;
     const int k = D.k, n = D.n, len = D.len;
     const uint32_t ss = D.ss;
@@ -980,7 +906,7 @@ __device__ __forceinline__ void ragged_group_run(const GroupDesc &D, Flag flag, 
     if (k < 1 || n < k || n > 256 || (n > k && !rows)) {
         after_select();
         if (lane == 0) status_out[g] = RSMI_DEC_UNSUPPORTED;
-        return;
+        return false;
     }
 #if DEC_TRACE
     const uint64_t tr0 = trace_now();
@@ -994,40 +920,17 @@ __device__ __forceinline__ void ragged_group_run(const GroupDesc &D, Flag flag, 
 #endif
     if (cnt < k || e == 0) {
         if (lane == 0) status_out[g] = cnt < k ? RSMI_DEC_TOO_FEW : RSMI_DEC_OK;
-        return;
+        return false;
     }
-    if (e > NR || k > kmax || (uint64_t)n * ss >= 0x80000000ull) {
+    if (k > kmax || (uint64_t)n * ss >= 0x80000000ull) {
         if (lane == 0) {
             status_out[g] = kDefer;
             if (dm.word) atomicMax(dm.word, dm.epoch);
         }
-        return;
+        return false;
     }
     const int lpad = rag_lpad((uint32_t)len, ss);
     const uint32_t sel_lane = lane < k ? (uint32_t)L.sel[lane] : 0u;
-#if DEC_LAGRANGE
-    const uint32_t miss_lane = lane < e ? (uint32_t)L.miss[lane] : 0u;
-#else
-    // The system's code-row bytes (lane c: column c of rows R_0..R_{NR-1}, R_r
-    // = survivor k - e + r, clamped for r >= e), as buffer loads issued before
-    // the first survivor loads: waiting for them is vmcnt(survivor loads), not
-    // 0.  (Through a generic pointer they were flat loads, each followed by a
-    // full vmcnt(0) lgkmcnt(0) wait that also waited for the survivor ring.)
-    const uint32_t col = lane < e ? (uint32_t)L.miss[lane]
-                                  : (lane < e + k ? (uint32_t)L.sel[lane - e] : 0u);
-    uint32_t cv[NR], Rr[NR];
-    {
-        const __amdgpu_buffer_rsrc_t rr = group_rsrc(rows, (uint32_t)((n - k) * k));
-        const uint32_t cc = col < (uint32_t)k ? col : 0u;
-#pragma unroll
-        for (int r = 0; r < NR; ++r) {
-            const int ri = k - e + r < k ? k - e + r : k - 1;
-            Rr[r] = __builtin_amdgcn_readlane(sel_lane, ri);
-            const uint32_t ro = Rr[r] >= (uint32_t)k ? (Rr[r] - (uint32_t)k) * (uint32_t)k : 0u;
-            cv[r] = __builtin_amdgcn_raw_buffer_load_b8(rr, ro + cc, 0, 0);
-        }
-    }
-#endif
     auto rebuild = [&](auto wc) {
         constexpr int W = decltype(wc)::value;
         Rebuild<W> B;
@@ -1037,19 +940,18 @@ __device__ __forceinline__ void ragged_group_run(const GroupDesc &D, Flag flag, 
         B.e = e;
         B.len = len;
         B.lpad = lpad;
+        // rows rb0 .. rb0 + nb0 - 1 of the e missing ones (lane d: row rb0 + d)
+        const uint32_t miss_lane = lane + rb0 < e ? (uint32_t)L.miss[lane + rb0] : 0u;
         B.so_lane = sel_lane * ss;
-        B.mo_lane = (lane < e ? (uint32_t)L.miss[lane] : 0u) * ss;
+        B.mo_lane = miss_lane * ss;
+        const int nb0 = e - rb0 < NR ? e - rb0 : NR;
         if (len > 0) B.start_tile(0, lane);  // the first survivors fly while the coefficients form
-#if DEC_LAGRANGE
-        lagrange_coefs<NR>(k, e, sel_lane, miss_lane, L, T, lane);
-        const int st = RSMI_DEC_OK;  // distinct points: never singular
-#else
-        const int st = gauss_jordan_regs<NR>(k, e, col, cv, Rr, L, T, lane);
-#endif
+        lagrange_coefs<NR>(k, nb0, sel_lane, miss_lane, L, T, lane);  // distinct points: never singular
 #if DEC_TRACE
         const uint64_t tr2 = trace_now();
 #endif
-        if (st == RSMI_DEC_OK && len > 0) B.run(L, lane);
+        if (len > 0) B.run(L, lane, 0, nb0);
+        const int st = RSMI_DEC_OK;
 #if DEC_TRACE
         const uint64_t tr3 = trace_now();
         if (lane == 0 && g_dec_trace) {
@@ -1070,7 +972,9 @@ __device__ __forceinline__ void ragged_group_run(const GroupDesc &D, Flag flag, 
         else if (w == 4) st = rebuild(std::integral_constant<int, 4>{});
         else st = rebuild(std::integral_constant<int, 5>{});
     }
+    if (rb0 + NR < e) return true;  // more rows: the status waits for the last block
     if (lane == 0) status_out[g] = st;
+    return false;
 }
 
 // One group from its rsmi_group descriptor (scalar loads) and the code
@@ -1091,15 +995,19 @@ __device__ __forceinline__ void ragged_group(int64_t g, const rsmi_group &d, uin
     D.rows = (D.k >= 1 && D.n > D.k && D.n <= 256)
                  ? reinterpret_cast<const uint8_t *>(code_dir[D.k * 257 + D.n])
                  : nullptr;
-    ragged_group_run<WC, NR>(
-        D,
-        [&](int b, int idx) {
-            // words b/32 and b/32 + 1 cover shards b..b+63 (readlane ignores exec)
-            const uint32_t lo = __builtin_amdgcn_readlane(w8, (b >> 5) & 7);
-            const uint32_t hi = __builtin_amdgcn_readlane(w8, ((b >> 5) + 1) & 7);
-            return ((((idx & 32) ? hi : lo) >> (idx & 31)) & 1u) != 0;
-        },
-        base, status_out, T, L, kmax, lane);
+    for (int rb0 = 0;; rb0 += NR) {
+        const bool more = ragged_group_run<WC, NR>(
+            D,
+            [&](int b, int idx) {
+                // words b/32 and b/32 + 1 cover shards b..b+63 (readlane ignores exec)
+                const uint32_t lo = __builtin_amdgcn_readlane(w8, (b >> 5) & 7);
+                const uint32_t hi = __builtin_amdgcn_readlane(w8, ((b >> 5) + 1) & 7);
+                return ((((idx & 32) ? hi : lo) >> (idx & 31)) & 1u) != 0;
+            },
+            base, status_out, T, L, kmax, lane, DeferMark{nullptr, 0}, NoHook{}, rb0);
+        wave_sync();  // the LDS slice is rewritten by the next block or group
+        if (!more) break;
+    }
 }
 
 // Every group of the batch, tile width chosen per group (rsmi_decode_ragged_dev:
@@ -1137,18 +1045,17 @@ __global__ __launch_bounds__(256, DEC_RAG_OCC) void k_decode_ragged(
 // and the block's waves take groups from an LDS counter, so a wave whose
 // groups lost many data shards (long eliminations and multiplies: costs the
 // plan cannot see) does not hold the round up while its neighbours idle.
-template <int W, int OCC>
-__global__ __launch_bounds__(64 * kClsWaves, OCC) void k_decode_ragged_cls(
-    const uint32_t *__restrict__ rec, const uint32_t *__restrict__ wst, int nb, int maxb, uint8_t *base,
-    const uint32_t *__restrict__ present, int32_t *status_out, const uint32_t *ptab,
-    const uint8_t *gftab, int kmax, DeferMark dm) {
+// One class workgroup: its cnt records at rec[i0 ..) (and their present
+// words) staged in LDS, its waves taking groups from an LDS counter.
+template <int W>
+__device__ __forceinline__ void cls_block(const uint32_t *__restrict__ rec, uint32_t i0, uint32_t cnt,
+                                          int maxb, uint8_t *base, const uint32_t *__restrict__ present,
+                                          int32_t *status_out, const uint32_t *ptab, const uint8_t *gftab,
+                                          int kmax, DeferMark dm, int b) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
 #if DEC_TRACE
     const uint64_t tk0 = trace_now();
 #endif
-    const int b = blockIdx.x;
-    if (b >= nb) return;  // (whole block: before any barrier)
-    const uint32_t i0 = wst[b], cnt = wst[b + 1] - i0;
     uint32_t *srec = reinterpret_cast<uint32_t *>(smem + kRagTabBytes + kClsWaves * rag_lds_bytes(kmax, kClsRows));
     uint32_t *spw = srec + (size_t)maxb * 8;
     uint32_t *next = spw + (size_t)maxb * 8;
@@ -1165,6 +1072,8 @@ __global__ __launch_bounds__(64 * kClsWaves, OCC) void k_decode_ragged_cls(
 #if DEC_TRACE
     const uint64_t tk1 = trace_now();
     const int w = b * kClsWaves + wid;
+#else
+    (void)b;
 #endif
     for (;;) {
         uint32_t i = 0;
@@ -1194,18 +1103,61 @@ __global__ __launch_bounds__(64 * kClsWaves, OCC) void k_decode_ragged_cls(
 #endif
         // lane-derived values (LDS row addresses) are recomputed per group:
         // hoisted out of the loop they stay live across it and spill
-        int lane_g = lane;
-        asm volatile("" : "+v"(lane_g));
-        ragged_group_run<W, kClsRows>(
-            D,
-            [&](int bb, int idx) {
-                const uint32_t lo = __builtin_amdgcn_readlane(pw, (bb >> 5) & 7);
-                const uint32_t hi = __builtin_amdgcn_readlane(pw, ((bb >> 5) + 1) & 7);
-                return ((((idx & 32) ? hi : lo) >> (idx & 31)) & 1u) != 0;
-            },
-            base, status_out, T, L, kmax, lane_g, dm);
-        wave_sync();  // the LDS slice is rewritten by the next group
+        for (int rb0 = 0;; rb0 += kClsRows) {  // blocks of kClsRows missing rows
+            int lane_g = lane;
+            asm volatile("" : "+v"(lane_g));
+            const bool more = ragged_group_run<W, kClsRows>(
+                D,
+                [&](int bb, int idx) {
+                    const uint32_t lo = __builtin_amdgcn_readlane(pw, (bb >> 5) & 7);
+                    const uint32_t hi = __builtin_amdgcn_readlane(pw, ((bb >> 5) + 1) & 7);
+                    return ((((idx & 32) ? hi : lo) >> (idx & 31)) & 1u) != 0;
+                },
+                base, status_out, T, L, kmax, lane_g, dm, NoHook{}, rb0);
+            wave_sync();  // the LDS slice is rewritten by the next block or group
+            if (!more) break;
+        }
     }
+}
+
+template <int W, int OCC>
+__global__ __launch_bounds__(64 * kClsWaves, OCC) void k_decode_ragged_cls(
+    const uint32_t *__restrict__ rec, const uint32_t *__restrict__ wst, int nb, int maxb, uint8_t *base,
+    const uint32_t *__restrict__ present, int32_t *status_out, const uint32_t *ptab,
+    const uint8_t *gftab, int kmax, DeferMark dm) {
+    const int b = blockIdx.x;
+    if (b >= nb) return;  // (whole block: before any barrier)
+    cls_block<W>(rec, wst[b], wst[b + 1] - wst[b], maxb, base, present, status_out, ptab, gftab, kmax, dm, b);
+}
+
+// Several classes in one launch (DEC_MIX): the grid is the classes' workgroups
+// back to back, widest class first, so the short narrow-tile groups fill the
+// tail the long wide-tile groups leave instead of each class paying its own
+// ramp and drain.  CMASK: bit c = class c included (0: W = 1 ... 3: W = 5).
+struct MixGrid {
+    const uint32_t *wst[4];
+    int nb[4];
+};
+template <int OCC, int CMASK>
+__global__ __launch_bounds__(64 * kClsWaves, OCC) void k_decode_ragged_mix(
+    const uint32_t *__restrict__ rec, MixGrid M, int maxb, uint8_t *base,
+    const uint32_t *__restrict__ present, int32_t *status_out, const uint32_t *ptab,
+    const uint8_t *gftab, int kmax, DeferMark dm) {
+    int b = blockIdx.x;
+#define RSMI_MIX_CLASS(c, W)                                                                        \
+    if (CMASK & (1 << c)) {                                                                         \
+        if (b < M.nb[c]) {                                                                          \
+            cls_block<W>(rec, M.wst[c][b], M.wst[c][b + 1] - M.wst[c][b], maxb, base, present,      \
+                         status_out, ptab, gftab, kmax, dm, b);                                     \
+            return;                                                                                 \
+        }                                                                                           \
+        b -= M.nb[c];                                                                               \
+    }
+    RSMI_MIX_CLASS(3, 5)
+    RSMI_MIX_CLASS(2, 4)
+    RSMI_MIX_CLASS(1, 2)
+    RSMI_MIX_CLASS(0, 1)
+#undef RSMI_MIX_CLASS
 }
 
 // The deferred groups: one 256-thread workgroup per group.  Gauss-Jordan on
@@ -1418,7 +1370,25 @@ hipError_t launch_decode_ragged_cls(const rsmi_group *groups, const ClsLaunch &C
                                                         DeferMark{C.defer, C.epoch});
         return hipGetLastError();
     };
-    hipError_t e = launch(k_decode_ragged_cls<5, DEC_CLS_OCC5>, 3);
+    // classes in one launch: CMASK's classes, OCC waves per SIMD
+    auto mix = [&](auto kern, int cmask) {
+        MixGrid M{};
+        int nb = 0, maxb = 0;
+        for (int c = 0; c < 4; ++c) {
+            M.wst[c] = C.wst[c];
+            M.nb[c] = (cmask >> c) & 1 ? C.nw[c] : 0;
+            nb += M.nb[c];
+            if (M.nb[c] > 0) maxb = maxb > C.maxb[c] ? maxb : C.maxb[c];
+        }
+        if (nb <= 0) return hipSuccess;
+        kern<<<(unsigned)nb, 64 * kClsWaves, cls_lds_bytes(kmax, maxb), cs[3]>>>(
+            C.rec, M, maxb, base, present_bits, status, ptab, gftab, kmax, DeferMark{C.defer, C.epoch});
+        return hipGetLastError();
+    };
+    hipError_t e = hipSuccess;
+    if (DEC_MIX == 2) return mix(k_decode_ragged_mix<DEC_CLS_OCC5, 15>, 15);
+    e = launch(k_decode_ragged_cls<5, DEC_CLS_OCC5>, 3);
+    if (DEC_MIX == 1) return e == hipSuccess ? mix(k_decode_ragged_mix<DEC_CLS_OCC4, 7>, 7) : e;
     if (e == hipSuccess) e = launch(k_decode_ragged_cls<4, DEC_CLS_OCC4>, 2);
     if (e == hipSuccess) e = launch(k_decode_ragged_cls<2, DEC_CLS_OCC2>, 1);
     if (e == hipSuccess) e = launch(k_decode_ragged_cls<1, DEC_CLS_OCC1>, 0);

@@ -82,6 +82,7 @@ extern "C" int rsmi_ragged_plan_create(const rsmi_group *g, int64_t ngroups,
     *out = nullptr;
     uint64_t extent = 0;
     int kmax = 1;
+    bool need_big = false;
     bool bs = ngroups < (int64_t(1) << 20);
     std::vector<int> code_of((size_t)ngroups, -1);
     std::vector<uint8_t> seen(257 * 257, 0);
@@ -100,6 +101,8 @@ extern "C" int rsmi_ragged_plan_create(const rsmi_group *g, int64_t ngroups,
             if (rc) return rc;
         }
         if (d.n == d.k || d.len == 0) continue;  // nothing to compute
+        // the class decode kernels defer these to the workgroup kernel
+        if (d.k > 32 || (uint64_t)d.n * d.shard_stride >= 0x80000000ull) need_big = true;
         const uint64_t end = d.offset + (uint64_t)(d.n - 1) * d.shard_stride +
                              ((d.len + 15u) & ~15u);
         extent = std::max(extent, end);
@@ -134,6 +137,7 @@ extern "C" int rsmi_ragged_plan_create(const rsmi_group *g, int64_t ngroups,
     P->ngroups = ngroups;
     P->kmax = kmax;
     P->bitslice = bs;
+    P->cls.need_big = need_big ? 1 : 0;
     P->bytes = (uint32_t)std::min<uint64_t>(extent, 0x7FFFFFFFull);
     std::vector<uint32_t> colmap, waves;
     if (bs) {

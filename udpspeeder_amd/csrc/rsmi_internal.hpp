@@ -97,6 +97,8 @@ struct ClsLaunch {
     int maxb[4];             // most records one workgroup of class c holds
     uint32_t *defer;         // device word: set to epoch when a group is left for the big kernel
     uint32_t epoch;          // this call's mark (plans count calls)
+    int need_big;            // the plan holds groups the class kernels defer (k > 32, or
+                             // slots spanning >= 2 GiB): launch the big kernel after them
 };
 // The (k,n) code's parity rows on the current device (nullptr: not resident).
 const uint8_t *device_code_rows(int k, int n);
