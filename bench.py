@@ -389,6 +389,7 @@ def extra_configs(u, synth, torch, dev, buf, G):
     out["rtc_f10_5_encode"] = rtc_config(u, synth, torch, dev)
     out["f2_cook_decook"] = cook_config(torch, dev, buf, G)
     out["f1_f2_frame_encode_cook"] = frame_cook_config(torch, dev)
+    out["f1_collector_200_connections"] = collector_config(torch, dev)
     out["dropin_latency_us"] = dropin_latency_both(u)
     return out
 
@@ -568,6 +569,85 @@ def frame_cook_config(torch, dev, groups=65536, reps=4):
             "cooked_packets_per_s": round(nout / (t * 1e-3), 1),
             "what": "rsmi_fenc_run_cooked_dev: plan upload + k_frame + k_bs_20_30 + carry + k_cook, "
                     "device-resident, key on, device-drawn IVs", "lengths_ok": ok}
+
+
+def collector_config(torch, dev, ncon=200, flushes=12, seed=5):
+    """The cross-connection collector (rsmi_fenc_run_many): 200 connections
+    (max_conn_num, common.h:112), each with its own fec_encode_manager_t
+    (-f 20:10, mode 0, mtu 1250; connection.h:244-245), each flushing 64-256
+    datagrams of 64-1200 B per 8 ms timer tick (fec_manager.h:30, the timer's
+    input(0, 0) included).  One flush = plan every manager on the host, then
+    the byte work: framing + encode + do_cook into device memory, either as
+    ONE collector launch set or as 200 rsmi_fenc_run_cooked_dev calls.
+    Reports the GPU time of the run part (HIP events, per flush, median) and
+    the wall time of the whole flush including the host planning."""
+    import numpy as np
+    from udpspeeder_amd.cook import CookContext
+    from udpspeeder_amd.fec import FecCollector, FecEncoder
+    rng = np.random.default_rng(seed)
+    ctx = CookContext(b"bench-key")
+    res = {}
+    for mode in ("collector", "per_connection"):
+        encs = [FecEncoder("20:10", 0, 1250, 200, seq0=i * 7919) for i in range(ncon)]
+        col = FecCollector() if mode == "collector" else None
+        S = FecEncoder.slot_stride_for(1250)
+        slots = out = None
+        gpu_ms, wall_ms, npk_tot, nev_tot = [], [], 0, 0
+        r2 = np.random.default_rng(seed)  # the same traffic for both modes
+        for f in range(flushes):
+            nper = r2.integers(64, 257, ncon)
+            lens = [np.concatenate([r2.integers(64, 1201, n), [-1]]).astype(np.int32) for n in nper]
+            tot = int(sum(int(np.maximum(l, 0).sum()) for l in lens))
+            inbuf = torch.randint(0, 256, (tot + 64,), dtype=torch.uint8, device=dev)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            o, plans = 0, []
+            for ci in range(ncon):
+                l = lens[ci]
+                offs = np.concatenate([[0], np.cumsum(np.maximum(l, 0))[:-1]]).astype(np.uint64) + np.uint64(o)
+                o += int(np.maximum(l, 0).sum())
+                plans.append(encs[ci].plan(l, offs, inbuf))
+            nsl = sum(p.n_slots for p in plans)
+            npk = sum(len(p.packets) for p in plans)
+            if slots is None or slots.numel() < nsl * S:
+                slots = torch.empty(max(nsl, 1) * S * 2, dtype=torch.uint8, device=dev)
+                out = torch.empty_like(slots)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            if mode == "collector":
+                col.run_many(encs, slots, S, cook=ctx, seed=f, out=out)
+            else:
+                base = 0
+                for ci in range(ncon):
+                    p = plans[ci]
+                    sv = slots[base * S:(base + max(p.n_slots, 1)) * S]
+                    ov = out[base * S:(base + max(p.n_slots, 1)) * S]
+                    encs[ci].run_cooked(sv, S, ctx, f, out=ov)
+                    base += p.n_slots
+            e1.record()
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            if f >= 2:  # the first flushes pay allocations and run-time compiles
+                gpu_ms.append(e0.elapsed_time(e1))
+                wall_ms.append((t1 - t0) * 1e3)
+                npk_tot += npk
+                nev_tot += sum(len(l) for l in lens)
+            del inbuf
+        for e in encs:
+            e.close()
+        if col is not None:
+            col.close()
+        res[mode] = {"run_ms_per_flush": round(statistics.median(gpu_ms), 4),
+                     "flush_wall_ms": round(statistics.median(wall_ms), 3),
+                     "cooked_packets_per_s_run": round(npk_tot / (sum(gpu_ms) * 1e-3), 1),
+                     "packets_per_flush": round(npk_tot / len(gpu_ms), 1)}
+    ctx.close()
+    res["what"] = ("200 connections x 64-256 datagrams (64-1200 B) per 8 ms flush, -f 20:10 mode 0: "
+                   "framing + encode + do_cook into device memory, one collector launch set vs 200 "
+                   "rsmi_fenc_run_cooked_dev calls; run = GPU time from the first launch to the last")
+    res["speedup_run"] = round(res["per_connection"]["run_ms_per_flush"] /
+                               res["collector"]["run_ms_per_flush"], 2)
+    return res
 
 
 def dropin_latency(u, calls=300):

@@ -24,11 +24,10 @@
  * Every packet the reference's output() would return is listed, in the
  * reference's order, as (slot, length); packet bytes are slots_base +
  * slot*slot_stride + RSMI_FEC_SLOT_PACKET .. + length.  Results are byte-identical to the
- * reference's packets, with one documented difference: in mode 0 the bytes of
- * the last data shard past the blob's end are zero here, where the reference
- * sends whatever its blob buffer held there before (stale bytes of earlier
- * groups, fec_manager.cpp:67-75); the parity covers the zeros.  The receiver
- * never reads those bytes (blob_decode_t::output, fec_manager.cpp:97-129).
+ * reference's packets, including mode 0's bytes of the last data shard past
+ * the blob's end: the reference sends whatever its blob buffer held there
+ * (stale bytes of earlier groups, fec_manager.cpp:67-75), and so does this
+ * (the encoder keeps a device copy of that buffer).
  *
  * Packets still waiting for their group at the end of a batch (the
  * reference's pending input_buf / blob) are copied into a device carry area
@@ -138,6 +137,31 @@ int rsmi_fenc_run_cooked_dev(rsmi_fenc *enc, uint8_t *slots_base, int64_t slot_s
                              const struct rsmi_cook_ctx *ctx, uint64_t seed, uint8_t *out,
                              int32_t *out_len, void *stream);
 
+/* ---- the collector: many connections' managers in one launch set -----------
+ *
+ * A server keeps one manager per connection (connection.h:244-245), up to
+ * max_conn_num = 200 (common.h:112), each flushing on its own 8 ms timer
+ * (fec_manager.h:30), so a flush is a handful of groups per connection.
+ * rsmi_fenc_run_many runs n planned encoders' batches (each planned with
+ * rsmi_fenc_plan on its own state, unchanged) as one launch set: one framing
+ * launch over all their jobs, one encode launch per (k, n) code over all
+ * their groups of that code, one carry pass and, with a cook context, one
+ * do_cook over all their packets.  The encoders' slots share one slot array:
+ * slots_base holds sum(n_slots) slots of slot_stride bytes (slot_stride >=
+ * every encoder's slot_stride_min).  Groups are laid out bucketed by code, so
+ * afterwards rsmi_fenc_packets / rsmi_fenc_groups of each encoder report slots
+ * of the shared array.  With ctx, out_len receives the cooked length of every
+ * packet, the encoders' packet lists concatenated in the order of enc[]; IVs
+ * are drawn from (seed, that concatenated index).  An encoder may appear once
+ * per call.  The collector keeps the combined plan's staging (two sets, so a
+ * call may be planned while the previous one runs). */
+typedef struct rsmi_fcol rsmi_fcol;
+int rsmi_fcol_create(rsmi_fcol **out);
+void rsmi_fcol_destroy(rsmi_fcol *col);
+int rsmi_fenc_run_many(rsmi_fcol *col, rsmi_fenc *const *enc, int32_t n, uint8_t *slots_base,
+                       int64_t slot_stride, const struct rsmi_cook_ctx *ctx, uint64_t seed,
+                       uint8_t *out, int32_t *out_len, void *stream);
+
 /* ---- receive side: fec_decode_manager_t ------------------
  *
  * fec_decode_manager_t::input / output (fec_manager.cpp:469-797) take every
@@ -186,6 +210,18 @@ int rsmi_fdec_plan(rsmi_fdec *dec, int64_t n, const int32_t *len, const uint64_t
 /* Gather, decode, pack and copy back the planned groups on `stream`
  * (asynchronous; dev_base must stay valid until it completes). */
 int rsmi_fdec_run_dev(rsmi_fdec *dec, void *stream);
+
+/* The receive-side collector (see rsmi_fenc_run_many): n planned decoders'
+ * batches in one launch set -- one gather into a staging area shared across
+ * decoders and bucketed by (k, n), one decode per code, one pass packing each
+ * decoder's rows to copy back, one moving their carries -- then each
+ * decoder's rows to its own pinned buffer.  Afterwards each decoder's
+ * rsmi_fdec_outputs works as after rsmi_fdec_run_dev.  The collector keeps
+ * the shared staging; a call waits for its previous call. */
+typedef struct rsmi_fdcol rsmi_fdcol;
+int rsmi_fdcol_create(rsmi_fdcol **out);
+void rsmi_fdcol_destroy(rsmi_fdcol *col);
+int rsmi_fdec_run_many(rsmi_fdcol *col, rsmi_fdec *const *dec, int32_t n, void *stream);
 
 /* Wait for the run and resolve the output list: *n_out packets. */
 int rsmi_fdec_outputs(rsmi_fdec *dec, int64_t *n_out);

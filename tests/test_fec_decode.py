@@ -255,3 +255,46 @@ def test_gpu_per_call_interface(gpu):
         assert dec.input(p) == dm.input(p)
         assert dec.output() == dm.output()
     dec.close()
+
+
+@pytest.mark.gpu
+def test_gpu_decode_collector_200_connections_match_reference(fx, gpu):
+    """The receive-side collector (rsmi_fdec_run_many): 200 decoders, one per
+    connection (connection.h:244-245, max_conn_num = 200, common.h:112), each
+    fed its own golden channel (case i % len(DEC_CASES), cut into 3 batches at its own
+    points, so groups straddle batches through each decoder's ring), planned
+    one by one, run together: every connection's return codes, output events
+    and output bytes equal the reference's."""
+    import torch
+    from udpspeeder_amd.fec import FecDecodeCollector, FecDecoder
+    ncon = 200
+    cases = [_case(fx, NAMES[i % len(NAMES)]) for i in range(ncon)]
+    packed = [_pack(c["chan"]) for c in cases]
+    devs = [torch.from_numpy(h).cuda() for h, _, _ in packed]
+    decs = [FecDecoder() for _ in range(ncon)]
+    col = FecDecodeCollector()
+    rng = np.random.default_rng(9)
+    cuts = []
+    for c in cases:
+        n = len(c["chan"])
+        a, b = sorted(rng.integers(1, n, 2))
+        cuts.append([0, int(a), int(b), n])
+    ret = [[] for _ in range(ncon)]
+    out = [[] for _ in range(ncon)]
+    for bi in range(3):
+        for ci in range(ncon):
+            host, lens, offs = packed[ci]
+            a, b = cuts[ci][bi], cuts[ci][bi + 1]
+            ret[ci] += list(decs[ci].plan(host, lens[a:b], offs[a:b], devs[ci]).ret)
+        col.run_many(decs)
+        for ci in range(ncon):
+            a = cuts[ci][bi]
+            out[ci] += [(bts, e + a) for bts, e in decs[ci].outputs()]
+    for ci, c in enumerate(cases):
+        assert ret[ci] == c["ret"], ci
+        assert [e for _, e in out[ci]] == c["out_event"], ci
+        assert [len(b) for b, _ in out[ci]] == c["out_len"], ci
+        assert hashlib.sha256(b"".join(b for b, _ in out[ci])).digest() == c["sha"], ci
+    col.close()
+    for d in decs:
+        d.close()

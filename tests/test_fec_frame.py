@@ -303,3 +303,78 @@ def test_gpu_frames_cooked_match_reference(fx, gpu, cook_oracle, name, nbatch, h
                if ck != cook_oracle.do_cook(e, v, key)]
         assert not bad, (len(bad), bad[:5])
     enc.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cook", [False, True])
+def test_gpu_collector_200_connections_match_reference(fx, gpu, cook, cook_oracle):
+    """The cross-connection collector (rsmi_fenc_run_many): 200 managers --
+    max_conn_num, common.h:112, one per connection (connection.h:244-245) --
+    each fed its own golden event stream (case i % 10, cut into 3 batches at
+    per-connection points, so groups straddle batches through each manager's
+    carry area), planned one by one, run together per flush: every
+    connection's packets equal the reference's (order, events, bytes).  With
+    cook, the cooked packets are do_cook of those (the oracle, each with the
+    IV the device drew), de_cook restores them."""
+    import torch
+    from udpspeeder_amd.cook import CookContext
+    from udpspeeder_amd.fec import FecCollector, FecEncoder
+    ncon = 200
+    cases = [_case(fx, NAMES[i % len(NAMES)]) for i in range(ncon)]
+    encs = [FecEncoder(c["rs"], c["mode"], c["mtu"], c["ql"], seq0=c["seq0"]) for c in cases]
+    rng = np.random.default_rng(200)
+    cuts = []
+    for c in cases:
+        n = len(c["lens"])
+        a, b = sorted(rng.integers(1, n, 2))
+        cuts.append([0, int(a), int(b), n])
+    col = FecCollector()
+    ctx = CookContext(b"collector-key") if cook else None
+    got = [[] for _ in range(ncon)]
+    for bi in range(3):
+        chunks, offs_all, o = [], [], 0
+        for ci, c in enumerate(cases):
+            a, b = cuts[ci][bi], cuts[ci][bi + 1]
+            offs = np.zeros(b - a, np.uint64)
+            for i in range(a, b):
+                offs[i - a] = o
+                if c["ev"][i] is not None:
+                    chunks.append(c["ev"][i])
+                    o += len(c["ev"][i])
+            offs_all.append(offs)
+        inbuf = torch.from_numpy(np.frombuffer(b"".join(chunks) + bytes(32), np.uint8).copy()).cuda()
+        plans = [encs[ci].plan(c["lens"][cuts[ci][bi]:cuts[ci][bi + 1]], offs_all[ci], inbuf)
+                 for ci, c in enumerate(cases)]
+        # one stride for the shared array: every encoder's minimum, plus do_cook's tail
+        S = FecEncoder.slot_stride_for(max(p.slot_stride_min for p in plans) - 128)
+        nsl = sum(p.n_slots for p in plans)
+        slots = torch.full((max(1, nsl) * S,), 0xEE, dtype=torch.uint8, device="cuda")
+        out = torch.full_like(slots, 0x11) if cook else None
+        ol = col.run_many(encs, slots, S, cook=ctx, seed=77 + bi, out=out)
+        torch.cuda.synchronize()
+        h = slots.cpu().numpy()
+        hc = out.cpu().numpy() if cook else None
+        olh = ol.cpu().numpy() if cook else None
+        q = 0
+        for ci, c in enumerate(cases):
+            pk = encs[ci].packets_now()
+            a = cuts[ci][bi]
+            for s, l, e in pk:
+                plain = h[s * S + 120:s * S + 120 + l].tobytes()
+                got[ci].append((plain, int(e) + a))
+                if cook:
+                    cl = int(olh[q])
+                    assert cl > l
+                    ck = hc[s * S + 120:s * S + 120 + cl].tobytes()
+                    st, back, nl = cook_oracle.de_cook(ck, b"collector-key")
+                    assert st == 0 and back[:nl] == plain, (ci, q)
+                q += 1
+        del inbuf
+    for ci, c in enumerate(cases):
+        pk = [p for p, _ in got[ci]]
+        assert [e for _, e in got[ci]] == list(c["pk_event"]), ci
+        assert [len(p) for p in pk] == list(c["pk_len"]), ci
+        assert hashlib.sha256(b"".join(pk)).digest() == c["sha"], ci
+    col.close()
+    for e in encs:
+        e.close()

@@ -55,10 +55,6 @@ constexpr int kWaves = 4;      // waves per block (one group each)
 constexpr int kRing = DEC_RING;  // survivors in flight per wave
 constexpr int kRows = 10;      // max e handled by the one-wave kernels
 constexpr int kPass = 5;       // rows accumulated per pass over the survivors
-#ifndef DEC_REG_ROWS
-#define DEC_REG_ROWS 5
-#endif
-constexpr int kRegRows = DEC_REG_ROWS;  // fused kernel: register Gauss-Jordan up to this e (LDS form above)
 constexpr int kTile = 1280;    // bytes per lane-tile pass (64 x 16 + 64 x 4)
 #ifndef DEC_ST_SGPR
 #define DEC_ST_SGPR 0          // 1: row offset of the rebuilt-row stores in soffset (see bitslice.hip
@@ -147,12 +143,6 @@ __device__ __forceinline__ Tables load_tables(uint8_t *smem, const uint32_t *pta
     return Tables{s01, s2, lexp, llog, linv};
 }
 
-// c * x for a byte x (upper bits zero), c given by its split table (t, t2)
-__device__ __forceinline__ uint32_t gmul_t(uint4 t, uint32_t t2, uint32_t x) {
-    return xor3(__builtin_amdgcn_perm(t.y, t.x, x & 7u), __builtin_amdgcn_perm(t.w, t.z, (x >> 3) & 7u),
-                __builtin_amdgcn_perm(t2, t2, x >> 6));
-}
-
 __device__ __forceinline__ uint32_t gmul(const uint8_t *lexp, const uint8_t *llog, uint32_t a,
                                          uint32_t b) {
     return (a && b) ? lexp[llog[a] + llog[b]] : 0u;
@@ -221,11 +211,14 @@ struct WaveLds {  // per-wave LDS slice
     int rows;
 };
 
-__host__ __device__ inline int aug_bytes(int k) { return (kRows * (kRows + k) + 15) & ~15; }
+
+// fused kernel: split-table rows per survivor in the wave's slice, one block
+// of kPass rows at a time (each block's Lagrange coefficients are computed
+// when its pass starts)
+constexpr int kTabRows = 5;
 
 __host__ __device__ inline int wave_lds_bytes(int k) {
-    // sel[256] miss[256] aug[kRows*(kRows+k)] tab[k*kRows*32]
-    return 512 + aug_bytes(k) + k * kRows * 32;
+    return 512 + k * kTabRows * 32;  // sel[256] miss[256] tab[k * kTabRows * 32]
 }
 
 // Ragged kernels' slice: sel[64] miss[64] t01[k*rows] t2[k*rows] (k <= 32;
@@ -274,13 +267,9 @@ __device__ __forceinline__ int select_survivors(int k, int n, Flag flag, const W
 // missing data rows: lane s < k holds survivor s's shard index in sel_lane,
 // lane d < e missing row d's in miss_lane.  Leaves coef[r][j]'s split table at
 // (t01, t2)[j * rows + r], where Rebuild reads them.
-template <int NR>
-__device__ __forceinline__ void lagrange_coefs(int k, int e, uint32_t sel_lane, uint32_t miss_lane,
-                                               const WaveLds &L, const LTables &T, int lane) {
-    const bool act = lane < k;
-    const uint32_t xs = T.px[sel_lane & 255u];
-    const uint32_t xm = T.px[miss_lane & 255u];
-    // B_s: two chains of independent lookups
+// B_s = sum_{t < k} lz[x_s ^ x_t] for lane s (xs: lane s holds x_s), in two
+// chains of independent lookups.
+__device__ __forceinline__ uint32_t lagrange_b(int k, uint32_t xs, const LTables &T) {
     uint32_t b0 = 0, b1 = 0;
     int t = 0;
     for (; t + 1 < k; t += 2) {
@@ -290,7 +279,16 @@ __device__ __forceinline__ void lagrange_coefs(int k, int e, uint32_t sel_lane, 
         b1 += T.lz[xs ^ x1];
     }
     if (t < k) b0 += T.lz[xs ^ (uint32_t)__builtin_amdgcn_readlane((int)xs, t)];
-    const uint32_t B = b0 + b1;
+    return b0 + b1;
+}
+
+// log L_s(x_d) for the e <= NR rows d whose points lane d of xm holds; lane s
+// < k (survivor s: point xs, B_s in B) gets store(r, v) with v the log of
+// coefficient (row r, survivor s), 0..254.
+template <int NR, class Store>
+__device__ __forceinline__ void lagrange_rows(int k, int e, uint32_t xs, uint32_t B, uint32_t xm,
+                                              const LTables &T, int lane, Store store) {
+    const bool act = lane < k;
     // lz[x_d ^ x_s] of rows 2i and 2i + 1 packed in q[i] (each half <= 254,
     // and a wave sum of halves <= 64 * 254 < 2^16): A_d for two rows per sum
     constexpr int NQ = (NR + 1) / 2;
@@ -311,7 +309,6 @@ __device__ __forceinline__ void lagrange_coefs(int k, int e, uint32_t sel_lane, 
         }
     }
     if (act) {
-        const int base = lane * L.rows;
 #pragma unroll
         for (int r = 0; r < NR; ++r) {
             if (r < e) {
@@ -322,11 +319,23 @@ __device__ __forceinline__ void lagrange_coefs(int k, int e, uint32_t sel_lane, 
                 v = (v & 255u) + (v >> 8);       // <= 255 + 127
                 v = (v & 255u) + (v >> 8);       // <= 255
                 v = min(v, v - 255u);            // 255 -> 0
-                L.t01[base + r] = T.t01[v];
-                L.t2[base + r] = T.t2[v];
+                store(r, v);
             }
         }
     }
+}
+
+template <int NR>
+__device__ __forceinline__ void lagrange_coefs(int k, int e, uint32_t sel_lane, uint32_t miss_lane,
+                                               const WaveLds &L, const LTables &T, int lane) {
+    const uint32_t xs = T.px[sel_lane & 255u];
+    const uint32_t xm = T.px[miss_lane & 255u];
+    const uint32_t B = lagrange_b(k, xs, T);
+    const int base = lane * L.rows;
+    lagrange_rows<NR>(k, e, xs, B, xm, T, lane, [&](int r, uint32_t v) {
+        L.t01[base + r] = T.t01[v];
+        L.t2[base + r] = T.t2[v];
+    });
     wave_sync();
 }
 
@@ -494,29 +503,17 @@ __global__ __launch_bounds__(256, DEC_OCC) void k_decode_fused(UniformArgs a, co
                                                       const uint8_t *prows, int32_t *status_out,
                                                       const uint32_t *ptab, const uint8_t *gftab) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    uint4 *s01 = reinterpret_cast<uint4 *>(smem);                  // 256 x 16 B
-    uint32_t *s2 = reinterpret_cast<uint32_t *>(smem + 4096);      // 256 x 4 B
-    uint8_t *lexp = smem + 5120;                                   // 512
-    uint8_t *llog = smem + 5632;                                   // 256
-    uint8_t *linv = smem + 5888;                                   // 256: x^-1
     const int k = a.k, n = a.n;
+    (void)prows;
     const int wbytes = wave_lds_bytes(k);
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
-    const int rows_bytes = ((n - k) * k + 15) & ~15;
-    uint8_t *lrows = smem + kTabBytes;  // the code's parity rows, (n-k) x k
-    uint8_t *wl = smem + kTabBytes + rows_bytes + wid * wbytes;
-    WaveLds L{wl, wl + 256, wl + 512,
-              reinterpret_cast<uint32_t *>(wl + 512 + ((kRows * (kRows + k) + 15) & ~15))};
+    // LTables | per wave: sel[256] miss[256] tab[k][kTabRows] (8 dwords per entry)
+    uint8_t *wl = smem + kLTabBytes + wid * wbytes;
+    WaveLds L{wl, wl + 256, nullptr, reinterpret_cast<uint32_t *>(wl + 512)};
 
-    for (int i = threadIdx.x; i < 256; i += blockDim.x) {
-        s01[i] = reinterpret_cast<const uint4 *>(ptab + i * kPtabDwords)[0];
-        s2[i] = ptab[i * kPtabDwords + 4];
-    }
-    for (int i = threadIdx.x; i < 768; i += blockDim.x) smem[5120 + i] = gftab[i];
-    for (int i = threadIdx.x; i < 256; i += blockDim.x)
-        linv[i] = i ? gftab[255 - gftab[512 + i]] : 0;  // exp[255 - log x]
-    for (int i = threadIdx.x; i < (n - k) * k; i += blockDim.x) lrows[i] = prows[i];
+    // the LTables image (Lagrange coefficients need no parity rows)
+    const LTables LT = load_ltables(smem, ptab, gftab);
     __syncthreads();
 
     const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
@@ -532,6 +529,9 @@ __global__ __launch_bounds__(256, DEC_OCC) void k_decode_fused(UniformArgs a, co
     uint32_t pf = (g0 < a.ngroups && lane < n) ? present[g0 * n + lane] : 0u;
     uint32_t pf_next = 0;
     for (int64_t g = g0; g < a.ngroups; g += nwaves, pf = pf_next) {
+#if DEC_TRACE
+        const uint64_t tr0 = trace_now();
+#endif
         {
             const int64_t gn = g + nwaves;
             pf_next = (gn < a.ngroups && lane < n) ? present[gn * n + lane] : 0u;
@@ -570,6 +570,9 @@ __global__ __launch_bounds__(256, DEC_OCC) void k_decode_fused(UniformArgs a, co
             continue;
         }
 
+#if DEC_TRACE
+        const uint64_t tr1 = trace_now();
+#endif
         // ---- 2. descriptor + first loads ---------------------------------------
         // descriptor inputs through readfirstlane (cdna_hip_programming.md T20)
         const uint64_t gb = (uint64_t)(uintptr_t)(a.base + g * a.group_stride);
@@ -611,111 +614,12 @@ __global__ __launch_bounds__(256, DEC_OCC) void k_decode_fused(UniformArgs a, co
         start_tile(0);  // the first survivors fly while the matrix is inverted
 
         // ---- 3. Gauss-Jordan on [A | M], e x (e+k) ------------------------------
-        const int W = e + k;
-        if (W <= 64 && e <= kRegRows) {
-            // lane c holds column c: a missing data index (c < e) or survivor c - e
-            const uint32_t col = lane < e ? (uint32_t)L.miss[lane]
-                                          : (lane < W ? (uint32_t)L.sel[lane - e] : 0u);
-            uint32_t a[kRegRows];
-#pragma unroll
-            for (int r = 0; r < kRegRows; ++r) {
-                a[r] = 0;
-                if (r < e) {
-                    const uint32_t R = __builtin_amdgcn_readlane(sel_lane, k - e + r);
-                    const uint8_t *prow = lrows + (R - k) * k;
-                    const uint32_t v = prow[col < (uint32_t)k ? col : 0u];
-                    a[r] = (lane >= e && col >= (uint32_t)k) ? (uint32_t)(col == R) : v;
-                }
-            }
-#pragma unroll
-            for (int p = 0; p < kRegRows; ++p) {
-                if (p < e) {
-                    const uint32_t piv = __builtin_amdgcn_readlane(a[p], p);
-                    if (piv == 0) {
-                        st = RSMI_DEC_SINGULAR;
-                        break;
-                    }
-                    const uint32_t ip = __builtin_amdgcn_readfirstlane(linv[piv]);
-                    a[p] = gmul_t(s01[ip], s2[ip], a[p]);
-#pragma unroll
-                    for (int r = 0; r < kRegRows; ++r) {
-                        if (r < e && r != p) {
-                            const uint32_t f = __builtin_amdgcn_readlane(a[r], p);
-                            a[r] ^= gmul_t(s01[f], s2[f], a[p]);
-                        }
-                        __builtin_amdgcn_sched_barrier(0);
-                    }
-                }
-            }
-            st = __builtin_amdgcn_readfirstlane(st);
-            if (st != RSMI_DEC_OK) {
-                if (lane == 0 && status_out) status_out[g] = st;
-                continue;
-            }
-            // coef[r][j] sits in lane e + j: expand into split tables tab[j][r]
-            if (lane >= e && lane < W) {
-                uint32_t *dst = L.tab + (lane - e) * kRows * 8;
-#pragma unroll
-                for (int r = 0; r < kRegRows; ++r) {
-                    if (r < e) {
-                        reinterpret_cast<uint4 *>(dst + r * 8)[0] = s01[a[r]];
-                        dst[r * 8 + 4] = s2[a[r]];
-                    }
-                }
-            }
-            wave_sync();
-        } else {
-        for (int t = lane; t < e * W; t += 64) {
-            const int r = t / W, c = t - r * W;
-            const int R = L.sel[k - e + r];
-            const uint8_t *prow = lrows + (R - k) * k;
-            uint8_t v;
-            if (c < e) {
-                v = prow[L.miss[c]];
-            } else {
-                const int s = L.sel[c - e];
-                v = (s >= k) ? (uint8_t)(s == R) : prow[s];
-            }
-            L.aug[t] = v;
-        }
-        wave_sync();
-        for (int p = 0; p < e && st == RSMI_DEC_OK; ++p) {
-            const uint32_t piv = __builtin_amdgcn_readfirstlane(L.aug[p * W + p]);
-            if (piv == 0) {
-                st = RSMI_DEC_SINGULAR;
-                break;
-            }
-            const uint32_t ipiv = __builtin_amdgcn_readfirstlane(lexp[255 - llog[piv]]);
-            for (int c = p + 1 + lane; c < W; c += 64)
-                L.aug[p * W + c] = (uint8_t)gmul(lexp, llog, ipiv, L.aug[p * W + c]);
-            wave_sync();
-            const int cols = W - p - 1;
-            for (int t = lane; t < e * cols; t += 64) {
-                const int r = t / cols;
-                if (r == p) continue;
-                const int c = p + 1 + (t - r * cols);
-                const uint32_t f = L.aug[r * W + p];
-                if (f) L.aug[r * W + c] ^= (uint8_t)gmul(lexp, llog, f, L.aug[p * W + c]);
-            }
-            wave_sync();
-        }
-        st = __builtin_amdgcn_readfirstlane(st);
-        if (st != RSMI_DEC_OK) {
-            if (lane == 0 && status_out) status_out[g] = st;
-            continue;
-        }
-        // expand coef[r][j] = aug[r][e + j] into split tables tab[j][r]
-        for (int t = lane; t < e * k; t += 64) {
-            const int r = t / k, j = t - r * k;
-            const uint32_t c = L.aug[r * W + e + j];
-            const uint4 t01 = s01[c];
-            uint32_t *dst = L.tab + (j * kRows + r) * 8;
-            reinterpret_cast<uint4 *>(dst)[0] = t01;
-            dst[4] = s2[c];
-        }
-        wave_sync();
-        }
+        // ---- 3. coefficients: Lagrange form (see LTables), computed per block
+        // of kPass rows when the block's pass starts, below
 
+#if DEC_TRACE
+        const uint64_t tr2 = trace_now();
+#endif
         // ---- 4. stream the survivors: passes over (tile, block of kPass rows) --
         // the 3-bit split selectors of a survivor's 5 dwords
         auto split = [](const u32x4 &v, uint32_t d, uint32_t (&s0)[5], uint32_t (&s1)[5],
@@ -737,9 +641,23 @@ __global__ __launch_bounds__(256, DEC_OCC) void k_decode_fused(UniformArgs a, co
             rq[q] = __builtin_amdgcn_raw_buffer_load_b128(r, v16, DEC_NOMEM ? 0u : so, LDAUX);
             rd[q] = __builtin_amdgcn_raw_buffer_load_b32(r, v4, DEC_NOMEM ? 0u : so, LDAUX);
         };
-        for (int toff = 0; toff < a.len; toff += kTile) {
-            for (int rb = 0; rb < e; rb += kPass) {
-                if (toff || rb) start_tile(toff);  // pass 0's loads are already in flight
+        for (int rb = 0; rb < e; rb += kPass) {
+            if (rb) start_tile(0);  // block 0's first loads are already in flight
+            {   // coefficients of rows rb .. rb + kPass - 1 into the slice's table rows
+                const uint32_t xs = LT.px[sel_lane & 255u];
+                const uint32_t B = lagrange_b(k, xs, LT);
+                const uint32_t xm = lane + rb < e ? (uint32_t)LT.px[L.miss[lane + rb]] : 0u;
+                lagrange_rows<kPass>(k, e - rb < kPass ? e - rb : kPass, xs, B, xm, LT, lane,
+                                     [&](int r, uint32_t v) {
+                                         uint32_t *dst = L.tab + (lane * kTabRows + r) * 8;
+                                         reinterpret_cast<uint4 *>(dst)[0] = LT.t01[v];
+                                         dst[4] = LT.t2[v];
+                                     });
+                wave_sync();
+            }
+            const int rt = rb;  // table row of row rb + r: r
+            for (int toff = 0; toff < a.len; toff += kTile) {
+                if (toff) start_tile(toff);  // the pass's first loads
                 uint32_t acc[kPass][5];
 #pragma unroll
                 for (int r = 0; r < kPass; ++r)
@@ -759,8 +677,8 @@ __global__ __launch_bounds__(256, DEC_OCC) void k_decode_fused(UniformArgs a, co
                             split(rq[q + 1], rd[q + 1], b0, b1, b2);
                             refill(q, j);
                             refill(q + 1, j + 1);
-                            const uint32_t *ta = L.tab + (j * kRows + rb) * 8;
-                            const uint32_t *tb = ta + kRows * 8;
+                            const uint32_t *ta = L.tab + (j * kTabRows + rb - rt) * 8;
+                            const uint32_t *tb = ta + kTabRows * 8;
 #pragma unroll
                             for (int r = 0; r < kPass; ++r) {
                                 if (rb + r < e) {
@@ -784,7 +702,7 @@ __global__ __launch_bounds__(256, DEC_OCC) void k_decode_fused(UniformArgs a, co
                             if (j < k) split(rq[q], rd[q], a0, a1, a2);
                             refill(q, j);  // every iteration: see Rebuild::run
                             if (j >= k) continue;
-                            const uint32_t *ta = L.tab + (z + (j * kRows + rb) * 8);
+                            const uint32_t *ta = L.tab + (z + (j * kTabRows + rb - rt) * 8);
                             // rows in this pass, as an opaque SGPR per survivor: a
                             // loop-invariant "rb + r < e" is hoisted as a lane-mask
                             // boolean and re-materialised with v_cndmask + v_cmp at
@@ -823,6 +741,14 @@ __global__ __launch_bounds__(256, DEC_OCC) void k_decode_fused(UniformArgs a, co
             }
         }
         if (lane == 0 && status_out) status_out[g] = RSMI_DEC_OK;
+#if DEC_TRACE
+        if (lane == 0 && g_dec_trace) {  // phases of the group (scripts/c2_trace.py)
+            uint64_t *t = g_dec_trace + g * 8;
+            t[0] = tr0; t[1] = tr1; t[2] = tr2; t[3] = trace_now();
+            t[4] = (uint64_t)5 | ((uint64_t)k << 8) | ((uint64_t)e << 16) | ((uint64_t)a.len << 32);
+            t[5] = (uint64_t)(bid * kWaves + wid);
+        }
+#endif
         wave_sync();  // the LDS slice is rewritten by the next group
     }
 }
@@ -1298,16 +1224,14 @@ bool decode_fused_ok(int k, int n, int64_t group_stride, int64_t shard_stride, i
     const int m = n - k;
     const int emax = k < m ? k : m;
     return emax <= kRows && k <= 64 && n * shard_stride < (int64_t(1) << 31) && len > 0 &&
-           kTabBytes + ((m * k + 15) & ~15) + kWaves * wave_lds_bytes(k) <= 64 * 1024 &&
-           group_stride >= n * shard_stride;
+           kLTabBytes + kWaves * wave_lds_bytes(k) <= 64 * 1024 && group_stride >= n * shard_stride;
 }
 
 hipError_t launch_decode_fused(const UniformArgs &a, const uint8_t *present,
                                const uint8_t *parity_rows, int32_t *status,
                                const uint32_t *ptab, const uint8_t *gftab, hipStream_t s,
                                bool host_shards) {
-    const size_t lds = kTabBytes + (size_t)(((a.n - a.k) * a.k + 15) & ~15) +
-                       (size_t)kWaves * wave_lds_bytes(a.k);
+    const size_t lds = kLTabBytes + (size_t)kWaves * wave_lds_bytes(a.k);
     int64_t blocks = (a.ngroups + kWaves - 1) / kWaves;
     const int64_t cap = 256 * 8;
     if (blocks > cap) blocks = cap;

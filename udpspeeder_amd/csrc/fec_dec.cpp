@@ -209,6 +209,7 @@ struct Batch {
     std::vector<Bucket> buckets;
     std::map<int, int> bucket_of;  // k*257+n -> bucket
     std::vector<GatherCopy> gathers;
+    std::vector<std::pair<int64_t, int>> gather_ref;  // (job, shard index) of each gather
     std::vector<CarryCopy> carries;
     std::vector<Out> outs;
     std::vector<uint8_t> present;  // all buckets' present flags
@@ -642,9 +643,11 @@ int rsmi_fdec_plan(rsmi_fdec *D, int64_t n, const int32_t *len, const uint64_t *
     }
     D->B->staging_bytes = so;
     D->B->present.assign((size_t)po, 0);
+    D->B->gather_ref.clear();
     for (GatherCopy &G : D->B->gathers) {
         const Job &J = D->B->jobs[(size_t)(G.dst >> 8)];
         const int idx = (int)(G.dst & 0xff);
+        D->B->gather_ref.push_back({(int64_t)(G.dst >> 8), idx});
         const Bucket &B = D->B->buckets[(size_t)J.bucket];
         G.dst = (uint64_t)(B.staging_off + (J.row * B.n + idx) * B.stride);  // offset; based at run time
         G.dst_len = (uint32_t)B.stride;
@@ -673,9 +676,12 @@ int rsmi_fdec_plan(rsmi_fdec *D, int64_t n, const int32_t *len, const uint64_t *
     return RSMI_OK;
 }
 
-int rsmi_fdec_run_dev(rsmi_fdec *D, void *stream) {
-    if (!D || !D->B->planned) return fail(RSMI_ERR_INVALID, "rsmi_fdec_run_dev without a plan");
-    if (D->plan_only) return fail(RSMI_ERR_INVALID, "rsmi_fdec_run_dev on a plan-only decoder");
+}  // extern "C"
+
+namespace {
+// Bind the decoder to the current device and order stream s after its
+// previous batch, which reads and writes the shared device buffers.
+int bind_dec(rsmi_fdec *D, hipStream_t s) {
     int cur;
     if (hipGetDevice(&cur) != hipSuccess) return fail(RSMI_ERR_HIP, "fdec: no usable GPU");
     if (D->device < 0) {
@@ -686,12 +692,22 @@ int rsmi_fdec_run_dev(rsmi_fdec *D, void *stream) {
     } else if (cur != D->device) {
         return fail(RSMI_ERR_INVALID, "rsmi_fdec_run_dev on another device than the decoder's");
     }
-    hipStream_t s = (hipStream_t)stream;
-    // the previous batch reads and writes the shared device buffers: order after
-    // it even on another stream, and never free one of them under it
     Batch &prev = D->bat[D->bi ^ 1];
     if (prev.in_flight && hipStreamWaitEvent(s, prev.done, 0) != hipSuccess)
         return fail(RSMI_ERR_HIP, "fdec: hipStreamWaitEvent");
+    return RSMI_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int rsmi_fdec_run_dev(rsmi_fdec *D, void *stream) {
+    if (!D || !D->B->planned) return fail(RSMI_ERR_INVALID, "rsmi_fdec_run_dev without a plan");
+    if (D->plan_only) return fail(RSMI_ERR_INVALID, "rsmi_fdec_run_dev on a plan-only decoder");
+    hipStream_t s = (hipStream_t)stream;
+    int rc0 = bind_dec(D, s);
+    if (rc0) return rc0;
+    Batch &prev = D->bat[D->bi ^ 1];
     int64_t max_rows = 0;
     for (const Bucket &B : D->B->buckets) max_rows = std::max(max_rows, B.rows);
     if ((size_t)D->buff_num * kRingBytes > D->dcarry_cap || (size_t)D->B->staging_bytes + 16 > D->stage_cap ||
@@ -819,6 +835,207 @@ int rsmi_fdec_output_list(const rsmi_fdec *D, const uint8_t **ptr, int32_t *len,
         if (ptr) ptr[i] = X.outs[i].ptr;
         if (len) len[i] = X.outs[i].len;
         if (event) event[i] = X.outs[i].event;
+    }
+    return RSMI_OK;
+}
+
+}  // extern "C"
+
+// ---- the receive-side collector: many decoders' planned batches in one set --
+//
+// The counterpart of rsmi_fenc_run_many (fec_enc.cpp): each connection's
+// fec_decode_manager_t (connection.h:244-245) plans its received packets on
+// its own state; rsmi_fdec_run_many then runs their byte work together: one
+// gather over every decoder's shards into a shared staging area bucketed by
+// (k, n) across decoders, one decode per (k, n) code, one pass that packs the
+// rows each decoder copies back and one that moves their carries, then each
+// decoder's rows to its own pinned buffer.  A bucket's shard length is the
+// longest of its decoders' (column-wise code: a group's rebuilt bytes below
+// its own length do not depend on the bytes past it).  Carry-tagged addresses
+// resolve to each decoder's own ring.
+struct rsmi_fdcol {
+    int device = -1;
+    uint8_t *dstage = nullptr, *dmeta = nullptr;
+    size_t stage_cap = 0, meta_cap = 0;
+    int32_t *dstatus = nullptr;
+    size_t status_cap = 0;
+    uint8_t *hmeta[2] = {nullptr, nullptr};
+    size_t hmeta_cap[2] = {0, 0};
+    hipEvent_t done[2] = {nullptr, nullptr};
+    bool in_flight[2] = {false, false};
+    int cur = 0;
+};
+
+extern "C" {
+
+int rsmi_fdcol_create(rsmi_fdcol **out) {
+    if (!out) return fail(RSMI_ERR_INVALID, "null out");
+    *out = new rsmi_fdcol();
+    return RSMI_OK;
+}
+
+void rsmi_fdcol_destroy(rsmi_fdcol *C) {
+    if (!C) return;
+    for (int i = 0; i < 2; ++i) {
+        if (C->in_flight[i]) (void)hipEventSynchronize(C->done[i]);
+        if (C->done[i]) (void)hipEventDestroy(C->done[i]);
+        if (C->hmeta[i]) (void)hipHostFree(C->hmeta[i]);
+    }
+    for (uint8_t *p : {C->dstage, C->dmeta}) if (p) (void)hipFree(p);
+    if (C->dstatus) (void)hipFree(C->dstatus);
+    delete C;
+}
+
+int rsmi_fdec_run_many(rsmi_fdcol *C, rsmi_fdec *const *dec, int32_t n, void *stream) {
+    if (!C || n < 0 || (n && !dec)) return fail(RSMI_ERR_INVALID, "rsmi_fdec_run_many: bad arguments");
+    for (int i = 0; i < n; ++i) {
+        const rsmi_fdec *D = dec[i];
+        if (!D || !D->B->planned) return fail(RSMI_ERR_INVALID, "rsmi_fdec_run_many: decoder without a plan");
+        if (D->plan_only) return fail(RSMI_ERR_INVALID, "rsmi_fdec_run_many: plan-only decoder");
+        for (int j = 0; j < i; ++j)
+            if (dec[j] == D) return fail(RSMI_ERR_INVALID, "rsmi_fdec_run_many: a decoder listed twice");
+    }
+    hipStream_t s = (hipStream_t)stream;
+    int cur;
+    if (hipGetDevice(&cur) != hipSuccess) return fail(RSMI_ERR_HIP, "fdcol: no usable GPU");
+    if (C->device < 0) {
+        for (auto &ev : C->done)
+            if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess)
+                return fail(RSMI_ERR_HIP, "fdcol: hipEventCreate");
+        C->device = cur;
+    } else if (C->device != cur) {
+        return fail(RSMI_ERR_INVALID, "rsmi_fdec_run_many on another device than the collector's");
+    }
+    // the shared staging / metadata buffers are rewritten: after the last call
+    for (int i = 0; i < 2; ++i)
+        if (C->in_flight[i]) {
+            if (hipEventSynchronize(C->done[i]) != hipSuccess) return fail(RSMI_ERR_HIP, "fdcol: wait");
+            C->in_flight[i] = false;
+        }
+    for (int i = 0; i < n; ++i) {
+        rsmi_fdec *D = dec[i];
+        int rc = bind_dec(D, s);
+        if (rc) return rc;
+        Batch &prev = D->bat[D->bi ^ 1];
+        if ((size_t)D->buff_num * kRingBytes > D->dcarry_cap || (size_t)D->B->d2h_bytes + 16 > D->blob_cap) {
+            rc = wait_batch(prev);
+            if (rc) return rc;
+        }
+        rc = dev_grow(&D->dcarry, &D->dcarry_cap, (size_t)D->buff_num * kRingBytes);
+        if (!rc) rc = dev_grow(&D->dblob, &D->blob_cap, (size_t)D->B->d2h_bytes + 16);
+        if (!rc) rc = host_grow(&D->B->hblob, &D->B->hblob_cap, (size_t)D->B->d2h_bytes + 16);
+        if (rc) return rc;
+    }
+    // ---- shared buckets: (k, n) across decoders, rows appended decoder by decoder
+    struct CB {
+        int k, nn, len = 0;
+        int64_t rows = 0, stride = 0, off = 0, poff = 0;
+    };
+    std::map<int, CB> cbs;
+    std::vector<std::vector<int64_t>> rowbase((size_t)n);  // per decoder bucket: first shared row
+    for (int i = 0; i < n; ++i) {
+        const rsmi_fdec *D = dec[i];
+        for (const Bucket &B : D->B->buckets) {
+            CB &c = cbs.emplace(B.k * 257 + B.n, CB{B.k, B.n}).first->second;
+            rowbase[(size_t)i].push_back(c.rows);
+            c.rows += B.rows;
+            c.len = std::max(c.len, B.len);
+        }
+    }
+    int64_t so = 0, po = 0, max_rows = 0;
+    for (auto &kv : cbs) {
+        CB &c = kv.second;
+        c.stride = (c.len + 127) & ~int64_t(127);
+        c.off = so;
+        c.poff = po;
+        so += c.rows * c.nn * c.stride;
+        po += (c.rows * c.nn + 15) & ~int64_t(15);
+        max_rows = std::max(max_rows, c.rows);
+    }
+    int rc = dev_grow(&C->dstage, &C->stage_cap, (size_t)so + 16);
+    if (!rc) rc = dev_grow(&C->dstatus, &C->status_cap, (size_t)max_rows * 4 + 16);
+    if (rc) return rc;
+    std::vector<GatherCopy> gathers;
+    std::vector<uint8_t> present((size_t)po, 0);
+    std::vector<CarryCopy> packs, carries;
+    auto resolve = [](const rsmi_fdec *D, uint64_t a) -> uint64_t {
+        return (a & rsmi::kCarryTag) ? (uint64_t)(uintptr_t)D->dcarry + (a & rsmi::kCarryOff) : a;
+    };
+    auto shard_at = [&](const rsmi_fdec *D, size_t di, const Job &J, int idx) -> uint64_t {
+        const Bucket &B = D->B->buckets[(size_t)J.bucket];
+        const CB &c = cbs[B.k * 257 + B.n];
+        const int64_t row = rowbase[di][(size_t)J.bucket] + J.row;
+        return (uint64_t)(uintptr_t)C->dstage + (uint64_t)(c.off + (row * c.nn + idx) * c.stride);
+    };
+    for (int i = 0; i < n; ++i) {
+        const rsmi_fdec *D = dec[i];
+        const Batch &X = *D->B;
+        for (size_t g = 0; g < X.gathers.size(); ++g) {
+            const Job &J = X.jobs[(size_t)X.gather_ref[g].first];
+            const int idx = X.gather_ref[g].second;
+            const Bucket &B = X.buckets[(size_t)J.bucket];
+            const CB &c = cbs[B.k * 257 + B.n];
+            GatherCopy G = X.gathers[g];
+            G.src = resolve(D, G.src);
+            G.dst = shard_at(D, (size_t)i, J, idx);
+            G.dst_len = (uint32_t)c.stride;
+            gathers.push_back(G);
+            present[(size_t)(c.poff + (rowbase[(size_t)i][(size_t)J.bucket] + J.row) * c.nn + idx)] = 1;
+        }
+        int64_t ro = 0;
+        for (const auto &jr : X.d2h_rows) {
+            const Job &J = X.jobs[(size_t)jr.first];
+            packs.push_back(CarryCopy{shard_at(D, (size_t)i, J, jr.second), (uint64_t)(uintptr_t)(D->dblob + ro),
+                                      (uint32_t)J.len, 0});
+            ro += (J.len + 15) & ~15;
+        }
+        for (const CarryCopy &cc : X.carries)
+            carries.push_back(CarryCopy{resolve(D, cc.src), resolve(D, cc.dst), cc.len, 0});
+    }
+    const size_t gb = gathers.size() * sizeof(GatherCopy), pb = present.size(),
+                 kb = packs.size() * sizeof(CarryCopy), cb = carries.size() * sizeof(CarryCopy);
+    const size_t go = 0, pof = (gb + 255) & ~size_t(255), ko = (pof + pb + 255) & ~size_t(255),
+                 co = (ko + kb + 255) & ~size_t(255), all = co + cb + 16;
+    C->cur ^= 1;
+    rc = dev_grow(&C->dmeta, &C->meta_cap, all);
+    if (!rc) rc = host_grow(&C->hmeta[C->cur], &C->hmeta_cap[C->cur], all);
+    if (rc) return rc;
+    uint8_t *hm = C->hmeta[C->cur];
+    if (gb) std::memcpy(hm + go, gathers.data(), gb);
+    if (pb) std::memcpy(hm + pof, present.data(), pb);
+    if (kb) std::memcpy(hm + ko, packs.data(), kb);
+    if (cb) std::memcpy(hm + co, carries.data(), cb);
+    const rsmi::CarryBase none{{nullptr, nullptr}};  // every address is absolute
+    hipError_t e = hipMemcpyAsync(C->dmeta, hm, all, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess)
+        e = rsmi::launch_gather(reinterpret_cast<const GatherCopy *>(C->dmeta + go), (int64_t)gathers.size(),
+                                none, s);
+    if (e != hipSuccess) return fail(RSMI_ERR_HIP, std::string("fdcol gather: ") + hipGetErrorString(e));
+    for (auto &kv : cbs) {
+        const CB &c = kv.second;
+        if (c.len == 0 || c.rows == 0) continue;
+        rc = rsmi_decode_dev(c.k, c.nn, C->dstage + c.off, (int64_t)c.nn * c.stride, c.stride, c.len, c.rows,
+                             C->dmeta + pof + c.poff, C->dstatus, stream);
+        if (rc) return rc;
+    }
+    e = rsmi::launch_carry(reinterpret_cast<const CarryCopy *>(C->dmeta + ko), (int64_t)packs.size(), none, s);
+    if (e == hipSuccess)
+        e = rsmi::launch_carry(reinterpret_cast<const CarryCopy *>(C->dmeta + co), (int64_t)carries.size(), none,
+                               s);
+    for (int i = 0; e == hipSuccess && i < n; ++i) {
+        rsmi_fdec *D = dec[i];
+        if (D->B->d2h_bytes)
+            e = hipMemcpyAsync(D->B->hblob, D->dblob, (size_t)D->B->d2h_bytes, hipMemcpyDeviceToHost, s);
+    }
+    if (e == hipSuccess) e = hipEventRecord(C->done[C->cur], s);
+    for (int i = 0; e == hipSuccess && i < n; ++i) e = hipEventRecord(dec[i]->B->done, s);
+    if (e != hipSuccess) return fail(RSMI_ERR_HIP, std::string("fdcol run: ") + hipGetErrorString(e));
+    C->in_flight[C->cur] = true;
+    for (int i = 0; i < n; ++i) {
+        rsmi_fdec *D = dec[i];
+        D->B->in_flight = true;
+        D->B->planned = false;
+        D->B->ran = true;
     }
     return RSMI_OK;
 }

@@ -12,6 +12,7 @@
 #include <new>
 #include <cstdio>
 #include <cstring>
+#include <map>
 #include <string>
 #include <vector>
 
@@ -610,14 +611,11 @@ int rsmi_fenc_run_cooked_dev(rsmi_fenc *E, uint8_t *slots, int64_t S, const rsmi
 
 namespace {
 
-int run_dev(rsmi_fenc *E, uint8_t *slots, int64_t S, void *stream, const CookSpec *ck) {
-    if (!E || !E->planned) return fail(RSMI_ERR_INVALID, "rsmi_fenc_run_dev without a plan");
-    if (E->plan_only) return fail(RSMI_ERR_INVALID, "rsmi_fenc_run_dev on a plan-only encoder");
-    if (E->n_slots && (!slots || ((uintptr_t)slots & 15)))
-        return fail(RSMI_ERR_INVALID, "slots_base must be 16-aligned");
-    if (S % 16 || S < E->stride_min)
-        return fail(RSMI_ERR_INVALID, "slot_stride must be a multiple of 16 >= slot_stride_min (" +
-                                          std::to_string(E->stride_min) + ")");
+// Device-side preparation of a planned batch on stream s: bind the encoder to
+// the current device, order s after its previous batch (which writes the
+// carry area and blob buffer this one reads), grow the carry buffer the batch
+// fills and create the blob buffer.
+int prepare_run(rsmi_fenc *E, hipStream_t s) {
     int cur;
     if (hipGetDevice(&cur) != hipSuccess) return fail(RSMI_ERR_HIP, "fenc: no usable GPU");
     if (E->device < 0) {
@@ -634,9 +632,6 @@ int run_dev(rsmi_fenc *E, uint8_t *slots, int64_t S, void *stream, const CookSpe
     } else if (cur != E->device) {
         return fail(RSMI_ERR_INVALID, "rsmi_fenc_run_dev on another device than the encoder's");
     }
-    hipStream_t s = (hipStream_t)stream;
-    // the previous batch (other set) writes the carry area and blob buffer this
-    // one reads: order after it even when it ran on another stream
     PlanSet &prev = E->ps[E->pcur ^ 1];
     if (prev.in_flight && hipStreamWaitEvent(s, prev.done, 0) != hipSuccess)
         return fail(RSMI_ERR_HIP, "fenc: hipStreamWaitEvent");
@@ -646,16 +641,30 @@ int run_dev(rsmi_fenc *E, uint8_t *slots, int64_t S, void *stream, const CookSpe
         int rcw = wait_set(prev);
         if (rcw) return rcw;
     }
-    // carry buffer this batch fills; resolve tagged carry offsets
-    int rc0 = grow(&E->dcarry[E->carry_cur], &E->carry_cap[E->carry_cur], E->carry_need, false);
-    if (rc0) return rc0;
-    const rsmi::CarryBase carry{{E->dcarry[0], E->dcarry[1]}};
+    int rc = grow(&E->dcarry[E->carry_cur], &E->carry_cap[E->carry_cur], E->carry_need, false);
+    if (rc) return rc;
     if (!E->dshadow) {
         if (hipMalloc(&E->dshadow, rsmi::kBlobBufBytes) != hipSuccess)
             return fail(RSMI_ERR_NOMEM, "fenc: hipMalloc(blob buffer)");
         if (hipMemsetAsync(E->dshadow, 0, rsmi::kBlobBufBytes, s) != hipSuccess)
             return fail(RSMI_ERR_HIP, "fenc: clear blob buffer");
     }
+    return RSMI_OK;
+}
+
+int run_dev(rsmi_fenc *E, uint8_t *slots, int64_t S, void *stream, const CookSpec *ck) {
+    if (!E || !E->planned) return fail(RSMI_ERR_INVALID, "rsmi_fenc_run_dev without a plan");
+    if (E->plan_only) return fail(RSMI_ERR_INVALID, "rsmi_fenc_run_dev on a plan-only encoder");
+    if (E->n_slots && (!slots || ((uintptr_t)slots & 15)))
+        return fail(RSMI_ERR_INVALID, "slots_base must be 16-aligned");
+    if (S % 16 || S < E->stride_min)
+        return fail(RSMI_ERR_INVALID, "slot_stride must be a multiple of 16 >= slot_stride_min (" +
+                                          std::to_string(E->stride_min) + ")");
+    hipStream_t s = (hipStream_t)stream;
+    int rc0 = prepare_run(E, s);
+    if (rc0) return rc0;
+    PlanSet &prev = E->ps[E->pcur ^ 1];
+    const rsmi::CarryBase carry{{E->dcarry[0], E->dcarry[1]}};
     // cooked runs: the packet list goes up with the plan (the cook kernel reads
     // each packet's slot and length from it)
     const size_t npk = ck ? E->P->packets.size() : 0;
@@ -718,3 +727,249 @@ int run_dev(rsmi_fenc *E, uint8_t *slots, int64_t S, void *stream, const CookSpe
 }
 
 }  // namespace
+
+// ---- the collector: many managers' planned batches as one launch set --------
+//
+// A server keeps one fec_encode_manager_t per connection (connection.h:244-245),
+// up to max_conn_num = 200 (common.h:112), each flushing on its own 8 ms timer
+// (fec_manager.h:30): every flush is a handful of groups.  Run one by one,
+// 200 managers cost 200 small launch sequences.  rsmi_fenc_run_many takes
+// the managers' plans as they are (each planned on its own state, exactly as
+// rsmi_fenc_plan does for one) and runs their byte work together: one k_frame
+// over every manager's jobs, one stale-byte pass, one encode launch per
+// (k, n) code over all managers' groups of that code, one blob-buffer update,
+// one carry pass and one cook.  For that the managers' slots are laid out in
+// one array, groups bucketed by code (so a bucket is a uniform batch for the
+// bit-sliced encoders; its shard length is the bucket's longest, and a
+// shorter group's parity bytes past its own fec_len are never sent), and
+// every slot reference of the plans is remapped: rsmi_fenc_packets /
+// rsmi_fenc_groups then report slots of the shared array.  Carry-tagged
+// addresses and blob-buffer locations are resolved to absolute device
+// addresses, since each manager has its own buffers.
+struct rsmi_fcol {
+    struct Set {
+        HostArr<FrameGroup> jobs;
+        HostArr<FrameSrc> srcs;
+        HostArr<CarryCopy> carry;
+        HostArr<rsmi::ByteRun> stale, upd;
+        HostArr<rsmi_fenc_packet> packets;
+        hipEvent_t done = nullptr;
+        bool in_flight = false;
+    } set[2];
+    int cur = 0;
+    int device = -1;
+    uint8_t *dplan[2] = {nullptr, nullptr};
+    size_t plan_cap[2] = {0, 0};
+};
+
+extern "C" {
+
+int rsmi_fcol_create(rsmi_fcol **out) {
+    if (!out) return fail(RSMI_ERR_INVALID, "null out");
+    *out = new rsmi_fcol();
+    return RSMI_OK;
+}
+
+void rsmi_fcol_destroy(rsmi_fcol *C) {
+    if (!C) return;
+    for (auto &B : C->set) {
+        if (B.in_flight) (void)hipEventSynchronize(B.done);
+        if (B.done) (void)hipEventDestroy(B.done);
+    }
+    for (int i = 0; i < 2; ++i)
+        if (C->dplan[i]) (void)hipFree(C->dplan[i]);
+    delete C;
+}
+
+int rsmi_fenc_run_many(rsmi_fcol *C, rsmi_fenc *const *enc, int32_t n, uint8_t *slots, int64_t S,
+                       const rsmi_cook_ctx *ctx, uint64_t seed, uint8_t *out, int32_t *out_len,
+                       void *stream) {
+    if (!C || n < 0 || (n && !enc)) return fail(RSMI_ERR_INVALID, "rsmi_fenc_run_many: bad arguments");
+    int64_t total_slots = 0, total_pk = 0;
+    for (int i = 0; i < n; ++i) {
+        rsmi_fenc *E = enc[i];
+        if (!E || !E->planned) return fail(RSMI_ERR_INVALID, "rsmi_fenc_run_many: encoder without a plan");
+        if (E->plan_only) return fail(RSMI_ERR_INVALID, "rsmi_fenc_run_many: plan-only encoder");
+        for (int j = 0; j < i; ++j)
+            if (enc[j] == E) return fail(RSMI_ERR_INVALID, "rsmi_fenc_run_many: an encoder listed twice");
+        if (S % 16 || S < E->stride_min)
+            return fail(RSMI_ERR_INVALID, "slot_stride must be a multiple of 16 >= every encoder's "
+                                          "slot_stride_min (" + std::to_string(E->stride_min) + ")");
+        total_slots += E->n_slots;
+        total_pk += (int64_t)E->P->packets.size();
+    }
+    if (total_slots && (!slots || ((uintptr_t)slots & 15)))
+        return fail(RSMI_ERR_INVALID, "slots_base must be 16-aligned");
+    if (ctx && total_pk && !out_len) return fail(RSMI_ERR_INVALID, "rsmi_fenc_run_many: null out_len");
+    if (out && ((uintptr_t)out & 15)) return fail(RSMI_ERR_INVALID, "cooked out must be 16-aligned");
+    hipStream_t s = (hipStream_t)stream;
+    int cur;
+    if (hipGetDevice(&cur) != hipSuccess) return fail(RSMI_ERR_HIP, "fcol: no usable GPU");
+    if (C->device < 0) {
+        for (auto &B : C->set)
+            if (hipEventCreateWithFlags(&B.done, hipEventDisableTiming) != hipSuccess)
+                return fail(RSMI_ERR_HIP, "fcol: hipEventCreate");
+        C->device = cur;
+    } else if (C->device != cur) {
+        return fail(RSMI_ERR_INVALID, "rsmi_fenc_run_many on another device than the collector's");
+    }
+    for (int i = 0; i < n; ++i) {
+        int rc = prepare_run(enc[i], s);
+        if (rc) return rc;
+    }
+    // the other set's upload may still read its pinned arrays: refill this one
+    C->cur ^= 1;
+    rsmi_fcol::Set &B = C->set[C->cur];
+    if (B.in_flight) {
+        if (hipEventSynchronize(B.done) != hipSuccess) return fail(RSMI_ERR_HIP, "fcol: wait");
+        B.in_flight = false;
+    }
+    // ---- slot layout: every group bucketed by code, then the lone mode-1 slots
+    struct Bucket {
+        int k, nn, len;
+        int64_t count, slot0;
+    };
+    std::map<int, Bucket> buckets;  // key k * 257 + n
+    for (int i = 0; i < n; ++i) {
+        const rsmi_fenc *E = enc[i];
+        for (size_t g = 0; g < E->g_k.size(); ++g) {
+            const int k = E->g_k[g], nn = k + E->g_m[g];
+            Bucket &b = buckets.emplace(k * 257 + nn, Bucket{k, nn, 0, 0, 0}).first->second;
+            b.count += 1;
+            b.len = std::max(b.len, (int)E->g_len[g]);
+        }
+    }
+    {
+        int64_t next = 0;
+        for (auto &kv : buckets) {
+            kv.second.slot0 = next;
+            next += kv.second.count * kv.second.nn;
+        }
+    }
+    std::vector<std::vector<int64_t>> smap((size_t)n);
+    {
+        std::map<int, int64_t> fill;
+        int64_t lone = 0;
+        for (auto &kv : buckets) lone += kv.second.count * kv.second.nn;
+        for (int i = 0; i < n; ++i) {
+            rsmi_fenc *E = enc[i];
+            std::vector<int64_t> &m = smap[(size_t)i];
+            m.assign((size_t)E->n_slots, -1);
+            int64_t gend = 0;
+            for (size_t g = 0; g < E->g_k.size(); ++g) {
+                const int k = E->g_k[g], nn = k + E->g_m[g];
+                const Bucket &b = buckets[k * 257 + nn];
+                int64_t &f = fill[k * 257 + nn];
+                const int64_t ns0 = b.slot0 + f * nn;
+                f += 1;
+                for (int j = 0; j < nn; ++j) m[(size_t)(E->g_slot0[g] + j)] = ns0 + j;
+                gend = std::max(gend, E->g_slot0[g] + nn);
+                E->g_slot0[g] = ns0;  // rsmi_fenc_groups reports the shared array
+            }
+            for (int64_t sl = 0; sl < E->n_slots; ++sl)
+                if (m[(size_t)sl] < 0) m[(size_t)sl] = lone++;  // mode-1 packets sent ahead of a group
+        }
+    }
+    // ---- the combined plan, every reference rewritten
+    B.jobs.clear(); B.srcs.clear(); B.carry.clear(); B.stale.clear(); B.upd.clear(); B.packets.clear();
+    auto resolve = [](const rsmi_fenc *E, uint64_t a) -> uint64_t {
+        return (a & kCarryTag) ? (uint64_t)(uintptr_t)(E->dcarry[(a & kCarryBuf1) ? 1 : 0]) + (a & rsmi::kCarryOff)
+                               : a;
+    };
+    auto loc = [](const rsmi_fenc *E, const std::vector<int64_t> &m, uint64_t l) -> uint64_t {
+        return (l & rsmi::kShadowLoc) ? (rsmi::kAbsLoc | (uint64_t)(uintptr_t)E->dshadow)
+                                      : (uint64_t)m[(size_t)l];
+    };
+    for (int i = 0; i < n; ++i) {
+        rsmi_fenc *E = enc[i];
+        const std::vector<int64_t> &m = smap[(size_t)i];
+        const uint32_t src0 = (uint32_t)B.srcs.size();
+        for (size_t j = 0; j < E->P->srcs.size(); ++j) {
+            FrameSrc f = E->P->srcs[j];
+            f.addr = resolve(E, f.addr);
+            B.srcs.push_back(f);
+        }
+        for (size_t j = 0; j < E->P->jobs.size(); ++j) {
+            FrameGroup G = E->P->jobs[j];
+            G.slot0 = (uint64_t)m[(size_t)G.slot0];  // a group's slots stay contiguous
+            G.src0 += src0;
+            B.jobs.push_back(G);
+        }
+        for (size_t j = 0; j < E->P->carry.size(); ++j) {
+            CarryCopy c = E->P->carry[j];
+            c.src = resolve(E, c.src);
+            c.dst = resolve(E, c.dst);
+            B.carry.push_back(c);
+        }
+        for (size_t j = 0; j < E->P->stale.size(); ++j) {
+            rsmi::ByteRun r = E->P->stale[j];
+            r.dst = loc(E, m, r.dst);
+            r.src = loc(E, m, r.src);
+            B.stale.push_back(r);
+        }
+        for (size_t j = 0; j < E->P->shadow_upd.size(); ++j) {
+            rsmi::ByteRun r = E->P->shadow_upd[j];
+            r.dst = loc(E, m, r.dst);
+            r.src = loc(E, m, r.src);
+            B.upd.push_back(r);
+        }
+        for (size_t j = 0; j < E->P->packets.size(); ++j) {
+            rsmi_fenc_packet &p = E->P->packets[j];
+            p.slot = m[(size_t)p.slot];  // rsmi_fenc_packets reports the shared array
+            if (ctx) B.packets.push_back(p);
+        }
+    }
+    // ---- upload + launches
+    const size_t gb = B.jobs.size() * sizeof(FrameGroup), sb = B.srcs.size() * sizeof(FrameSrc),
+                 cb = B.carry.size() * sizeof(CarryCopy), rb = B.stale.size() * sizeof(rsmi::ByteRun),
+                 ub = B.upd.size() * sizeof(rsmi::ByteRun), pb = B.packets.size() * sizeof(rsmi_fenc_packet);
+    const size_t go = 0, so = (gb + 255) & ~size_t(255), co = (so + sb + 255) & ~size_t(255),
+                 ro = (co + cb + 255) & ~size_t(255), uo = (ro + rb + 255) & ~size_t(255),
+                 po = (uo + ub + 255) & ~size_t(255);
+    int rc = grow(&C->dplan[C->cur], &C->plan_cap[C->cur], po + pb + 16, false);
+    if (rc) return rc;
+    uint8_t *dp = C->dplan[C->cur];
+    hipError_t e = hipSuccess;
+    if (gb) e = hipMemcpyAsync(dp + go, B.jobs.p, gb, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess && sb) e = hipMemcpyAsync(dp + so, B.srcs.p, sb, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess && cb) e = hipMemcpyAsync(dp + co, B.carry.p, cb, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess && rb) e = hipMemcpyAsync(dp + ro, B.stale.p, rb, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess && ub) e = hipMemcpyAsync(dp + uo, B.upd.p, ub, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess && pb) e = hipMemcpyAsync(dp + po, B.packets.p, pb, hipMemcpyHostToDevice, s);
+    const rsmi::CarryBase none{{nullptr, nullptr}};  // every address is absolute now
+    if (e == hipSuccess)
+        e = rsmi::launch_frame(reinterpret_cast<const FrameGroup *>(dp + go), (int64_t)B.jobs.size(),
+                               reinterpret_cast<const FrameSrc *>(dp + so), none, slots, S, s);
+    if (e == hipSuccess)
+        e = rsmi::launch_byte_runs(reinterpret_cast<const rsmi::ByteRun *>(dp + ro), (int64_t)B.stale.size(),
+                                   slots, S, nullptr, s);
+    if (e != hipSuccess) return fail(RSMI_ERR_HIP, std::string("fcol frame: ") + hipGetErrorString(e));
+    for (auto &kv : buckets) {
+        const Bucket &b = kv.second;
+        if (b.nn == b.k || b.count == 0) continue;  // no parity (y = 0)
+        rc = rsmi_encode_dev(b.k, b.nn, slots + b.slot0 * S + rsmi::kSlotShard, (int64_t)b.nn * S, S, b.len,
+                             b.count, stream);
+        if (rc) return rc;
+    }
+    e = rsmi::launch_byte_runs(reinterpret_cast<const rsmi::ByteRun *>(dp + uo), (int64_t)B.upd.size(), slots, S,
+                               nullptr, s);
+    if (e == hipSuccess)
+        e = rsmi::launch_carry(reinterpret_cast<const CarryCopy *>(dp + co), (int64_t)B.carry.size(), none, s);
+    if (e != hipSuccess) return fail(RSMI_ERR_HIP, std::string("fcol carry: ") + hipGetErrorString(e));
+    if (ctx && pb) {
+        rc = rsmi::cook_packets(ctx, slots, S, reinterpret_cast<const rsmi_fenc_packet *>(dp + po),
+                                (int64_t)B.packets.size(), out_len, out, seed, s);
+        if (rc) return rc;
+    }
+    if (hipEventRecord(B.done, s) != hipSuccess) return fail(RSMI_ERR_HIP, "fcol: event");
+    B.in_flight = true;
+    for (int i = 0; i < n; ++i) {
+        rsmi_fenc *E = enc[i];
+        if (hipEventRecord(E->P->done, s) != hipSuccess) return fail(RSMI_ERR_HIP, "fenc event");
+        E->P->in_flight = true;
+        E->planned = false;
+    }
+    return RSMI_OK;
+}
+
+}  // extern "C"

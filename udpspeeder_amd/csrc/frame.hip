@@ -350,8 +350,9 @@ __global__ __launch_bounds__(kThreads) void k_byte_runs(const ByteRun *runs, int
     const int lane = threadIdx.x & 63;
     const int64_t w0 = (int64_t)blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
     auto at = [&](uint64_t loc, uint32_t off) {
-        return (loc & kShadowLoc) ? shadow + off
-                                  : slots + (int64_t)loc * slot_stride + kSlotShard + off;
+        if (loc & kShadowLoc) return shadow + off;
+        if (loc & kAbsLoc) return reinterpret_cast<uint8_t *>((uintptr_t)(loc & ~kAbsLoc)) + off;
+        return slots + (int64_t)loc * slot_stride + kSlotShard + off;
     };
     for (int64_t w = w0; w < nruns; w += (int64_t)gridDim.x * (kThreads / 64)) {
         const ByteRun R = runs[w];

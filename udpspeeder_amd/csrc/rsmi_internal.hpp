@@ -293,6 +293,9 @@ hipError_t launch_gather(const GatherCopy *jobs, int64_t njobs, CarryBase carry,
 // location is a slot index (byte slots + slot*stride + kSlotShard + off) or,
 // with kShadowLoc, the buffer itself (byte shadow + off).
 constexpr uint64_t kShadowLoc = 1ull << 63;
+// ... or, with kAbsLoc, an absolute device address (the collector's runs over
+// many encoders, each with its own blob buffer: rsmi_fenc_run_many).
+constexpr uint64_t kAbsLoc = 1ull << 62;
 constexpr int kBlobBufBytes = (255 + 5) * 3800;  // blob_encode_t::input_buf, fec_manager.h:257
 struct ByteRun {
     uint64_t dst, src;

@@ -170,6 +170,14 @@ class FecEncoder:
               "rsmi_fenc_run_cooked_dev")
         return out_len
 
+    def packets_now(self):
+        """The last plan's packet list as it stands now (after
+        FecCollector.run_many: slots of the shared slot array)."""
+        pk = (rsmi_fenc_packet * max(1, len(self._last_packets)))()
+        check(lib().rsmi_fenc_packets(self._h, pk), "rsmi_fenc_packets")
+        dt = np.dtype([("slot", np.int64), ("len", np.int32), ("event", np.int32)])
+        return np.frombuffer(bytes(pk), dt)[:len(self._last_packets)].copy()
+
     @staticmethod
     def slot_stride_for(fec_len_max: int) -> int:
         """A multiple of 128 that fits fec_len_max-byte shards and do_cook's
@@ -291,3 +299,79 @@ class FecDecoder:
         """fec_decode_manager_t::output: the packets the last input() produced."""
         r, self._ready = getattr(self, "_ready", []), []
         return r
+
+
+class FecCollector:
+    """rsmi_fenc_run_many: many connections' encoders (each planned on its own
+    state with FecEncoder.plan) run as one launch set over one slot array
+    (include/rsmi_fec.h, "the collector").  After run_many each encoder's
+    packets_now() lists its packets at slots of the shared array."""
+
+    def __init__(self):
+        h = C.c_void_p()
+        check(lib().rsmi_fcol_create(C.byref(h)), "rsmi_fcol_create")
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().rsmi_fcol_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def run_many(self, encoders, slots, slot_stride: int, cook=None, seed: int = 0, out=None,
+                 out_len=None, stream=None):
+        """Frame + encode (+ do_cook into `out`, None: in place) every encoder's
+        planned batch on `stream`.  slots: CUDA uint8 of >= sum(n_slots) *
+        slot_stride bytes.  With cook, returns the int32 cooked lengths of all
+        packets, the encoders' lists concatenated in order."""
+        import torch
+        s = stream if stream is not None else torch.cuda.current_stream()
+        n_slots = sum(e._last_nslots for e in encoders)
+        n_pk = sum(len(e._last_packets) for e in encoders)
+        if slots.numel() < n_slots * int(slot_stride):
+            raise ValueError(f"slots holds {slots.numel()} bytes; the encoders need {n_slots * slot_stride}")
+        if cook is not None and out_len is None:
+            out_len = torch.empty(max(n_pk, 1), dtype=torch.int32, device="cuda")
+        if out is not None and out.numel() < n_slots * int(slot_stride):
+            raise ValueError("out is shorter than the shared slot array")
+        arr = (C.c_void_p * max(1, len(encoders)))(*[e._h.value for e in encoders])
+        check(lib().rsmi_fenc_run_many(self._h, arr, len(encoders),
+                                       slots.data_ptr() if slots.numel() else None, int(slot_stride),
+                                       cook._h if cook is not None else None, C.c_uint64(seed & (2**64 - 1)),
+                                       out.data_ptr() if out is not None else None,
+                                       out_len.data_ptr() if out_len is not None else None, s.cuda_stream),
+              "rsmi_fenc_run_many")
+        return out_len
+
+
+class FecDecodeCollector:
+    """rsmi_fdec_run_many: many connections' decoders (each planned on its own
+    state with FecDecoder.plan) run as one launch set; afterwards each
+    decoder's outputs() works as after its own run()."""
+
+    def __init__(self):
+        h = C.c_void_p()
+        check(lib().rsmi_fdcol_create(C.byref(h)), "rsmi_fdcol_create")
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().rsmi_fdcol_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def run_many(self, decoders, stream=None):
+        import torch
+        s = stream if stream is not None else torch.cuda.current_stream()
+        arr = (C.c_void_p * max(1, len(decoders)))(*[d._h.value for d in decoders])
+        check(lib().rsmi_fdec_run_many(self._h, arr, len(decoders), s.cuda_stream), "rsmi_fdec_run_many")
