@@ -97,6 +97,15 @@ int rsmi_cook_to(const rsmi_cook_ctx *ctx, const rsmi_packet_batch *batch, uint8
 int rsmi_decook_to(const rsmi_cook_ctx *ctx, const rsmi_packet_batch *batch, uint8_t *out,
                    void *stream);
 
+/* rsmi_decook_dev (in place in the batch), with every packet's de-cooked
+ * bytes (whole 16-byte pieces up to round_up(len, 16)) also stored at the same
+ * offset of mirror: pinned host memory, typically the receive buffer the
+ * batch was copied from.  The receive side: the device keeps the de-cooked
+ * packets for the FEC gather, the host gets them for the decode planner and
+ * the outputs, and only packet bytes cross PCIe -- no whole-batch D2H copy. */
+int rsmi_decook_mirror(const rsmi_cook_ctx *ctx, const rsmi_packet_batch *batch, uint8_t *mirror,
+                       void *stream);
+
 /* Synchronous host-memory forms (one H2D, one launch, one D2H; packet i at
  * host + i*stride): the per-packet mirror of do_cook/de_cook for callers that
  * have not moved to device batches. */

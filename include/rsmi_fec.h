@@ -137,6 +137,20 @@ int rsmi_fenc_run_cooked_dev(rsmi_fenc *enc, uint8_t *slots_base, int64_t slot_s
                              const struct rsmi_cook_ctx *ctx, uint64_t seed, uint8_t *out,
                              int32_t *out_len, void *stream);
 
+/* Bytes a packet of len bytes takes in a packed cooked output: its cooked
+ * form (crc 4 + iv <= 32 + iv_len 1 more) rounded up to whole 16-byte pieces. */
+#define RSMI_FEC_COOK_SPAN(len) ((((int64_t)(len)) + 37 + 15) & ~(int64_t)15)
+
+/* rsmi_fenc_run_cooked_dev with the cooked packets packed back to back, so the
+ * buffer handed to the socket (or copied to the host for sendmmsg) holds only
+ * packet bytes: packet p at out + sum over q < p of RSMI_FEC_COOK_SPAN(len_q)
+ * (len from rsmi_fenc_packets), out_len[p] cooked bytes.  out: device or
+ * pinned host memory, 16-aligned, out_cap >= that sum over all packets
+ * (RSMI_ERR_INVALID otherwise).  Every packet fits (out_len >= 0). */
+int rsmi_fenc_run_cooked_packed_dev(rsmi_fenc *enc, uint8_t *slots_base, int64_t slot_stride,
+                                    const struct rsmi_cook_ctx *ctx, uint64_t seed, uint8_t *out,
+                                    int64_t out_cap, int32_t *out_len, void *stream);
+
 /* ---- the collector: many connections' managers in one launch set -----------
  *
  * A server keeps one manager per connection (connection.h:244-245), up to

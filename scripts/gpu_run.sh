@@ -10,6 +10,8 @@
 #                then the trace split by grid size (kernel_by_grid.txt)
 #   c3           scripts/bench_c3.py (c3.json)
 #   py:SCRIPT    python SCRIPT (SCRIPT.log), e.g. py:scripts/bench_cook.py
+#   kt:SCRIPT[,ARG...]  SCRIPT under rocprofv3 --kernel-trace --memory-copy-trace
+#                --stats (kt_<script>/: kernel and copy stats, script log)
 set -o pipefail
 R=$PWD
 O=$R/gpurun_out/$1
@@ -49,6 +51,14 @@ for step in "$@"; do
       f=${step#py:}
       timeout -k 10 400 python -u $f > $O/$(basename $f).log 2>&1 || { tail $O/$(basename $f).log; exit 1; }
       tail -20 $O/$(basename $f).log ;;
+    kt:*)
+      IFS=',' read -ra A <<< "${step#kt:}"
+      d=$O/kt_$(basename ${A[0]} .py)
+      (cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --memory-copy-trace --stats \
+          --output-format csv -d $d -o run -- python3 $R/${A[0]} "${A[@]:1}" > $d.log 2>&1) || { tail $d.log; exit 1; }
+      python scripts/kstats.py $d/run_kernel_stats.csv | head -25
+      rm -f $d/run_kernel_trace.csv $d/run_memory_copy_trace.csv
+      tail -5 $d.log ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

@@ -243,11 +243,14 @@ def test_gpu_per_call_interface(gpu):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", NAMES)
-@pytest.mark.parametrize("nbatch,host", [(1, True), (3, False)])
-def test_gpu_frames_cooked_match_reference(fx, gpu, cook_oracle, name, nbatch, host):
+@pytest.mark.parametrize("nbatch,host,packed", [(1, True, False), (3, False, False), (2, False, True),
+                                                (1, True, True)])
+def test_gpu_frames_cooked_match_reference(fx, gpu, cook_oracle, name, nbatch, host, packed):
     """rsmi_fenc_run_cooked_dev: framing + encode + do_cook in one run, cooked
     packets written straight into pinned host memory (or another device
-    buffer).  IVs are the device draw of (seed, packet index), so every cooked
+    buffer), in the slot layout or packed back to back
+    (rsmi_fenc_run_cooked_packed_dev).  IVs are the device draw of (seed,
+    packet index), so every cooked
     packet is checked byte for byte against the oracle's do_cook of the
     reference manager's packet (tests/golden/fec_encode.npz) where the fixture
     holds full bytes, and through the oracle's de_cook against the fixture's
@@ -274,19 +277,28 @@ def test_gpu_frames_cooked_match_reference(fx, gpu, cook_oracle, name, nbatch, h
                 o += len(ev[i])
         inbuf = torch.from_numpy(np.frombuffer(b"".join(chunks) + bytes(32), np.uint8).copy()).cuda()
         p = enc.plan(lens[a:b], offs, inbuf)
-        S = FecEncoder.slot_stride_for(max(p.slot_stride_min - 128, 0))
+        # packed: the smallest legal stride (the packed output needs no tail room)
+        S = p.slot_stride_min if packed else FecEncoder.slot_stride_for(max(p.slot_stride_min - 128, 0))
         slots = torch.full((max(1, p.n_slots) * S,), 0xEE, dtype=torch.uint8, device="cuda")
-        out = torch.zeros(max(1, p.n_slots) * S, dtype=torch.uint8)
+        if packed:
+            po, ptot = enc.packed_offsets()
+            out = torch.zeros(max(ptot, 16), dtype=torch.uint8)
+        else:
+            out = torch.zeros(max(1, p.n_slots) * S, dtype=torch.uint8)
         out = out.pin_memory() if host else out.cuda()
         seed = 1000 + bi
-        ol = enc.run_cooked(slots, S, ctx, seed, out=out)
+        if packed:
+            ol = enc.run_cooked_packed(slots, S, ctx, seed, out)
+        else:
+            ol = enc.run_cooked(slots, S, ctx, seed, out=out)
         torch.cuda.synchronize()
         ol = ol.cpu().numpy()[:len(p.packets)]
         h = out.cpu().numpy()
         iv, ivl = device_ivs(seed, 0, len(p.packets))
         for i, (s, ln, _) in enumerate(p.packets):
             assert ol[i] == ln + 4 + ivl[i] + 1, (bi, i)
-            cooked.append(h[s * S + 120:s * S + 120 + ol[i]].tobytes())
+            o = int(po[i]) if packed else s * S + 120
+            cooked.append(h[o:o + ol[i]].tobytes())
             ivs.append(iv[i, :ivl[i]].tobytes())
         del inbuf
     assert len(cooked) == len(c["pk_len"])

@@ -321,3 +321,42 @@ def test_out_of_place_and_pinned_host(gpu, cook_oracle, host):
     back = dec.cpu().numpy().reshape(npk, stride)
     for j in range(npk):
         assert (back[j, :lens[j]] == buf[j, :lens[j]]).all(), j
+
+
+@pytest.mark.gpu
+def test_decook_mirror_to_pinned_host(gpu, cook_oracle):
+    """rsmi_decook_mirror: de_cook in place on the device and the same bytes
+    into a pinned host buffer (the tunnel's receive side), including packets
+    whose de_cook fails (a flipped byte): the host copy equals the device's
+    in-place result wherever de_cook wrote, and the payloads equal the input."""
+    import torch
+    from udpspeeder_amd.cook import CookContext
+    rng = np.random.default_rng(77)
+    npk, stride, key = 257, 1408, b"mirror-key"
+    lens = rng.integers(0, 1340, npk).astype(np.int32)
+    lens[:3] = [0, 1, 16]
+    buf = rng.integers(0, 256, (npk, stride), dtype=np.uint8)
+    iv, ivl = cook_ivs(9, 0, npk)
+    ref, out_ref = _oracle_cook(cook_oracle, buf, lens, iv, ivl, key, 0)
+    bad = rng.choice(npk, 20, replace=False)
+    for j in bad:
+        ref[j, rng.integers(0, out_ref[j])] ^= 0x40
+    ctx = CookContext(key)
+    d = torch.from_numpy(ref.reshape(-1).copy()).to(gpu)
+    host = torch.full((npk * stride,), 0x5A, dtype=torch.uint8).pin_memory()
+    ln = torch.from_numpy(out_ref.astype(np.int32)).to(gpu)
+    ol = ctx.decook_mirror(d, ln, host, cap=stride, stride=stride).cpu().numpy()
+    torch.cuda.synchronize()
+    dev = d.cpu().numpy().reshape(npk, stride)
+    h = host.numpy().reshape(npk, stride)
+    for j in range(npk):
+        e = (int(out_ref[j]) + 15) // 16 * 16
+        assert (h[j, :e] == dev[j, :e]).all(), j
+        assert (h[j, e:] == 0x5A).all(), j  # nothing past the packet's pieces
+        if j in bad:
+            continue
+        assert ol[j] == lens[j], j
+        assert (h[j, :lens[j]] == buf[j, :lens[j]]).all(), j
+    rc = [cook_oracle.de_cook(ref[j, :out_ref[j]].tobytes(), key)[0] for j in bad]
+    assert [int(ol[j]) < 0 for j in bad] == [r != 0 for r in rc]
+

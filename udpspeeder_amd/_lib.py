@@ -124,6 +124,7 @@ def _bind(lib: C.CDLL) -> C.CDLL:
         "rsmi_decook_dev": ([vp, vp, vp], i32),
         "rsmi_cook_to": ([vp, vp, vp, vp, vp, C.c_uint64, vp], i32),
         "rsmi_decook_to": ([vp, vp, vp, vp], i32),
+        "rsmi_decook_mirror": ([vp, vp, vp, vp], i32),
         "rsmi_cook_host": ([vp, vp, i64, i64, C.c_int32, vp, vp, vp, vp, C.c_uint64], i32),
         "rsmi_decook_host": ([vp, vp, i64, i64, C.c_int32, vp, vp], i32),
         "rsmi_fec_config_init": ([vp, C.c_char_p, i32, i32, i32], i32),
@@ -135,6 +136,7 @@ def _bind(lib: C.CDLL) -> C.CDLL:
         "rsmi_fenc_groups": ([vp, vp, vp, vp, vp, vp, vp], i32),
         "rsmi_fenc_run_dev": ([vp, vp, i64, vp], i32),
         "rsmi_fenc_run_cooked_dev": ([vp, vp, i64, vp, C.c_uint64, vp, vp, vp], i32),
+        "rsmi_fenc_run_cooked_packed_dev": ([vp, vp, i64, vp, C.c_uint64, vp, i64, vp, vp], i32),
         "rsmi_fcol_create": ([vp], i32),
         "rsmi_fcol_destroy": ([vp], None),
         "rsmi_fenc_run_many": ([vp, vp, C.c_int32, vp, i64, vp, C.c_uint64, vp, vp, vp], i32),

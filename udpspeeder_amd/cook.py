@@ -143,6 +143,16 @@ class CookContext:
                                  C.c_uint64(seed & (2**64 - 1)), _stream_ptr(stream)), "rsmi_cook_to")
         return out_len
 
+    def decook_mirror(self, buf, lens, mirror, *, cap: int, stride: Optional[int] = None, offsets=None,
+                      out_len=None, stream=None):
+        """de_cook every packet of buf in place and store its de-cooked bytes
+        (16-byte pieces up to round_up(len, 16)) at the same offset of
+        `mirror`, pinned host memory (rsmi_decook_mirror).  Returns out_len."""
+        b, out_len = self._batch(buf, lens, out_len, stride, offsets, cap)
+        check(lib().rsmi_decook_mirror(self._h, C.byref(b), self._out_ptr(mirror, self._extent(buf, b)),
+                                       _stream_ptr(stream)), "rsmi_decook_mirror")
+        return out_len
+
     def decook_to(self, buf, lens, out, *, cap: int, stride: Optional[int] = None, offsets=None,
                   out_len=None, stream=None):
         """de_cook every packet of buf into out at the same offset (rsmi_decook_to);

@@ -384,7 +384,9 @@ __global__ __launch_bounds__(kThreads, COOK_OCC) void k_cook(CookArgs a) {
         int L = -1, ivl = 0;
         const uint64_t po = have ? packet_off(a, pk) : 0u;
         uint8_t *pkt = have ? a.base + po : nullptr;
-        uint8_t *opkt = have ? (a.dst ? a.dst : a.base) + po : nullptr;  // where the output goes
+        uint8_t *opkt = !have ? nullptr
+                        : a.dst_off ? a.dst + a.dst_off[pk]
+                                    : (a.dst ? a.dst : a.base) + po;  // where the output goes
         // round 0 is read up to the packet's cap (every packet owns cap bytes), so
         // these loads fly together with the length load instead of after it
         u32x4 cur[kPpl];
@@ -394,8 +396,10 @@ __global__ __launch_bounds__(kThreads, COOK_OCC) void k_cook(CookArgs a) {
             if (obs) ivl = a.iv ? a.iv_len[pk] : 4 + (int)(splitmix(a.seed, (uint64_t)pk, 0) % 29u);
         }
         const int out = L + (ck ? 4 : 0) + (obs ? ivl + 1 : 0);
+        // (a packed output has room for any iv_len <= RSMI_COOK_IV_MAX)
         const bool ok = have && L >= 0 && L <= RSMI_COOK_MAX_LEN && ivl <= RSMI_COOK_IV_MAX &&
-                        round16(out) <= a.cap && ((uintptr_t)pkt & 3) == 0;
+                        (a.dst_off || round16(out) <= a.cap) && round16(L) <= a.cap &&
+                        ((uintptr_t)pkt & 3) == 0;
         const int ext = ok ? round16(out) : 0;
         const uint32_t magic = ivl ? 0xFFFFFFFFu / (uint32_t)ivl : 0u;
         if (ok && ivl && !a.iv && 8 * hl < ivl) {  // device-drawn IV: 8 bytes per draw, one per lane
@@ -420,7 +424,9 @@ __global__ __launch_bounds__(kThreads, COOK_OCC) void k_cook(CookArgs a) {
         u32x4 dt = {0, 0, 0, 0};                // this lane's tail piece, if any
         int Pt = -1;
         for (int r = 0; r < nrm; ++r) {
-            if (r) load_round(cur, pkt, r, hl, ext);   // rounds past the first (long packets)
+            // rounds past the first (long packets); a packed output's tail may
+            // end past the source slot, whose bytes there are never used
+            if (r) load_round(cur, pkt, r, hl, min(ext, a.cap & ~15));
             const int qr = min(max(Q - 96 * r, 0), 96);
             // pieces at or past every packet's last crc piece in this round:
             // skip their CRC (a wave-uniform branch per piece slot)
@@ -514,12 +520,13 @@ __global__ __launch_bounds__(kThreads, COOK_OCC) void k_decook(CookArgs a) {
         // (de_cook keeps its round-0 loads behind the length: loading up to the
         // cap here spills registers and measured slower)
         int L = -1;
-        uint8_t *pkt = nullptr, *opkt = nullptr;
+        uint8_t *pkt = nullptr, *opkt = nullptr, *mpkt = nullptr;
         if (have) {
             L = packet_len(a, pk);
             const uint64_t po = packet_off(a, pk);
             pkt = a.base + po;
             opkt = (a.dst ? a.dst : a.base) + po;  // where the output goes
+            if (a.mirror) mpkt = a.mirror + po;    // and its copy (the host's)
         }
         const bool ok = have && L >= 0 && L <= RSMI_COOK_MAX_LEN && round16(L) <= a.cap &&
                         ((uintptr_t)pkt & 3) == 0;
@@ -595,6 +602,7 @@ __global__ __launch_bounds__(kThreads, COOK_OCC) void k_decook(CookArgs a) {
                     if (P + 16 <= L1) o = cur[p] ^ mk ^ mi;
                     else o = cur[p] ^ (mk & piece_mask(L - P)) ^ (mi & piece_mask(L1 - P));
                     st_piece(opkt + P, o);
+                    if (mpkt) st_piece(mpkt + P, o);
                 }
                 if (ck && kLpp * p < qr_max) rc.add(T, crc_in(o, P, Lc), p, kLpp * p + hl, qr);
                 if (ivl) ivr = iv_step(ivr, sstep, (uint32_t)ivl);

@@ -232,6 +232,16 @@ extern "C" int rsmi_cook_to(const rsmi_cook_ctx *c, const rsmi_packet_batch *b, 
     return launch(a, c, false, (hipStream_t)stream);
 }
 
+extern "C" int rsmi_decook_mirror(const rsmi_cook_ctx *c, const rsmi_packet_batch *b, uint8_t *mirror,
+                                  void *stream) {
+    if (!c) return fail(RSMI_ERR_INVALID, "null cook context");
+    if (int rc = check_batch(b)) return rc;
+    if (!mirror || ((uintptr_t)mirror & 15)) return fail(RSMI_ERR_INVALID, "mirror must be a 16-aligned pointer");
+    rsmi::CookArgs a = make_args(c, b);
+    a.mirror = mirror;
+    return launch(a, c, true, (hipStream_t)stream);
+}
+
 extern "C" int rsmi_decook_to(const rsmi_cook_ctx *c, const rsmi_packet_batch *b, uint8_t *out,
                               void *stream) {
     if (!c) return fail(RSMI_ERR_INVALID, "null cook context");
@@ -244,10 +254,12 @@ extern "C" int rsmi_decook_to(const rsmi_cook_ctx *c, const rsmi_packet_batch *b
 
 namespace rsmi {
 int cook_packets(const rsmi_cook_ctx *c, uint8_t *slots, int64_t S, const rsmi_fenc_packet *pk,
-                 int64_t npk, int32_t *out_len, uint8_t *dst, uint64_t seed, hipStream_t s) {
+                 int64_t npk, int32_t *out_len, uint8_t *dst, const int64_t *dst_off, uint64_t seed,
+                 hipStream_t s) {
     CookArgs a{};
     a.base = slots;
     a.dst = dst;
+    a.dst_off = dst_off;
     a.pk = pk;
     a.pk_off = kSlotHeader;
     a.stride = S;

@@ -46,6 +46,7 @@ struct Pending {
     uint64_t addr;  // batch-input device address or tagged carry offset
     uint32_t len;
     int64_t emitted;  // mode 1: index in this batch's packet list of its early send, -1 if none
+    int64_t run;      // mode 1: the PacketRun of that send (its slot is set when the group closes)
 };
 
 // A growable array in pinned host memory (plain memory when no device is
@@ -115,7 +116,8 @@ struct PlanSet {
     HostArr<CarryCopy> carry;
     HostArr<rsmi::ByteRun> stale;       // stale bytes of this batch's groups
     HostArr<rsmi::ByteRun> shadow_upd;  // the buffer at the batch end -> dshadow
-    HostArr<rsmi_fenc_packet> packets;  // what output() returns, in order (pinned: cooked runs upload it)
+    HostArr<rsmi_fenc_packet> packets;  // what output() returns, in order (rsmi_fenc_packets)
+    HostArr<rsmi::PacketRun> pruns;     // the same as runs of slots (cooked runs upload these)
     hipEvent_t done = nullptr;
     bool in_flight = false;
 };
@@ -280,7 +282,10 @@ void close_group(rsmi_fenc *E, int k, int m, int fec_len) {
         const Pending &p = E->pend[j];
         E->P->srcs.push_back(FrameSrc{p.addr, p.len, E->cfg.mode == 0 ? off : 0u});
         off += 2 + p.len;
-        if (p.emitted >= 0) E->P->packets[(size_t)p.emitted].slot = slot0 + (int64_t)j;
+        if (p.emitted >= 0) {
+            E->P->packets[(size_t)p.emitted].slot = slot0 + (int64_t)j;
+            E->P->pruns[(size_t)p.run].slot = slot0 + (int64_t)j;
+        }
     }
     E->P->jobs.push_back(G);
     if (E->cfg.mode == 0) stale_runs(E, slot0, k, fec_len, E->blob_len);
@@ -298,6 +303,16 @@ void close_group(rsmi_fenc *E, int k, int m, int fec_len) {
         if (!extend) E->runs.push_back(Run{slot0, 0, k, n, fec_len});
         E->runs.back().count += 1;
     }
+}
+
+// Mode 1: the open group's last input goes out as a data packet now; its slot
+// is known once the group closes (close_group) or the batch ends.
+void emit_data(rsmi_fenc *E, int32_t event) {
+    Pending &p = E->pend.back();
+    p.emitted = (int64_t)E->P->packets.size();
+    p.run = (int64_t)E->P->pruns.size();
+    E->P->packets.push_back(rsmi_fenc_packet{-1, 8 + (int)p.len + 2, event});
+    E->P->pruns.push_back(rsmi::PacketRun{-1, p.emitted, 0, 8 + (int)p.len + 2, 1});
 }
 
 // fec_encode_manager_t::input (fec_manager.cpp:206-447) for one event,
@@ -323,7 +338,7 @@ int input_event(rsmi_fenc *E, int32_t event, bool has, int len, uint64_t addr) {
         delayed = true;
     }
     auto append = [&]() {  // fec_encode_manager_t::append (:174-204)
-        E->pend.push_back(Pending{addr, (uint32_t)len, -1});
+        E->pend.push_back(Pending{addr, (uint32_t)len, -1, -1});
         if (mode == 0) E->blob_len += 2 + len;
     };
     if (has && !delayed) append();
@@ -367,8 +382,7 @@ int input_event(rsmi_fenc *E, int32_t event, bool has, int len, uint64_t addr) {
                 E->P->packets.push_back(rsmi_fenc_packet{-1, 8 + fec_len, event});
         } else {
             if (has) {  // the packet that completed the group goes with the parity (:376-381)
-                E->pend.back().emitted = (int64_t)E->P->packets.size();
-                E->P->packets.push_back(rsmi_fenc_packet{-1, 8 + (int)E->pend.back().len + 2, event});
+                emit_data(E, event);
             }
             for (int i = k; i < k + m; ++i)
                 E->P->packets.push_back(rsmi_fenc_packet{-1, 8 + fec_len, event});
@@ -377,16 +391,17 @@ int input_event(rsmi_fenc *E, int32_t event, bool has, int len, uint64_t addr) {
         close_group(E, k, m, fec_len);
         if (mode == 0) {
             for (int i = 0; i < k + m; ++i) E->P->packets[(size_t)(first_pk + i)].slot = slot0 + i;
+            E->P->pruns.push_back(rsmi::PacketRun{slot0, first_pk, 0, 8 + fec_len, k + m});
         } else {
             int64_t q = first_pk + (has ? 1 : 0);
+            if (m > 0) E->P->pruns.push_back(rsmi::PacketRun{slot0 + k, q, 0, 8 + fec_len, m});
             for (int i = k; i < k + m; ++i) E->P->packets[(size_t)q++].slot = slot0 + i;
         }
         E->seq++;
         E->pend.clear();
         E->blob_len = 4;
     } else if (has && mode == 1) {  // encode_fast_send (:394-429): the data packet goes now
-        E->pend.back().emitted = (int64_t)E->P->packets.size();
-        E->P->packets.push_back(rsmi_fenc_packet{-1, 8 + len + 2, event});
+        emit_data(E, event);
     }
     if (has && delayed) append();  // :436-439
     return 0;
@@ -400,6 +415,7 @@ struct CookSpec {  // rsmi_fenc_run_cooked_dev: do_cook on the batch's packets a
     uint64_t seed;
     uint8_t *out;
     int32_t *out_len;
+    int64_t out_cap;  // >= 0: packed output (rsmi_fenc_run_cooked_packed_dev)
 };
 int run_dev(rsmi_fenc *E, uint8_t *slots, int64_t S, void *stream, const CookSpec *ck);
 }  // namespace
@@ -514,6 +530,7 @@ int rsmi_fenc_plan(rsmi_fenc *E, int64_t n_events, const int32_t *len, const uin
     E->P->srcs.clear();
     E->P->carry.clear();
     E->P->packets.clear();
+    E->P->pruns.clear();
     E->g_slot0.clear();
     E->g_k.clear();
     E->g_m.clear();
@@ -525,7 +542,7 @@ int rsmi_fenc_plan(rsmi_fenc *E, int64_t n_events, const int32_t *len, const uin
     E->P->shadow_upd.clear();
     E->n_slots = 0;
     E->stride_min = rsmi::kSlotShard;
-    for (Pending &p : E->pend) p.emitted = -1;  // sent in an earlier batch
+    for (Pending &p : E->pend) p.emitted = p.run = -1;  // sent in an earlier batch
     for (int64_t i = 0; i < n_events; ++i) {
         const bool has = len[i] >= 0;
         if (has && !in_off) return fail(RSMI_ERR_INVALID, "packet without in_off");
@@ -551,6 +568,7 @@ int rsmi_fenc_plan(rsmi_fenc *E, int64_t n_events, const int32_t *len, const uin
         E->P->srcs.push_back(FrameSrc{p.addr, p.len, 0});
         E->P->jobs.push_back(G);
         E->P->packets[(size_t)p.emitted].slot = slot;
+        E->P->pruns[(size_t)p.run].slot = slot;
         E->stride_min = std::max(E->stride_min, (int32_t)((rsmi::kSlotShard + p.len + 2 + 15) & ~15u));
     }
     shadow_update(E);
@@ -603,7 +621,19 @@ int rsmi_fenc_run_cooked_dev(rsmi_fenc *E, uint8_t *slots, int64_t S, const rsmi
     if (E && E->planned && !E->P->packets.empty() && !out_len)
         return fail(RSMI_ERR_INVALID, "rsmi_fenc_run_cooked_dev: null out_len");
     if (out && ((uintptr_t)out & 15)) return fail(RSMI_ERR_INVALID, "cooked out must be 16-aligned");
-    const CookSpec ck{ctx, seed, out, out_len};
+    const CookSpec ck{ctx, seed, out, out_len, -1};
+    return run_dev(E, slots, S, stream, &ck);
+}
+
+int rsmi_fenc_run_cooked_packed_dev(rsmi_fenc *E, uint8_t *slots, int64_t S, const rsmi_cook_ctx *ctx,
+                                    uint64_t seed, uint8_t *out, int64_t out_cap, int32_t *out_len,
+                                    void *stream) {
+    if (!ctx) return fail(RSMI_ERR_INVALID, "rsmi_fenc_run_cooked_packed_dev: null cook context");
+    if (E && E->planned && !E->P->packets.empty() && (!out_len || !out))
+        return fail(RSMI_ERR_INVALID, "rsmi_fenc_run_cooked_packed_dev: null out / out_len");
+    if (out && ((uintptr_t)out & 15)) return fail(RSMI_ERR_INVALID, "cooked out must be 16-aligned");
+    if (out_cap < 0) return fail(RSMI_ERR_INVALID, "rsmi_fenc_run_cooked_packed_dev: out_cap < 0");
+    const CookSpec ck{ctx, seed, out, out_len, out_cap};
     return run_dev(E, slots, S, stream, &ck);
 }
 
@@ -665,18 +695,31 @@ int run_dev(rsmi_fenc *E, uint8_t *slots, int64_t S, void *stream, const CookSpe
     if (rc0) return rc0;
     PlanSet &prev = E->ps[E->pcur ^ 1];
     const rsmi::CarryBase carry{{E->dcarry[0], E->dcarry[1]}};
-    // cooked runs: the packet list goes up with the plan (the cook kernel reads
-    // each packet's slot and length from it)
-    const size_t npk = ck ? E->P->packets.size() : 0;
+    // cooked runs: the packet list's runs go up with the plan and are expanded
+    // on the device into the (slot, length) list the cook kernel reads
+    const size_t npk = ck ? E->P->packets.size() : 0, nrun = ck ? E->P->pruns.size() : 0;
     const size_t gb = E->P->jobs.size() * sizeof(FrameGroup), sb = E->P->srcs.size() * sizeof(FrameSrc),
                  cb = E->P->carry.size() * sizeof(CarryCopy),
                  rb = E->P->stale.size() * sizeof(rsmi::ByteRun),
                  ub = E->P->shadow_upd.size() * sizeof(rsmi::ByteRun),
-                 pb = npk * sizeof(rsmi_fenc_packet);
+                 pb = nrun * sizeof(rsmi::PacketRun), xb = npk * sizeof(rsmi_fenc_packet);
+    const bool packed = ck && ck->out_cap >= 0;
+    if (packed) {  // each run's first packet's place in the packed output
+        int64_t o = 0;
+        for (size_t i = 0; i < nrun; ++i) {
+            E->P->pruns[i].out0 = o;
+            o += (int64_t)E->P->pruns[i].count * RSMI_FEC_COOK_SPAN(E->P->pruns[i].len);
+        }
+        if (o > ck->out_cap)
+            return fail(RSMI_ERR_INVALID, "rsmi_fenc_run_cooked_packed_dev: out_cap " + std::to_string(ck->out_cap) +
+                                              " < packed bytes " + std::to_string(o));
+    }
+    const size_t db = packed ? npk * sizeof(int64_t) : 0;
     const size_t go = 0, so = (gb + 255) & ~size_t(255), co = (so + sb + 255) & ~size_t(255),
                  ro = (co + cb + 255) & ~size_t(255), uo = (ro + rb + 255) & ~size_t(255),
-                 po = (uo + ub + 255) & ~size_t(255);
-    const size_t all = po + pb + 16;
+                 po = (uo + ub + 255) & ~size_t(255), xo = (po + pb + 255) & ~size_t(255),
+                 dq = (xo + xb + 255) & ~size_t(255);
+    const size_t all = dq + db + 16;
     if (all > E->plan_cap) {
         int rcw = wait_set(prev);
         if (rcw) return rcw;
@@ -690,7 +733,11 @@ int run_dev(rsmi_fenc *E, uint8_t *slots, int64_t S, void *stream, const CookSpe
     if (e == hipSuccess && rb) e = hipMemcpyAsync(E->dplan + ro, E->P->stale.p, rb, hipMemcpyHostToDevice, s);
     if (e == hipSuccess && ub)
         e = hipMemcpyAsync(E->dplan + uo, E->P->shadow_upd.p, ub, hipMemcpyHostToDevice, s);
-    if (e == hipSuccess && pb) e = hipMemcpyAsync(E->dplan + po, E->P->packets.p, pb, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess && pb) e = hipMemcpyAsync(E->dplan + po, E->P->pruns.p, pb, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess)
+        e = rsmi::launch_expand_packets(reinterpret_cast<const rsmi::PacketRun *>(E->dplan + po), (int64_t)nrun,
+                                        reinterpret_cast<rsmi_fenc_packet *>(E->dplan + xo),
+                                        packed ? reinterpret_cast<int64_t *>(E->dplan + dq) : nullptr, s);
     if (e == hipSuccess)
         e = rsmi::launch_frame(reinterpret_cast<const FrameGroup *>(E->dplan + go), (int64_t)E->P->jobs.size(),
                                reinterpret_cast<const FrameSrc *>(E->dplan + so), carry, slots, S, s);
@@ -715,8 +762,9 @@ int run_dev(rsmi_fenc *E, uint8_t *slots, int64_t S, void *stream, const CookSpe
     // do_cook on every packet output() returned (my_send, packet.cpp:165-168),
     // after the blob buffer update above has read the plain shards
     if (npk) {
-        rc = rsmi::cook_packets(ck->ctx, slots, S, reinterpret_cast<const rsmi_fenc_packet *>(E->dplan + po),
-                                (int64_t)npk, ck->out_len, ck->out, ck->seed, s);
+        rc = rsmi::cook_packets(ck->ctx, slots, S, reinterpret_cast<const rsmi_fenc_packet *>(E->dplan + xo),
+                                (int64_t)npk, ck->out_len, ck->out,
+                                packed ? reinterpret_cast<const int64_t *>(E->dplan + dq) : nullptr, ck->seed, s);
         if (rc) return rc;
     }
     e = hipEventRecord(E->P->done, s);
@@ -752,7 +800,7 @@ struct rsmi_fcol {
         HostArr<FrameSrc> srcs;
         HostArr<CarryCopy> carry;
         HostArr<rsmi::ByteRun> stale, upd;
-        HostArr<rsmi_fenc_packet> packets;
+        HostArr<rsmi::PacketRun> pruns;
         hipEvent_t done = nullptr;
         bool in_flight = false;
     } set[2];
@@ -871,7 +919,7 @@ int rsmi_fenc_run_many(rsmi_fcol *C, rsmi_fenc *const *enc, int32_t n, uint8_t *
         }
     }
     // ---- the combined plan, every reference rewritten
-    B.jobs.clear(); B.srcs.clear(); B.carry.clear(); B.stale.clear(); B.upd.clear(); B.packets.clear();
+    B.jobs.clear(); B.srcs.clear(); B.carry.clear(); B.stale.clear(); B.upd.clear(); B.pruns.clear();
     auto resolve = [](const rsmi_fenc *E, uint64_t a) -> uint64_t {
         return (a & kCarryTag) ? (uint64_t)(uintptr_t)(E->dcarry[(a & kCarryBuf1) ? 1 : 0]) + (a & rsmi::kCarryOff)
                                : a;
@@ -880,6 +928,7 @@ int rsmi_fenc_run_many(rsmi_fcol *C, rsmi_fenc *const *enc, int32_t n, uint8_t *
         return (l & rsmi::kShadowLoc) ? (rsmi::kAbsLoc | (uint64_t)(uintptr_t)E->dshadow)
                                       : (uint64_t)m[(size_t)l];
     };
+    int64_t pk_base = 0;
     for (int i = 0; i < n; ++i) {
         rsmi_fenc *E = enc[i];
         const std::vector<int64_t> &m = smap[(size_t)i];
@@ -916,17 +965,25 @@ int rsmi_fenc_run_many(rsmi_fcol *C, rsmi_fenc *const *enc, int32_t n, uint8_t *
         for (size_t j = 0; j < E->P->packets.size(); ++j) {
             rsmi_fenc_packet &p = E->P->packets[j];
             p.slot = m[(size_t)p.slot];  // rsmi_fenc_packets reports the shared array
-            if (ctx) B.packets.push_back(p);
         }
+        if (ctx)
+            for (size_t j = 0; j < E->P->pruns.size(); ++j) {
+                rsmi::PacketRun r = E->P->pruns[j];
+                r.slot = m[(size_t)r.slot];  // a run lies inside one group (or is one lone slot)
+                r.first += pk_base;
+                B.pruns.push_back(r);
+            }
+        pk_base += (int64_t)E->P->packets.size();
     }
     // ---- upload + launches
     const size_t gb = B.jobs.size() * sizeof(FrameGroup), sb = B.srcs.size() * sizeof(FrameSrc),
                  cb = B.carry.size() * sizeof(CarryCopy), rb = B.stale.size() * sizeof(rsmi::ByteRun),
-                 ub = B.upd.size() * sizeof(rsmi::ByteRun), pb = B.packets.size() * sizeof(rsmi_fenc_packet);
+                 ub = B.upd.size() * sizeof(rsmi::ByteRun), pb = B.pruns.size() * sizeof(rsmi::PacketRun),
+                 xb = ctx ? (size_t)total_pk * sizeof(rsmi_fenc_packet) : 0;
     const size_t go = 0, so = (gb + 255) & ~size_t(255), co = (so + sb + 255) & ~size_t(255),
                  ro = (co + cb + 255) & ~size_t(255), uo = (ro + rb + 255) & ~size_t(255),
-                 po = (uo + ub + 255) & ~size_t(255);
-    int rc = grow(&C->dplan[C->cur], &C->plan_cap[C->cur], po + pb + 16, false);
+                 po = (uo + ub + 255) & ~size_t(255), xo = (po + pb + 255) & ~size_t(255);
+    int rc = grow(&C->dplan[C->cur], &C->plan_cap[C->cur], xo + xb + 16, false);
     if (rc) return rc;
     uint8_t *dp = C->dplan[C->cur];
     hipError_t e = hipSuccess;
@@ -935,7 +992,10 @@ int rsmi_fenc_run_many(rsmi_fcol *C, rsmi_fenc *const *enc, int32_t n, uint8_t *
     if (e == hipSuccess && cb) e = hipMemcpyAsync(dp + co, B.carry.p, cb, hipMemcpyHostToDevice, s);
     if (e == hipSuccess && rb) e = hipMemcpyAsync(dp + ro, B.stale.p, rb, hipMemcpyHostToDevice, s);
     if (e == hipSuccess && ub) e = hipMemcpyAsync(dp + uo, B.upd.p, ub, hipMemcpyHostToDevice, s);
-    if (e == hipSuccess && pb) e = hipMemcpyAsync(dp + po, B.packets.p, pb, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess && pb) e = hipMemcpyAsync(dp + po, B.pruns.p, pb, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess)
+        e = rsmi::launch_expand_packets(reinterpret_cast<const rsmi::PacketRun *>(dp + po), (int64_t)B.pruns.size(),
+                                        reinterpret_cast<rsmi_fenc_packet *>(dp + xo), nullptr, s);
     const rsmi::CarryBase none{{nullptr, nullptr}};  // every address is absolute now
     if (e == hipSuccess)
         e = rsmi::launch_frame(reinterpret_cast<const FrameGroup *>(dp + go), (int64_t)B.jobs.size(),
@@ -956,9 +1016,9 @@ int rsmi_fenc_run_many(rsmi_fcol *C, rsmi_fenc *const *enc, int32_t n, uint8_t *
     if (e == hipSuccess)
         e = rsmi::launch_carry(reinterpret_cast<const CarryCopy *>(dp + co), (int64_t)B.carry.size(), none, s);
     if (e != hipSuccess) return fail(RSMI_ERR_HIP, std::string("fcol carry: ") + hipGetErrorString(e));
-    if (ctx && pb) {
-        rc = rsmi::cook_packets(ctx, slots, S, reinterpret_cast<const rsmi_fenc_packet *>(dp + po),
-                                (int64_t)B.packets.size(), out_len, out, seed, s);
+    if (ctx && total_pk) {
+        rc = rsmi::cook_packets(ctx, slots, S, reinterpret_cast<const rsmi_fenc_packet *>(dp + xo), total_pk,
+                                out_len, out, nullptr, seed, s);
         if (rc) return rc;
     }
     if (hipEventRecord(B.done, s) != hipSuccess) return fail(RSMI_ERR_HIP, "fcol: event");

@@ -362,7 +362,31 @@ __global__ __launch_bounds__(kThreads) void k_byte_runs(const ByteRun *runs, int
     }
 }
 
+// Packet runs -> the packet list the cook kernel reads: one wave per run.
+// With dst_off, also each packet's offset in the packed cooked output.
+__global__ __launch_bounds__(kThreads) void k_expand_packets(const PacketRun *runs, int64_t nruns,
+                                                              rsmi_fenc_packet *pk, int64_t *dst_off) {
+    const int lane = threadIdx.x & 63;
+    const int64_t w0 = (int64_t)blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
+    for (int64_t w = w0; w < nruns; w += (int64_t)gridDim.x * (kThreads / 64)) {
+        const PacketRun R = runs[w];
+        for (int c = lane; c < R.count; c += 64) {
+            pk[R.first + c] = rsmi_fenc_packet{R.slot + c, R.len, 0};
+            if (dst_off) dst_off[R.first + c] = R.out0 + (int64_t)c * RSMI_FEC_COOK_SPAN(R.len);
+        }
+    }
+}
+
 }  // namespace
+
+hipError_t launch_expand_packets(const PacketRun *runs, int64_t nruns, rsmi_fenc_packet *pk, int64_t *dst_off,
+                                 hipStream_t s) {
+    if (nruns <= 0) return hipSuccess;
+    int64_t blocks = (nruns + kThreads / 64 - 1) / (kThreads / 64);
+    if (blocks > 8192) blocks = 8192;
+    k_expand_packets<<<(unsigned)blocks, kThreads, 0, s>>>(runs, nruns, pk, dst_off);
+    return hipGetLastError();
+}
 
 hipError_t launch_byte_runs(const ByteRun *runs, int64_t nruns, uint8_t *slots, int64_t slot_stride,
                             uint8_t *shadow, hipStream_t s) {

@@ -226,6 +226,9 @@ struct CookArgs {
     const uint64_t *offset;
     const rsmi_fenc_packet *pk;  // or an FEC packet list: packet i at pk[i].slot * stride + pk_off,
     int32_t pk_off;              // pk[i].len bytes (len unused)
+    uint8_t *mirror;             // de_cook only: the output also at mirror + its offset (pinned host)
+    const int64_t *dst_off;      // packed output: packet i's output at dst + dst_off[i], room for
+                                 // RSMI_FEC_COOK_SPAN(len) bytes (NULL: dst + its own offset)
     int64_t stride, count;
     int32_t cap, flags;
     const int32_t *len;
@@ -241,7 +244,8 @@ size_t cook_lds_bytes(bool decook);
 // list); output at the same offset of dst (NULL: in place), IVs drawn on the
 // device from seed (cook_host.cpp).
 int cook_packets(const rsmi_cook_ctx *ctx, uint8_t *slots, int64_t S, const rsmi_fenc_packet *pk,
-                 int64_t npk, int32_t *out_len, uint8_t *dst, uint64_t seed, hipStream_t s);
+                 int64_t npk, int32_t *out_len, uint8_t *dst, const int64_t *dst_off, uint64_t seed,
+                 hipStream_t s);
 hipError_t launch_cook(const CookArgs &a, bool decook, int max_blocks, hipStream_t s);
 
 
@@ -306,5 +310,17 @@ hipError_t launch_byte_runs(const ByteRun *runs, int64_t nruns, uint8_t *slots, 
 hipError_t launch_frame(const FrameGroup *groups, int64_t ngroups, const FrameSrc *srcs,
                         CarryBase carry, uint8_t *slots, int64_t slot_stride, hipStream_t s);
 hipError_t launch_carry(const CarryCopy *jobs, int64_t njobs, CarryBase carry, hipStream_t s);
+// A run of a batch's packet list (what output() returned): packets first ..
+// first + count - 1 sit in slots slot .. slot + count - 1, len bytes each (a
+// mode-0 group is one run; fec_enc.cpp).  Cooked runs upload the runs and
+// expand them into the rsmi_fenc_packet list on the device (k_expand_packets).
+// Packed cooked output (rsmi_fenc_run_cooked_packed_dev): the run's packets
+// go to out0, out0 + span, ... with span = RSMI_FEC_COOK_SPAN(len).
+struct PacketRun {
+    int64_t slot, first, out0;
+    int32_t len, count;
+};
+hipError_t launch_expand_packets(const PacketRun *runs, int64_t nruns, rsmi_fenc_packet *pk, int64_t *dst_off,
+                                 hipStream_t s);
 
 }  // namespace rsmi

@@ -170,6 +170,43 @@ class FecEncoder:
               "rsmi_fenc_run_cooked_dev")
         return out_len
 
+    @staticmethod
+    def cook_span(lens):
+        """RSMI_FEC_COOK_SPAN: bytes a packet of len bytes takes in a packed
+        cooked output (its cooked form rounded up to 16-byte pieces)."""
+        return (np.asarray(lens, np.int64) + 37 + 15) // 16 * 16
+
+    def packed_offsets(self):
+        """Where run_cooked_packed puts each packet of the last plan, and the
+        total bytes: (int64 offsets, total)."""
+        sp = self.cook_span(self._last_packets["len"])
+        offs = np.zeros(len(sp), np.int64)
+        if len(sp) > 1:
+            np.cumsum(sp[:-1], out=offs[1:])
+        return offs, int(sp.sum())
+
+    def run_cooked_packed(self, slots, slot_stride: int, cook, seed: int, out, out_len=None,
+                          stream=None):
+        """run_cooked with the cooked packets back to back in `out` (CUDA or
+        pinned uint8, 16-aligned): packet p at packed_offsets()[0][p] --
+        rsmi_fenc_run_cooked_packed_dev.  Returns the int32 CUDA tensor of
+        cooked lengths."""
+        import torch
+        s = stream if stream is not None else torch.cuda.current_stream()
+        npk = len(self._last_packets)
+        if out_len is None:
+            out_len = torch.empty(max(npk, 1), dtype=torch.int32, device="cuda")
+        elif out_len.dtype != torch.int32 or not out_len.is_cuda or out_len.numel() < npk:
+            raise ValueError(f"out_len must be an int32 CUDA tensor of >= {npk} entries")
+        self._check_slots(slots, slot_stride, "slots")
+        if out.dtype != torch.uint8 or not (out.is_cuda or out.is_pinned()) or out.data_ptr() % 16:
+            raise TypeError("out must be a 16-aligned CUDA or pinned uint8 tensor")
+        check(lib().rsmi_fenc_run_cooked_packed_dev(
+            self._h, slots.data_ptr() if slots.numel() else None, int(slot_stride), cook._h,
+            C.c_uint64(seed & (2**64 - 1)), out.data_ptr(), int(out.numel()), out_len.data_ptr(),
+            s.cuda_stream), "rsmi_fenc_run_cooked_packed_dev")
+        return out_len
+
     def packets_now(self):
         """The last plan's packet list as it stands now (after
         FecCollector.run_many: slots of the shared slot array)."""

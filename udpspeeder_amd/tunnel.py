@@ -51,34 +51,36 @@ class Sender:
         self.h_in = torch.empty(batch * self.sin, dtype=torch.uint8).pin_memory()
         self.d_in = torch.empty(batch * self.sin, dtype=torch.uint8, device="cuda")
         self.slots = None
-        self.h_out = None
+        self.d_out = self.h_out = None
         self.seed = seq0
 
     def _emit(self, p, sock_out, to, drop):
+        """Frame + encode + cook the planned batch in one run
+        (rsmi_fenc_run_cooked_packed_dev): the cooked packets land back to back
+        in device memory, and only those bytes cross PCIe for sendmmsg."""
         torch = self.torch
         S = self.s
         if p.n_slots == 0 or len(p.packets) == 0:
             return 0
-        need = p.n_slots * S
-        if self.slots is None or self.slots.numel() < need:
-            self.slots = torch.empty(need, dtype=torch.uint8, device="cuda")
-            self.h_out = torch.empty(need, dtype=torch.uint8).pin_memory()
+        offs, total = self.enc.packed_offsets()
+        if self.slots is None or self.slots.numel() < p.n_slots * S:
+            self.slots = torch.empty(p.n_slots * S, dtype=torch.uint8, device="cuda")
+        if self.d_out is None or self.d_out.numel() < total:
+            self.d_out = torch.empty(total, dtype=torch.uint8, device="cuda")
+            self.h_out = torch.empty(total, dtype=torch.uint8).pin_memory()
         with torch.cuda.stream(self.stream):
-            self.enc.run(self.slots, S, stream=self.stream)
-            offs = torch.from_numpy(p.packets["slot"].astype(np.int64) * S + SLOT_PACKET).to(
-                "cuda", non_blocking=True)
-            lens = torch.from_numpy(p.packets["len"].astype(np.int32)).to("cuda", non_blocking=True)
             self.seed += 1
-            out_len = self.cook.cook(self.slots, lens, cap=S - SLOT_PACKET, offsets=offs,
-                                     seed=self.seed, stream=self.stream)
-            self.h_out[:need].copy_(self.slots[:need], non_blocking=True)
+            out_len = self.enc.run_cooked_packed(self.slots, S, self.cook, self.seed, self.d_out,
+                                                 stream=self.stream)
+            self.h_out[:total].copy_(self.d_out[:total], non_blocking=True)
             ol = out_len.to("cpu", non_blocking=True)
         self.stream.synchronize()
-        ol = ol.numpy().copy()
+        ol = ol.numpy()[:len(p.packets)].copy()
         if drop is not None:
             ol[drop(p)] = -1  # lost on the way (tests / benches)
-        return io.send_batch(sock_out, _View(self.h_out, S), SLOT_PACKET, ol,
-                             slots=p.packets["slot"], to=to)
+        keep = ol >= 0
+        ptrs = (offs + self.h_out.data_ptr()).astype(np.uint64)
+        return io.send_ptrs(sock_out, ptrs[keep], ol[keep], to)
 
     def step(self, sock_in, sock_out, to, timeout_ms: int = 50, drop=None):
         """One batch: returns (datagrams read, packets sent)."""
@@ -126,11 +128,12 @@ class Receiver:
             return 0, 0
         with torch.cuda.stream(self.stream):
             self.d[:n * S].copy_(self.h[:n * S], non_blocking=True)
-            offs = torch.arange(n, dtype=torch.int64, device="cuda") * S
             lt = torch.from_numpy(np.maximum(lens, 0).astype(np.int32)).to("cuda", non_blocking=True)
-            out_len = self.cook.decook(self.d, lt, cap=S, offsets=offs, stream=self.stream)
-            # the planner reads headers and mode-1 length prefixes on the host
-            self.h[:n * S].copy_(self.d[:n * S], non_blocking=True)
+            # de_cook in place on the device (the FEC gather reads it there) and
+            # into the pinned receive buffer (the planner reads headers and the
+            # outputs point into it): only packet bytes come back over PCIe
+            out_len = self.cook.decook_mirror(self.d[:n * S], lt, self.h, cap=S, stride=S,
+                                              stream=self.stream)
             ol = out_len.to("cpu", non_blocking=True)
         self.stream.synchronize()
         ol = ol.numpy().copy()
