@@ -129,9 +129,11 @@ int bitslice_code_k(int idx);  // (k, n) of generated code idx
 int bitslice_code_n(int idx);
 // Ragged bucketed launch over a host-built plan (ragged.cpp): colmap entries
 // (group << 12) | piece, waves = {code index, first column} pairs.
+bool bitslice_code_lo(int idx);  // ragged encode: runs in the low-register kernel
 hipError_t launch_encode_bitslice_ragged(const rsmi_group *groups, const uint32_t *colmap,
-                                         const uint32_t *waves, uint32_t nwaves, uint8_t *base,
-                                         uint32_t bytes, hipStream_t s);
+                                         const uint32_t *waves, uint32_t nwaves, uint32_t nhi,
+                                         uint8_t *base, uint32_t bytes, hipStream_t s,
+                                         hipStream_t aux, hipEvent_t fork, hipEvent_t join);
 
 // Codes without a build-time network (bitslice_rtc.cpp): emitted and compiled
 // with hipRTC in the background when first made resident.
