@@ -381,11 +381,13 @@ __global__ __launch_bounds__(kThreads, COOK_OCC) void k_cook(CookArgs a) {
         CT(0);
         const int64_t pk = kPpw * pw + sub;
         const bool have = pk < a.count;
+        // the packet's index in its batch: IV draw, out_len and packed place
+        const int64_t gi = have && a.pk_idx ? (int64_t)a.pk[pk].event : pk;
         int L = -1, ivl = 0;
         const uint64_t po = have ? packet_off(a, pk) : 0u;
         uint8_t *pkt = have ? a.base + po : nullptr;
         uint8_t *opkt = !have ? nullptr
-                        : a.dst_off ? a.dst + a.dst_off[pk]
+                        : a.dst_off ? a.dst + a.dst_off[gi]
                                     : (a.dst ? a.dst : a.base) + po;  // where the output goes
         // round 0 is read up to the packet's cap (every packet owns cap bytes), so
         // these loads fly together with the length load instead of after it
@@ -393,7 +395,7 @@ __global__ __launch_bounds__(kThreads, COOK_OCC) void k_cook(CookArgs a) {
         load_round(cur, pkt, 0, hl, cap_extent(a, pkt, have));
         if (have) {
             L = packet_len(a, pk);
-            if (obs) ivl = a.iv ? a.iv_len[pk] : 4 + (int)(splitmix(a.seed, (uint64_t)pk, 0) % 29u);
+            if (obs) ivl = a.iv ? a.iv_len[pk] : 4 + (int)(splitmix(a.seed, (uint64_t)gi, 0) % 29u);
         }
         const int out = L + (ck ? 4 : 0) + (obs ? ivl + 1 : 0);
         // (a packed output has room for any iv_len <= RSMI_COOK_IV_MAX)
@@ -403,7 +405,7 @@ __global__ __launch_bounds__(kThreads, COOK_OCC) void k_cook(CookArgs a) {
         const int ext = ok ? round16(out) : 0;
         const uint32_t magic = ivl ? 0xFFFFFFFFu / (uint32_t)ivl : 0u;
         if (ok && ivl && !a.iv && 8 * hl < ivl) {  // device-drawn IV: 8 bytes per draw, one per lane
-            const uint64_t z = splitmix(a.seed, (uint64_t)pk, 1 + (uint64_t)hl);
+            const uint64_t z = splitmix(a.seed, (uint64_t)gi, 1 + (uint64_t)hl);
             reinterpret_cast<uint32_t *>(ovl)[2 * hl] = (uint32_t)z;
             reinterpret_cast<uint32_t *>(ovl)[2 * hl + 1] = (uint32_t)(z >> 32);
         }
@@ -489,7 +491,7 @@ __global__ __launch_bounds__(kThreads, COOK_OCC) void k_cook(CookArgs a) {
             const u32x4 lo = piece_mask(L - Pt), hi = piece_mask(out - Pt);
             st_piece(opkt + Pt, ((dt ^ m) & lo) | ((o ^ k) & hi & ~lo) | (dt & ~hi));
         }
-        if (have && hl == 0) a.out_len[pk] = ok ? out : -1;
+        if (have && hl == 0) a.out_len[gi] = ok ? out : -1;
         wave_sync();  // the scratch slice is rewritten by the next packet
 #if COOK_TRACE
         CT(4);

@@ -262,6 +262,7 @@ int cook_packets(const rsmi_cook_ctx *c, uint8_t *slots, int64_t S, const rsmi_f
     a.dst_off = dst_off;
     a.pk = pk;
     a.pk_off = kSlotHeader;
+    a.pk_idx = 1;
     a.stride = S;
     a.count = npk;
     a.cap = (int32_t)(S - kSlotHeader);

@@ -118,6 +118,7 @@ struct PlanSet {
     HostArr<rsmi::ByteRun> shadow_upd;  // the buffer at the batch end -> dshadow
     HostArr<rsmi_fenc_packet> packets;  // what output() returns, in order (rsmi_fenc_packets)
     HostArr<rsmi::PacketRun> pruns;     // the same as runs of slots (cooked runs upload these)
+    int64_t n_data_pk = 0, n_par_pk = 0;  // packets of cook lists A (data) and B (parity)
     hipEvent_t done = nullptr;
     bool in_flight = false;
 };
@@ -163,6 +164,9 @@ struct rsmi_fenc {
     size_t carry_cap[2] = {0, 0};
     int carry_cur = 0;  // pending packets live in dcarry[carry_cur] (or the batch input)
     size_t carry_need = 0;  // bytes of dcarry[carry_cur] the last plan fills
+    // cooked runs into another buffer: the data packets cook on `aux` beside the encoder
+    hipStream_t aux = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr;
 
     int tail_x() const { return cfg.rs_cnt; }
     int y_of(int x) const { return cfg.rs_y[x - 1]; }
@@ -312,7 +316,9 @@ void emit_data(rsmi_fenc *E, int32_t event) {
     p.emitted = (int64_t)E->P->packets.size();
     p.run = (int64_t)E->P->pruns.size();
     E->P->packets.push_back(rsmi_fenc_packet{-1, 8 + (int)p.len + 2, event});
-    E->P->pruns.push_back(rsmi::PacketRun{-1, p.emitted, 0, 8 + (int)p.len + 2, 1});
+    E->P->pruns.push_back(rsmi::PacketRun{-1, 0, (int32_t)p.emitted, (int32_t)E->P->n_data_pk,
+                                          (int32_t)E->P->n_par_pk, 8 + (int)p.len + 2, 1, 1});
+    E->P->n_data_pk += 1;
 }
 
 // fec_encode_manager_t::input (fec_manager.cpp:206-447) for one event,
@@ -391,10 +397,18 @@ int input_event(rsmi_fenc *E, int32_t event, bool has, int len, uint64_t addr) {
         close_group(E, k, m, fec_len);
         if (mode == 0) {
             for (int i = 0; i < k + m; ++i) E->P->packets[(size_t)(first_pk + i)].slot = slot0 + i;
-            E->P->pruns.push_back(rsmi::PacketRun{slot0, first_pk, 0, 8 + fec_len, k + m});
+            E->P->pruns.push_back(rsmi::PacketRun{slot0, 0, (int32_t)first_pk, (int32_t)E->P->n_data_pk,
+                                                  (int32_t)E->P->n_par_pk, 8 + fec_len, (uint16_t)(k + m),
+                                                  (uint16_t)k});
+            E->P->n_data_pk += k;
+            E->P->n_par_pk += m;
         } else {
             int64_t q = first_pk + (has ? 1 : 0);
-            if (m > 0) E->P->pruns.push_back(rsmi::PacketRun{slot0 + k, q, 0, 8 + fec_len, m});
+            if (m > 0) {
+                E->P->pruns.push_back(rsmi::PacketRun{slot0 + k, 0, (int32_t)q, (int32_t)E->P->n_data_pk,
+                                                      (int32_t)E->P->n_par_pk, 8 + fec_len, (uint16_t)m, 0});
+                E->P->n_par_pk += m;
+            }
             for (int i = k; i < k + m; ++i) E->P->packets[(size_t)q++].slot = slot0 + i;
         }
         E->seq++;
@@ -504,6 +518,9 @@ void rsmi_fenc_destroy(rsmi_fenc *E) {
         if (E->dcarry[i]) (void)hipFree(E->dcarry[i]);
     for (PlanSet &B : E->ps)
         if (B.done) (void)hipEventDestroy(B.done);
+    if (E->aux) (void)hipStreamDestroy(E->aux);
+    if (E->fork) (void)hipEventDestroy(E->fork);
+    if (E->join) (void)hipEventDestroy(E->join);
     delete E;
 }
 
@@ -531,6 +548,7 @@ int rsmi_fenc_plan(rsmi_fenc *E, int64_t n_events, const int32_t *len, const uin
     E->P->carry.clear();
     E->P->packets.clear();
     E->P->pruns.clear();
+    E->P->n_data_pk = E->P->n_par_pk = 0;
     E->g_slot0.clear();
     E->g_k.clear();
     E->g_m.clear();
@@ -652,6 +670,10 @@ int prepare_run(rsmi_fenc *E, hipStream_t s) {
         for (PlanSet &B : E->ps)
             if (hipEventCreateWithFlags(&B.done, hipEventDisableTiming) != hipSuccess)
                 return fail(RSMI_ERR_HIP, "fenc: hipEventCreate");
+        if (hipStreamCreateWithFlags(&E->aux, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&E->fork, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&E->join, hipEventDisableTiming) != hipSuccess)
+            return fail(RSMI_ERR_HIP, "fenc: aux stream");
         E->device = cur;
         // start compiling the run-time networks of the -f table's codes now, so
         // they are ready by the time those group sizes come (bitslice_rtc.cpp)
@@ -696,8 +718,10 @@ int run_dev(rsmi_fenc *E, uint8_t *slots, int64_t S, void *stream, const CookSpe
     PlanSet &prev = E->ps[E->pcur ^ 1];
     const rsmi::CarryBase carry{{E->dcarry[0], E->dcarry[1]}};
     // cooked runs: the packet list's runs go up with the plan and are expanded
-    // on the device into the (slot, length) list the cook kernel reads
+    // on the device into the two cook lists (data packets, parity packets)
     const size_t npk = ck ? E->P->packets.size() : 0, nrun = ck ? E->P->pruns.size() : 0;
+    if (npk > (size_t)INT32_MAX) return fail(RSMI_ERR_INVALID, "fenc: more than 2^31 packets in one batch");
+    const int64_t na = ck ? E->P->n_data_pk : 0, nb = ck ? E->P->n_par_pk : 0;
     const size_t gb = E->P->jobs.size() * sizeof(FrameGroup), sb = E->P->srcs.size() * sizeof(FrameSrc),
                  cb = E->P->carry.size() * sizeof(CarryCopy),
                  rb = E->P->stale.size() * sizeof(rsmi::ByteRun),
@@ -737,6 +761,7 @@ int run_dev(rsmi_fenc *E, uint8_t *slots, int64_t S, void *stream, const CookSpe
     if (e == hipSuccess)
         e = rsmi::launch_expand_packets(reinterpret_cast<const rsmi::PacketRun *>(E->dplan + po), (int64_t)nrun,
                                         reinterpret_cast<rsmi_fenc_packet *>(E->dplan + xo),
+                                        reinterpret_cast<rsmi_fenc_packet *>(E->dplan + xo) + na,
                                         packed ? reinterpret_cast<int64_t *>(E->dplan + dq) : nullptr, s);
     if (e == hipSuccess)
         e = rsmi::launch_frame(reinterpret_cast<const FrameGroup *>(E->dplan + go), (int64_t)E->P->jobs.size(),
@@ -746,6 +771,21 @@ int run_dev(rsmi_fenc *E, uint8_t *slots, int64_t S, void *stream, const CookSpe
         e = rsmi::launch_byte_runs(reinterpret_cast<const rsmi::ByteRun *>(E->dplan + ro),
                                    (int64_t)E->P->stale.size(), slots, S, E->dshadow, s);
     if (e != hipSuccess) return fail(RSMI_ERR_HIP, std::string("fenc frame: ") + hipGetErrorString(e));
+    // do_cook (my_send, packet.cpp:165-168) of the data packets, final now:
+    // into another buffer they cook on the aux stream beside the encoder (the
+    // cook is LDS- and latency-bound, the encoder memory- and VALU-bound)
+    const rsmi_fenc_packet *lists = reinterpret_cast<const rsmi_fenc_packet *>(E->dplan + xo);
+    const int64_t *doff = packed ? reinterpret_cast<const int64_t *>(E->dplan + dq) : nullptr;
+    const bool side = npk && ck->out && na;
+    if (side) {
+        e = hipEventRecord(E->fork, s);
+        if (e == hipSuccess) e = hipStreamWaitEvent(E->aux, E->fork, 0);
+        if (e != hipSuccess) return fail(RSMI_ERR_HIP, std::string("fenc fork: ") + hipGetErrorString(e));
+        rc = rsmi::cook_packets(ck->ctx, slots, S, lists, na, ck->out_len, ck->out, doff, ck->seed, E->aux);
+        if (rc) return rc;
+        e = hipEventRecord(E->join, E->aux);
+        if (e != hipSuccess) return fail(RSMI_ERR_HIP, std::string("fenc join: ") + hipGetErrorString(e));
+    }
     // parity of every group
     for (const Run &r : E->runs) {
         rc = rsmi_encode_dev(r.k, r.n, slots + r.slot0 * S + rsmi::kSlotShard, (int64_t)r.n * S, S,
@@ -759,13 +799,14 @@ int run_dev(rsmi_fenc *E, uint8_t *slots, int64_t S, void *stream, const CookSpe
         e = rsmi::launch_carry(reinterpret_cast<const CarryCopy *>(E->dplan + co),
                                (int64_t)E->P->carry.size(), carry, s);
     if (e != hipSuccess) return fail(RSMI_ERR_HIP, std::string("fenc carry: ") + hipGetErrorString(e));
-    // do_cook on every packet output() returned (my_send, packet.cpp:165-168),
-    // after the blob buffer update above has read the plain shards
+    // the parity packets (and in place, after the blob buffer update above has
+    // read the plain shards, the data packets too)
     if (npk) {
-        rc = rsmi::cook_packets(ck->ctx, slots, S, reinterpret_cast<const rsmi_fenc_packet *>(E->dplan + xo),
-                                (int64_t)npk, ck->out_len, ck->out,
-                                packed ? reinterpret_cast<const int64_t *>(E->dplan + dq) : nullptr, ck->seed, s);
+        rc = side || !na ? RSMI_OK
+                         : rsmi::cook_packets(ck->ctx, slots, S, lists, na, ck->out_len, ck->out, doff, ck->seed, s);
+        if (!rc && nb) rc = rsmi::cook_packets(ck->ctx, slots, S, lists + na, nb, ck->out_len, ck->out, doff, ck->seed, s);
         if (rc) return rc;
+        if (side && hipStreamWaitEvent(s, E->join, 0) != hipSuccess) return fail(RSMI_ERR_HIP, "fenc: join wait");
     }
     e = hipEventRecord(E->P->done, s);
     if (e != hipSuccess) return fail(RSMI_ERR_HIP, std::string("fenc event: ") + hipGetErrorString(e));
@@ -833,7 +874,7 @@ int rsmi_fenc_run_many(rsmi_fcol *C, rsmi_fenc *const *enc, int32_t n, uint8_t *
                        const rsmi_cook_ctx *ctx, uint64_t seed, uint8_t *out, int32_t *out_len,
                        void *stream) {
     if (!C || n < 0 || (n && !enc)) return fail(RSMI_ERR_INVALID, "rsmi_fenc_run_many: bad arguments");
-    int64_t total_slots = 0, total_pk = 0;
+    int64_t total_slots = 0, total_pk = 0, total_a = 0;
     for (int i = 0; i < n; ++i) {
         rsmi_fenc *E = enc[i];
         if (!E || !E->planned) return fail(RSMI_ERR_INVALID, "rsmi_fenc_run_many: encoder without a plan");
@@ -845,7 +886,9 @@ int rsmi_fenc_run_many(rsmi_fcol *C, rsmi_fenc *const *enc, int32_t n, uint8_t *
                                           "slot_stride_min (" + std::to_string(E->stride_min) + ")");
         total_slots += E->n_slots;
         total_pk += (int64_t)E->P->packets.size();
+        total_a += E->P->n_data_pk;
     }
+    if (total_pk > INT32_MAX) return fail(RSMI_ERR_INVALID, "rsmi_fenc_run_many: more than 2^31 packets");
     if (total_slots && (!slots || ((uintptr_t)slots & 15)))
         return fail(RSMI_ERR_INVALID, "slots_base must be 16-aligned");
     if (ctx && total_pk && !out_len) return fail(RSMI_ERR_INVALID, "rsmi_fenc_run_many: null out_len");
@@ -928,7 +971,7 @@ int rsmi_fenc_run_many(rsmi_fcol *C, rsmi_fenc *const *enc, int32_t n, uint8_t *
         return (l & rsmi::kShadowLoc) ? (rsmi::kAbsLoc | (uint64_t)(uintptr_t)E->dshadow)
                                       : (uint64_t)m[(size_t)l];
     };
-    int64_t pk_base = 0;
+    int64_t pk_base = 0, a_base = 0, b_base = 0;
     for (int i = 0; i < n; ++i) {
         rsmi_fenc *E = enc[i];
         const std::vector<int64_t> &m = smap[(size_t)i];
@@ -970,10 +1013,14 @@ int rsmi_fenc_run_many(rsmi_fcol *C, rsmi_fenc *const *enc, int32_t n, uint8_t *
             for (size_t j = 0; j < E->P->pruns.size(); ++j) {
                 rsmi::PacketRun r = E->P->pruns[j];
                 r.slot = m[(size_t)r.slot];  // a run lies inside one group (or is one lone slot)
-                r.first += pk_base;
+                r.first += (int32_t)pk_base;
+                r.afirst += (int32_t)a_base;  // one cook list: every data packet, then every parity packet
+                r.bfirst += (int32_t)(total_a + b_base);
                 B.pruns.push_back(r);
             }
         pk_base += (int64_t)E->P->packets.size();
+        a_base += E->P->n_data_pk;
+        b_base += E->P->n_par_pk;
     }
     // ---- upload + launches
     const size_t gb = B.jobs.size() * sizeof(FrameGroup), sb = B.srcs.size() * sizeof(FrameSrc),
@@ -995,6 +1042,7 @@ int rsmi_fenc_run_many(rsmi_fcol *C, rsmi_fenc *const *enc, int32_t n, uint8_t *
     if (e == hipSuccess && pb) e = hipMemcpyAsync(dp + po, B.pruns.p, pb, hipMemcpyHostToDevice, s);
     if (e == hipSuccess)
         e = rsmi::launch_expand_packets(reinterpret_cast<const rsmi::PacketRun *>(dp + po), (int64_t)B.pruns.size(),
+                                        reinterpret_cast<rsmi_fenc_packet *>(dp + xo),
                                         reinterpret_cast<rsmi_fenc_packet *>(dp + xo), nullptr, s);
     const rsmi::CarryBase none{{nullptr, nullptr}};  // every address is absolute now
     if (e == hipSuccess)

@@ -362,16 +362,19 @@ __global__ __launch_bounds__(kThreads) void k_byte_runs(const ByteRun *runs, int
     }
 }
 
-// Packet runs -> the packet list the cook kernel reads: one wave per run.
-// With dst_off, also each packet's offset in the packed cooked output.
+// Packet runs -> the two cook lists: one wave per run.  With dst_off, also
+// each packet's offset in the packed cooked output.
 __global__ __launch_bounds__(kThreads) void k_expand_packets(const PacketRun *runs, int64_t nruns,
-                                                              rsmi_fenc_packet *pk, int64_t *dst_off) {
+                                                              rsmi_fenc_packet *pk_a, rsmi_fenc_packet *pk_b,
+                                                              int64_t *dst_off) {
     const int lane = threadIdx.x & 63;
     const int64_t w0 = (int64_t)blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
     for (int64_t w = w0; w < nruns; w += (int64_t)gridDim.x * (kThreads / 64)) {
         const PacketRun R = runs[w];
-        for (int c = lane; c < R.count; c += 64) {
-            pk[R.first + c] = rsmi_fenc_packet{R.slot + c, R.len, 0};
+        for (int c = lane; c < (int)R.count; c += 64) {
+            const rsmi_fenc_packet p{R.slot + c, R.len, R.first + c};
+            if (c < (int)R.ndata) pk_a[R.afirst + c] = p;
+            else pk_b[R.bfirst + c - (int)R.ndata] = p;
             if (dst_off) dst_off[R.first + c] = R.out0 + (int64_t)c * RSMI_FEC_COOK_SPAN(R.len);
         }
     }
@@ -379,12 +382,12 @@ __global__ __launch_bounds__(kThreads) void k_expand_packets(const PacketRun *ru
 
 }  // namespace
 
-hipError_t launch_expand_packets(const PacketRun *runs, int64_t nruns, rsmi_fenc_packet *pk, int64_t *dst_off,
-                                 hipStream_t s) {
+hipError_t launch_expand_packets(const PacketRun *runs, int64_t nruns, rsmi_fenc_packet *pk_a,
+                                 rsmi_fenc_packet *pk_b, int64_t *dst_off, hipStream_t s) {
     if (nruns <= 0) return hipSuccess;
     int64_t blocks = (nruns + kThreads / 64 - 1) / (kThreads / 64);
     if (blocks > 8192) blocks = 8192;
-    k_expand_packets<<<(unsigned)blocks, kThreads, 0, s>>>(runs, nruns, pk, dst_off);
+    k_expand_packets<<<(unsigned)blocks, kThreads, 0, s>>>(runs, nruns, pk_a, pk_b, dst_off);
     return hipGetLastError();
 }
 

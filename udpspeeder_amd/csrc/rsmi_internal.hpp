@@ -228,6 +228,8 @@ struct CookArgs {
     const uint64_t *offset;
     const rsmi_fenc_packet *pk;  // or an FEC packet list: packet i at pk[i].slot * stride + pk_off,
     int32_t pk_off;              // pk[i].len bytes (len unused)
+    int32_t pk_idx;              // 1: pk[i].event is packet i's index in the batch (IV draw, out_len,
+                                 // dst_off), a cook list of k_expand_packets
     uint8_t *mirror;             // de_cook only: the output also at mirror + its offset (pinned host)
     const int64_t *dst_off;      // packed output: packet i's output at dst + dst_off[i], room for
                                  // RSMI_FEC_COOK_SPAN(len) bytes (NULL: dst + its own offset)
@@ -242,9 +244,10 @@ struct CookArgs {
 };
 size_t cook_lds_bytes(bool decook);
 // do_cook over an FEC packet list (rsmi_fenc_run_cooked_dev): packet p at
-// slots + pk[p].slot * S + RSMI_FEC_SLOT_PACKET, pk[p].len bytes (device
-// list); output at the same offset of dst (NULL: in place), IVs drawn on the
-// device from seed (cook_host.cpp).
+// slots + pk[p].slot * S + RSMI_FEC_SLOT_PACKET, pk[p].len bytes (a device
+// cook list of k_expand_packets: pk[p].event = the packet's index i in the
+// batch); output at the same offset of dst (NULL: in place) or at dst +
+// dst_off[i], out_len[i], IVs drawn on the device from (seed, i) (cook_host.cpp).
 int cook_packets(const rsmi_cook_ctx *ctx, uint8_t *slots, int64_t S, const rsmi_fenc_packet *pk,
                  int64_t npk, int32_t *out_len, uint8_t *dst, const int64_t *dst_off, uint64_t seed,
                  hipStream_t s);
@@ -315,14 +318,20 @@ hipError_t launch_carry(const CarryCopy *jobs, int64_t njobs, CarryBase carry, h
 // A run of a batch's packet list (what output() returned): packets first ..
 // first + count - 1 sit in slots slot .. slot + count - 1, len bytes each (a
 // mode-0 group is one run; fec_enc.cpp).  Cooked runs upload the runs and
-// expand them into the rsmi_fenc_packet list on the device (k_expand_packets).
-// Packed cooked output (rsmi_fenc_run_cooked_packed_dev): the run's packets
-// go to out0, out0 + span, ... with span = RSMI_FEC_COOK_SPAN(len).
+// expand them on the device (k_expand_packets) into two cook lists: A, the
+// data packets (final once framed: cooked beside the encoder), and B, the
+// parity packets.  A list entry's `event` is the packet's index in the batch
+// (its IV draw, out_len and packed place).  Packed cooked output
+// (rsmi_fenc_run_cooked_packed_dev): the run's packets go to out0, out0 +
+// span, ... with span = RSMI_FEC_COOK_SPAN(len).
 struct PacketRun {
-    int64_t slot, first, out0;
-    int32_t len, count;
+    int64_t slot, out0;
+    int32_t first;           // index of the run's first packet in the batch
+    int32_t afirst, bfirst;  // where its data packets start in list A, its parity packets in B
+    int32_t len;
+    uint16_t count, ndata;   // packets [0, ndata) are data packets, the rest parity
 };
-hipError_t launch_expand_packets(const PacketRun *runs, int64_t nruns, rsmi_fenc_packet *pk, int64_t *dst_off,
-                                 hipStream_t s);
+hipError_t launch_expand_packets(const PacketRun *runs, int64_t nruns, rsmi_fenc_packet *pk_a,
+                                 rsmi_fenc_packet *pk_b, int64_t *dst_off, hipStream_t s);
 
 }  // namespace rsmi
