@@ -567,7 +567,9 @@ def frame_cook_config(torch, dev, groups=65536, reps=4):
     return {"datagrams_in": npk, "datagram_len": plen, "groups": groups, "packets_out": nout,
             "run_ms": round(t, 4), "datagrams_in_per_s": round(npk / (t * 1e-3), 1),
             "cooked_packets_per_s": round(nout / (t * 1e-3), 1),
-            "what": "rsmi_fenc_run_cooked_dev: plan upload + k_frame + k_bs_20_30 + carry + k_cook, "
+            "what": "rsmi_fenc_run_cooked_dev: plan upload (groups, records, packet runs) + "
+                    "k_expand_packets + k_frame + k_bs2_20_30 + carry, k_cook of the data packets on "
+                    "a forked stream beside the encoder and of the parity packets after it; "
                     "device-resident, key on, device-drawn IVs", "lengths_ok": ok}
 
 
