@@ -119,6 +119,7 @@ struct PlanSet {
     HostArr<rsmi_fenc_packet> packets;  // what output() returns, in order (rsmi_fenc_packets)
     HostArr<rsmi::PacketRun> pruns;     // the same as runs of slots (cooked runs upload these)
     int64_t n_data_pk = 0, n_par_pk = 0;  // packets of cook lists A (data) and B (parity)
+    uint32_t max_src = 0;  // most records of one job (> kFrameLdsSrc: k_frame reads them repeatedly)
     hipEvent_t done = nullptr;
     bool in_flight = false;
 };
@@ -175,6 +176,22 @@ struct rsmi_fenc {
 };
 
 namespace {
+
+// The framing records (16 B per input packet, the plan's largest array) are
+// read by k_frame straight from the pinned plan array over PCIe, once per
+// group as its block starts, instead of being copied up first: the reads
+// spread over the kernel's run and hide behind its work.  RSMI_FENC_SRC_COPY=1
+// copies them up instead (A/B), as does a plan array that is not pinned.
+const FrameSrc *mapped_srcs(const HostArr<FrameSrc> &a) {
+    static const bool copy = [] {
+        const char *v = std::getenv("RSMI_FENC_SRC_COPY");
+        return v && *v && *v != '0';
+    }();
+    if (copy || !a.pinned || !a.p) return nullptr;
+    void *d = nullptr;
+    if (hipHostGetDevicePointer(&d, a.p, 0) != hipSuccess) return nullptr;
+    return static_cast<const FrameSrc *>(d);
+}
 
 int wait_set(PlanSet &B) {
     if (B.in_flight) {
@@ -292,6 +309,7 @@ void close_group(rsmi_fenc *E, int k, int m, int fec_len) {
         }
     }
     E->P->jobs.push_back(G);
+    E->P->max_src = std::max(E->P->max_src, E->cfg.mode == 0 ? G.nsrc : (uint32_t)G.nframe);
     if (E->cfg.mode == 0) stale_runs(E, slot0, k, fec_len, E->blob_len);
     E->g_slot0.push_back(slot0);
     E->g_k.push_back(k);
@@ -544,6 +562,7 @@ int rsmi_fenc_plan(rsmi_fenc *E, int64_t n_events, const int32_t *len, const uin
     int rc = wait_set(*E->P);
     if (rc) return rc;
     E->P->jobs.clear();
+    E->P->max_src = 0;
     E->P->srcs.clear();
     E->P->carry.clear();
     E->P->packets.clear();
@@ -722,7 +741,10 @@ int run_dev(rsmi_fenc *E, uint8_t *slots, int64_t S, void *stream, const CookSpe
     const size_t npk = ck ? E->P->packets.size() : 0, nrun = ck ? E->P->pruns.size() : 0;
     if (npk > (size_t)INT32_MAX) return fail(RSMI_ERR_INVALID, "fenc: more than 2^31 packets in one batch");
     const int64_t na = ck ? E->P->n_data_pk : 0, nb = ck ? E->P->n_par_pk : 0;
-    const size_t gb = E->P->jobs.size() * sizeof(FrameGroup), sb = E->P->srcs.size() * sizeof(FrameSrc),
+    const FrameSrc *zsrc = E->P->srcs.empty() || E->P->max_src > rsmi::kFrameLdsSrc ? nullptr
+                                                                                     : mapped_srcs(E->P->srcs);
+    const size_t gb = E->P->jobs.size() * sizeof(FrameGroup),
+                 sb = zsrc ? 0 : E->P->srcs.size() * sizeof(FrameSrc),
                  cb = E->P->carry.size() * sizeof(CarryCopy),
                  rb = E->P->stale.size() * sizeof(rsmi::ByteRun),
                  ub = E->P->shadow_upd.size() * sizeof(rsmi::ByteRun),
@@ -765,7 +787,7 @@ int run_dev(rsmi_fenc *E, uint8_t *slots, int64_t S, void *stream, const CookSpe
                                         packed ? reinterpret_cast<int64_t *>(E->dplan + dq) : nullptr, s);
     if (e == hipSuccess)
         e = rsmi::launch_frame(reinterpret_cast<const FrameGroup *>(E->dplan + go), (int64_t)E->P->jobs.size(),
-                               reinterpret_cast<const FrameSrc *>(E->dplan + so), carry, slots, S, s);
+                               zsrc ? zsrc : reinterpret_cast<const FrameSrc *>(E->dplan + so), carry, slots, S, s);
     // stale bytes past each blob, before the parity is computed over them
     if (e == hipSuccess)
         e = rsmi::launch_byte_runs(reinterpret_cast<const rsmi::ByteRun *>(E->dplan + ro),
@@ -1023,7 +1045,10 @@ int rsmi_fenc_run_many(rsmi_fcol *C, rsmi_fenc *const *enc, int32_t n, uint8_t *
         b_base += E->P->n_par_pk;
     }
     // ---- upload + launches
-    const size_t gb = B.jobs.size() * sizeof(FrameGroup), sb = B.srcs.size() * sizeof(FrameSrc),
+    uint32_t max_src = 0;
+    for (int i = 0; i < n; ++i) max_src = std::max(max_src, enc[i]->P->max_src);
+    const FrameSrc *zsrc = B.srcs.empty() || max_src > rsmi::kFrameLdsSrc ? nullptr : mapped_srcs(B.srcs);
+    const size_t gb = B.jobs.size() * sizeof(FrameGroup), sb = zsrc ? 0 : B.srcs.size() * sizeof(FrameSrc),
                  cb = B.carry.size() * sizeof(CarryCopy), rb = B.stale.size() * sizeof(rsmi::ByteRun),
                  ub = B.upd.size() * sizeof(rsmi::ByteRun), pb = B.pruns.size() * sizeof(rsmi::PacketRun),
                  xb = ctx ? (size_t)total_pk * sizeof(rsmi_fenc_packet) : 0;
@@ -1047,7 +1072,7 @@ int rsmi_fenc_run_many(rsmi_fcol *C, rsmi_fenc *const *enc, int32_t n, uint8_t *
     const rsmi::CarryBase none{{nullptr, nullptr}};  // every address is absolute now
     if (e == hipSuccess)
         e = rsmi::launch_frame(reinterpret_cast<const FrameGroup *>(dp + go), (int64_t)B.jobs.size(),
-                               reinterpret_cast<const FrameSrc *>(dp + so), none, slots, S, s);
+                               zsrc ? zsrc : reinterpret_cast<const FrameSrc *>(dp + so), none, slots, S, s);
     if (e == hipSuccess)
         e = rsmi::launch_byte_runs(reinterpret_cast<const rsmi::ByteRun *>(dp + ro), (int64_t)B.stale.size(),
                                    slots, S, nullptr, s);

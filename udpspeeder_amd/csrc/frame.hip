@@ -23,7 +23,7 @@ namespace rsmi {
 namespace {
 
 constexpr int kThreads = 256;
-constexpr int kLdsSrc = 1024;  // source records staged in LDS per group
+constexpr int kLdsSrc = (int)kFrameLdsSrc;  // source records staged in LDS per group
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef u32x4 u32x4_a4 __attribute__((aligned(4)));

@@ -280,6 +280,7 @@ struct CarryBase {
                                : reinterpret_cast<const uint8_t *>(a);
     }
 };
+constexpr uint32_t kFrameLdsSrc = 1024;  // k_frame stages a job's records in LDS up to this many
 struct FrameSrc {
     uint64_t addr;      // payload address (carry-tagged or device)
     uint32_t len;
