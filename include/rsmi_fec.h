@@ -137,6 +137,20 @@ int rsmi_fenc_run_cooked_dev(rsmi_fenc *enc, uint8_t *slots_base, int64_t slot_s
                              const struct rsmi_cook_ctx *ctx, uint64_t seed, uint8_t *out,
                              int32_t *out_len, void *stream);
 
+/* The last plan's packet list as runs (diagnostics and tests): packets first
+ * .. first + count - 1 sit in slots slot .. slot + count - 1, len bytes each;
+ * the first ndata are data packets, at afirst.. of the data-packet cook list,
+ * the rest parity packets at bfirst.. of the parity list.  Cooked runs upload
+ * these instead of the per-packet list and expand them on the device.  out0
+ * is filled in by packed cooked runs.  n receives the run count; out (NULL:
+ * count only) n entries. */
+typedef struct rsmi_fenc_packet_run {
+    int64_t slot, out0;
+    int32_t first, afirst, bfirst, len;
+    uint16_t count, ndata;
+} rsmi_fenc_packet_run;
+int rsmi_fenc_packet_runs(const rsmi_fenc *enc, int64_t *n, rsmi_fenc_packet_run *out);
+
 /* Bytes a packet of len bytes takes in a packed cooked output: its cooked
  * form (crc 4 + iv <= 32 + iv_len 1 more) rounded up to whole 16-byte pieces. */
 #define RSMI_FEC_COOK_SPAN(len) ((((int64_t)(len)) + 37 + 15) & ~(int64_t)15)

@@ -92,6 +92,51 @@ def test_planner_matches_reference_fixtures(fx, name, nbatch):
     enc.close()
 
 
+@pytest.mark.parametrize("name", NAMES)
+@pytest.mark.parametrize("nbatch", [1, 3])
+def test_packet_runs_expand_to_the_packet_list(fx, name, nbatch):
+    """The runs a cooked run uploads (no GPU): expanded as k_expand_packets
+    does, they give every packet of rsmi_fenc_packets once, in order, with its
+    slot and length; data packets (a group's first k slots, or a mode-1 packet
+    sent ahead in a slot of its own) fill cook list A and parity packets list
+    B, each in packet order."""
+    from udpspeeder_amd.fec import FecEncoder
+    c = _case(fx, name)
+    enc = FecEncoder(c["rs"], c["mode"], c["mtu"], c["ql"], seq0=c["seq0"])
+    lens = c["lens"]
+    cuts = np.linspace(0, len(lens), nbatch + 1).astype(int)
+    for a, b in zip(cuts[:-1], cuts[1:]):
+        p = enc.plan_host(lens[a:b], np.zeros(b - a, np.uint64))
+        runs = enc.packet_runs()
+        npk = len(p.packets)
+        slot, ln = np.full(npk, -1, np.int64), np.full(npk, -1, np.int64)
+        la, lb = [], []
+        for r in runs:
+            for c_ in range(int(r["count"])):
+                i = int(r["first"]) + c_
+                assert slot[i] == -1, "packet listed twice"
+                slot[i], ln[i] = int(r["slot"]) + c_, int(r["len"])
+                if c_ < int(r["ndata"]):
+                    la.append((int(r["afirst"]) + c_, i))
+                else:
+                    lb.append((int(r["bfirst"]) + c_ - int(r["ndata"]), i))
+        assert (slot == p.packets["slot"]).all() and (ln == p.packets["len"]).all()
+        for lst in (la, lb):
+            lst.sort()
+            assert [x for x, _ in lst] == list(range(len(lst)))
+            assert [i for _, i in lst] == sorted(i for _, i in lst)
+        # data / parity by slot: a slot of group g is parity iff its index >= k
+        g = p.groups
+        kind = {}
+        for s0, k, m in zip(g["slot0"], g["k"], g["m"]):
+            for j in range(int(k) + int(m)):
+                kind[int(s0) + j] = j >= int(k)
+        par = {i for _, i in lb}
+        for i in range(npk):
+            assert (i in par) == kind.get(int(p.packets["slot"][i]), False), i
+    enc.close()
+
+
 def _run_gpu(enc, lens, ev, cuts, torch):
     """Run the events through the GPU in batches; returns the emitted packets."""
     out = []

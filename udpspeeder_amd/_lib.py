@@ -134,6 +134,7 @@ def _bind(lib: C.CDLL) -> C.CDLL:
         "rsmi_fenc_plan": ([vp, i64, vp, vp, vp, vp, vp, vp, vp], i32),
         "rsmi_fenc_packets": ([vp, vp], i32),
         "rsmi_fenc_groups": ([vp, vp, vp, vp, vp, vp, vp], i32),
+        "rsmi_fenc_packet_runs": ([vp, vp, vp], i32),
         "rsmi_fenc_run_dev": ([vp, vp, i64, vp], i32),
         "rsmi_fenc_run_cooked_dev": ([vp, vp, i64, vp, C.c_uint64, vp, vp, vp], i32),
         "rsmi_fenc_run_cooked_packed_dev": ([vp, vp, i64, vp, C.c_uint64, vp, i64, vp, vp], i32),

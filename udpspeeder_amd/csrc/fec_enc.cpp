@@ -635,6 +635,14 @@ int rsmi_fenc_packets(const rsmi_fenc *E, rsmi_fenc_packet *out) {
     return RSMI_OK;
 }
 
+int rsmi_fenc_packet_runs(const rsmi_fenc *E, int64_t *n, rsmi_fenc_packet_run *out) {
+    if (!E || !n) return fail(RSMI_ERR_INVALID, "bad fenc_packet_runs args");
+    *n = (int64_t)E->P->pruns.size();
+    static_assert(sizeof(rsmi_fenc_packet_run) == sizeof(rsmi::PacketRun), "rsmi_fenc_packet_run layout");
+    if (out && *n) std::memcpy(out, E->P->pruns.data(), E->P->pruns.size() * sizeof(rsmi::PacketRun));
+    return RSMI_OK;
+}
+
 int rsmi_fenc_groups(const rsmi_fenc *E, int64_t *n, int64_t *slot0, int32_t *k, int32_t *m,
                      int32_t *fec_len, uint32_t *seq) {
     if (!E) return fail(RSMI_ERR_INVALID, "null encoder");

@@ -170,6 +170,22 @@ class FecEncoder:
               "rsmi_fenc_run_cooked_dev")
         return out_len
 
+    RUN_DTYPE = np.dtype([("slot", np.int64), ("out0", np.int64), ("first", np.int32),
+                          ("afirst", np.int32), ("bfirst", np.int32), ("len", np.int32),
+                          ("count", np.uint16), ("ndata", np.uint16)], align=True)  # 40 B, as in C
+
+    def packet_runs(self) -> np.ndarray:
+        """The last plan's packet list as runs (rsmi_fenc_packet_runs): what a
+        cooked run uploads and expands on the device into its two cook lists."""
+        n = C.c_int64()
+        check(lib().rsmi_fenc_packet_runs(self._h, C.byref(n), None), "rsmi_fenc_packet_runs")
+        assert self.RUN_DTYPE.itemsize == 40
+        out = np.zeros(n.value, self.RUN_DTYPE)
+        if n.value:
+            check(lib().rsmi_fenc_packet_runs(self._h, C.byref(n), out.ctypes.data),
+                  "rsmi_fenc_packet_runs")
+        return out
+
     @staticmethod
     def cook_span(lens):
         """RSMI_FEC_COOK_SPAN: bytes a packet of len bytes takes in a packed
