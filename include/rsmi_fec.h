@@ -151,16 +151,22 @@ typedef struct rsmi_fenc_packet_run {
 } rsmi_fenc_packet_run;
 int rsmi_fenc_packet_runs(const rsmi_fenc *enc, int64_t *n, rsmi_fenc_packet_run *out);
 
-/* Bytes a packet of len bytes takes in a packed cooked output: its cooked
- * form (crc 4 + iv <= 32 + iv_len 1 more) rounded up to whole 16-byte pieces. */
-#define RSMI_FEC_COOK_SPAN(len) ((((int64_t)(len)) + 37 + 15) & ~(int64_t)15)
+/* A packet's place in a packed cooked output: a 16-aligned span of
+ * RSMI_FEC_COOK_LEAD scratch bytes, then the packet, whose cooked form (crc 4
+ * + iv <= 32 + iv_len 1 more) fits the rest.  The lead puts every packet at the
+ * offset within a 16-byte piece it has in its slot (RSMI_FEC_SLOT_PACKET mod
+ * 16), so the cook works on whole aligned pieces. */
+#define RSMI_FEC_COOK_LEAD (RSMI_FEC_SLOT_PACKET % 16)
+#define RSMI_FEC_COOK_SPAN(len) ((((int64_t)(len)) + 37 + RSMI_FEC_COOK_LEAD + 15) & ~(int64_t)15)
 
 /* rsmi_fenc_run_cooked_dev with the cooked packets packed back to back, so the
- * buffer handed to the socket (or copied to the host for sendmmsg) holds only
- * packet bytes: packet p at out + sum over q < p of RSMI_FEC_COOK_SPAN(len_q)
- * (len from rsmi_fenc_packets), out_len[p] cooked bytes.  out: device or
- * pinned host memory, 16-aligned, out_cap >= that sum over all packets
- * (RSMI_ERR_INVALID otherwise).  Every packet fits (out_len >= 0). */
+ * buffer handed to the socket (or copied to the host for sendmmsg) holds
+ * little more than packet bytes: packet p's span starts at out + sum over
+ * q < p of RSMI_FEC_COOK_SPAN(len_q) (len from rsmi_fenc_packets), the packet
+ * RSMI_FEC_COOK_LEAD bytes into it, out_len[p] cooked bytes.  out: device or
+ * pinned host memory, 16-aligned, out_cap >= the sum over all packets
+ * (RSMI_ERR_INVALID otherwise).  Every packet fits (out_len >= 0).  The bytes
+ * of a span around its packet are unspecified. */
 int rsmi_fenc_run_cooked_packed_dev(rsmi_fenc *enc, uint8_t *slots_base, int64_t slot_stride,
                                     const struct rsmi_cook_ctx *ctx, uint64_t seed, uint8_t *out,
                                     int64_t out_cap, int32_t *out_len, void *stream);

@@ -19,6 +19,6 @@ for r in $(seq 1 $ROUNDS); do
         --output-format csv -d $O/p_${v}_$r -o run -- python3 $R/$SCRIPT > $O/${v}_$r.log 2>&1) || { tail $O/${v}_$r.log; exit 1; }
     python scripts/kstats.py $O/p_${v}_$r/run_kernel_stats.csv > $O/${v}_$r.txt
     rm -rf $O/p_${v}_$r
-    echo "== $v round $r"; grep -E "decode|bs_ragged" $O/${v}_$r.txt; grep -h "ms" $O/${v}_$r.log | tail -2 | cut -c1-200
+    echo "== $v round $r"; grep -E "${KPAT:-decode|bs_ragged}" $O/${v}_$r.txt; grep -h "ms" $O/${v}_$r.log | tail -2 | cut -c1-200
   done
 done

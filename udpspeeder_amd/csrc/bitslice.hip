@@ -13,15 +13,6 @@
 #ifndef BS_SPLIT
 #define BS_SPLIT 1  // uniform launches of codes with a split-k network use the 2-wave form
 #endif
-#ifndef BS_RAG_SPLIT
-#define BS_RAG_SPLIT 0  // ragged encode: 1 = low-register codes in their own kernel after the
-                        // others, 2 = the same on a forked stream, running beside them
-#endif
-#ifndef BS_RAG_LO_OCC
-#define BS_RAG_LO_OCC 4
-#endif
-// Codes whose network fits 128 VGPRs (at most 6 parity rows, or k <= 2).
-__host__ __device__ constexpr bool bs_rag_lo(int k, int n) { return n - k <= 6 || k <= 2; }
 #ifndef BS_PERSIST
 #define BS_PERSIST 0  // 1: balanced persistent grid (measured 5 % slower than one wave per chunk)
 #endif
@@ -50,9 +41,7 @@ BS_FOR_EACH_SPLIT(BS_SPLIT_KERNEL)
 #undef BS_SPLIT_KERNEL
 
 // One launch over every bucket of the built-in codes (code = index in the
-// generated list).  With BS_RAG_SPLIT the codes whose networks fit 128 VGPRs
-// (bs_rag_lo) get a kernel of their own at 4 waves/SIMD, and k_bs_ragged
-// keeps the others at 3.
+// generated list).
 __global__ __launch_bounds__(256, BS_OCC) void k_bs_ragged(const BsGroup *groups,
                                                            const uint32_t *colmap,
                                                            const uint32_t *waves, uint32_t nwaves,
@@ -61,36 +50,15 @@ __global__ __launch_bounds__(256, BS_OCC) void k_bs_ragged(const BsGroup *groups
     uint32_t code;
     if (!bs_rag_setup(groups, colmap, waves, nwaves, base, bytes, io, code)) return;
     int idx = 0;
-#define BS_RAG_CASE(K, N)                                          \
-    if ((!BS_RAG_SPLIT || !bs_rag_lo(K, N)) && code == (uint32_t)idx) { \
-        bs_code_##K##_##N(io);                                     \
-        return;                                                    \
-    }                                                              \
+#define BS_RAG_CASE(K, N)              \
+    if (code == (uint32_t)idx) {       \
+        bs_code_##K##_##N(io);         \
+        return;                        \
+    }                                  \
     ++idx;
     BS_FOR_EACH_CODE(BS_RAG_CASE)
 #undef BS_RAG_CASE
 }
-
-#if BS_RAG_SPLIT
-__global__ __launch_bounds__(256, BS_RAG_LO_OCC) void k_bs_ragged_lo(const BsGroup *groups,
-                                                                     const uint32_t *colmap,
-                                                                     const uint32_t *waves,
-                                                                     uint32_t nwaves, uint8_t *base,
-                                                                     uint32_t bytes) {
-    RagIO io;
-    uint32_t code;
-    if (!bs_rag_setup(groups, colmap, waves, nwaves, base, bytes, io, code)) return;
-    int idx = 0;
-#define BS_RAG_CASE(K, N)                                    \
-    if (bs_rag_lo(K, N) && code == (uint32_t)idx) {          \
-        bs_code_##K##_##N(io);                               \
-        return;                                              \
-    }                                                        \
-    ++idx;
-    BS_FOR_EACH_CODE(BS_RAG_CASE)
-#undef BS_RAG_CASE
-}
-#endif
 
 }  // namespace
 
@@ -126,45 +94,15 @@ int bitslice_code_n(int i) {
     return 0;
 }
 
-bool bitslice_code_lo(int i) {
-    return BS_RAG_SPLIT && bs_rag_lo(bitslice_code_k(i), bitslice_code_n(i));
-}
-
-// Waves [0, nhi) run the other codes, [nhi, nwaves) the bs_rag_lo ones (the
-// plan orders them so when BS_RAG_SPLIT is on).
 hipError_t launch_encode_bitslice_ragged(const rsmi_group *groups, const uint32_t *colmap,
-                                         const uint32_t *waves, uint32_t nwaves, uint32_t nhi,
-                                         uint8_t *base, uint32_t bytes, hipStream_t s,
-                                         hipStream_t aux, hipEvent_t fork, hipEvent_t join) {
+                                         const uint32_t *waves, uint32_t nwaves, uint8_t *base,
+                                         uint32_t bytes, hipStream_t s) {
     if (nwaves == 0) return hipSuccess;
-    const BsGroup *g = reinterpret_cast<const BsGroup *>(groups);
-    if (!BS_RAG_SPLIT) nhi = nwaves;
-    hipError_t e = hipSuccess;
-    const bool two = BS_RAG_SPLIT == 2 && aux && nhi && nhi < nwaves;
-    if (two) {  // the low-register kernel runs beside the other on a forked stream
-        e = hipEventRecord(fork, s);
-        if (e == hipSuccess) e = hipStreamWaitEvent(aux, fork, 0);
-        if (e != hipSuccess) return e;
-    }
-    if (nhi) {
-        uint32_t blocks = (nhi + 3) / 4;
-        if (BS_RAG_XCD) blocks = (blocks + 7) & ~7u;  // whole rounds of 8 XCDs (the remap)
-        k_bs_ragged<<<blocks, 256, 0, s>>>(g, colmap, waves, nhi, base, bytes);
-        e = hipGetLastError();
-    }
-#if BS_RAG_SPLIT
-    if (e == hipSuccess && nhi < nwaves) {
-        const uint32_t nlo = nwaves - nhi;
-        k_bs_ragged_lo<<<(nlo + 3) / 4, 256, 0, two ? aux : s>>>(g, colmap, waves + 2 * (size_t)nhi, nlo,
-                                                                base, bytes);
-        e = hipGetLastError();
-        if (e == hipSuccess && two) {
-            e = hipEventRecord(join, aux);
-            if (e == hipSuccess) e = hipStreamWaitEvent(s, join, 0);
-        }
-    }
-#endif
-    return e;
+    uint32_t blocks = (nwaves + 3) / 4;
+    if (BS_RAG_XCD) blocks = (blocks + 7) & ~7u;  // whole rounds of 8 XCDs (the remap)
+    k_bs_ragged<<<blocks, 256, 0, s>>>(reinterpret_cast<const BsGroup *>(groups), colmap, waves,
+                                       nwaves, base, bytes);
+    return hipGetLastError();
 }
 
 hipError_t launch_encode_bitslice_ragged_rtc(int k, int n, const rsmi_group *groups,

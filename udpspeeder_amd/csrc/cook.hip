@@ -344,15 +344,9 @@ __device__ __forceinline__ void load_round(u32x4 (&d)[kPpl], const uint8_t *pkt,
     }
 }
 
-// Bytes of round 0 that may be read before the packet's length is known:
-// whole pieces within its cap (the packet owns them), none if misaligned.
-// Pieces past the packet's extent are loaded but never stored.
-__device__ __forceinline__ int cap_extent(const CookArgs &a, const uint8_t *pkt, bool have) {
-    return (have && ((uintptr_t)pkt & 3) == 0) ? min(a.cap & ~15, kRound) : 0;
-}
-
+// Key stream at packet offset P (>= -12: the stream has a 16-byte lead).
 __device__ __forceinline__ u32x4 ks_piece(const CookArgs &a, int P) {
-    return a.ks ? *reinterpret_cast<const u32x4 *>(a.ks + P) : u32x4{0, 0, 0, 0};
+    return a.ks ? *reinterpret_cast<const u32x4_a4 *>(a.ks + P) : u32x4{0, 0, 0, 0};
 }
 
 // CRC input of piece P: bytes below n, the first 4 bytes complemented (init ~0).
@@ -361,6 +355,20 @@ __device__ __forceinline__ u32x4 ks_piece(const CookArgs &a, int P) {
 __device__ __forceinline__ u32x4 crc_in(u32x4 v, int P, int n) {
     if (__ballot(P + 16 > n)) v &= piece_mask(n - P);
     if (P == 0) v.x = ~v.x;
+    return v;
+}
+
+// The same on the packet's 16-byte grid when the packet starts ph (0, 4, 8 or
+// 12) bytes into a piece: piece P's bytes below ph are not the packet's (zero
+// for the CRC: leading zeros leave a zero register as it is), the message's
+// first 4 bytes are dword ph / 4 of piece 0.
+__device__ __forceinline__ u32x4 crc_in_ph(u32x4 v, int P, int n, int ph) {
+    if (__ballot(P + 16 > n)) v &= piece_mask(n - P);
+    if (P == 0) {
+        v &= ~piece_mask(ph);
+#pragma unroll
+        for (int d = 0; d < 4; ++d) v[d] = (4 * d == ph) ? ~v[d] : v[d];
+    }
     return v;
 }
 
@@ -389,20 +397,30 @@ __global__ __launch_bounds__(kThreads, COOK_OCC) void k_cook(CookArgs a) {
         uint8_t *opkt = !have ? nullptr
                         : a.dst_off ? a.dst + a.dst_off[gi]
                                     : (a.dst ? a.dst : a.base) + po;  // where the output goes
+        // a.phase: work on the 16-byte grid the packet sits in (an FEC packet
+        // starts 8 bytes into one, RSMI_FEC_SLOT_PACKET): whole-piece loads and
+        // stores line up with memory; the ph bytes before the packet are the
+        // slot's scratch.  Grid coordinates below: packet byte x is grid byte x + ph.
+        const int ph = (a.phase && have && ((uintptr_t)pkt & 3) == 0 &&
+                        (((uintptr_t)pkt ^ (uintptr_t)opkt) & 15) == 0)
+                           ? (int)((uintptr_t)pkt & 15) : 0;
+        const uint8_t *pga = pkt - ph;
+        uint8_t *oga = opkt - ph;
         // round 0 is read up to the packet's cap (every packet owns cap bytes), so
         // these loads fly together with the length load instead of after it
         u32x4 cur[kPpl];
-        load_round(cur, pkt, 0, hl, cap_extent(a, pkt, have));
+        load_round(cur, pga, 0, hl, have && ((uintptr_t)pkt & 3) == 0 ? min((a.cap + ph) & ~15, kRound) : 0);
         if (have) {
             L = packet_len(a, pk);
             if (obs) ivl = a.iv ? a.iv_len[pk] : 4 + (int)(splitmix(a.seed, (uint64_t)gi, 0) % 29u);
         }
         const int out = L + (ck ? 4 : 0) + (obs ? ivl + 1 : 0);
         // (a packed output has room for any iv_len <= RSMI_COOK_IV_MAX)
+        const int Lg = L + ph, outg = out + ph;  // payload end and output end on the grid
         const bool ok = have && L >= 0 && L <= RSMI_COOK_MAX_LEN && ivl <= RSMI_COOK_IV_MAX &&
-                        (a.dst_off || round16(out) <= a.cap) && round16(L) <= a.cap &&
+                        (a.dst_off || round16(outg) - ph <= a.cap) && round16(Lg) - ph <= a.cap &&
                         ((uintptr_t)pkt & 3) == 0;
-        const int ext = ok ? round16(out) : 0;
+        const int ext = ok ? round16(outg) : 0;
         const uint32_t magic = ivl ? 0xFFFFFFFFu / (uint32_t)ivl : 0u;
         if (ok && ivl && !a.iv && 8 * hl < ivl) {  // device-drawn IV: 8 bytes per draw, one per lane
             const uint64_t z = splitmix(a.seed, (uint64_t)gi, 1 + (uint64_t)hl);
@@ -419,8 +437,8 @@ __global__ __launch_bounds__(kThreads, COOK_OCC) void k_cook(CookArgs a) {
         wave_sync();
         CT(1);
         const uint32_t sstep = ivl ? mod_ivl(16u * kLpp, (uint32_t)ivl, magic) : 0u;
-        const int Q = (L + 15) >> 4;            // pieces holding payload (crc input)
-        const int P0 = L & ~15;                 // first piece that holds tail bytes
+        const int Q = (Lg + 15) >> 4;           // pieces holding payload (crc input)
+        const int P0 = Lg & ~15;                // first piece that holds tail bytes
         const int nrm = wave_max((ext + kRound - 1) / kRound);
         uint32_t acc = 0;
         u32x4 dt = {0, 0, 0, 0};                // this lane's tail piece, if any
@@ -428,21 +446,23 @@ __global__ __launch_bounds__(kThreads, COOK_OCC) void k_cook(CookArgs a) {
         for (int r = 0; r < nrm; ++r) {
             // rounds past the first (long packets); a packed output's tail may
             // end past the source slot, whose bytes there are never used
-            if (r) load_round(cur, pkt, r, hl, min(ext, a.cap & ~15));
+            if (r) load_round(cur, pga, r, hl, min(ext, (a.cap + ph) & ~15));
             const int qr = min(max(Q - 96 * r, 0), 96);
             // pieces at or past every packet's last crc piece in this round:
             // skip their CRC (a wave-uniform branch per piece slot)
             const int qr_max = COOK_SKIP ? wave_max(qr) : 96;
             RoundCrc<COOK_2CH != 0> rc;
-            uint32_t ivr = ivl ? mod_ivl((uint32_t)(r * kRound + 16 * hl), (uint32_t)ivl, magic) : 0u;
+            uint32_t ivr = ivl ? mod_ivl((uint32_t)(r * kRound + 16 * hl + 16 * ivl - ph), (uint32_t)ivl, magic)
+                               : 0u;
 #pragma unroll
             for (int p = 0; p < kPpl; ++p) {
-                const int P = r * kRound + 16 * (kLpp * p + hl);
-                if (ck && kLpp * p < qr_max) rc.add(T, crc_in(cur[p], P, L), p, kLpp * p + hl, qr);
-                if (P < ext && P + 16 <= L) {  // wholly payload: obscure + xor, store now
-                    u32x4 m = ks_piece(a, P);
+                const int P = r * kRound + 16 * (kLpp * p + hl);  // grid offset
+                if (ck && kLpp * p < qr_max) rc.add(T, crc_in_ph(cur[p], P, Lg, ph), p, kLpp * p + hl, qr);
+                // wholly payload (the head piece's bytes before the packet are scratch)
+                if (P < ext && P + 16 <= Lg) {  // obscure + xor, store now
+                    u32x4 m = ks_piece(a, P - ph);
                     if (ivl) m ^= iv_window_at(iv2w, ivr);
-                    st_piece(opkt + P, cur[p] ^ m);
+                    st_piece(oga + P, cur[p] ^ m);
                 } else if (P < ext && P >= P0) {
                     dt = cur[p];
                     Pt = P;
@@ -459,11 +479,11 @@ __global__ __launch_bounds__(kThreads, COOK_OCC) void k_cook(CookArgs a) {
         }
         CT(2);
         uint32_t crc = 0;
-        if (ck && L > 0) crc = ~unshift(T, acc, (uint32_t)(16 * Q - L));
+        if (ck && L > 0) crc = ~unshift(T, acc, (uint32_t)(16 * Q - Lg));
         // ---- tail: crc (BE), iv, iv_len appended after the payload -------------
         if (ok) {
             for (int t = hl; t < 64; t += kLpp) {
-                const int pos = P0 + t;
+                const int pos = P0 + t - ph;  // packet offset of overlay byte t
                 uint32_t v = 0;
                 if (pos >= L && pos < out) {
                     const int u = pos - L;
@@ -484,12 +504,12 @@ __global__ __launch_bounds__(kThreads, COOK_OCC) void k_cook(CookArgs a) {
             // the overlay holds the tail bytes before encrypt_0: the piece's key
             // stream covers payload and tail alike (one 16-B load, where a byte
             // load per tail byte stood in the overlay loop's dependent chain)
-            const u32x4 k = ks_piece(a, Pt);
+            const u32x4 k = ks_piece(a, Pt - ph);
             u32x4 m = k;
-            if (ivl) m ^= iv_window(iv2w, (uint32_t)Pt, (uint32_t)ivl, magic);
+            if (ivl) m ^= iv_window(iv2w, (uint32_t)(Pt + 16 * ivl - ph), (uint32_t)ivl, magic);
             const u32x4 o = *reinterpret_cast<const u32x4 *>(ovl + (Pt - P0));
-            const u32x4 lo = piece_mask(L - Pt), hi = piece_mask(out - Pt);
-            st_piece(opkt + Pt, ((dt ^ m) & lo) | ((o ^ k) & hi & ~lo) | (dt & ~hi));
+            const u32x4 lo = piece_mask(Lg - Pt), hi = piece_mask(outg - Pt);
+            st_piece(oga + Pt, ((dt ^ m) & lo) | ((o ^ k) & hi & ~lo) | (dt & ~hi));
         }
         if (have && hl == 0) a.out_len[gi] = ok ? out : -1;
         wave_sync();  // the scratch slice is rewritten by the next packet

@@ -23,7 +23,8 @@ struct rsmi_cook_ctx {
     int flags = 0;
     int max_blocks = 0;
     uint32_t *tabs = nullptr;
-    uint8_t *ks = nullptr;  // NULL when there is no XOR stage
+    uint8_t *ks = nullptr;  // NULL when there is no XOR stage; position p at ks[p], p >= -kCookKsLead
+    uint8_t *ks_mem = nullptr;  // the allocation (ks - kCookKsLead)
     // synchronous host path
     std::mutex mu;
     uint8_t *hbuf = nullptr;
@@ -176,10 +177,15 @@ extern "C" int rsmi_cook_ctx_create(const char *key, int flags, rsmi_cook_ctx **
     if (e == hipSuccess)
         e = hipMemcpy(c->tabs, t.blob.data(), sizeof(uint32_t) * t.blob.size(), hipMemcpyHostToDevice);
     if (e == hipSuccess && klen && !(flags & RSMI_COOK_NO_XOR)) {
-        std::vector<uint8_t> ks(rsmi::kCookKsBytes);
-        for (size_t p = 0; p < ks.size(); ++p) ks[p] = (uint8_t)key[p % klen];
-        e = hipMalloc(&c->ks, ks.size());
-        if (e == hipSuccess) e = hipMemcpy(c->ks, ks.data(), ks.size(), hipMemcpyHostToDevice);
+        // key[p % klen] for p in [-kCookKsLead, kCookKsBytes): the lead serves the
+        // phase pieces' bytes before a packet (never used, kept periodic)
+        const int lead = rsmi::kCookKsLead;
+        std::vector<uint8_t> ks(rsmi::kCookKsBytes + lead);
+        for (size_t i = 0; i < ks.size(); ++i)
+            ks[i] = (uint8_t)key[(size_t)(((int64_t)i - lead) % (int64_t)klen + klen) % klen];
+        e = hipMalloc(&c->ks_mem, ks.size());
+        if (e == hipSuccess) e = hipMemcpy(c->ks_mem, ks.data(), ks.size(), hipMemcpyHostToDevice);
+        if (e == hipSuccess) c->ks = c->ks_mem + lead;
     }
     if (e != hipSuccess) {
         rsmi_cook_ctx_destroy(c);
@@ -192,7 +198,7 @@ extern "C" int rsmi_cook_ctx_create(const char *key, int flags, rsmi_cook_ctx **
 extern "C" void rsmi_cook_ctx_destroy(rsmi_cook_ctx *c) {
     if (!c) return;
     if (c->tabs) (void)hipFree(c->tabs);
-    if (c->ks) (void)hipFree(c->ks);
+    if (c->ks_mem) (void)hipFree(c->ks_mem);
     if (c->hbuf) (void)hipFree(c->hbuf);
     delete c;
 }
@@ -263,6 +269,7 @@ int cook_packets(const rsmi_cook_ctx *c, uint8_t *slots, int64_t S, const rsmi_f
     a.pk = pk;
     a.pk_off = kSlotHeader;
     a.pk_idx = 1;
+    a.phase = 1;  // slot bytes before a packet are the slot's own scratch (RSMI_FEC_SLOT_PACKET)
     a.stride = S;
     a.count = npk;
     a.cap = (int32_t)(S - kSlotHeader);

@@ -165,9 +165,6 @@ struct rsmi_fenc {
     size_t carry_cap[2] = {0, 0};
     int carry_cur = 0;  // pending packets live in dcarry[carry_cur] (or the batch input)
     size_t carry_need = 0;  // bytes of dcarry[carry_cur] the last plan fills
-    // cooked runs into another buffer: the data packets cook on `aux` beside the encoder
-    hipStream_t aux = nullptr;
-    hipEvent_t fork = nullptr, join = nullptr;
 
     int tail_x() const { return cfg.rs_cnt; }
     int y_of(int x) const { return cfg.rs_y[x - 1]; }
@@ -536,9 +533,6 @@ void rsmi_fenc_destroy(rsmi_fenc *E) {
         if (E->dcarry[i]) (void)hipFree(E->dcarry[i]);
     for (PlanSet &B : E->ps)
         if (B.done) (void)hipEventDestroy(B.done);
-    if (E->aux) (void)hipStreamDestroy(E->aux);
-    if (E->fork) (void)hipEventDestroy(E->fork);
-    if (E->join) (void)hipEventDestroy(E->join);
     delete E;
 }
 
@@ -697,10 +691,6 @@ int prepare_run(rsmi_fenc *E, hipStream_t s) {
         for (PlanSet &B : E->ps)
             if (hipEventCreateWithFlags(&B.done, hipEventDisableTiming) != hipSuccess)
                 return fail(RSMI_ERR_HIP, "fenc: hipEventCreate");
-        if (hipStreamCreateWithFlags(&E->aux, hipStreamNonBlocking) != hipSuccess ||
-            hipEventCreateWithFlags(&E->fork, hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&E->join, hipEventDisableTiming) != hipSuccess)
-            return fail(RSMI_ERR_HIP, "fenc: aux stream");
         E->device = cur;
         // start compiling the run-time networks of the -f table's codes now, so
         // they are ready by the time those group sizes come (bitslice_rtc.cpp)
@@ -748,7 +738,7 @@ int run_dev(rsmi_fenc *E, uint8_t *slots, int64_t S, void *stream, const CookSpe
     // on the device into the two cook lists (data packets, parity packets)
     const size_t npk = ck ? E->P->packets.size() : 0, nrun = ck ? E->P->pruns.size() : 0;
     if (npk > (size_t)INT32_MAX) return fail(RSMI_ERR_INVALID, "fenc: more than 2^31 packets in one batch");
-    const int64_t na = ck ? E->P->n_data_pk : 0, nb = ck ? E->P->n_par_pk : 0;
+    const int64_t na = ck ? E->P->n_data_pk : 0;
     const FrameSrc *zsrc = E->P->srcs.empty() || E->P->max_src > rsmi::kFrameLdsSrc ? nullptr
                                                                                      : mapped_srcs(E->P->srcs);
     const size_t gb = E->P->jobs.size() * sizeof(FrameGroup),
@@ -761,7 +751,7 @@ int run_dev(rsmi_fenc *E, uint8_t *slots, int64_t S, void *stream, const CookSpe
     if (packed) {  // each run's first packet's place in the packed output
         int64_t o = 0;
         for (size_t i = 0; i < nrun; ++i) {
-            E->P->pruns[i].out0 = o;
+            E->P->pruns[i].out0 = o + RSMI_FEC_COOK_LEAD;
             o += (int64_t)E->P->pruns[i].count * RSMI_FEC_COOK_SPAN(E->P->pruns[i].len);
         }
         if (o > ck->out_cap)
@@ -801,21 +791,6 @@ int run_dev(rsmi_fenc *E, uint8_t *slots, int64_t S, void *stream, const CookSpe
         e = rsmi::launch_byte_runs(reinterpret_cast<const rsmi::ByteRun *>(E->dplan + ro),
                                    (int64_t)E->P->stale.size(), slots, S, E->dshadow, s);
     if (e != hipSuccess) return fail(RSMI_ERR_HIP, std::string("fenc frame: ") + hipGetErrorString(e));
-    // do_cook (my_send, packet.cpp:165-168) of the data packets, final now:
-    // into another buffer they cook on the aux stream beside the encoder (the
-    // cook is LDS- and latency-bound, the encoder memory- and VALU-bound)
-    const rsmi_fenc_packet *lists = reinterpret_cast<const rsmi_fenc_packet *>(E->dplan + xo);
-    const int64_t *doff = packed ? reinterpret_cast<const int64_t *>(E->dplan + dq) : nullptr;
-    const bool side = npk && ck->out && na;
-    if (side) {
-        e = hipEventRecord(E->fork, s);
-        if (e == hipSuccess) e = hipStreamWaitEvent(E->aux, E->fork, 0);
-        if (e != hipSuccess) return fail(RSMI_ERR_HIP, std::string("fenc fork: ") + hipGetErrorString(e));
-        rc = rsmi::cook_packets(ck->ctx, slots, S, lists, na, ck->out_len, ck->out, doff, ck->seed, E->aux);
-        if (rc) return rc;
-        e = hipEventRecord(E->join, E->aux);
-        if (e != hipSuccess) return fail(RSMI_ERR_HIP, std::string("fenc join: ") + hipGetErrorString(e));
-    }
     // parity of every group
     for (const Run &r : E->runs) {
         rc = rsmi_encode_dev(r.k, r.n, slots + r.slot0 * S + rsmi::kSlotShard, (int64_t)r.n * S, S,
@@ -829,14 +804,16 @@ int run_dev(rsmi_fenc *E, uint8_t *slots, int64_t S, void *stream, const CookSpe
         e = rsmi::launch_carry(reinterpret_cast<const CarryCopy *>(E->dplan + co),
                                (int64_t)E->P->carry.size(), carry, s);
     if (e != hipSuccess) return fail(RSMI_ERR_HIP, std::string("fenc carry: ") + hipGetErrorString(e));
-    // the parity packets (and in place, after the blob buffer update above has
-    // read the plain shards, the data packets too)
+    // do_cook (my_send, packet.cpp:165-168) of every packet, after the blob
+    // buffer update above has read the plain shards: one launch over both cook
+    // lists, which lie back to back.  (Cooking the data packets on a forked
+    // stream beside the encoder measured no faster: the two kernels slow each
+    // other down)
     if (npk) {
-        rc = side || !na ? RSMI_OK
-                         : rsmi::cook_packets(ck->ctx, slots, S, lists, na, ck->out_len, ck->out, doff, ck->seed, s);
-        if (!rc && nb) rc = rsmi::cook_packets(ck->ctx, slots, S, lists + na, nb, ck->out_len, ck->out, doff, ck->seed, s);
+        rc = rsmi::cook_packets(ck->ctx, slots, S, reinterpret_cast<const rsmi_fenc_packet *>(E->dplan + xo),
+                                (int64_t)npk, ck->out_len, ck->out,
+                                packed ? reinterpret_cast<const int64_t *>(E->dplan + dq) : nullptr, ck->seed, s);
         if (rc) return rc;
-        if (side && hipStreamWaitEvent(s, E->join, 0) != hipSuccess) return fail(RSMI_ERR_HIP, "fenc: join wait");
     }
     e = hipEventRecord(E->P->done, s);
     if (e != hipSuccess) return fail(RSMI_ERR_HIP, std::string("fenc event: ") + hipGetErrorString(e));

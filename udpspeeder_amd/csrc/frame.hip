@@ -23,6 +23,10 @@ namespace rsmi {
 namespace {
 
 constexpr int kThreads = 256;
+#ifndef FRAME_THREADS
+#define FRAME_THREADS 256  // k_frame's threads per group (one workgroup frames one group)
+#endif
+constexpr int kFThreads = FRAME_THREADS;
 constexpr int kLdsSrc = (int)kFrameLdsSrc;  // source records staged in LDS per group
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -147,8 +151,14 @@ __device__ u32x4 stream_piece(const V &src, uint32_t j, uint32_t jend, int64_t b
     return acc;
 }
 
-constexpr int kBatch = 4;     // pieces per thread per step: their loads are in flight together
-constexpr int kSlowMax = 1024;  // boundary pieces queued per job (more are assembled in place)
+#ifndef FRAME_BATCH
+#define FRAME_BATCH 4
+#endif
+constexpr int kBatch = FRAME_BATCH;     // pieces per thread per step: their loads are in flight together
+#ifndef FRAME_SLOW_MAX
+#define FRAME_SLOW_MAX 1024
+#endif
+constexpr int kSlowMax = FRAME_SLOW_MAX;  // boundary pieces queued per job (more are assembled in place)
 
 struct Piece {
     uint32_t i, q, j;
@@ -208,10 +218,10 @@ __device__ __forceinline__ void frame_job(const FrameGroup &G, const View<kGloba
     const uint32_t pps = (G.fec_len + 15) >> 4;
     const uint32_t total = pps * G.nframe;
     const uint32_t magic = pps == 1 ? 0u : (uint32_t)(0xFFFFFFFFu / pps) + 1u;
-    for (uint32_t t0 = threadIdx.x; t0 < total; t0 += kBatch * kThreads) {
+    for (uint32_t t0 = threadIdx.x; t0 < total; t0 += kBatch * kFThreads) {
         Piece P[kBatch];
 #pragma unroll
-        for (int u = 0; u < kBatch; ++u) P[u] = piece_at(G, min(t0 + u * kThreads, total - 1), pps, magic);
+        for (int u = 0; u < kBatch; ++u) P[u] = piece_at(G, min(t0 + u * kFThreads, total - 1), pps, magic);
         if (G.mode == 0) {  // kBatch interleaved searches (same trip count)
             uint32_t n = nsrc;
             while (n > 1) {
@@ -236,7 +246,7 @@ __device__ __forceinline__ void frame_job(const FrameGroup &G, const View<kGloba
         for (int u = 0; u < kBatch; ++u) v[u] = window(A[u], 0, 16);
 #pragma unroll
         for (int u = 0; u < kBatch; ++u) {
-            const uint32_t t = t0 + u * kThreads;
+            const uint32_t t = t0 + u * kFThreads;
             if (t >= total) continue;
             if (fast[u]) {
                 put_piece(s0, slot_stride, P[u], v[u]);
@@ -249,13 +259,13 @@ __device__ __forceinline__ void frame_job(const FrameGroup &G, const View<kGloba
     __syncthreads();
     const uint32_t nq = *nslow;
     if (nq <= (uint32_t)kSlowMax) {
-        for (uint32_t k = threadIdx.x; k < nq; k += kThreads) {
+        for (uint32_t k = threadIdx.x; k < nq; k += kFThreads) {
             Piece Q = piece_at(G, slow[k], pps, magic);
             if (G.mode == 0) Q.j = find_record(src, nsrc, Q.b);
             put_piece(s0, slot_stride, Q, slow_piece(G, src, nsrc, Q));
         }
     } else {  // queue overflow (thousands of tiny records): every boundary piece in place
-        for (uint32_t t = threadIdx.x; t < total; t += kThreads) {
+        for (uint32_t t = threadIdx.x; t < total; t += kFThreads) {
             Piece Q = piece_at(G, t, pps, magic);
             if (G.mode == 0) Q.j = find_record(src, nsrc, Q.b);
             const int64_t q0 = G.mode == 0 ? (int64_t)src.off(Q.j) + 2 : 2;
@@ -265,7 +275,7 @@ __device__ __forceinline__ void frame_job(const FrameGroup &G, const View<kGloba
     }
 }
 
-__global__ __launch_bounds__(kThreads) void k_frame(const FrameGroup *groups, int64_t ngroups,
+__global__ __launch_bounds__(kFThreads) void k_frame(const FrameGroup *groups, int64_t ngroups,
                                                      const FrameSrc *srcs, CarryBase carry,
                                                      uint8_t *slots, int64_t slot_stride) {
     __shared__ LdsSrc lsrc;
@@ -278,7 +288,7 @@ __global__ __launch_bounds__(kThreads) void k_frame(const FrameGroup *groups, in
         const uint32_t nsrc = G.mode == 0 ? G.nsrc : G.nframe;
         const bool in_lds = nsrc <= (uint32_t)kLdsSrc;
         if (in_lds)
-            for (uint32_t t = threadIdx.x; t < nsrc; t += kThreads) {
+            for (uint32_t t = threadIdx.x; t < nsrc; t += kFThreads) {
                 const FrameSrc f = gs[t];
                 lsrc.addr[t] = (uint64_t)(uintptr_t)carry.resolve(f.addr);
                 lsrc.off[t] = f.off;
@@ -289,7 +299,7 @@ __global__ __launch_bounds__(kThreads) void k_frame(const FrameGroup *groups, in
         uint8_t *s0 = slots + (int64_t)G.slot0 * slot_stride;
         // headers: seq | mode | k | m | index (fec_manager.cpp:318-333); mode-1
         // data packets carry k = m = 0 (:321-323)
-        for (uint32_t j = threadIdx.x; j < G.nslots; j += kThreads) {
+        for (uint32_t j = threadIdx.x; j < G.nslots; j += kFThreads) {
             const bool zero_km = G.mode == 1 && j < G.nframe;
             const uint32_t w1 = (uint32_t)G.mode |
                                 (zero_km ? 0u : ((uint32_t)G.k << 8 | (uint32_t)G.m << 16)) |
@@ -412,7 +422,7 @@ hipError_t launch_frame(const FrameGroup *groups, int64_t ngroups, const FrameSr
                         CarryBase carry, uint8_t *slots, int64_t slot_stride, hipStream_t s) {
     if (ngroups <= 0) return hipSuccess;
     const int64_t blocks = ngroups < 65536 ? ngroups : 65536;
-    k_frame<<<(unsigned)blocks, kThreads, 0, s>>>(groups, ngroups, srcs, carry, slots, slot_stride);
+    k_frame<<<(unsigned)blocks, kFThreads, 0, s>>>(groups, ngroups, srcs, carry, slots, slot_stride);
     return hipGetLastError();
 }
 

@@ -50,9 +50,6 @@ struct rsmi_ragged_plan {
     uint32_t bytes = 0;       // extent of the batch from base (bitslice path)
     uint32_t nwaves = 0;
     uint32_t nwaves_builtin = 0;  // waves [0, nwaves_builtin) belong to build-time codes
-    uint32_t nwaves_hi = 0;       // ... of which [0, nwaves_hi) are not bitslice_code_lo
-    hipStream_t aux = nullptr;    // the low-register kernel's forked stream (BS_RAG_SPLIT 2)
-    hipEvent_t fork = nullptr, join = nullptr;
     struct RtcBucket {
         int k, n;
         uint32_t first, count;  // slice of the wave list
@@ -180,20 +177,8 @@ extern "C" int rsmi_ragged_plan_create(const rsmi_group *g, int64_t ngroups,
                 const int na = rsmi::bitslice_code_n(a), nb2 = rsmi::bitslice_code_n(b);
                 return na != nb2 ? na > nb2 : ka > kb;
             });
-        // the low-register kernel's codes after the others (same order within)
-        std::stable_partition(order.begin(), order.begin() + std::min(nb, nbuiltin),
-                              [](int b) { return !rsmi::bitslice_code_lo(b); });
-        bool lo_seen = false;
         for (int b : order) {
-            if (b < nbuiltin && !lo_seen && rsmi::bitslice_code_lo(b)) {
-                P->nwaves_hi = (uint32_t)(waves.size() / 2);
-                lo_seen = true;
-            }
-            if (b == nbuiltin) {
-                P->nwaves_builtin = (uint32_t)(waves.size() / 2);
-                if (!lo_seen) P->nwaves_hi = P->nwaves_builtin;
-                lo_seen = true;
-            }
+            if (b == nbuiltin) P->nwaves_builtin = (uint32_t)(waves.size() / 2);
             const uint32_t first = (uint32_t)(waves.size() / 2);
             for (uint64_t w = 0; w < (cols[(size_t)b] + 127) / 128; ++w) {
                 waves.push_back((uint32_t)b);
@@ -206,7 +191,6 @@ extern "C" int rsmi_ragged_plan_create(const rsmi_group *g, int64_t ngroups,
         }
         P->nwaves = (uint32_t)(waves.size() / 2);
         if (nb <= nbuiltin) P->nwaves_builtin = P->nwaves;
-        if (!lo_seen) P->nwaves_hi = P->nwaves_builtin;
     }
     // decode classes: the width each group's tiles take (decode.hip).  Each
     // class kernel runs one resident round of workgroups; the class's groups
@@ -331,14 +315,6 @@ extern "C" int rsmi_ragged_plan_create(const rsmi_group *g, int64_t ngroups,
         delete P;
         return fail(RSMI_ERR_HIP, std::string("ragged plan upload: ") + hipGetErrorString(e));
     }
-    if (P->nwaves_hi < P->nwaves_builtin) {  // forked stream for the low-register kernel
-        if (hipStreamCreateWithFlags(&P->aux, hipStreamNonBlocking) != hipSuccess ||
-            hipEventCreateWithFlags(&P->fork, hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&P->join, hipEventDisableTiming) != hipSuccess) {
-            rsmi_ragged_plan_destroy(P);
-            return fail(RSMI_ERR_HIP, "ragged plan: aux stream");
-        }
-    }
     *out = P;
     return RSMI_OK;
 }
@@ -350,8 +326,8 @@ extern "C" int rsmi_encode_ragged_plan(const rsmi_ragged_plan *P, uint8_t *base,
     hipStream_t s = (hipStream_t)stream;
     hipError_t e;
     if (P->bitslice) {
-        e = rsmi::launch_encode_bitslice_ragged(P->d_groups, P->d_colmap, P->d_waves, P->nwaves_builtin,
-                                                P->nwaves_hi, base, P->bytes, s, P->aux, P->fork, P->join);
+        e = rsmi::launch_encode_bitslice_ragged(P->d_groups, P->d_colmap, P->d_waves,
+                                                P->nwaves_builtin, base, P->bytes, s);
         for (size_t i = 0; e == hipSuccess && i < P->rtc.size(); ++i) {
             const auto &b = P->rtc[i];
             e = rsmi::launch_encode_bitslice_ragged_rtc(b.k, b.n, P->d_groups, P->d_colmap,
@@ -394,8 +370,5 @@ extern "C" int rsmi_ragged_plan_uses_bitslice(const rsmi_ragged_plan *P) {
 extern "C" void rsmi_ragged_plan_destroy(rsmi_ragged_plan *P) {
     if (!P) return;
     if (P->mem) (void)hipFree(P->mem);
-    if (P->aux) (void)hipStreamDestroy(P->aux);
-    if (P->fork) (void)hipEventDestroy(P->fork);
-    if (P->join) (void)hipEventDestroy(P->join);
     delete P;
 }

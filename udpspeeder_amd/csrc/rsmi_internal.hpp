@@ -129,11 +129,9 @@ int bitslice_code_k(int idx);  // (k, n) of generated code idx
 int bitslice_code_n(int idx);
 // Ragged bucketed launch over a host-built plan (ragged.cpp): colmap entries
 // (group << 12) | piece, waves = {code index, first column} pairs.
-bool bitslice_code_lo(int idx);  // ragged encode: runs in the low-register kernel
 hipError_t launch_encode_bitslice_ragged(const rsmi_group *groups, const uint32_t *colmap,
-                                         const uint32_t *waves, uint32_t nwaves, uint32_t nhi,
-                                         uint8_t *base, uint32_t bytes, hipStream_t s,
-                                         hipStream_t aux, hipEvent_t fork, hipEvent_t join);
+                                         const uint32_t *waves, uint32_t nwaves, uint8_t *base,
+                                         uint32_t bytes, hipStream_t s);
 
 // Codes without a build-time network (bitslice_rtc.cpp): emitted and compiled
 // with hipRTC in the background when first made resident.
@@ -220,6 +218,7 @@ constexpr int kCookTabDecook = kCookZH2;                            // k_decook'
 constexpr int kCookTabWords = kCookZH2 + (COOK_2CH ? 1024 : 0);     // the blob, k_cook's tables
 static_assert(!(COOK_NIB && COOK_S16), "COOK_NIB and COOK_S16 are alternatives");
 constexpr int kCookKsBytes = 65536 + 128;  // key stream covers every byte position used
+constexpr int kCookKsLead = 16;            // ... and 16 bytes before position 0 (phase pieces)
 
 struct CookArgs {
     uint8_t *base;
@@ -230,6 +229,8 @@ struct CookArgs {
     int32_t pk_off;              // pk[i].len bytes (len unused)
     int32_t pk_idx;              // 1: pk[i].event is packet i's index in the batch (IV draw, out_len,
                                  // dst_off), a cook list of k_expand_packets
+    int32_t phase;               // 1: the bytes of a packet's first 16-byte piece before it (source and
+                                 // output alike) are scratch, so k_cook works on whole aligned pieces
     uint8_t *mirror;             // de_cook only: the output also at mirror + its offset (pinned host)
     const int64_t *dst_off;      // packed output: packet i's output at dst + dst_off[i], room for
                                  // RSMI_FEC_COOK_SPAN(len) bytes (NULL: dst + its own offset)
@@ -276,11 +277,18 @@ constexpr uint64_t kCarryTag = 1ull << 63, kCarryBuf1 = 1ull << 62, kCarryOff = 
 struct CarryBase {
     const uint8_t *buf[2];
     __host__ __device__ const uint8_t *resolve(uint64_t a) const {
-        return (a & kCarryTag) ? buf[(a & kCarryBuf1) ? 1 : 0] + (a & kCarryOff)
-                               : reinterpret_cast<const uint8_t *>(a);
+        // a mask select, not buf[i]: an indexed member (which LLVM makes of a
+        // plain ?: as well) sends the struct to scratch in k_frame
+        const uint64_t b0 = (uint64_t)(uintptr_t)buf[0], b1 = (uint64_t)(uintptr_t)buf[1];
+        const uint8_t *b = reinterpret_cast<const uint8_t *>(
+            (uintptr_t)(b0 ^ ((b0 ^ b1) & (0 - ((a >> 62) & 1)))));
+        return (a & kCarryTag) ? b + (a & kCarryOff) : reinterpret_cast<const uint8_t *>(a);
     }
 };
-constexpr uint32_t kFrameLdsSrc = 1024;  // k_frame stages a job's records in LDS up to this many
+#ifndef FRAME_LDS_SRC
+#define FRAME_LDS_SRC 1024
+#endif
+constexpr uint32_t kFrameLdsSrc = FRAME_LDS_SRC;  // k_frame stages a job's records in LDS up to this many
 struct FrameSrc {
     uint64_t addr;      // payload address (carry-tagged or device)
     uint32_t len;

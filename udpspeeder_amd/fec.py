@@ -29,6 +29,7 @@ from ._lib import check, lib, rsmi_fec_config, rsmi_fenc_packet
 
 HEADER = 8
 SLOT_PACKET = 120   # RSMI_FEC_SLOT_PACKET: packet offset in a slot
+COOK_LEAD = SLOT_PACKET % 16  # RSMI_FEC_COOK_LEAD: first packet's offset in a packed cooked output
 SLOT_SHARD = 128    # RSMI_FEC_SLOT_SHARD: shard offset (128-byte aligned rows)
 
 
@@ -189,16 +190,17 @@ class FecEncoder:
     @staticmethod
     def cook_span(lens):
         """RSMI_FEC_COOK_SPAN: bytes a packet of len bytes takes in a packed
-        cooked output (its cooked form rounded up to 16-byte pieces)."""
-        return (np.asarray(lens, np.int64) + 37 + 15) // 16 * 16
+        cooked output (COOK_LEAD scratch bytes, then its cooked form, rounded
+        up to 16-byte pieces)."""
+        return (np.asarray(lens, np.int64) + 37 + COOK_LEAD + 15) // 16 * 16
 
     def packed_offsets(self):
         """Where run_cooked_packed puts each packet of the last plan, and the
         total bytes: (int64 offsets, total)."""
         sp = self.cook_span(self._last_packets["len"])
-        offs = np.zeros(len(sp), np.int64)
+        offs = np.full(len(sp), COOK_LEAD, np.int64)
         if len(sp) > 1:
-            np.cumsum(sp[:-1], out=offs[1:])
+            offs[1:] += np.cumsum(sp[:-1])
         return offs, int(sp.sum())
 
     def run_cooked_packed(self, slots, slot_stride: int, cook, seed: int, out, out_len=None,
