@@ -93,7 +93,7 @@ def bitmat(c: int):
 RING = int(os.environ.get("BS_RING", "4"))  # raw-load ring: shard j+RING is requested while shard j is computed
 
 
-MAX_ROWS = 10  # parity rows per pass: 8 accumulators each (at 12 rows the 168-VGPR budget spills)
+MAX_ROWS = int(os.environ.get("BS_MAX_ROWS", "10"))  # parity rows per pass: 8 accumulators each (at 12 rows the 168-VGPR budget spills)
 
 
 def row_blocks(m: int):
