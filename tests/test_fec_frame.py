@@ -137,6 +137,34 @@ def test_packet_runs_expand_to_the_packet_list(fx, name, nbatch):
     enc.close()
 
 
+@pytest.mark.gpu
+def test_gpu_packed_cook_bounds(gpu):
+    """rsmi_fenc_run_cooked_packed_dev refuses an out_cap one byte short of the
+    packed spans, before any launch; with the exact size every packet fits and
+    sits RSMI_FEC_COOK_LEAD bytes into its 16-aligned span."""
+    import torch
+    from udpspeeder_amd.cook import CookContext
+    from udpspeeder_amd.fec import COOK_LEAD, FecEncoder
+    enc = FecEncoder("20:10", 0, 1250, 200, seq0=3)
+    ctx = CookContext(b"k")
+    lens = np.array([1000, 17, 0, 1200, 64, -1], np.int32)
+    offs = np.array([0, 1008, 1040, 1056, 2272, 0], np.uint64)
+    inbuf = torch.randint(0, 256, (4096,), dtype=torch.uint8, device="cuda")
+    p = enc.plan(lens, offs, inbuf)
+    S = p.slot_stride_min
+    slots = torch.zeros(p.n_slots * S, dtype=torch.uint8, device="cuda")
+    po, total = enc.packed_offsets()
+    assert total % 16 == 0 and (po % 16 == COOK_LEAD).all()
+    short = torch.zeros(total, dtype=torch.uint8, device="cuda")
+    with pytest.raises(Exception, match="out_cap"):
+        enc.run_cooked_packed(slots, S, ctx, 1, short[:total - 16])
+    ol = enc.run_cooked_packed(slots, S, ctx, 1, short).cpu().numpy()[:len(p.packets)]
+    assert (ol >= p.packets["len"] + 9).all()
+    assert (po + ol <= np.append(po[1:] - COOK_LEAD, total)).all()
+    enc.close()
+    ctx.close()
+
+
 def _run_gpu(enc, lens, ev, cuts, torch):
     """Run the events through the GPU in batches; returns the emitted packets."""
     out = []

@@ -55,6 +55,10 @@ constexpr int kWaves = 4;      // waves per block (one group each)
 constexpr int kRing = DEC_RING;  // survivors in flight per wave
 constexpr int kRows = 10;      // max e handled by the one-wave kernels
 constexpr int kPass = 5;       // rows accumulated per pass over the survivors
+#ifndef DEC_FPASS
+#define DEC_FPASS 5            // ... in the fused uniform kernel (<= kTabRows)
+#endif
+constexpr int kFPass = DEC_FPASS;
 constexpr int kTile = 1280;    // bytes per lane-tile pass (64 x 16 + 64 x 4)
 #ifndef DEC_ST_SGPR
 #define DEC_ST_SGPR 0          // 1: row offset of the rebuilt-row stores in soffset (see bitslice.hip
@@ -86,6 +90,9 @@ constexpr int kTile = 1280;    // bytes per lane-tile pass (64 x 16 + 64 x 4)
 #endif
 #ifndef DEC_ROWGUARD
 #define DEC_ROWGUARD 1         // fused kernel: row guards on an opaque SGPR (see the MAC loop)
+#endif
+#ifndef DEC_GRID_PER_CU
+#define DEC_GRID_PER_CU 8      // fused kernel: blocks per CU in the (persistent) grid
 #endif
 #ifndef DEC_PAIR
 #define DEC_PAIR 0             // uniform kernel: fold survivors in pairs (fewer XORs, more VGPRs)
@@ -615,12 +622,12 @@ __global__ __launch_bounds__(256, DEC_OCC) void k_decode_fused(UniformArgs a, co
 
         // ---- 3. Gauss-Jordan on [A | M], e x (e+k) ------------------------------
         // ---- 3. coefficients: Lagrange form (see LTables), computed per block
-        // of kPass rows when the block's pass starts, below
+        // of kFPass rows when the block's pass starts, below
 
 #if DEC_TRACE
         const uint64_t tr2 = trace_now();
 #endif
-        // ---- 4. stream the survivors: passes over (tile, block of kPass rows) --
+        // ---- 4. stream the survivors: passes over (tile, block of kFPass rows) --
         // the 3-bit split selectors of a survivor's 5 dwords
         auto split = [](const u32x4 &v, uint32_t d, uint32_t (&s0)[5], uint32_t (&s1)[5],
                         uint32_t (&s2)[5]) {
@@ -641,13 +648,13 @@ __global__ __launch_bounds__(256, DEC_OCC) void k_decode_fused(UniformArgs a, co
             rq[q] = __builtin_amdgcn_raw_buffer_load_b128(r, v16, DEC_NOMEM ? 0u : so, LDAUX);
             rd[q] = __builtin_amdgcn_raw_buffer_load_b32(r, v4, DEC_NOMEM ? 0u : so, LDAUX);
         };
-        for (int rb = 0; rb < e; rb += kPass) {
+        for (int rb = 0; rb < e; rb += kFPass) {
             if (rb) start_tile(0);  // block 0's first loads are already in flight
-            {   // coefficients of rows rb .. rb + kPass - 1 into the slice's table rows
+            {   // coefficients of rows rb .. rb + kFPass - 1 into the slice's table rows
                 const uint32_t xs = LT.px[sel_lane & 255u];
                 const uint32_t B = lagrange_b(k, xs, LT);
                 const uint32_t xm = lane + rb < e ? (uint32_t)LT.px[L.miss[lane + rb]] : 0u;
-                lagrange_rows<kPass>(k, e - rb < kPass ? e - rb : kPass, xs, B, xm, LT, lane,
+                lagrange_rows<kFPass>(k, e - rb < kFPass ? e - rb : kFPass, xs, B, xm, LT, lane,
                                      [&](int r, uint32_t v) {
                                          uint32_t *dst = L.tab + (lane * kTabRows + r) * 8;
                                          reinterpret_cast<uint4 *>(dst)[0] = LT.t01[v];
@@ -658,9 +665,9 @@ __global__ __launch_bounds__(256, DEC_OCC) void k_decode_fused(UniformArgs a, co
             const int rt = rb;  // table row of row rb + r: r
             for (int toff = 0; toff < a.len; toff += kTile) {
                 if (toff) start_tile(toff);  // the pass's first loads
-                uint32_t acc[kPass][5];
+                uint32_t acc[kFPass][5];
 #pragma unroll
-                for (int r = 0; r < kPass; ++r)
+                for (int r = 0; r < kFPass; ++r)
 #pragma unroll
                     for (int w = 0; w < 5; ++w) acc[r][w] = 0;
                 int z = 0;  // VGPR zero: one address add per survivor (see Rebuild::run)
@@ -680,7 +687,7 @@ __global__ __launch_bounds__(256, DEC_OCC) void k_decode_fused(UniformArgs a, co
                             const uint32_t *ta = L.tab + (j * kTabRows + rb - rt) * 8;
                             const uint32_t *tb = ta + kTabRows * 8;
 #pragma unroll
-                            for (int r = 0; r < kPass; ++r) {
+                            for (int r = 0; r < kFPass; ++r) {
                                 if (rb + r < e) {
                                     const uint4 t = reinterpret_cast<const uint4 *>(ta + r * 8)[0];
                                     const uint32_t t2 = ta[r * 8 + 4];
@@ -710,7 +717,7 @@ __global__ __launch_bounds__(256, DEC_OCC) void k_decode_fused(UniformArgs a, co
                             int nr = e - rb;
                             if (DEC_ROWGUARD) asm volatile("" : "+s"(nr));
 #pragma unroll
-                            for (int r = 0; r < kPass; ++r) {
+                            for (int r = 0; r < kFPass; ++r) {
                                 if (DEC_FAKE ? r < DEC_FAKE : r < nr) {  // DEC_FAKE: measurement only
                                     const uint4 t = reinterpret_cast<const uint4 *>(ta + r * 8)[0];
                                     const uint32_t t2 = ta[r * 8 + 4];
@@ -725,7 +732,7 @@ __global__ __launch_bounds__(256, DEC_OCC) void k_decode_fused(UniformArgs a, co
                     }
                 }
 #pragma unroll
-                for (int r = 0; r < kPass; ++r) {
+                for (int r = 0; r < kFPass; ++r) {
                     if (rb + r < e) {
                         const uint32_t so = __builtin_amdgcn_readlane(mo_lane, rb + r);
                         const u32x4 v = {acc[r][0], acc[r][1], acc[r][2], acc[r][3]};
@@ -1233,7 +1240,7 @@ hipError_t launch_decode_fused(const UniformArgs &a, const uint8_t *present,
                                bool host_shards) {
     const size_t lds = kLTabBytes + (size_t)kWaves * wave_lds_bytes(a.k);
     int64_t blocks = (a.ngroups + kWaves - 1) / kWaves;
-    const int64_t cap = 256 * 8;
+    const int64_t cap = 256 * DEC_GRID_PER_CU;
     if (blocks > cap) blocks = cap;
     if (blocks < 1) blocks = 1;
     if (host_shards)
