@@ -138,15 +138,16 @@ int rsmi_fenc_run_cooked_dev(rsmi_fenc *enc, uint8_t *slots_base, int64_t slot_s
                              int32_t *out_len, void *stream);
 
 /* The last plan's packet list as runs (diagnostics and tests): packets first
- * .. first + count - 1 sit in slots slot .. slot + count - 1, len bytes each;
- * the first ndata are data packets, at afirst.. of the data-packet cook list,
- * the rest parity packets at bfirst.. of the parity list.  Cooked runs upload
- * these instead of the per-packet list and expand them on the device.  out0
- * is filled in by packed cooked runs.  n receives the run count; out (NULL:
+ * .. first + count - 1 sit in slots slot .. slot + count - 1 of framing job
+ * `job`, len bytes each; the first ndata are data packets of clean shards
+ * (framed and cooked in one pass by a fused cooked run), at afirst.. of that
+ * cook list, the rest at bfirst.. of the other.  Cooked runs upload these
+ * instead of the per-packet list and expand them on the device.  out0 is
+ * filled in by packed cooked runs.  n receives the run count; out (NULL:
  * count only) n entries. */
 typedef struct rsmi_fenc_packet_run {
     int64_t slot, out0;
-    int32_t first, afirst, bfirst, len;
+    int32_t first, afirst, bfirst, len, job;
     uint16_t count, ndata;
 } rsmi_fenc_packet_run;
 int rsmi_fenc_packet_runs(const rsmi_fenc *enc, int64_t *n, rsmi_fenc_packet_run *out);

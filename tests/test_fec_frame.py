@@ -97,9 +97,10 @@ def test_planner_matches_reference_fixtures(fx, name, nbatch):
 def test_packet_runs_expand_to_the_packet_list(fx, name, nbatch):
     """The runs a cooked run uploads (no GPU): expanded as k_expand_packets
     does, they give every packet of rsmi_fenc_packets once, in order, with its
-    slot and length; data packets (a group's first k slots, or a mode-1 packet
-    sent ahead in a slot of its own) fill cook list A and parity packets list
-    B, each in packet order."""
+    slot and length; list A (data packets of clean shards: a mode-0 group's
+    leading data shards that end before its blob does, every mode-1 data
+    packet) and list B (the rest, every parity packet) each keep packet
+    order."""
     from udpspeeder_amd.fec import FecEncoder
     c = _case(fx, name)
     enc = FecEncoder(c["rs"], c["mode"], c["mtu"], c["ql"], seq0=c["seq0"])
@@ -125,7 +126,8 @@ def test_packet_runs_expand_to_the_packet_list(fx, name, nbatch):
             lst.sort()
             assert [x for x, _ in lst] == list(range(len(lst)))
             assert [i for _, i in lst] == sorted(i for _, i in lst)
-        # data / parity by slot: a slot of group g is parity iff its index >= k
+        # list A holds data packets only (of clean shards: a run's leading
+        # data packets), every parity packet is in list B
         g = p.groups
         kind = {}
         for s0, k, m in zip(g["slot0"], g["k"], g["m"]):
@@ -133,7 +135,11 @@ def test_packet_runs_expand_to_the_packet_list(fx, name, nbatch):
                 kind[int(s0) + j] = j >= int(k)
         par = {i for _, i in lb}
         for i in range(npk):
-            assert (i in par) == kind.get(int(p.packets["slot"][i]), False), i
+            if kind.get(int(p.packets["slot"][i]), False):
+                assert i in par, i
+        if c["mode"] == 1:  # mode-1 data shards are always clean
+            assert all(not kind.get(int(p.packets["slot"][i]), False) for _, i in la)
+            assert len(la) == sum(1 for i in range(npk) if not kind.get(int(p.packets["slot"][i]), False))
     enc.close()
 
 

@@ -34,6 +34,7 @@
 #include "../../include/rsmi_cook.h"
 
 namespace rsmi {
+#include "frame_piece.hpp"
 namespace {
 
 #ifndef COOK_TRACE
@@ -645,11 +646,256 @@ __global__ __launch_bounds__(kThreads, COOK_OCC) void k_decook(CookArgs a) {
     }
 }
 
+// ---- the fused framing cook -------------------------------------------------
+// k_cook with k_frame in front: each list-A packet is a data packet of a clean
+// shard (FrameGroup.nclean), so its bytes are the 8-byte header followed by
+// the shard's stream -- blob positions i * fec_len.. in mode 0, the shard's
+// own [u16 len][payload] zero-padded in mode 1 (fec_manager.cpp:318-344, the
+// stream layout of k_frame, frame_piece.hpp).  A packet sits 8 bytes into its
+// 16-byte grid (RSMI_FEC_SLOT_PACKET), so grid piece 0 holds the header and
+// grid piece 1 + q is exactly shard piece q: each is assembled from the source
+// records, stored plain into the slot (the encoder reads it) and cooked into
+// the output in the same pass -- the framing's writes and the cook's reads of
+// the data packets are one kernel.  The <= kFuseRecs records a
+// shard overlaps are staged per packet in LDS.
+constexpr int kScrFuse = kScrCook + 8 * kFuseRecs + 4 * (kFuseRecs + 1) + 12;  // + record addr / off
+// Half rounds (48 pieces, 768 bytes per packet): a round's assembly keeps its
+// pieces' source windows in flight, twice the registers of a plain load.
+constexpr int kPplF = kPpl / 2;
+constexpr int kRoundF = 16 * kLpp * kPplF;
+
+// acc = Z_{16 qr}(acc) for qr <= N kLpp pieces (shift_pieces for shorter rounds).
+template <int N>
+__device__ __forceinline__ uint32_t shift_pieces_n(const uint32_t *T, uint32_t acc, int qr) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        const uint32_t n = zh(T, acc);
+        acc = i < qr / kLpp ? n : acc;
+    }
+    return nib_map(T + kCookLane + 128 * (qr % kLpp), acc);
+}
+
+// A packet's staged records: blob offsets off[0..n] (off[n] = the end of the
+// last), payload addresses addr[0..n).
+struct LdsRecs {
+    const uint64_t *a;
+    const uint32_t *o;
+    __device__ __forceinline__ uint32_t off(uint32_t j) const { return o[j]; }
+    __device__ __forceinline__ uint32_t len(uint32_t j) const { return o[j + 1] - o[j] - 2; }
+    __device__ __forceinline__ const uint8_t *addr(uint32_t j) const {
+        return reinterpret_cast<const uint8_t *>(a[j]);
+    }
+};
+
+__global__ __launch_bounds__(kThreads, COOK_OCC) void k_cook_frame(CookArgs a, FuseArgs f) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    const bool ck = !(a.flags & RSMI_COOK_NO_CHECKSUM);
+    const bool obs = !(a.flags & RSMI_COOK_NO_OBSCURE);
+    if (ck) load_tables(lds, a.tabs, kCookTabDecook);
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63, sub = lane / kLpp, hl = lane % kLpp;
+    uint8_t *scr = reinterpret_cast<uint8_t *>(lds + kCookTabDecook) + (wid * kPpw + sub) * kScrFuse;
+    uint32_t *iv2w = reinterpret_cast<uint32_t *>(scr);
+    uint8_t *ovl = scr + 64;
+    uint64_t *raddr = reinterpret_cast<uint64_t *>(scr + kScrCook);
+    uint32_t *roff = reinterpret_cast<uint32_t *>(scr + kScrCook + 8 * kFuseRecs);
+    const uint32_t *T = lds;
+    const int64_t nunits = (a.count + kPpw - 1) / kPpw;
+
+    for (int64_t pw = (int64_t)blockIdx.x * (kThreads / 64) + wid; pw < nunits;
+         pw += (int64_t)gridDim.x * (kThreads / 64)) {
+        const int64_t pk = kPpw * pw + sub;
+        const bool have = pk < a.count;
+        const int64_t gi = have ? (int64_t)a.pk[pk].event : pk;
+        int L = -1, ivl = 0;
+        FrameGroup G{};
+        int64_t slot = 0;
+        if (have) {
+            slot = a.pk[pk].slot;
+            L = a.pk[pk].len;
+            G = f.groups[f.job[pk]];
+        }
+        const uint64_t po = have ? (uint64_t)slot * (uint64_t)a.stride + (uint64_t)a.pk_off : 0u;
+        uint8_t *pkt = have ? a.base + po : nullptr;
+        uint8_t *opkt = !have ? nullptr : a.dst_off ? a.dst + a.dst_off[gi] : a.dst + po;
+        const int ph = (int)((uintptr_t)pkt & 15);
+        uint8_t *pga = pkt - ph;
+        uint8_t *oga = opkt - ph;
+        const uint32_t i = (uint32_t)(slot - (int64_t)G.slot0);  // shard index in its group
+        const bool m0 = G.mode == 0;
+        const uint32_t fl = G.fec_len;
+        // the records the shard overlaps: j0 = the one holding its first byte
+        // (mode 1: the shard's own), j1 = the first past its end
+        uint32_t j0 = i, nrec = 1;
+        if (have && m0) {
+            const FrameSrc *gs = f.srcs + G.src0;
+            const uint32_t s0 = max(i * fl, 4u), e0 = (i + 1) * fl;
+            uint32_t lo = 0, n = G.nsrc;  // largest j with off_j <= s0
+            while (n > 1) {
+                const uint32_t h = n >> 1;
+                lo = gs[lo + h].off <= s0 ? lo + h : lo;
+                n -= h;
+            }
+            j0 = lo;
+            uint32_t j1 = j0 + 1;
+            while (j1 < G.nsrc && j1 < j0 + kFuseRecs + 1 && gs[j1].off < e0) ++j1;
+            nrec = j1 - j0;
+        }
+        if (have && hl < (int)nrec && nrec <= (uint32_t)kFuseRecs) {
+            const FrameSrc r = f.srcs[G.src0 + j0 + hl];
+            raddr[hl] = (uint64_t)(uintptr_t)f.carry.resolve(r.addr);
+            const uint32_t o = m0 ? r.off : 0u;
+            roff[hl] = o;
+            if (hl == (int)nrec - 1) roff[nrec] = o + 2 + r.len;
+        }
+        if (have && obs) ivl = 4 + (int)(splitmix(a.seed, (uint64_t)gi, 0) % 29u);
+        const int out = L + (ck ? 4 : 0) + (obs ? ivl + 1 : 0);
+        const int Lg = L + ph, outg = out + ph;
+        // whole grid pieces of the plain packet: header, then the shard to fec_len
+        const int pext = 16 + (int)((fl + 15) & ~15u);
+        const bool ok = have && ph == 8 && (((uintptr_t)opkt & 15) == 8) && L >= 0 &&
+                        L <= RSMI_COOK_MAX_LEN && nrec <= (uint32_t)kFuseRecs && i < G.nclean &&
+                        (a.dst_off || round16(outg) - ph <= a.cap) && pext - ph <= a.cap;
+        const int ext = ok ? round16(outg) : 0;
+        const int xall = ok ? max(ext, pext) : 0;  // pieces to assemble
+        const uint32_t magic = ivl ? 0xFFFFFFFFu / (uint32_t)ivl : 0u;
+        if (ok && ivl && 8 * hl < ivl) {
+            const uint64_t z = splitmix(a.seed, (uint64_t)gi, 1 + (uint64_t)hl);
+            reinterpret_cast<uint32_t *>(ovl)[2 * hl] = (uint32_t)z;
+            reinterpret_cast<uint32_t *>(ovl)[2 * hl + 1] = (uint32_t)(z >> 32);
+        }
+        wave_sync();
+        if (ok && ivl) {
+            for (int t = hl; t < ivl + 20; t += kLpp) {
+                const uint32_t j = mod_ivl((uint32_t)t, (uint32_t)ivl, magic);
+                scr[t] = ovl[j];
+            }
+        }
+        wave_sync();
+        const LdsRecs rv{raddr, roff};
+        const uint32_t sbase = m0 ? i * fl : 0u;                   // stream position of shard byte 0
+        const uint32_t slen = m0 ? G.blob_len : roff[1];           // stream end
+        const uint32_t w1 = (uint32_t)G.mode |
+                            (m0 ? ((uint32_t)G.k << 8 | (uint32_t)G.m << 16) : 0u) |
+                            ((G.idx0 + i) & 0xffu) << 24;         // header (fec_manager.cpp:318-333)
+        const uint32_t sstep = ivl ? mod_ivl(16u * kLpp, (uint32_t)ivl, magic) : 0u;
+        const int Q = (Lg + 15) >> 4;
+        const int P0 = Lg & ~15;
+        const int nrm = wave_max((xall + kRoundF - 1) / kRoundF);
+        uint32_t acc = 0;
+        u32x4 dt = {0, 0, 0, 0};
+        int Pt = -1;
+        for (int r = 0; r < nrm; ++r) {
+            // ---- frame: the round's pieces from the staged records
+            u32x4 cur[kPplF];
+            int slow = 0;  // bit p: piece p crosses a record or stream boundary
+            const uint8_t *A[kPplF];
+#pragma unroll
+            for (int p = 0; p < kPplF; ++p) {
+                const int P = r * kRoundF + 16 * (kLpp * p + hl);
+                A[p] = reinterpret_cast<const uint8_t *>(raddr);  // readable dummy
+                if (P > 0 && P < xall) {
+                    const uint32_t b = sbase + (uint32_t)(P - 16);
+                    const uint32_t bb = m0 ? max(b, 4u) : b;
+                    uint32_t t = 0;
+                    for (uint32_t u = 1; u < nrec; ++u) t = roff[u] <= bb ? u : t;
+                    const uint32_t q0 = roff[t] + 2, q1 = roff[t + 1];
+                    if (b >= q0 && b + 16 <= q1) A[p] = rv.addr(t) + (b - q0);
+                    else slow |= 1 << p;
+                }
+            }
+#pragma unroll
+            for (int p = 0; p < kPplF; ++p) cur[p] = fpiece::window(A[p], 0, 16);
+#pragma unroll
+            for (int p = 0; p < kPplF; ++p) {
+                const int P = r * kRoundF + 16 * (kLpp * p + hl);
+                if (P == 0) {
+                    cur[p] = u32x4{0u, 0u, __builtin_bswap32(G.seq), w1};
+                } else if (P >= xall) {
+                    cur[p] = u32x4{0u, 0u, 0u, 0u};
+                } else if (slow & (1 << p)) {
+                    const uint32_t b = sbase + (uint32_t)(P - 16);
+                    const uint32_t bb = m0 ? max(b, 4u) : b;
+                    uint32_t t = 0;
+                    for (uint32_t u = 1; u < nrec; ++u) t = roff[u] <= bb ? u : t;
+                    cur[p] = fpiece::stream_piece(rv, t, nrec, (int64_t)b, (int64_t)slen, m0, G.nsrc);
+                }
+                if (P < pext && ok) st_piece(pga + P, cur[p]);  // the plain packet, for the encoder
+            }
+            // ---- cook (k_cook's round, one Horner chain)
+            const int qr = min(max(Q - kPplF * kLpp * r, 0), kPplF * kLpp);
+            const int qr_max = COOK_SKIP ? wave_max(qr) : kPplF * kLpp;
+            RoundCrc<false> rc;
+            uint32_t ivr = ivl ? mod_ivl((uint32_t)(r * kRoundF + 16 * hl + 16 * ivl - ph), (uint32_t)ivl, magic)
+                               : 0u;
+#pragma unroll
+            for (int p = 0; p < kPplF; ++p) {
+                const int P = r * kRoundF + 16 * (kLpp * p + hl);
+                if (ck && kLpp * p < qr_max) rc.add(T, crc_in_ph(cur[p], P, Lg, ph), p, kLpp * p + hl, qr);
+                if (P < ext && P + 16 <= Lg) {
+                    u32x4 m = ks_piece(a, P - ph);
+                    if (ivl) m ^= iv_window_at(iv2w, ivr);
+                    st_piece(oga + P, cur[p] ^ m);
+                } else if (P < ext && P >= P0) {
+                    dt = cur[p];
+                    Pt = P;
+                }
+                if (ivl) ivr = iv_step(ivr, sstep, (uint32_t)ivl);
+                if (COOK_SB && p % COOK_SB == COOK_SB - 1) __builtin_amdgcn_sched_barrier(0);
+            }
+            if (ck) {
+                const uint32_t c = rc.finish(T, qr);
+                const uint32_t nacc = (r ? shift_pieces_n<kPplF>(T, acc, qr) : 0u) ^ c;
+                acc = qr > 0 ? nacc : acc;
+            }
+        }
+        uint32_t crc = 0;
+        if (ck && L > 0) crc = ~unshift(T, acc, (uint32_t)(16 * Q - Lg));
+        if (ok) {
+            for (int t = hl; t < 64; t += kLpp) {
+                const int pos = P0 + t - ph;
+                uint32_t v = 0;
+                if (pos >= L && pos < out) {
+                    const int u = pos - L;
+                    if (ck && u < 4) {
+                        v = (crc >> (24 - 8 * u)) & 0xffu;
+                        if (ivl) v ^= scr[mod_ivl((uint32_t)pos, (uint32_t)ivl, magic)];
+                    } else {
+                        const int w = u - (ck ? 4 : 0);
+                        v = w < ivl ? scr[w] : (uint32_t)ivl;
+                    }
+                }
+                ovl[t] = (uint8_t)v;
+            }
+        }
+        wave_sync();
+        if (Pt >= 0) {
+            const u32x4 k = ks_piece(a, Pt - ph);
+            u32x4 m = k;
+            if (ivl) m ^= iv_window(iv2w, (uint32_t)(Pt + 16 * ivl - ph), (uint32_t)ivl, magic);
+            const u32x4 o = *reinterpret_cast<const u32x4 *>(ovl + (Pt - P0));
+            const u32x4 lo = piece_mask(Lg - Pt), hi = piece_mask(outg - Pt);
+            st_piece(oga + Pt, ((dt ^ m) & lo) | ((o ^ k) & hi & ~lo) | (dt & ~hi));
+        }
+        if (have && hl == 0) a.out_len[gi] = ok ? out : -1;
+        wave_sync();
+    }
+}
+
 }  // namespace
 
 size_t cook_lds_bytes(bool decook) {
     return (size_t)(decook ? kCookTabDecook : kCookTabWords) * 4 +
            (size_t)(kThreads / kLpp) * (decook ? kScrDecook : kScrCook);
+}
+
+hipError_t launch_cook_frame(const CookArgs &a, const FuseArgs &f, int max_blocks, hipStream_t s) {
+    if (a.count <= 0) return hipSuccess;
+    const int64_t units = (a.count + kPpw - 1) / kPpw;
+    int64_t blocks = (units + kThreads / 64 - 1) / (kThreads / 64);
+    if (blocks > max_blocks) blocks = max_blocks;
+    const size_t lds = (size_t)kCookTabDecook * 4 + (size_t)(kThreads / kLpp) * kScrFuse;
+    k_cook_frame<<<(unsigned)blocks, kThreads, lds, s>>>(a, f);
+    return hipGetLastError();
 }
 
 hipError_t launch_cook(const CookArgs &a, bool decook, int max_blocks, hipStream_t s) {

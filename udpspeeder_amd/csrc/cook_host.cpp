@@ -280,6 +280,30 @@ int cook_packets(const rsmi_cook_ctx *c, uint8_t *slots, int64_t S, const rsmi_f
     a.ks = c->ks;
     return launch(a, c, false, s);
 }
+int cook_frame_packets(const rsmi_cook_ctx *c, uint8_t *slots, int64_t S, const rsmi_fenc_packet *pk,
+                       int64_t npk, int32_t *out_len, uint8_t *dst, const int64_t *dst_off, uint64_t seed,
+                       const FuseArgs &f, hipStream_t s) {
+    if (npk <= 0) return RSMI_OK;
+    CookArgs a{};
+    a.base = slots;
+    a.dst = dst;
+    a.dst_off = dst_off;
+    a.pk = pk;
+    a.pk_off = kSlotHeader;
+    a.pk_idx = 1;
+    a.phase = 1;
+    a.stride = S;
+    a.count = npk;
+    a.cap = (int32_t)(S - kSlotHeader);
+    a.flags = c->flags;
+    a.out_len = out_len;
+    a.seed = seed;
+    a.tabs = c->tabs;
+    a.ks = c->ks;
+    const hipError_t e = launch_cook_frame(a, f, c->max_blocks, s);
+    if (e != hipSuccess) return fail(RSMI_ERR_HIP, std::string("cook_frame launch: ") + hipGetErrorString(e));
+    return RSMI_OK;
+}
 }  // namespace rsmi
 
 namespace {

@@ -118,7 +118,7 @@ struct PlanSet {
     HostArr<rsmi::ByteRun> shadow_upd;  // the buffer at the batch end -> dshadow
     HostArr<rsmi_fenc_packet> packets;  // what output() returns, in order (rsmi_fenc_packets)
     HostArr<rsmi::PacketRun> pruns;     // the same as runs of slots (cooked runs upload these)
-    int64_t n_data_pk = 0, n_par_pk = 0;  // packets of cook lists A (data) and B (parity)
+    int64_t n_data_pk = 0, n_par_pk = 0;  // packets of cook lists A (clean data shards) and B (others)
     uint32_t max_src = 0;  // most records of one job (> kFrameLdsSrc: k_frame reads them repeatedly)
     hipEvent_t done = nullptr;
     bool in_flight = false;
@@ -188,6 +188,16 @@ const FrameSrc *mapped_srcs(const HostArr<FrameSrc> &a) {
     void *d = nullptr;
     if (hipHostGetDevicePointer(&d, a.p, 0) != hipSuccess) return nullptr;
     return static_cast<const FrameSrc *>(d);
+}
+
+// RSMI_FENC_FUSE=0: cooked runs cook every packet after the encoder instead
+// of framing and cooking the clean data packets in one pass (A/B).
+bool fuse_enabled() {
+    static const bool on = [] {
+        const char *v = std::getenv("RSMI_FENC_FUSE");
+        return !(v && *v == '0');
+    }();
+    return on;
 }
 
 int wait_set(PlanSet &B) {
@@ -276,6 +286,36 @@ void shadow_update(rsmi_fenc *E) {
     E->shadow_len = std::max(E->shadow_len, lo);
 }
 
+// Data shards 0..n-1 of the group being closed that the fused framing cook
+// can frame (k_cook_frame): mode 1's are all clean ([u16 len][payload], zero
+// padding); mode 0's end before the blob does (no stale blob-buffer bytes)
+// and overlap at most kFuseRecs records each (the kernel stages them per
+// packet).
+int clean_shards(const rsmi_fenc *E, int k, int fec_len) {
+    if (E->cfg.mode == 1) return k;
+    const int kc = std::min(k, E->blob_len / fec_len);
+    // records' blob offsets: 4, then each after the last's 2 + len bytes
+    size_t j0 = 0;  // the record holding the shard's first byte (or the first record)
+    uint32_t o0 = 4;
+    for (int i = 0; i < kc; ++i) {
+        const uint32_t s = (uint32_t)i * (uint32_t)fec_len, e = s + (uint32_t)fec_len;
+        while (j0 + 1 < E->pend.size() && o0 + 2 + E->pend[j0].len <= s) {
+            o0 += 2 + E->pend[j0].len;
+            ++j0;
+        }
+        size_t j1 = j0;
+        uint32_t o = o0;
+        int n = 0;
+        while (j1 < E->pend.size() && o < e) {
+            o += 2 + E->pend[j1].len;
+            ++j1;
+            ++n;
+        }
+        if (n > rsmi::kFuseRecs) return i;
+    }
+    return kc;
+}
+
 // Close the open group (the about_to_fec branch, fec_manager.cpp:248-367).
 // Early-sent mode-1 packets of the group are pointed at their group slots.
 void close_group(rsmi_fenc *E, int k, int m, int fec_len) {
@@ -303,8 +343,10 @@ void close_group(rsmi_fenc *E, int k, int m, int fec_len) {
         if (p.emitted >= 0) {
             E->P->packets[(size_t)p.emitted].slot = slot0 + (int64_t)j;
             E->P->pruns[(size_t)p.run].slot = slot0 + (int64_t)j;
+            E->P->pruns[(size_t)p.run].job = (int32_t)E->P->jobs.size();  // G, pushed below
         }
     }
+    G.nclean = (uint16_t)clean_shards(E, k, fec_len);
     E->P->jobs.push_back(G);
     E->P->max_src = std::max(E->P->max_src, E->cfg.mode == 0 ? G.nsrc : (uint32_t)G.nframe);
     if (E->cfg.mode == 0) stale_runs(E, slot0, k, fec_len, E->blob_len);
@@ -331,8 +373,9 @@ void emit_data(rsmi_fenc *E, int32_t event) {
     p.emitted = (int64_t)E->P->packets.size();
     p.run = (int64_t)E->P->pruns.size();
     E->P->packets.push_back(rsmi_fenc_packet{-1, 8 + (int)p.len + 2, event});
+    // (a mode-1 data shard is [u16 len][payload] zero-padded: always clean)
     E->P->pruns.push_back(rsmi::PacketRun{-1, 0, (int32_t)p.emitted, (int32_t)E->P->n_data_pk,
-                                          (int32_t)E->P->n_par_pk, 8 + (int)p.len + 2, 1, 1});
+                                          (int32_t)E->P->n_par_pk, 8 + (int)p.len + 2, -1, 1, 1});
     E->P->n_data_pk += 1;
 }
 
@@ -412,16 +455,19 @@ int input_event(rsmi_fenc *E, int32_t event, bool has, int len, uint64_t addr) {
         close_group(E, k, m, fec_len);
         if (mode == 0) {
             for (int i = 0; i < k + m; ++i) E->P->packets[(size_t)(first_pk + i)].slot = slot0 + i;
+            const int nc = E->P->jobs[E->P->jobs.size() - 1].nclean;
             E->P->pruns.push_back(rsmi::PacketRun{slot0, 0, (int32_t)first_pk, (int32_t)E->P->n_data_pk,
-                                                  (int32_t)E->P->n_par_pk, 8 + fec_len, (uint16_t)(k + m),
-                                                  (uint16_t)k});
-            E->P->n_data_pk += k;
-            E->P->n_par_pk += m;
+                                                  (int32_t)E->P->n_par_pk, 8 + fec_len,
+                                                  (int32_t)E->P->jobs.size() - 1, (uint16_t)(k + m),
+                                                  (uint16_t)nc});
+            E->P->n_data_pk += nc;
+            E->P->n_par_pk += k + m - nc;
         } else {
             int64_t q = first_pk + (has ? 1 : 0);
             if (m > 0) {
                 E->P->pruns.push_back(rsmi::PacketRun{slot0 + k, 0, (int32_t)q, (int32_t)E->P->n_data_pk,
-                                                      (int32_t)E->P->n_par_pk, 8 + fec_len, (uint16_t)m, 0});
+                                                      (int32_t)E->P->n_par_pk, 8 + fec_len,
+                                                      (int32_t)E->P->jobs.size() - 1, (uint16_t)m, 0});
                 E->P->n_par_pk += m;
             }
             for (int i = k; i < k + m; ++i) E->P->packets[(size_t)q++].slot = slot0 + i;
@@ -596,10 +642,12 @@ int rsmi_fenc_plan(rsmi_fenc *E, int64_t n_events, const int32_t *len, const uin
         G.nframe = 1;
         G.mode = 1;
         G.idx0 = (uint8_t)j;
+        G.nclean = 1;
         E->P->srcs.push_back(FrameSrc{p.addr, p.len, 0});
         E->P->jobs.push_back(G);
         E->P->packets[(size_t)p.emitted].slot = slot;
         E->P->pruns[(size_t)p.run].slot = slot;
+        E->P->pruns[(size_t)p.run].job = (int32_t)E->P->jobs.size() - 1;
         E->stride_min = std::max(E->stride_min, (int32_t)((rsmi::kSlotShard + p.len + 2 + 15) & ~15u));
     }
     shadow_update(E);
@@ -758,12 +806,16 @@ int run_dev(rsmi_fenc *E, uint8_t *slots, int64_t S, void *stream, const CookSpe
             return fail(RSMI_ERR_INVALID, "rsmi_fenc_run_cooked_packed_dev: out_cap " + std::to_string(ck->out_cap) +
                                               " < packed bytes " + std::to_string(o));
     }
-    const size_t db = packed ? npk * sizeof(int64_t) : 0;
+    // into another buffer, list A's packets (data packets of clean shards) are
+    // framed and cooked in one pass (k_cook_frame), before the encoder reads
+    // their plain bytes; in place, every packet is cooked after the encoder
+    const bool fuse = npk && ck->out && na > 0 && fuse_enabled();
+    const size_t db = packed ? npk * sizeof(int64_t) : 0, jb = fuse ? (size_t)na * sizeof(int32_t) : 0;
     const size_t go = 0, so = (gb + 255) & ~size_t(255), co = (so + sb + 255) & ~size_t(255),
                  ro = (co + cb + 255) & ~size_t(255), uo = (ro + rb + 255) & ~size_t(255),
                  po = (uo + ub + 255) & ~size_t(255), xo = (po + pb + 255) & ~size_t(255),
-                 dq = (xo + xb + 255) & ~size_t(255);
-    const size_t all = dq + db + 16;
+                 dq = (xo + xb + 255) & ~size_t(255), jo = (dq + db + 255) & ~size_t(255);
+    const size_t all = jo + jb + 16;
     if (all > E->plan_cap) {
         int rcw = wait_set(prev);
         if (rcw) return rcw;
@@ -782,10 +834,21 @@ int run_dev(rsmi_fenc *E, uint8_t *slots, int64_t S, void *stream, const CookSpe
         e = rsmi::launch_expand_packets(reinterpret_cast<const rsmi::PacketRun *>(E->dplan + po), (int64_t)nrun,
                                         reinterpret_cast<rsmi_fenc_packet *>(E->dplan + xo),
                                         reinterpret_cast<rsmi_fenc_packet *>(E->dplan + xo) + na,
-                                        packed ? reinterpret_cast<int64_t *>(E->dplan + dq) : nullptr, s);
+                                        packed ? reinterpret_cast<int64_t *>(E->dplan + dq) : nullptr,
+                                        fuse ? reinterpret_cast<int32_t *>(E->dplan + jo) : nullptr, s);
+    const FrameSrc *dsrc = zsrc ? zsrc : reinterpret_cast<const FrameSrc *>(E->dplan + so);
     if (e == hipSuccess)
         e = rsmi::launch_frame(reinterpret_cast<const FrameGroup *>(E->dplan + go), (int64_t)E->P->jobs.size(),
-                               zsrc ? zsrc : reinterpret_cast<const FrameSrc *>(E->dplan + so), carry, slots, S, s);
+                               dsrc, carry, slots, S, s, fuse);
+    if (e != hipSuccess) return fail(RSMI_ERR_HIP, std::string("fenc frame: ") + hipGetErrorString(e));
+    const int64_t *doff = packed ? reinterpret_cast<const int64_t *>(E->dplan + dq) : nullptr;
+    const rsmi_fenc_packet *lists = reinterpret_cast<const rsmi_fenc_packet *>(E->dplan + xo);
+    if (fuse) {  // do_cook (my_send, packet.cpp:165-168) of list A, framing it on the way
+        const rsmi::FuseArgs fa{reinterpret_cast<const FrameGroup *>(E->dplan + go), dsrc, carry,
+                                reinterpret_cast<const int32_t *>(E->dplan + jo)};
+        rc = rsmi::cook_frame_packets(ck->ctx, slots, S, lists, na, ck->out_len, ck->out, doff, ck->seed, fa, s);
+        if (rc) return rc;
+    }
     // stale bytes past each blob, before the parity is computed over them
     if (e == hipSuccess)
         e = rsmi::launch_byte_runs(reinterpret_cast<const rsmi::ByteRun *>(E->dplan + ro),
@@ -804,15 +867,14 @@ int run_dev(rsmi_fenc *E, uint8_t *slots, int64_t S, void *stream, const CookSpe
         e = rsmi::launch_carry(reinterpret_cast<const CarryCopy *>(E->dplan + co),
                                (int64_t)E->P->carry.size(), carry, s);
     if (e != hipSuccess) return fail(RSMI_ERR_HIP, std::string("fenc carry: ") + hipGetErrorString(e));
-    // do_cook (my_send, packet.cpp:165-168) of every packet, after the blob
-    // buffer update above has read the plain shards: one launch over both cook
+    // do_cook of the other packets (every packet in place), after the blob
+    // buffer update above has read the plain shards: one launch over the
     // lists, which lie back to back.  (Cooking the data packets on a forked
     // stream beside the encoder measured no faster: the two kernels slow each
     // other down)
-    if (npk) {
-        rc = rsmi::cook_packets(ck->ctx, slots, S, reinterpret_cast<const rsmi_fenc_packet *>(E->dplan + xo),
-                                (int64_t)npk, ck->out_len, ck->out,
-                                packed ? reinterpret_cast<const int64_t *>(E->dplan + dq) : nullptr, ck->seed, s);
+    if (npk && (int64_t)npk > (fuse ? na : 0)) {
+        rc = rsmi::cook_packets(ck->ctx, slots, S, lists + (fuse ? na : 0), (int64_t)npk - (fuse ? na : 0),
+                                ck->out_len, ck->out, doff, ck->seed, s);
         if (rc) return rc;
     }
     e = hipEventRecord(E->P->done, s);
@@ -983,6 +1045,7 @@ int rsmi_fenc_run_many(rsmi_fcol *C, rsmi_fenc *const *enc, int32_t n, uint8_t *
         rsmi_fenc *E = enc[i];
         const std::vector<int64_t> &m = smap[(size_t)i];
         const uint32_t src0 = (uint32_t)B.srcs.size();
+        const size_t job_base = B.jobs.size();
         for (size_t j = 0; j < E->P->srcs.size(); ++j) {
             FrameSrc f = E->P->srcs[j];
             f.addr = resolve(E, f.addr);
@@ -1023,6 +1086,7 @@ int rsmi_fenc_run_many(rsmi_fcol *C, rsmi_fenc *const *enc, int32_t n, uint8_t *
                 r.first += (int32_t)pk_base;
                 r.afirst += (int32_t)a_base;  // one cook list: every data packet, then every parity packet
                 r.bfirst += (int32_t)(total_a + b_base);
+                r.job += (int32_t)job_base;
                 B.pruns.push_back(r);
             }
         pk_base += (int64_t)E->P->packets.size();
@@ -1053,7 +1117,7 @@ int rsmi_fenc_run_many(rsmi_fcol *C, rsmi_fenc *const *enc, int32_t n, uint8_t *
     if (e == hipSuccess)
         e = rsmi::launch_expand_packets(reinterpret_cast<const rsmi::PacketRun *>(dp + po), (int64_t)B.pruns.size(),
                                         reinterpret_cast<rsmi_fenc_packet *>(dp + xo),
-                                        reinterpret_cast<rsmi_fenc_packet *>(dp + xo), nullptr, s);
+                                        reinterpret_cast<rsmi_fenc_packet *>(dp + xo), nullptr, nullptr, s);
     const rsmi::CarryBase none{{nullptr, nullptr}};  // every address is absolute now
     if (e == hipSuccess)
         e = rsmi::launch_frame(reinterpret_cast<const FrameGroup *>(dp + go), (int64_t)B.jobs.size(),

@@ -20,6 +20,7 @@
 #include "rsmi_internal.hpp"
 
 namespace rsmi {
+#include "frame_piece.hpp"
 namespace {
 
 constexpr int kThreads = 256;
@@ -29,73 +30,8 @@ constexpr int kThreads = 256;
 constexpr int kFThreads = FRAME_THREADS;
 constexpr int kLdsSrc = (int)kFrameLdsSrc;  // source records staged in LDS per group
 
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-typedef u32x4 u32x4_a4 __attribute__((aligned(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-
-__device__ __forceinline__ uint32_t bswap32(uint32_t v) { return __builtin_bswap32(v); }
-
-// Bytes [lo, hi) of a 16-byte piece taken from src[a .. a + hi - lo): piece
-// byte p = src[a - lo + p].  Only the aligned dwords that hold wanted bytes are
-// read, so nothing outside the source range's own dwords is touched.
-__device__ __forceinline__ u32x4 window(const uint8_t *a, int lo, int hi) {
-    const uint8_t *w = a - lo;                      // address of piece byte 0
-    const uintptr_t wa = (uintptr_t)w;
-    const uint32_t *d = reinterpret_cast<const uint32_t *>(wa & ~uintptr_t(3));
-    const uint32_t sh = (uint32_t)(wa & 3);
-    // dword e covers piece bytes [4e - sh, 4e - sh + 4); wanted if it meets [lo, hi)
-    uint32_t e[5];
-    if (lo == 0 && hi == 16) {
-        const u32x4 v = *reinterpret_cast<const u32x4_a4 *>(d);
-        e[0] = v.x; e[1] = v.y; e[2] = v.z; e[3] = v.w;
-        e[4] = sh ? d[4] : 0u;
-    } else {
-#pragma unroll
-        for (int i = 0; i < 5; ++i) {
-            const int b0 = 4 * i - (int)sh;
-            e[i] = (b0 < hi && b0 + 4 > lo) ? d[i] : 0u;
-        }
-    }
-    u32x4 r;
-    r.x = __builtin_amdgcn_alignbyte(e[1], e[0], sh);
-    r.y = __builtin_amdgcn_alignbyte(e[2], e[1], sh);
-    r.z = __builtin_amdgcn_alignbyte(e[3], e[2], sh);
-    r.w = __builtin_amdgcn_alignbyte(e[4], e[3], sh);
-    return r;
-}
-
-// Keep bytes [lo, hi) of a piece.
-__device__ __forceinline__ u32x4 keep(u32x4 v, int lo, int hi) {
-    u32x4 m;
-#pragma unroll
-    for (int d = 0; d < 4; ++d) {
-        const int a = max(lo - 4 * d, 0), b = min(hi - 4 * d, 4);
-        const uint32_t hm = b >= 4 ? ~0u : (b <= 0 ? 0u : ((1u << (8 * b)) - 1u));
-        const uint32_t lm = a >= 4 ? ~0u : (a <= 0 ? 0u : ((1u << (8 * a)) - 1u));
-        m[d] = hm & ~lm;
-    }
-    return v & m;
-}
-
-// Big-endian constant c (nb <= 4 bytes) at stream position s0, placed into the
-// piece that starts at stream position b.
-__device__ __forceinline__ u32x4 konst(uint32_t c, int nb, int64_t s0, int64_t b) {
-    // the nb bytes in memory order as a little-endian integer, placed at piece
-    // byte p = s0 - b (-3 <= p <= 15) by per-dword shifts (no indexed writes)
-    const uint64_t v = nb == 4 ? (uint64_t)__builtin_bswap32(c)
-                               : (uint64_t)(((c & 0xffu) << 8) | ((c >> 8) & 0xffu));
-    const int p = (int)(s0 - b);
-    u32x4 r;
-#pragma unroll
-    for (int d = 0; d < 4; ++d) {
-        const int sh = 8 * (p - 4 * d);  // bit position of the constant in dword d
-        uint32_t w = 0;
-        if (sh >= 0 && sh < 32) w = (uint32_t)(v << sh);
-        else if (sh < 0 && sh > -8 * nb) w = (uint32_t)(v >> -sh);
-        r[d] = w;
-    }
-    return r;
-}
+using namespace fpiece;
 
 // Source records of the job being framed, staged in LDS (structure of arrays).
 struct LdsSrc {
@@ -118,38 +54,6 @@ struct View {
         return kGlobal ? carry.resolve(g[j].addr) : reinterpret_cast<const uint8_t *>(l->addr[j]);
     }
 };
-
-// The 16 stream bytes at [b, b+16) of a stream made of: an optional 4-byte
-// big-endian count at [0, 4), then records j0.. [u16 len BE][payload] at their
-// offsets, then zeros from stream_len on.  j is a record with off_j <= max(b, 4)
-// whose successor starts beyond it (the search result).
-template <class V>
-__device__ u32x4 stream_piece(const V &src, uint32_t j, uint32_t jend, int64_t b, int64_t stream_len,
-                              bool count_hdr, uint32_t count) {
-    u32x4 acc = {0, 0, 0, 0};
-    const int64_t end = min(b + 16, stream_len);
-    int64_t pos = b;
-    if (pos >= end) return acc;
-    if (count_hdr && pos < 4) {
-        acc |= konst(count, 4, 0, b);
-        pos = 4;
-    }
-    while (pos < end && j < jend) {
-        const int64_t p0 = src.off(j), q0 = p0 + 2, q1 = q0 + src.len(j);
-        if (pos < q0) {
-            acc |= konst(src.len(j) & 0xffffu, 2, p0, b);
-            pos = min(q0, end);
-        }
-        if (pos < end && pos < q1) {
-            const int64_t e = min(q1, end);
-            const int lo = (int)(pos - b), hi = (int)(e - b);
-            acc |= keep(window(src.addr(j) + (pos - q0), lo, hi), lo, hi);
-            pos = e;
-        }
-        if (pos >= q1) ++j;
-    }
-    return acc;
-}
 
 #ifndef FRAME_BATCH
 #define FRAME_BATCH 4
@@ -213,12 +117,13 @@ __device__ __forceinline__ void put_piece(uint8_t *s0, int64_t slot_stride, cons
 template <bool kGlobal>
 __device__ __forceinline__ void frame_job(const FrameGroup &G, const View<kGlobal> &src,
                                           uint8_t *s0, int64_t slot_stride, const uint8_t *dummy,
-                                          uint32_t *slow, uint32_t *nslow) {
+                                          uint32_t *slow, uint32_t *nslow, uint32_t first_shard) {
     const uint32_t nsrc = G.mode == 0 ? G.nsrc : G.nframe;
     const uint32_t pps = (G.fec_len + 15) >> 4;
     const uint32_t total = pps * G.nframe;
+    const uint32_t tbase = pps * first_shard;  // shards before it are framed elsewhere
     const uint32_t magic = pps == 1 ? 0u : (uint32_t)(0xFFFFFFFFu / pps) + 1u;
-    for (uint32_t t0 = threadIdx.x; t0 < total; t0 += kBatch * kFThreads) {
+    for (uint32_t t0 = tbase + threadIdx.x; t0 < total; t0 += kBatch * kFThreads) {
         Piece P[kBatch];
 #pragma unroll
         for (int u = 0; u < kBatch; ++u) P[u] = piece_at(G, min(t0 + u * kFThreads, total - 1), pps, magic);
@@ -265,7 +170,7 @@ __device__ __forceinline__ void frame_job(const FrameGroup &G, const View<kGloba
             put_piece(s0, slot_stride, Q, slow_piece(G, src, nsrc, Q));
         }
     } else {  // queue overflow (thousands of tiny records): every boundary piece in place
-        for (uint32_t t = threadIdx.x; t < total; t += kFThreads) {
+        for (uint32_t t = tbase + threadIdx.x; t < total; t += kFThreads) {
             Piece Q = piece_at(G, t, pps, magic);
             if (G.mode == 0) Q.j = find_record(src, nsrc, Q.b);
             const int64_t q0 = G.mode == 0 ? (int64_t)src.off(Q.j) + 2 : 2;
@@ -277,7 +182,7 @@ __device__ __forceinline__ void frame_job(const FrameGroup &G, const View<kGloba
 
 __global__ __launch_bounds__(kFThreads) void k_frame(const FrameGroup *groups, int64_t ngroups,
                                                      const FrameSrc *srcs, CarryBase carry,
-                                                     uint8_t *slots, int64_t slot_stride) {
+                                                     uint8_t *slots, int64_t slot_stride, int skip_clean) {
     __shared__ LdsSrc lsrc;
     __shared__ uint32_t slow[kSlowMax];
     __shared__ uint32_t nslow;
@@ -299,7 +204,8 @@ __global__ __launch_bounds__(kFThreads) void k_frame(const FrameGroup *groups, i
         uint8_t *s0 = slots + (int64_t)G.slot0 * slot_stride;
         // headers: seq | mode | k | m | index (fec_manager.cpp:318-333); mode-1
         // data packets carry k = m = 0 (:321-323)
-        for (uint32_t j = threadIdx.x; j < G.nslots; j += kFThreads) {
+        const uint32_t c0 = skip_clean ? (uint32_t)G.nclean : 0u;
+        for (uint32_t j = c0 + threadIdx.x; j < G.nslots; j += kFThreads) {
             const bool zero_km = G.mode == 1 && j < G.nframe;
             const uint32_t w1 = (uint32_t)G.mode |
                                 (zero_km ? 0u : ((uint32_t)G.k << 8 | (uint32_t)G.m << 16)) |
@@ -308,9 +214,9 @@ __global__ __launch_bounds__(kFThreads) void k_frame(const FrameGroup *groups, i
                 u32x2{bswap32(G.seq), w1};
         }
         if (in_lds)
-            frame_job(G, View<false>{gs, &lsrc, carry}, s0, slot_stride, dummy, slow, &nslow);
+            frame_job(G, View<false>{gs, &lsrc, carry}, s0, slot_stride, dummy, slow, &nslow, c0);
         else
-            frame_job(G, View<true>{gs, &lsrc, carry}, s0, slot_stride, dummy, slow, &nslow);
+            frame_job(G, View<true>{gs, &lsrc, carry}, s0, slot_stride, dummy, slow, &nslow, c0);
         __syncthreads();  // lsrc and the queue are reset for the next group
     }
 }
@@ -376,15 +282,19 @@ __global__ __launch_bounds__(kThreads) void k_byte_runs(const ByteRun *runs, int
 // each packet's offset in the packed cooked output.
 __global__ __launch_bounds__(kThreads) void k_expand_packets(const PacketRun *runs, int64_t nruns,
                                                               rsmi_fenc_packet *pk_a, rsmi_fenc_packet *pk_b,
-                                                              int64_t *dst_off) {
+                                                              int64_t *dst_off, int32_t *job_a) {
     const int lane = threadIdx.x & 63;
     const int64_t w0 = (int64_t)blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
     for (int64_t w = w0; w < nruns; w += (int64_t)gridDim.x * (kThreads / 64)) {
         const PacketRun R = runs[w];
         for (int c = lane; c < (int)R.count; c += 64) {
             const rsmi_fenc_packet p{R.slot + c, R.len, R.first + c};
-            if (c < (int)R.ndata) pk_a[R.afirst + c] = p;
-            else pk_b[R.bfirst + c - (int)R.ndata] = p;
+            if (c < (int)R.ndata) {
+                pk_a[R.afirst + c] = p;
+                if (job_a) job_a[R.afirst + c] = R.job;
+            } else {
+                pk_b[R.bfirst + c - (int)R.ndata] = p;
+            }
             if (dst_off) dst_off[R.first + c] = R.out0 + (int64_t)c * RSMI_FEC_COOK_SPAN(R.len);
         }
     }
@@ -393,11 +303,11 @@ __global__ __launch_bounds__(kThreads) void k_expand_packets(const PacketRun *ru
 }  // namespace
 
 hipError_t launch_expand_packets(const PacketRun *runs, int64_t nruns, rsmi_fenc_packet *pk_a,
-                                 rsmi_fenc_packet *pk_b, int64_t *dst_off, hipStream_t s) {
+                                 rsmi_fenc_packet *pk_b, int64_t *dst_off, int32_t *job_a, hipStream_t s) {
     if (nruns <= 0) return hipSuccess;
     int64_t blocks = (nruns + kThreads / 64 - 1) / (kThreads / 64);
     if (blocks > 8192) blocks = 8192;
-    k_expand_packets<<<(unsigned)blocks, kThreads, 0, s>>>(runs, nruns, pk_a, pk_b, dst_off);
+    k_expand_packets<<<(unsigned)blocks, kThreads, 0, s>>>(runs, nruns, pk_a, pk_b, dst_off, job_a);
     return hipGetLastError();
 }
 
@@ -419,10 +329,12 @@ hipError_t launch_gather(const GatherCopy *jobs, int64_t njobs, CarryBase carry,
 }
 
 hipError_t launch_frame(const FrameGroup *groups, int64_t ngroups, const FrameSrc *srcs,
-                        CarryBase carry, uint8_t *slots, int64_t slot_stride, hipStream_t s) {
+                        CarryBase carry, uint8_t *slots, int64_t slot_stride, hipStream_t s,
+                        bool skip_clean) {
     if (ngroups <= 0) return hipSuccess;
     const int64_t blocks = ngroups < 65536 ? ngroups : 65536;
-    k_frame<<<(unsigned)blocks, kFThreads, 0, s>>>(groups, ngroups, srcs, carry, slots, slot_stride);
+    k_frame<<<(unsigned)blocks, kFThreads, 0, s>>>(groups, ngroups, srcs, carry, slots, slot_stride,
+                                                   skip_clean ? 1 : 0);
     return hipGetLastError();
 }
 

@@ -270,6 +270,8 @@ struct FrameGroup {
     uint32_t blob_len;  // mode 0: blob bytes (blob_encode_t::current_len)
     uint16_t nslots, nframe;
     uint8_t mode, k, m, idx0;  // header bytes; idx0 = index of slot 0
+    uint16_t nclean;    // data shards 0..nclean-1 the fused framing cook can frame (k_cook_frame):
+                        // no stale blob bytes, at most kFuseRecs records each
 };
 // A payload address in a plan: a device address, or (kCarryTag set) an offset
 // into carry buffer 0 or 1 (kCarryBuf1), resolved by the kernels.
@@ -321,26 +323,44 @@ struct ByteRun {
 };
 hipError_t launch_byte_runs(const ByteRun *runs, int64_t nruns, uint8_t *slots, int64_t slot_stride,
                             uint8_t *shadow, hipStream_t s);
+// skip_clean: leave data shards 0..nclean-1 (and their headers) to k_cook_frame.
 hipError_t launch_frame(const FrameGroup *groups, int64_t ngroups, const FrameSrc *srcs,
-                        CarryBase carry, uint8_t *slots, int64_t slot_stride, hipStream_t s);
+                        CarryBase carry, uint8_t *slots, int64_t slot_stride, hipStream_t s,
+                        bool skip_clean = false);
 hipError_t launch_carry(const CarryCopy *jobs, int64_t njobs, CarryBase carry, hipStream_t s);
 // A run of a batch's packet list (what output() returned): packets first ..
 // first + count - 1 sit in slots slot .. slot + count - 1, len bytes each (a
 // mode-0 group is one run; fec_enc.cpp).  Cooked runs upload the runs and
 // expand them on the device (k_expand_packets) into two cook lists: A, the
-// data packets (final once framed: cooked beside the encoder), and B, the
-// parity packets.  A list entry's `event` is the packet's index in the batch
-// (its IV draw, out_len and packed place).  Packed cooked output
-// (rsmi_fenc_run_cooked_packed_dev): the run's packets go to out0, out0 +
-// span, ... with span = RSMI_FEC_COOK_SPAN(len).
+// data packets of clean shards (FrameGroup.nclean: framed and cooked in one
+// pass by k_cook_frame in a fused run), and B, every other packet.  A list
+// entry's `event` is the packet's index in the batch (its IV draw, out_len and
+// packed place).  Packed cooked output (rsmi_fenc_run_cooked_packed_dev): the
+// run's packets go to out0, out0 + span, ... with span = RSMI_FEC_COOK_SPAN(len).
 struct PacketRun {
     int64_t slot, out0;
     int32_t first;           // index of the run's first packet in the batch
-    int32_t afirst, bfirst;  // where its data packets start in list A, its parity packets in B
+    int32_t afirst, bfirst;  // where its list-A packets start in list A, its others in B
     int32_t len;
-    uint16_t count, ndata;   // packets [0, ndata) are data packets, the rest parity
+    int32_t job;             // the FrameGroup (job) its slots belong to
+    uint16_t count, ndata;   // packets [0, ndata) go to list A, the rest to B
 };
+// job_a (optional): list A's entries' jobs.
 hipError_t launch_expand_packets(const PacketRun *runs, int64_t nruns, rsmi_fenc_packet *pk_a,
-                                 rsmi_fenc_packet *pk_b, int64_t *dst_off, hipStream_t s);
+                                 rsmi_fenc_packet *pk_b, int64_t *dst_off, int32_t *job_a, hipStream_t s);
+// The fused framing cook (k_cook_frame): list A's packets are data packets of
+// clean shards (FrameGroup.nclean), framed from their source records into
+// their slots (for the encoder) and cooked into the output in the same pass.
+constexpr int kFuseRecs = 8;  // source records one fused shard may overlap
+struct FuseArgs {
+    const FrameGroup *groups;
+    const FrameSrc *srcs;
+    CarryBase carry;
+    const int32_t *job;  // per list entry: its group's FrameGroup index
+};
+int cook_frame_packets(const rsmi_cook_ctx *ctx, uint8_t *slots, int64_t S, const rsmi_fenc_packet *pk,
+                       int64_t npk, int32_t *out_len, uint8_t *dst, const int64_t *dst_off, uint64_t seed,
+                       const FuseArgs &f, hipStream_t s);
+hipError_t launch_cook_frame(const CookArgs &a, const FuseArgs &f, int max_blocks, hipStream_t s);
 
 }  // namespace rsmi

@@ -173,7 +173,8 @@ class FecEncoder:
 
     RUN_DTYPE = np.dtype([("slot", np.int64), ("out0", np.int64), ("first", np.int32),
                           ("afirst", np.int32), ("bfirst", np.int32), ("len", np.int32),
-                          ("count", np.uint16), ("ndata", np.uint16)], align=True)  # 40 B, as in C
+                          ("job", np.int32), ("count", np.uint16), ("ndata", np.uint16)],
+                         align=True)  # 40 B, as in C
 
     def packet_runs(self) -> np.ndarray:
         """The last plan's packet list as runs (rsmi_fenc_packet_runs): what a
