@@ -753,7 +753,8 @@ __global__ __launch_bounds__(kThreads, COOK_OCC) void k_cook_frame(CookArgs a, F
         // whole grid pieces of the plain packet: header, then the shard to fec_len
         const int pext = 16 + (int)((fl + 15) & ~15u);
         const bool ok = have && ph == 8 && (((uintptr_t)opkt & 15) == 8) && L >= 0 &&
-                        L <= RSMI_COOK_MAX_LEN && nrec <= (uint32_t)kFuseRecs && i < G.nclean &&
+                        L <= RSMI_COOK_MAX_LEN && nrec <= (uint32_t)kFuseRecs && i >= G.cfirst &&
+                        i < G.nclean &&
                         (a.dst_off || round16(outg) - ph <= a.cap) && pext - ph <= a.cap;
         const int ext = ok ? round16(outg) : 0;
         const int xall = ok ? max(ext, pext) : 0;  // pieces to assemble

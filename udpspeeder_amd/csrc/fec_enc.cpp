@@ -346,7 +346,13 @@ void close_group(rsmi_fenc *E, int k, int m, int fec_len) {
             E->P->pruns[(size_t)p.run].job = (int32_t)E->P->jobs.size();  // G, pushed below
         }
     }
-    G.nclean = (uint16_t)clean_shards(E, k, fec_len);
+    // mode 1: the shards whose packets went out in an earlier batch (carried,
+    // at the front) are framed by k_frame; the rest were emitted in this one
+    uint32_t cf = 0;
+    if (E->cfg.mode == 1)
+        while (cf < E->pend.size() && E->pend[cf].emitted < 0) ++cf;
+    G.cfirst = (uint16_t)cf;
+    G.nclean = (uint16_t)std::max((int)cf, clean_shards(E, k, fec_len));
     E->P->jobs.push_back(G);
     E->P->max_src = std::max(E->P->max_src, E->cfg.mode == 0 ? G.nsrc : (uint32_t)G.nframe);
     if (E->cfg.mode == 0) stale_runs(E, slot0, k, fec_len, E->blob_len);

@@ -117,16 +117,19 @@ __device__ __forceinline__ void put_piece(uint8_t *s0, int64_t slot_stride, cons
 template <bool kGlobal>
 __device__ __forceinline__ void frame_job(const FrameGroup &G, const View<kGlobal> &src,
                                           uint8_t *s0, int64_t slot_stride, const uint8_t *dummy,
-                                          uint32_t *slow, uint32_t *nslow, uint32_t first_shard) {
+                                          uint32_t *slow, uint32_t *nslow, uint32_t c0, uint32_t c1) {
     const uint32_t nsrc = G.mode == 0 ? G.nsrc : G.nframe;
     const uint32_t pps = (G.fec_len + 15) >> 4;
-    const uint32_t total = pps * G.nframe;
-    const uint32_t tbase = pps * first_shard;  // shards before it are framed elsewhere
+    // shards c0..c1-1 are framed elsewhere: piece index v of the others is
+    // piece t = v, or v + (c1 - c0) pps past shard c0
+    const uint32_t n1 = pps * c0, gap = pps * (c1 - c0);
+    const uint32_t total = pps * G.nframe - gap;
+    auto tof = [&](uint32_t v) { return v < n1 ? v : v + gap; };
     const uint32_t magic = pps == 1 ? 0u : (uint32_t)(0xFFFFFFFFu / pps) + 1u;
-    for (uint32_t t0 = tbase + threadIdx.x; t0 < total; t0 += kBatch * kFThreads) {
+    for (uint32_t t0 = threadIdx.x; t0 < total; t0 += kBatch * kFThreads) {
         Piece P[kBatch];
 #pragma unroll
-        for (int u = 0; u < kBatch; ++u) P[u] = piece_at(G, min(t0 + u * kFThreads, total - 1), pps, magic);
+        for (int u = 0; u < kBatch; ++u) P[u] = piece_at(G, tof(min(t0 + u * kFThreads, total - 1)), pps, magic);
         if (G.mode == 0) {  // kBatch interleaved searches (same trip count)
             uint32_t n = nsrc;
             while (n > 1) {
@@ -157,7 +160,7 @@ __device__ __forceinline__ void frame_job(const FrameGroup &G, const View<kGloba
                 put_piece(s0, slot_stride, P[u], v[u]);
             } else {
                 const uint32_t k = atomicAdd(nslow, 1u);
-                if (k < (uint32_t)kSlowMax) slow[k] = t;
+                if (k < (uint32_t)kSlowMax) slow[k] = tof(t);
             }
         }
     }
@@ -170,8 +173,8 @@ __device__ __forceinline__ void frame_job(const FrameGroup &G, const View<kGloba
             put_piece(s0, slot_stride, Q, slow_piece(G, src, nsrc, Q));
         }
     } else {  // queue overflow (thousands of tiny records): every boundary piece in place
-        for (uint32_t t = tbase + threadIdx.x; t < total; t += kFThreads) {
-            Piece Q = piece_at(G, t, pps, magic);
+        for (uint32_t v = threadIdx.x; v < total; v += kFThreads) {
+            Piece Q = piece_at(G, tof(v), pps, magic);
             if (G.mode == 0) Q.j = find_record(src, nsrc, Q.b);
             const int64_t q0 = G.mode == 0 ? (int64_t)src.off(Q.j) + 2 : 2;
             if (Q.b >= q0 && Q.b + 16 <= q0 + src.len(Q.j)) continue;
@@ -204,8 +207,9 @@ __global__ __launch_bounds__(kFThreads) void k_frame(const FrameGroup *groups, i
         uint8_t *s0 = slots + (int64_t)G.slot0 * slot_stride;
         // headers: seq | mode | k | m | index (fec_manager.cpp:318-333); mode-1
         // data packets carry k = m = 0 (:321-323)
-        const uint32_t c0 = skip_clean ? (uint32_t)G.nclean : 0u;
-        for (uint32_t j = c0 + threadIdx.x; j < G.nslots; j += kFThreads) {
+        const uint32_t c0 = skip_clean ? (uint32_t)G.cfirst : 0u, c1 = skip_clean ? (uint32_t)G.nclean : 0u;
+        for (uint32_t j = threadIdx.x; j < G.nslots; j += kFThreads) {
+            if (j >= c0 && j < c1) continue;
             const bool zero_km = G.mode == 1 && j < G.nframe;
             const uint32_t w1 = (uint32_t)G.mode |
                                 (zero_km ? 0u : ((uint32_t)G.k << 8 | (uint32_t)G.m << 16)) |
@@ -214,9 +218,9 @@ __global__ __launch_bounds__(kFThreads) void k_frame(const FrameGroup *groups, i
                 u32x2{bswap32(G.seq), w1};
         }
         if (in_lds)
-            frame_job(G, View<false>{gs, &lsrc, carry}, s0, slot_stride, dummy, slow, &nslow, c0);
+            frame_job(G, View<false>{gs, &lsrc, carry}, s0, slot_stride, dummy, slow, &nslow, c0, max(c0, c1));
         else
-            frame_job(G, View<true>{gs, &lsrc, carry}, s0, slot_stride, dummy, slow, &nslow, c0);
+            frame_job(G, View<true>{gs, &lsrc, carry}, s0, slot_stride, dummy, slow, &nslow, c0, max(c0, c1));
         __syncthreads();  // lsrc and the queue are reset for the next group
     }
 }

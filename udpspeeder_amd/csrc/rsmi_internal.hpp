@@ -270,8 +270,9 @@ struct FrameGroup {
     uint32_t blob_len;  // mode 0: blob bytes (blob_encode_t::current_len)
     uint16_t nslots, nframe;
     uint8_t mode, k, m, idx0;  // header bytes; idx0 = index of slot 0
-    uint16_t nclean;    // data shards 0..nclean-1 the fused framing cook can frame (k_cook_frame):
-                        // no stale blob bytes, at most kFuseRecs records each
+    uint16_t cfirst, nclean;  // data shards cfirst..nclean-1 the fused framing cook frames
+                              // (k_cook_frame): packets emitted in this batch, no stale blob
+                              // bytes, at most kFuseRecs records each
 };
 // A payload address in a plan: a device address, or (kCarryTag set) an offset
 // into carry buffer 0 or 1 (kCarryBuf1), resolved by the kernels.
@@ -323,7 +324,7 @@ struct ByteRun {
 };
 hipError_t launch_byte_runs(const ByteRun *runs, int64_t nruns, uint8_t *slots, int64_t slot_stride,
                             uint8_t *shadow, hipStream_t s);
-// skip_clean: leave data shards 0..nclean-1 (and their headers) to k_cook_frame.
+// skip_clean: leave data shards cfirst..nclean-1 (and their headers) to k_cook_frame.
 hipError_t launch_frame(const FrameGroup *groups, int64_t ngroups, const FrameSrc *srcs,
                         CarryBase carry, uint8_t *slots, int64_t slot_stride, hipStream_t s,
                         bool skip_clean = false);
