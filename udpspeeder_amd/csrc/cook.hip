@@ -725,21 +725,9 @@ __global__ __launch_bounds__(kThreads, COOK_OCC) void k_cook_frame(CookArgs a, F
         const uint32_t fl = G.fec_len;
         // the records the shard overlaps: j0 = the one holding its first byte
         // (mode 1: the shard's own), j1 = the first past its end
-        uint32_t j0 = i, nrec = 1;
-        if (have && m0) {
-            const FrameSrc *gs = f.srcs + G.src0;
-            const uint32_t s0 = max(i * fl, 4u), e0 = (i + 1) * fl;
-            uint32_t lo = 0, n = G.nsrc;  // largest j with off_j <= s0
-            while (n > 1) {
-                const uint32_t h = n >> 1;
-                lo = gs[lo + h].off <= s0 ? lo + h : lo;
-                n -= h;
-            }
-            j0 = lo;
-            uint32_t j1 = j0 + 1;
-            while (j1 < G.nsrc && j1 < j0 + kFuseRecs + 1 && gs[j1].off < e0) ++j1;
-            nrec = j1 - j0;
-        }
+        // (found by k_expand_packets)
+        const uint32_t rj = have ? f.rec[pk] : 1u;
+        const uint32_t j0 = rj >> 8, nrec = rj & 255u;
         if (have && hl < (int)nrec && nrec <= (uint32_t)kFuseRecs) {
             const FrameSrc r = f.srcs[G.src0 + j0 + hl];
             raddr[hl] = (uint64_t)(uintptr_t)f.carry.resolve(r.addr);

@@ -816,7 +816,7 @@ int run_dev(rsmi_fenc *E, uint8_t *slots, int64_t S, void *stream, const CookSpe
     // framed and cooked in one pass (k_cook_frame), before the encoder reads
     // their plain bytes; in place, every packet is cooked after the encoder
     const bool fuse = npk && ck->out && na > 0 && fuse_enabled();
-    const size_t db = packed ? npk * sizeof(int64_t) : 0, jb = fuse ? (size_t)na * sizeof(int32_t) : 0;
+    const size_t db = packed ? npk * sizeof(int64_t) : 0, jb = fuse ? (size_t)na * 2 * sizeof(int32_t) : 0;
     const size_t go = 0, so = (gb + 255) & ~size_t(255), co = (so + sb + 255) & ~size_t(255),
                  ro = (co + cb + 255) & ~size_t(255), uo = (ro + rb + 255) & ~size_t(255),
                  po = (uo + ub + 255) & ~size_t(255), xo = (po + pb + 255) & ~size_t(255),
@@ -836,13 +836,15 @@ int run_dev(rsmi_fenc *E, uint8_t *slots, int64_t S, void *stream, const CookSpe
     if (e == hipSuccess && ub)
         e = hipMemcpyAsync(E->dplan + uo, E->P->shadow_upd.p, ub, hipMemcpyHostToDevice, s);
     if (e == hipSuccess && pb) e = hipMemcpyAsync(E->dplan + po, E->P->pruns.p, pb, hipMemcpyHostToDevice, s);
+    const FrameSrc *dsrc = zsrc ? zsrc : reinterpret_cast<const FrameSrc *>(E->dplan + so);
     if (e == hipSuccess)
         e = rsmi::launch_expand_packets(reinterpret_cast<const rsmi::PacketRun *>(E->dplan + po), (int64_t)nrun,
                                         reinterpret_cast<rsmi_fenc_packet *>(E->dplan + xo),
                                         reinterpret_cast<rsmi_fenc_packet *>(E->dplan + xo) + na,
                                         packed ? reinterpret_cast<int64_t *>(E->dplan + dq) : nullptr,
-                                        fuse ? reinterpret_cast<int32_t *>(E->dplan + jo) : nullptr, s);
-    const FrameSrc *dsrc = zsrc ? zsrc : reinterpret_cast<const FrameSrc *>(E->dplan + so);
+                                        fuse ? reinterpret_cast<int32_t *>(E->dplan + jo) : nullptr, s,
+                                        reinterpret_cast<const FrameGroup *>(E->dplan + go), dsrc,
+                                        fuse ? reinterpret_cast<uint32_t *>(E->dplan + jo) + na : nullptr);
     if (e == hipSuccess)
         e = rsmi::launch_frame(reinterpret_cast<const FrameGroup *>(E->dplan + go), (int64_t)E->P->jobs.size(),
                                dsrc, carry, slots, S, s, fuse);
@@ -851,7 +853,8 @@ int run_dev(rsmi_fenc *E, uint8_t *slots, int64_t S, void *stream, const CookSpe
     const rsmi_fenc_packet *lists = reinterpret_cast<const rsmi_fenc_packet *>(E->dplan + xo);
     if (fuse) {  // do_cook (my_send, packet.cpp:165-168) of list A, framing it on the way
         const rsmi::FuseArgs fa{reinterpret_cast<const FrameGroup *>(E->dplan + go), dsrc, carry,
-                                reinterpret_cast<const int32_t *>(E->dplan + jo)};
+                                reinterpret_cast<const int32_t *>(E->dplan + jo),
+                                reinterpret_cast<const uint32_t *>(E->dplan + jo) + na};
         rc = rsmi::cook_frame_packets(ck->ctx, slots, S, lists, na, ck->out_len, ck->out, doff, ck->seed, fa, s);
         if (rc) return rc;
     }

@@ -286,7 +286,9 @@ __global__ __launch_bounds__(kThreads) void k_byte_runs(const ByteRun *runs, int
 // each packet's offset in the packed cooked output.
 __global__ __launch_bounds__(kThreads) void k_expand_packets(const PacketRun *runs, int64_t nruns,
                                                               rsmi_fenc_packet *pk_a, rsmi_fenc_packet *pk_b,
-                                                              int64_t *dst_off, int32_t *job_a) {
+                                                              int64_t *dst_off, int32_t *job_a,
+                                                              const FrameGroup *groups, const FrameSrc *srcs,
+                                                              uint32_t *rec_a) {
     const int lane = threadIdx.x & 63;
     const int64_t w0 = (int64_t)blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
     for (int64_t w = w0; w < nruns; w += (int64_t)gridDim.x * (kThreads / 64)) {
@@ -296,6 +298,26 @@ __global__ __launch_bounds__(kThreads) void k_expand_packets(const PacketRun *ru
             if (c < (int)R.ndata) {
                 pk_a[R.afirst + c] = p;
                 if (job_a) job_a[R.afirst + c] = R.job;
+                if (rec_a) {  // the records shard i overlaps: the one holding its first byte on
+                    const FrameGroup G = groups[R.job];
+                    const uint32_t i = (uint32_t)(R.slot + c - (int64_t)G.slot0);
+                    uint32_t j0 = i, n = 1;
+                    if (G.mode == 0) {
+                        const FrameSrc *gs = srcs + G.src0;
+                        const uint32_t s0 = max(i * G.fec_len, 4u), e0 = (i + 1) * G.fec_len;
+                        uint32_t lo = 0, m = G.nsrc;
+                        while (m > 1) {
+                            const uint32_t h = m >> 1;
+                            lo = gs[lo + h].off <= s0 ? lo + h : lo;
+                            m -= h;
+                        }
+                        uint32_t j1 = lo + 1;
+                        while (j1 < G.nsrc && j1 <= lo + kFuseRecs && gs[j1].off < e0) ++j1;
+                        j0 = lo;
+                        n = j1 - lo;
+                    }
+                    rec_a[R.afirst + c] = j0 << 8 | n;
+                }
             } else {
                 pk_b[R.bfirst + c - (int)R.ndata] = p;
             }
@@ -307,11 +329,13 @@ __global__ __launch_bounds__(kThreads) void k_expand_packets(const PacketRun *ru
 }  // namespace
 
 hipError_t launch_expand_packets(const PacketRun *runs, int64_t nruns, rsmi_fenc_packet *pk_a,
-                                 rsmi_fenc_packet *pk_b, int64_t *dst_off, int32_t *job_a, hipStream_t s) {
+                                 rsmi_fenc_packet *pk_b, int64_t *dst_off, int32_t *job_a, hipStream_t s,
+                                 const FrameGroup *groups, const FrameSrc *srcs, uint32_t *rec_a) {
     if (nruns <= 0) return hipSuccess;
     int64_t blocks = (nruns + kThreads / 64 - 1) / (kThreads / 64);
     if (blocks > 8192) blocks = 8192;
-    k_expand_packets<<<(unsigned)blocks, kThreads, 0, s>>>(runs, nruns, pk_a, pk_b, dst_off, job_a);
+    k_expand_packets<<<(unsigned)blocks, kThreads, 0, s>>>(runs, nruns, pk_a, pk_b, dst_off, job_a, groups,
+                                                           srcs, rec_a);
     return hipGetLastError();
 }
 

@@ -346,9 +346,12 @@ struct PacketRun {
     int32_t job;             // the FrameGroup (job) its slots belong to
     uint16_t count, ndata;   // packets [0, ndata) go to list A, the rest to B
 };
-// job_a (optional): list A's entries' jobs.
+// job_a (optional): list A's entries' jobs, and rec_a the source records
+// their shards overlap, (first << 8) | count (groups / srcs: the plan's).
 hipError_t launch_expand_packets(const PacketRun *runs, int64_t nruns, rsmi_fenc_packet *pk_a,
-                                 rsmi_fenc_packet *pk_b, int64_t *dst_off, int32_t *job_a, hipStream_t s);
+                                 rsmi_fenc_packet *pk_b, int64_t *dst_off, int32_t *job_a, hipStream_t s,
+                                 const FrameGroup *groups = nullptr, const FrameSrc *srcs = nullptr,
+                                 uint32_t *rec_a = nullptr);
 // The fused framing cook (k_cook_frame): list A's packets are data packets of
 // clean shards (FrameGroup.nclean), framed from their source records into
 // their slots (for the encoder) and cooked into the output in the same pass.
@@ -358,6 +361,7 @@ struct FuseArgs {
     const FrameSrc *srcs;
     CarryBase carry;
     const int32_t *job;  // per list entry: its group's FrameGroup index
+    const uint32_t *rec; // per list entry: (first record << 8) | records its shard overlaps
 };
 int cook_frame_packets(const rsmi_cook_ctx *ctx, uint8_t *slots, int64_t S, const rsmi_fenc_packet *pk,
                        int64_t npk, int32_t *out_len, uint8_t *dst, const int64_t *dst_off, uint64_t seed,
