@@ -725,9 +725,8 @@ __global__ __launch_bounds__(kThreads, COOK_OCC) void k_cook_frame(CookArgs a, F
         const uint32_t fl = G.fec_len;
         // the records the shard overlaps: j0 = the one holding its first byte
         // (mode 1: the shard's own), j1 = the first past its end
-        // (found by k_expand_packets)
         const uint32_t rj = have ? f.rec[pk] : 1u;
-        const uint32_t j0 = rj >> 8, nrec = rj & 255u;
+        const uint32_t j0 = m0 ? rj >> 8 : i, nrec = rj & 255u;  // (found by the planner)
         if (have && hl < (int)nrec && nrec <= (uint32_t)kFuseRecs) {
             const FrameSrc r = f.srcs[G.src0 + j0 + hl];
             raddr[hl] = (uint64_t)(uintptr_t)f.carry.resolve(r.addr);

@@ -118,6 +118,8 @@ struct PlanSet {
     HostArr<rsmi::ByteRun> shadow_upd;  // the buffer at the batch end -> dshadow
     HostArr<rsmi_fenc_packet> packets;  // what output() returns, in order (rsmi_fenc_packets)
     HostArr<rsmi::PacketRun> pruns;     // the same as runs of slots (cooked runs upload these)
+    HostArr<uint32_t> recs;             // per list-A packet: (first record << 8) | records its shard
+                                        // overlaps (mode 0; the fused framing cook stages them)
     int64_t n_data_pk = 0, n_par_pk = 0;  // packets of cook lists A (clean data shards) and B (others)
     uint32_t max_src = 0;  // most records of one job (> kFrameLdsSrc: k_frame reads them repeatedly)
     hipEvent_t done = nullptr;
@@ -198,6 +200,16 @@ bool fuse_enabled() {
         return !(v && *v == '0');
     }();
     return on;
+}
+
+// Device address of a pinned plan array (the kernels read it over PCIe), or
+// NULL when it is not pinned.
+template <class T>
+const T *mapped(const HostArr<T> &a) {
+    if (!a.pinned || !a.p) return nullptr;
+    void *d = nullptr;
+    if (hipHostGetDevicePointer(&d, a.p, 0) != hipSuccess) return nullptr;
+    return static_cast<const T *>(d);
 }
 
 int wait_set(PlanSet &B) {
@@ -291,7 +303,7 @@ void shadow_update(rsmi_fenc *E) {
 // padding); mode 0's end before the blob does (no stale blob-buffer bytes)
 // and overlap at most kFuseRecs records each (the kernel stages them per
 // packet).
-int clean_shards(const rsmi_fenc *E, int k, int fec_len) {
+int clean_shards(rsmi_fenc *E, int k, int fec_len) {
     if (E->cfg.mode == 1) return k;
     const int kc = std::min(k, E->blob_len / fec_len);
     // records' blob offsets: 4, then each after the last's 2 + len bytes
@@ -312,6 +324,7 @@ int clean_shards(const rsmi_fenc *E, int k, int fec_len) {
             ++n;
         }
         if (n > rsmi::kFuseRecs) return i;
+        E->P->recs.push_back((uint32_t)j0 << 8 | (uint32_t)n);
     }
     return kc;
 }
@@ -382,6 +395,7 @@ void emit_data(rsmi_fenc *E, int32_t event) {
     // (a mode-1 data shard is [u16 len][payload] zero-padded: always clean)
     E->P->pruns.push_back(rsmi::PacketRun{-1, 0, (int32_t)p.emitted, (int32_t)E->P->n_data_pk,
                                           (int32_t)E->P->n_par_pk, 8 + (int)p.len + 2, -1, 1, 1});
+    E->P->recs.push_back(1u);  // its own record (the kernel takes it from the slot)
     E->P->n_data_pk += 1;
 }
 
@@ -613,6 +627,7 @@ int rsmi_fenc_plan(rsmi_fenc *E, int64_t n_events, const int32_t *len, const uin
     E->P->carry.clear();
     E->P->packets.clear();
     E->P->pruns.clear();
+    E->P->recs.clear();
     E->P->n_data_pk = E->P->n_par_pk = 0;
     E->g_slot0.clear();
     E->g_k.clear();
@@ -816,6 +831,7 @@ int run_dev(rsmi_fenc *E, uint8_t *slots, int64_t S, void *stream, const CookSpe
     // framed and cooked in one pass (k_cook_frame), before the encoder reads
     // their plain bytes; in place, every packet is cooked after the encoder
     const bool fuse = npk && ck->out && na > 0 && fuse_enabled();
+    const uint32_t *zrec = fuse ? mapped(E->P->recs) : nullptr;  // read in place by k_cook_frame
     const size_t db = packed ? npk * sizeof(int64_t) : 0, jb = fuse ? (size_t)na * 2 * sizeof(int32_t) : 0;
     const size_t go = 0, so = (gb + 255) & ~size_t(255), co = (so + sb + 255) & ~size_t(255),
                  ro = (co + cb + 255) & ~size_t(255), uo = (ro + rb + 255) & ~size_t(255),
@@ -842,9 +858,10 @@ int run_dev(rsmi_fenc *E, uint8_t *slots, int64_t S, void *stream, const CookSpe
                                         reinterpret_cast<rsmi_fenc_packet *>(E->dplan + xo),
                                         reinterpret_cast<rsmi_fenc_packet *>(E->dplan + xo) + na,
                                         packed ? reinterpret_cast<int64_t *>(E->dplan + dq) : nullptr,
-                                        fuse ? reinterpret_cast<int32_t *>(E->dplan + jo) : nullptr, s,
-                                        reinterpret_cast<const FrameGroup *>(E->dplan + go), dsrc,
-                                        fuse ? reinterpret_cast<uint32_t *>(E->dplan + jo) + na : nullptr);
+                                        fuse ? reinterpret_cast<int32_t *>(E->dplan + jo) : nullptr, s);
+    if (e == hipSuccess && fuse && !zrec)
+        e = hipMemcpyAsync(reinterpret_cast<uint32_t *>(E->dplan + jo) + na, E->P->recs.p, (size_t)na * 4,
+                           hipMemcpyHostToDevice, s);
     if (e == hipSuccess)
         e = rsmi::launch_frame(reinterpret_cast<const FrameGroup *>(E->dplan + go), (int64_t)E->P->jobs.size(),
                                dsrc, carry, slots, S, s, fuse);
@@ -854,7 +871,7 @@ int run_dev(rsmi_fenc *E, uint8_t *slots, int64_t S, void *stream, const CookSpe
     if (fuse) {  // do_cook (my_send, packet.cpp:165-168) of list A, framing it on the way
         const rsmi::FuseArgs fa{reinterpret_cast<const FrameGroup *>(E->dplan + go), dsrc, carry,
                                 reinterpret_cast<const int32_t *>(E->dplan + jo),
-                                reinterpret_cast<const uint32_t *>(E->dplan + jo) + na};
+                                zrec ? zrec : reinterpret_cast<const uint32_t *>(E->dplan + jo) + na};
         rc = rsmi::cook_frame_packets(ck->ctx, slots, S, lists, na, ck->out_len, ck->out, doff, ck->seed, fa, s);
         if (rc) return rc;
     }

@@ -298,26 +298,7 @@ __global__ __launch_bounds__(kThreads) void k_expand_packets(const PacketRun *ru
             if (c < (int)R.ndata) {
                 pk_a[R.afirst + c] = p;
                 if (job_a) job_a[R.afirst + c] = R.job;
-                if (rec_a) {  // the records shard i overlaps: the one holding its first byte on
-                    const FrameGroup G = groups[R.job];
-                    const uint32_t i = (uint32_t)(R.slot + c - (int64_t)G.slot0);
-                    uint32_t j0 = i, n = 1;
-                    if (G.mode == 0) {
-                        const FrameSrc *gs = srcs + G.src0;
-                        const uint32_t s0 = max(i * G.fec_len, 4u), e0 = (i + 1) * G.fec_len;
-                        uint32_t lo = 0, m = G.nsrc;
-                        while (m > 1) {
-                            const uint32_t h = m >> 1;
-                            lo = gs[lo + h].off <= s0 ? lo + h : lo;
-                            m -= h;
-                        }
-                        uint32_t j1 = lo + 1;
-                        while (j1 < G.nsrc && j1 <= lo + kFuseRecs && gs[j1].off < e0) ++j1;
-                        j0 = lo;
-                        n = j1 - lo;
-                    }
-                    rec_a[R.afirst + c] = j0 << 8 | n;
-                }
+                (void)rec_a;
             } else {
                 pk_b[R.bfirst + c - (int)R.ndata] = p;
             }
