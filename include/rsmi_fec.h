@@ -148,7 +148,8 @@ int rsmi_fenc_run_cooked_dev(rsmi_fenc *enc, uint8_t *slots_base, int64_t slot_s
 typedef struct rsmi_fenc_packet_run {
     int64_t slot, out0;
     int32_t first, afirst, bfirst, len, job;
-    uint16_t count, ndata;
+    uint16_t count, ndata; /* the fused run cooks [0, ndata) from list A, the rest from B */
+    uint16_t nfr, pad;     /* list A holds [0, nfr): framed there */
 } rsmi_fenc_packet_run;
 int rsmi_fenc_packet_runs(const rsmi_fenc *enc, int64_t *n, rsmi_fenc_packet_run *out);
 

@@ -97,10 +97,11 @@ def test_planner_matches_reference_fixtures(fx, name, nbatch):
 def test_packet_runs_expand_to_the_packet_list(fx, name, nbatch):
     """The runs a cooked run uploads (no GPU): expanded as k_expand_packets
     does, they give every packet of rsmi_fenc_packets once, in order, with its
-    slot and length; list A (data packets of clean shards: a mode-0 group's
-    leading data shards that end before its blob does, every mode-1 data
-    packet) and list B (the rest, every parity packet) each keep packet
-    order."""
+    slot and length.  In a fused run, list A (the data shards the fused
+    framing cook frames: a mode-0 group's leading ones, every mode-1 data
+    packet) and list B (every packet it does not cook, every parity packet)
+    each keep packet order, and every packet is cooked once: from A if it is
+    among its run's first ndata, else from B."""
     from udpspeeder_amd.fec import FecEncoder
     c = _case(fx, name)
     enc = FecEncoder(c["rs"], c["mode"], c["mtu"], c["ql"], seq0=c["seq0"])
@@ -111,23 +112,26 @@ def test_packet_runs_expand_to_the_packet_list(fx, name, nbatch):
         runs = enc.packet_runs()
         npk = len(p.packets)
         slot, ln = np.full(npk, -1, np.int64), np.full(npk, -1, np.int64)
-        la, lb = [], []
+        la, lb, cooked = [], [], []
         for r in runs:
+            assert int(r["ndata"]) <= int(r["nfr"]) <= int(r["count"])
             for c_ in range(int(r["count"])):
                 i = int(r["first"]) + c_
                 assert slot[i] == -1, "packet listed twice"
                 slot[i], ln[i] = int(r["slot"]) + c_, int(r["len"])
-                if c_ < int(r["ndata"]):
+                if c_ < int(r["nfr"]):
                     la.append((int(r["afirst"]) + c_, i))
-                else:
+                if c_ >= int(r["ndata"]):
                     lb.append((int(r["bfirst"]) + c_ - int(r["ndata"]), i))
+                cooked.append(i)
+        assert sorted(cooked) == list(range(npk))
         assert (slot == p.packets["slot"]).all() and (ln == p.packets["len"]).all()
         for lst in (la, lb):
             lst.sort()
             assert [x for x, _ in lst] == list(range(len(lst)))
             assert [i for _, i in lst] == sorted(i for _, i in lst)
-        # list A holds data packets only (of clean shards: a run's leading
-        # data packets), every parity packet is in list B
+        # list A holds data packets only (a run's leading data packets),
+        # every parity packet is in list B
         g = p.groups
         kind = {}
         for s0, k, m in zip(g["slot0"], g["k"], g["m"]):
@@ -137,6 +141,7 @@ def test_packet_runs_expand_to_the_packet_list(fx, name, nbatch):
         for i in range(npk):
             if kind.get(int(p.packets["slot"][i]), False):
                 assert i in par, i
+        assert not any(kind.get(int(p.packets["slot"][i]), False) for _, i in la)
         if c["mode"] == 1:  # mode-1 data shards are always clean
             assert all(not kind.get(int(p.packets["slot"][i]), False) for _, i in la)
             assert len(la) == sum(1 for i in range(npk) if not kind.get(int(p.packets["slot"][i]), False))

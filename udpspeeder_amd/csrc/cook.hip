@@ -734,16 +734,20 @@ __global__ __launch_bounds__(kThreads, COOK_OCC) void k_cook_frame(CookArgs a, F
             roff[hl] = o;
             if (hl == (int)nrec - 1) roff[nrec] = o + 2 + r.len;
         }
-        if (have && obs) ivl = 4 + (int)(splitmix(a.seed, (uint64_t)gi, 0) % 29u);
+        // shards cfirst..nclean-1 are cooked here, nclean..nfr-1 only framed
+        // (their stale blob bytes come later; list B cooks them)
+        const bool ckit = have && i < G.nclean;
+        if (ckit && obs) ivl = 4 + (int)(splitmix(a.seed, (uint64_t)gi, 0) % 29u);
         const int out = L + (ck ? 4 : 0) + (obs ? ivl + 1 : 0);
         const int Lg = L + ph, outg = out + ph;
         // whole grid pieces of the plain packet: header, then the shard to fec_len
         const int pext = 16 + (int)((fl + 15) & ~15u);
         const bool ok = have && ph == 8 && (((uintptr_t)opkt & 15) == 8) && L >= 0 &&
                         L <= RSMI_COOK_MAX_LEN && nrec <= (uint32_t)kFuseRecs && i >= G.cfirst &&
-                        i < G.nclean &&
+                        i < G.nfr &&
                         (a.dst_off || round16(outg) - ph <= a.cap) && pext - ph <= a.cap;
-        const int ext = ok ? round16(outg) : 0;
+        const bool cookit = ok && ckit;
+        const int ext = cookit ? round16(outg) : 0;
         const int xall = ok ? max(ext, pext) : 0;  // pieces to assemble
         const uint32_t magic = ivl ? 0xFFFFFFFFu / (uint32_t)ivl : 0u;
         if (ok && ivl && 8 * hl < ivl) {
@@ -766,7 +770,7 @@ __global__ __launch_bounds__(kThreads, COOK_OCC) void k_cook_frame(CookArgs a, F
                             (m0 ? ((uint32_t)G.k << 8 | (uint32_t)G.m << 16) : 0u) |
                             ((G.idx0 + i) & 0xffu) << 24;         // header (fec_manager.cpp:318-333)
         const uint32_t sstep = ivl ? mod_ivl(16u * kLpp, (uint32_t)ivl, magic) : 0u;
-        const int Q = (Lg + 15) >> 4;
+        const int Q = cookit ? (Lg + 15) >> 4 : 0;
         const int P0 = Lg & ~15;
         const int nrm = wave_max((xall + kRoundF - 1) / kRoundF);
         uint32_t acc = 0;
@@ -787,7 +791,7 @@ __global__ __launch_bounds__(kThreads, COOK_OCC) void k_cook_frame(CookArgs a, F
                     uint32_t t = 0;
                     for (uint32_t u = 1; u < nrec; ++u) t = roff[u] <= bb ? u : t;
                     const uint32_t q0 = roff[t] + 2, q1 = roff[t + 1];
-                    if (b >= q0 && b + 16 <= q1) A[p] = rv.addr(t) + (b - q0);
+                    if (nrec && b >= q0 && b + 16 <= q1) A[p] = rv.addr(t) + (b - q0);
                     else slow |= 1 << p;
                 }
             }
@@ -837,8 +841,8 @@ __global__ __launch_bounds__(kThreads, COOK_OCC) void k_cook_frame(CookArgs a, F
             }
         }
         uint32_t crc = 0;
-        if (ck && L > 0) crc = ~unshift(T, acc, (uint32_t)(16 * Q - Lg));
-        if (ok) {
+        if (ck && L > 0 && cookit) crc = ~unshift(T, acc, (uint32_t)(16 * Q - Lg));
+        if (cookit) {
             for (int t = hl; t < 64; t += kLpp) {
                 const int pos = P0 + t - ph;
                 uint32_t v = 0;
@@ -864,7 +868,8 @@ __global__ __launch_bounds__(kThreads, COOK_OCC) void k_cook_frame(CookArgs a, F
             const u32x4 lo = piece_mask(Lg - Pt), hi = piece_mask(outg - Pt);
             st_piece(oga + Pt, ((dt ^ m) & lo) | ((o ^ k) & hi & ~lo) | (dt & ~hi));
         }
-        if (have && hl == 0) a.out_len[gi] = ok ? out : -1;
+        // (a packet only framed here gets its out_len from list B's cook)
+        if (have && hl == 0 && (cookit || !ok)) a.out_len[gi] = ok ? out : -1;
         wave_sync();
     }
 }

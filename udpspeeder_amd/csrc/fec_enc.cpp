@@ -120,7 +120,9 @@ struct PlanSet {
     HostArr<rsmi::PacketRun> pruns;     // the same as runs of slots (cooked runs upload these)
     HostArr<uint32_t> recs;             // per list-A packet: (first record << 8) | records its shard
                                         // overlaps (mode 0; the fused framing cook stages them)
-    int64_t n_data_pk = 0, n_par_pk = 0;  // packets of cook lists A (clean data shards) and B (others)
+    int64_t n_data_pk = 0, n_par_pk = 0;  // entries of the fused run's cook lists A (data shards the
+                                          // fused framing cook frames) and B (the packets it does not cook)
+    int32_t max_fl = 0;                   // largest fec_len of a group with list-A shards
     uint32_t max_src = 0;  // most records of one job (> kFrameLdsSrc: k_frame reads them repeatedly)
     hipEvent_t done = nullptr;
     bool in_flight = false;
@@ -298,18 +300,19 @@ void shadow_update(rsmi_fenc *E) {
     E->shadow_len = std::max(E->shadow_len, lo);
 }
 
-// Data shards 0..n-1 of the group being closed that the fused framing cook
-// can frame (k_cook_frame): mode 1's are all clean ([u16 len][payload], zero
-// padding); mode 0's end before the blob does (no stale blob-buffer bytes)
-// and overlap at most kFuseRecs records each (the kernel stages them per
-// packet).
-int clean_shards(rsmi_fenc *E, int k, int fec_len) {
-    if (E->cfg.mode == 1) return k;
+// Data shards of the group being closed that the fused framing cook
+// (k_cook_frame) frames, 0..nfr-1, and of those the ones it also cooks,
+// 0..nclean-1.  Mode 1's are all clean ([u16 len][payload], zero padding).
+// Mode 0's are framed while they overlap at most kFuseRecs records each (the
+// kernel stages them per packet; their (first << 8) | count go to recs) and
+// are clean when they end before the blob does (no stale blob-buffer bytes).
+std::pair<int, int> fused_shards(rsmi_fenc *E, int k, int fec_len) {
+    if (E->cfg.mode == 1) return {k, k};
     const int kc = std::min(k, E->blob_len / fec_len);
     // records' blob offsets: 4, then each after the last's 2 + len bytes
-    size_t j0 = 0;  // the record holding the shard's first byte (or the first record)
+    size_t j0 = 0;  // the record holding the shard's first byte (or the last record)
     uint32_t o0 = 4;
-    for (int i = 0; i < kc; ++i) {
+    for (int i = 0; i < k; ++i) {
         const uint32_t s = (uint32_t)i * (uint32_t)fec_len, e = s + (uint32_t)fec_len;
         while (j0 + 1 < E->pend.size() && o0 + 2 + E->pend[j0].len <= s) {
             o0 += 2 + E->pend[j0].len;
@@ -319,14 +322,14 @@ int clean_shards(rsmi_fenc *E, int k, int fec_len) {
         uint32_t o = o0;
         int n = 0;
         while (j1 < E->pend.size() && o < e) {
+            if (o + 2 + E->pend[j1].len > s) ++n;  // (past the blob's end: none)
             o += 2 + E->pend[j1].len;
             ++j1;
-            ++n;
         }
-        if (n > rsmi::kFuseRecs) return i;
-        E->P->recs.push_back((uint32_t)j0 << 8 | (uint32_t)n);
+        if (n > rsmi::kFuseRecs) return {std::min(i, kc), i};
+        E->P->recs.push_back(n ? (uint32_t)j0 << 8 | (uint32_t)n : 0u);
     }
-    return kc;
+    return {kc, k};
 }
 
 // Close the open group (the about_to_fec branch, fec_manager.cpp:248-367).
@@ -364,8 +367,11 @@ void close_group(rsmi_fenc *E, int k, int m, int fec_len) {
     uint32_t cf = 0;
     if (E->cfg.mode == 1)
         while (cf < E->pend.size() && E->pend[cf].emitted < 0) ++cf;
+    const std::pair<int, int> fs = fused_shards(E, k, fec_len);
     G.cfirst = (uint16_t)cf;
-    G.nclean = (uint16_t)std::max((int)cf, clean_shards(E, k, fec_len));
+    G.nclean = (uint16_t)std::max((int)cf, fs.first);
+    G.nfr = (uint16_t)std::max((int)cf, fs.second);
+    if (G.nfr > G.cfirst) E->P->max_fl = std::max(E->P->max_fl, (int32_t)fec_len);
     E->P->jobs.push_back(G);
     E->P->max_src = std::max(E->P->max_src, E->cfg.mode == 0 ? G.nsrc : (uint32_t)G.nframe);
     if (E->cfg.mode == 0) stale_runs(E, slot0, k, fec_len, E->blob_len);
@@ -394,7 +400,8 @@ void emit_data(rsmi_fenc *E, int32_t event) {
     E->P->packets.push_back(rsmi_fenc_packet{-1, 8 + (int)p.len + 2, event});
     // (a mode-1 data shard is [u16 len][payload] zero-padded: always clean)
     E->P->pruns.push_back(rsmi::PacketRun{-1, 0, (int32_t)p.emitted, (int32_t)E->P->n_data_pk,
-                                          (int32_t)E->P->n_par_pk, 8 + (int)p.len + 2, -1, 1, 1});
+                                          (int32_t)E->P->n_par_pk, 8 + (int)p.len + 2, -1, 1, 1, 1, 0});
+    E->P->max_fl = std::max(E->P->max_fl, (int32_t)p.len + 2);
     E->P->recs.push_back(1u);  // its own record (the kernel takes it from the slot)
     E->P->n_data_pk += 1;
 }
@@ -475,19 +482,19 @@ int input_event(rsmi_fenc *E, int32_t event, bool has, int len, uint64_t addr) {
         close_group(E, k, m, fec_len);
         if (mode == 0) {
             for (int i = 0; i < k + m; ++i) E->P->packets[(size_t)(first_pk + i)].slot = slot0 + i;
-            const int nc = E->P->jobs[E->P->jobs.size() - 1].nclean;
+            const FrameGroup &G = E->P->jobs[E->P->jobs.size() - 1];
             E->P->pruns.push_back(rsmi::PacketRun{slot0, 0, (int32_t)first_pk, (int32_t)E->P->n_data_pk,
                                                   (int32_t)E->P->n_par_pk, 8 + fec_len,
                                                   (int32_t)E->P->jobs.size() - 1, (uint16_t)(k + m),
-                                                  (uint16_t)nc});
-            E->P->n_data_pk += nc;
-            E->P->n_par_pk += k + m - nc;
+                                                  G.nclean, G.nfr, 0});
+            E->P->n_data_pk += G.nfr;
+            E->P->n_par_pk += k + m - G.nclean;
         } else {
             int64_t q = first_pk + (has ? 1 : 0);
             if (m > 0) {
                 E->P->pruns.push_back(rsmi::PacketRun{slot0 + k, 0, (int32_t)q, (int32_t)E->P->n_data_pk,
                                                       (int32_t)E->P->n_par_pk, 8 + fec_len,
-                                                      (int32_t)E->P->jobs.size() - 1, (uint16_t)m, 0});
+                                                      (int32_t)E->P->jobs.size() - 1, (uint16_t)m, 0, 0, 0});
                 E->P->n_par_pk += m;
             }
             for (int i = k; i < k + m; ++i) E->P->packets[(size_t)q++].slot = slot0 + i;
@@ -629,6 +636,7 @@ int rsmi_fenc_plan(rsmi_fenc *E, int64_t n_events, const int32_t *len, const uin
     E->P->pruns.clear();
     E->P->recs.clear();
     E->P->n_data_pk = E->P->n_par_pk = 0;
+    E->P->max_fl = 0;
     E->g_slot0.clear();
     E->g_k.clear();
     E->g_m.clear();
@@ -663,7 +671,7 @@ int rsmi_fenc_plan(rsmi_fenc *E, int64_t n_events, const int32_t *len, const uin
         G.nframe = 1;
         G.mode = 1;
         G.idx0 = (uint8_t)j;
-        G.nclean = 1;
+        G.nclean = G.nfr = 1;
         E->P->srcs.push_back(FrameSrc{p.addr, p.len, 0});
         E->P->jobs.push_back(G);
         E->P->packets[(size_t)p.emitted].slot = slot;
@@ -804,10 +812,21 @@ int run_dev(rsmi_fenc *E, uint8_t *slots, int64_t S, void *stream, const CookSpe
     PlanSet &prev = E->ps[E->pcur ^ 1];
     const rsmi::CarryBase carry{{E->dcarry[0], E->dcarry[1]}};
     // cooked runs: the packet list's runs go up with the plan and are expanded
-    // on the device into the two cook lists (data packets, parity packets)
+    // on the device into the cook list(s)
     const size_t npk = ck ? E->P->packets.size() : 0, nrun = ck ? E->P->pruns.size() : 0;
     if (npk > (size_t)INT32_MAX) return fail(RSMI_ERR_INVALID, "fenc: more than 2^31 packets in one batch");
-    const int64_t na = ck ? E->P->n_data_pk : 0;
+    // into another buffer, list A's packets (the data shards fused_shards
+    // picked) are framed in one pass with the cook of the clean ones
+    // (k_cook_frame), before the encoder reads their plain bytes; list B's
+    // (the rest) are cooked after the encoder, in the slots.  Every list-A
+    // packet must fit the kernel's bounds (it frames only those it cooks or
+    // can place): else, and in place, one list in packet order, cooked after
+    // the encoder.
+    const int64_t cap = S - rsmi::kSlotHeader, fl = E->P->max_fl;
+    const bool fuse = npk && ck->out && E->P->n_data_pk > 0 && fuse_enabled() && 8 + fl <= RSMI_COOK_MAX_LEN &&
+                      16 + ((fl + 15) & ~15) - 8 <= cap &&
+                      (ck->out_cap >= 0 || ((8 + fl + 4 + 33 + 8 + 15) & ~15) - 8 <= cap);
+    const int64_t na = fuse ? E->P->n_data_pk : 0, nlist = fuse ? na + E->P->n_par_pk : (int64_t)npk;
     const FrameSrc *zsrc = E->P->srcs.empty() || E->P->max_src > rsmi::kFrameLdsSrc ? nullptr
                                                                                      : mapped_srcs(E->P->srcs);
     const size_t gb = E->P->jobs.size() * sizeof(FrameGroup),
@@ -815,7 +834,7 @@ int run_dev(rsmi_fenc *E, uint8_t *slots, int64_t S, void *stream, const CookSpe
                  cb = E->P->carry.size() * sizeof(CarryCopy),
                  rb = E->P->stale.size() * sizeof(rsmi::ByteRun),
                  ub = E->P->shadow_upd.size() * sizeof(rsmi::ByteRun),
-                 pb = nrun * sizeof(rsmi::PacketRun), xb = npk * sizeof(rsmi_fenc_packet);
+                 pb = nrun * sizeof(rsmi::PacketRun), xb = (size_t)nlist * sizeof(rsmi_fenc_packet);
     const bool packed = ck && ck->out_cap >= 0;
     if (packed) {  // each run's first packet's place in the packed output
         int64_t o = 0;
@@ -827,10 +846,6 @@ int run_dev(rsmi_fenc *E, uint8_t *slots, int64_t S, void *stream, const CookSpe
             return fail(RSMI_ERR_INVALID, "rsmi_fenc_run_cooked_packed_dev: out_cap " + std::to_string(ck->out_cap) +
                                               " < packed bytes " + std::to_string(o));
     }
-    // into another buffer, list A's packets (data packets of clean shards) are
-    // framed and cooked in one pass (k_cook_frame), before the encoder reads
-    // their plain bytes; in place, every packet is cooked after the encoder
-    const bool fuse = npk && ck->out && na > 0 && fuse_enabled();
     const uint32_t *zrec = fuse ? mapped(E->P->recs) : nullptr;  // read in place by k_cook_frame
     const size_t db = packed ? npk * sizeof(int64_t) : 0, jb = fuse ? (size_t)na * 2 * sizeof(int32_t) : 0;
     const size_t go = 0, so = (gb + 255) & ~size_t(255), co = (so + sb + 255) & ~size_t(255),
@@ -858,11 +873,16 @@ int run_dev(rsmi_fenc *E, uint8_t *slots, int64_t S, void *stream, const CookSpe
                                         reinterpret_cast<rsmi_fenc_packet *>(E->dplan + xo),
                                         reinterpret_cast<rsmi_fenc_packet *>(E->dplan + xo) + na,
                                         packed ? reinterpret_cast<int64_t *>(E->dplan + dq) : nullptr,
-                                        fuse ? reinterpret_cast<int32_t *>(E->dplan + jo) : nullptr, s);
+                                        fuse ? reinterpret_cast<int32_t *>(E->dplan + jo) : nullptr, s,
+                                        reinterpret_cast<const FrameGroup *>(E->dplan + go), slots, S);
     if (e == hipSuccess && fuse && !zrec)
         e = hipMemcpyAsync(reinterpret_cast<uint32_t *>(E->dplan + jo) + na, E->P->recs.p, (size_t)na * 4,
                            hipMemcpyHostToDevice, s);
-    if (e == hipSuccess)
+    // (fused: k_frame only for the groups' other shards, if there are any)
+    bool frame = !fuse;
+    for (size_t j = 0; j < E->P->jobs.size() && !frame; ++j)
+        frame = E->P->jobs[j].cfirst > 0 || E->P->jobs[j].nfr < E->P->jobs[j].nframe;
+    if (e == hipSuccess && frame)
         e = rsmi::launch_frame(reinterpret_cast<const FrameGroup *>(E->dplan + go), (int64_t)E->P->jobs.size(),
                                dsrc, carry, slots, S, s, fuse);
     if (e != hipSuccess) return fail(RSMI_ERR_HIP, std::string("fenc frame: ") + hipGetErrorString(e));
@@ -898,9 +918,8 @@ int run_dev(rsmi_fenc *E, uint8_t *slots, int64_t S, void *stream, const CookSpe
     // lists, which lie back to back.  (Cooking the data packets on a forked
     // stream beside the encoder measured no faster: the two kernels slow each
     // other down)
-    if (npk && (int64_t)npk > (fuse ? na : 0)) {
-        rc = rsmi::cook_packets(ck->ctx, slots, S, lists + (fuse ? na : 0), (int64_t)npk - (fuse ? na : 0),
-                                ck->out_len, ck->out, doff, ck->seed, s);
+    if (nlist > na) {
+        rc = rsmi::cook_packets(ck->ctx, slots, S, lists + na, nlist - na, ck->out_len, ck->out, doff, ck->seed, s);
         if (rc) return rc;
     }
     e = hipEventRecord(E->P->done, s);
@@ -969,7 +988,7 @@ int rsmi_fenc_run_many(rsmi_fcol *C, rsmi_fenc *const *enc, int32_t n, uint8_t *
                        const rsmi_cook_ctx *ctx, uint64_t seed, uint8_t *out, int32_t *out_len,
                        void *stream) {
     if (!C || n < 0 || (n && !enc)) return fail(RSMI_ERR_INVALID, "rsmi_fenc_run_many: bad arguments");
-    int64_t total_slots = 0, total_pk = 0, total_a = 0;
+    int64_t total_slots = 0, total_pk = 0;
     for (int i = 0; i < n; ++i) {
         rsmi_fenc *E = enc[i];
         if (!E || !E->planned) return fail(RSMI_ERR_INVALID, "rsmi_fenc_run_many: encoder without a plan");
@@ -981,7 +1000,6 @@ int rsmi_fenc_run_many(rsmi_fcol *C, rsmi_fenc *const *enc, int32_t n, uint8_t *
                                           "slot_stride_min (" + std::to_string(E->stride_min) + ")");
         total_slots += E->n_slots;
         total_pk += (int64_t)E->P->packets.size();
-        total_a += E->P->n_data_pk;
     }
     if (total_pk > INT32_MAX) return fail(RSMI_ERR_INVALID, "rsmi_fenc_run_many: more than 2^31 packets");
     if (total_slots && (!slots || ((uintptr_t)slots & 15)))
@@ -1066,7 +1084,7 @@ int rsmi_fenc_run_many(rsmi_fcol *C, rsmi_fenc *const *enc, int32_t n, uint8_t *
         return (l & rsmi::kShadowLoc) ? (rsmi::kAbsLoc | (uint64_t)(uintptr_t)E->dshadow)
                                       : (uint64_t)m[(size_t)l];
     };
-    int64_t pk_base = 0, a_base = 0, b_base = 0;
+    int64_t pk_base = 0;
     for (int i = 0; i < n; ++i) {
         rsmi_fenc *E = enc[i];
         const std::vector<int64_t> &m = smap[(size_t)i];
@@ -1110,14 +1128,10 @@ int rsmi_fenc_run_many(rsmi_fcol *C, rsmi_fenc *const *enc, int32_t n, uint8_t *
                 rsmi::PacketRun r = E->P->pruns[j];
                 r.slot = m[(size_t)r.slot];  // a run lies inside one group (or is one lone slot)
                 r.first += (int32_t)pk_base;
-                r.afirst += (int32_t)a_base;  // one cook list: every data packet, then every parity packet
-                r.bfirst += (int32_t)(total_a + b_base);
-                r.job += (int32_t)job_base;
+                r.job += (int32_t)job_base;  // (one cook list, in packet order)
                 B.pruns.push_back(r);
             }
         pk_base += (int64_t)E->P->packets.size();
-        a_base += E->P->n_data_pk;
-        b_base += E->P->n_par_pk;
     }
     // ---- upload + launches
     uint32_t max_src = 0;

@@ -207,7 +207,7 @@ __global__ __launch_bounds__(kFThreads) void k_frame(const FrameGroup *groups, i
         uint8_t *s0 = slots + (int64_t)G.slot0 * slot_stride;
         // headers: seq | mode | k | m | index (fec_manager.cpp:318-333); mode-1
         // data packets carry k = m = 0 (:321-323)
-        const uint32_t c0 = skip_clean ? (uint32_t)G.cfirst : 0u, c1 = skip_clean ? (uint32_t)G.nclean : 0u;
+        const uint32_t c0 = skip_clean ? (uint32_t)G.cfirst : 0u, c1 = skip_clean ? (uint32_t)G.nfr : 0u;
         for (uint32_t j = threadIdx.x; j < G.nslots; j += kFThreads) {
             if (j >= c0 && j < c1) continue;
             const bool zero_km = G.mode == 1 && j < G.nframe;
@@ -282,27 +282,42 @@ __global__ __launch_bounds__(kThreads) void k_byte_runs(const ByteRun *runs, int
     }
 }
 
-// Packet runs -> the two cook lists: one wave per run.  With dst_off, also
-// each packet's offset in the packed cooked output.
+// Packet runs -> the cook list(s): one wave per run.  Unfused (no job_a), one
+// list in packet order (pk_a).  Fused, lists A (packets [0, nfr) of a run,
+// with their jobs in job_a) and B (packets [ndata, count)), and the parity
+// packets' 8-byte headers (fec_manager.cpp:318-333), which k_frame may not be
+// run to write.  With dst_off, also each packet's offset in the packed output.
 __global__ __launch_bounds__(kThreads) void k_expand_packets(const PacketRun *runs, int64_t nruns,
                                                               rsmi_fenc_packet *pk_a, rsmi_fenc_packet *pk_b,
                                                               int64_t *dst_off, int32_t *job_a,
-                                                              const FrameGroup *groups, const FrameSrc *srcs,
-                                                              uint32_t *rec_a) {
+                                                              const FrameGroup *groups, uint8_t *slots,
+                                                              int64_t slot_stride) {
     const int lane = threadIdx.x & 63;
     const int64_t w0 = (int64_t)blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
     for (int64_t w = w0; w < nruns; w += (int64_t)gridDim.x * (kThreads / 64)) {
         const PacketRun R = runs[w];
         for (int c = lane; c < (int)R.count; c += 64) {
             const rsmi_fenc_packet p{R.slot + c, R.len, R.first + c};
-            if (c < (int)R.ndata) {
-                pk_a[R.afirst + c] = p;
-                if (job_a) job_a[R.afirst + c] = R.job;
-                (void)rec_a;
+            if (!job_a) {
+                pk_a[R.first + c] = p;
             } else {
-                pk_b[R.bfirst + c - (int)R.ndata] = p;
+                if (c < (int)R.nfr) {
+                    pk_a[R.afirst + c] = p;
+                    job_a[R.afirst + c] = R.job;
+                }
+                if (c >= (int)R.ndata) pk_b[R.bfirst + c - (int)R.ndata] = p;
             }
             if (dst_off) dst_off[R.first + c] = R.out0 + (int64_t)c * RSMI_FEC_COOK_SPAN(R.len);
+            if (job_a) {
+                const FrameGroup G = groups[R.job];
+                const uint32_t j = (uint32_t)(R.slot + c - (int64_t)G.slot0);
+                if (j >= G.nframe) {  // a parity packet: seq | mode | k | m | index
+                    const uint32_t w1 = (uint32_t)G.mode | ((uint32_t)G.k << 8 | (uint32_t)G.m << 16) |
+                                        ((G.idx0 + j) & 0xffu) << 24;
+                    *reinterpret_cast<u32x2 *>(slots + (R.slot + c) * slot_stride + kSlotHeader) =
+                        u32x2{bswap32(G.seq), w1};
+                }
+            }
         }
     }
 }
@@ -311,12 +326,12 @@ __global__ __launch_bounds__(kThreads) void k_expand_packets(const PacketRun *ru
 
 hipError_t launch_expand_packets(const PacketRun *runs, int64_t nruns, rsmi_fenc_packet *pk_a,
                                  rsmi_fenc_packet *pk_b, int64_t *dst_off, int32_t *job_a, hipStream_t s,
-                                 const FrameGroup *groups, const FrameSrc *srcs, uint32_t *rec_a) {
+                                 const FrameGroup *groups, uint8_t *slots, int64_t slot_stride) {
     if (nruns <= 0) return hipSuccess;
     int64_t blocks = (nruns + kThreads / 64 - 1) / (kThreads / 64);
     if (blocks > 8192) blocks = 8192;
     k_expand_packets<<<(unsigned)blocks, kThreads, 0, s>>>(runs, nruns, pk_a, pk_b, dst_off, job_a, groups,
-                                                           srcs, rec_a);
+                                                           slots, slot_stride);
     return hipGetLastError();
 }
 

@@ -270,9 +270,10 @@ struct FrameGroup {
     uint32_t blob_len;  // mode 0: blob bytes (blob_encode_t::current_len)
     uint16_t nslots, nframe;
     uint8_t mode, k, m, idx0;  // header bytes; idx0 = index of slot 0
-    uint16_t cfirst, nclean;  // data shards cfirst..nclean-1 the fused framing cook frames
-                              // (k_cook_frame): packets emitted in this batch, no stale blob
-                              // bytes, at most kFuseRecs records each
+    // the fused framing cook (k_cook_frame) frames data shards cfirst..nfr-1
+    // (packets emitted in this batch, at most kFuseRecs source records each)
+    // and cooks cfirst..nclean-1 (no stale blob bytes: final once framed)
+    uint16_t cfirst, nclean, nfr, pad[3];
 };
 // A payload address in a plan: a device address, or (kCarryTag set) an offset
 // into carry buffer 0 or 1 (kCarryBuf1), resolved by the kernels.
@@ -344,14 +345,15 @@ struct PacketRun {
     int32_t afirst, bfirst;  // where its list-A packets start in list A, its others in B
     int32_t len;
     int32_t job;             // the FrameGroup (job) its slots belong to
-    uint16_t count, ndata;   // packets [0, ndata) go to list A, the rest to B
+    uint16_t count, ndata;   // packets [0, ndata) are cooked from list A, [ndata, count) from B
+    uint16_t nfr, pad;       // packets [0, nfr) are in list A (framed there; nfr >= ndata)
 };
-// job_a (optional): list A's entries' jobs, and rec_a the source records
-// their shards overlap, (first << 8) | count (groups / srcs: the plan's).
+// job_a (optional, the fused run): list A's entries' jobs; then the parity
+// packets' headers are written too (groups: the plan's; slots, slot_stride).
 hipError_t launch_expand_packets(const PacketRun *runs, int64_t nruns, rsmi_fenc_packet *pk_a,
                                  rsmi_fenc_packet *pk_b, int64_t *dst_off, int32_t *job_a, hipStream_t s,
-                                 const FrameGroup *groups = nullptr, const FrameSrc *srcs = nullptr,
-                                 uint32_t *rec_a = nullptr);
+                                 const FrameGroup *groups = nullptr, uint8_t *slots = nullptr,
+                                 int64_t slot_stride = 0);
 // The fused framing cook (k_cook_frame): list A's packets are data packets of
 // clean shards (FrameGroup.nclean), framed from their source records into
 // their slots (for the encoder) and cooked into the output in the same pass.

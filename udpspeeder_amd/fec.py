@@ -173,15 +173,16 @@ class FecEncoder:
 
     RUN_DTYPE = np.dtype([("slot", np.int64), ("out0", np.int64), ("first", np.int32),
                           ("afirst", np.int32), ("bfirst", np.int32), ("len", np.int32),
-                          ("job", np.int32), ("count", np.uint16), ("ndata", np.uint16)],
-                         align=True)  # 40 B, as in C
+                          ("job", np.int32), ("count", np.uint16), ("ndata", np.uint16),
+                          ("nfr", np.uint16), ("pad", np.uint16)],
+                         align=True)  # 48 B, as in C
 
     def packet_runs(self) -> np.ndarray:
         """The last plan's packet list as runs (rsmi_fenc_packet_runs): what a
         cooked run uploads and expands on the device into its two cook lists."""
         n = C.c_int64()
         check(lib().rsmi_fenc_packet_runs(self._h, C.byref(n), None), "rsmi_fenc_packet_runs")
-        assert self.RUN_DTYPE.itemsize == 40
+        assert self.RUN_DTYPE.itemsize == 48
         out = np.zeros(n.value, self.RUN_DTYPE)
         if n.value:
             check(lib().rsmi_fenc_packet_runs(self._h, C.byref(n), out.ctypes.data),
