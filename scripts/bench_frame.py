@@ -90,6 +90,7 @@ def main():
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(s)
+        tc = time.perf_counter()
         if args.cook in ("dev", "host"):
             enc.run_cooked(slots, S, ctx, rep + 1, out=out)
         else:
@@ -98,12 +99,14 @@ def main():
                 ctx.cook(slots, lens_d, cap=S - 120, offsets=offs_d, seed=rep + 1)
                 out[:p.n_slots * S].copy_(slots[:p.n_slots * S], non_blocking=True)
         e1.record(s)
+        tc = time.perf_counter() - tc
         torch.cuda.synchronize()
         if rep:
-            res.append((t_plan, e0.elapsed_time(e1)))
+            res.append((t_plan, e0.elapsed_time(e1), tc))
         g = p.groups
     t_plan = float(np.median([r[0] for r in res]))
     t_run = float(np.median([r[1] for r in res]))
+    t_call = float(np.median([r[2] for r in res]))
     ng = len(g["k"])
     kk, mm, fl = g["k"].astype(np.int64), g["m"].astype(np.int64), g["fec_len"].astype(np.int64)
     payload = int(lens.sum())
@@ -113,7 +116,7 @@ def main():
         "mode": args.mode, "packets": npk, "packet_len": plen, "groups": ng,
         "k": int(np.median(kk)), "m": int(np.median(mm)), "fec_len": int(np.median(fl)),
         "emitted_packets": int(len(p.packets)), "plan_ms": round(t_plan * 1e3, 3),
-        "run_ms": round(t_run, 4), "run_Mpps_in": round(npk / t_run / 1e3, 1),
+        "run_ms": round(t_run, 4), "call_host_ms": round(t_call * 1e3, 4), "run_Mpps_in": round(npk / t_run / 1e3, 1),
         "payload_GBps": round(payload / (t_run * 1e-3) / 1e9, 1),
         "frame_alg_bytes": frame_bytes, "encode_alg_bytes": enc_bytes,
         "run_alg_GBps": round((frame_bytes + enc_bytes) / (t_run * 1e-3) / 1e9, 1)}

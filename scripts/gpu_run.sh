@@ -57,7 +57,8 @@ for step in "$@"; do
       (cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --memory-copy-trace --stats \
           --output-format csv -d $d -o run -- python3 $R/${A[0]} "${A[@]:1}" > $d.log 2>&1) || { tail $d.log; exit 1; }
       python scripts/kstats.py $d/run_kernel_stats.csv | head -25
-      python scripts/ktimeline.py $d/run_kernel_trace.csv 30 > $d/timeline.txt
+      python scripts/ktimeline.py $d/run_kernel_trace.csv 40 $d/run_memory_copy_trace.csv > $d/timeline.txt
+      head -3 $d/run_memory_copy_trace.csv > $d/copy_trace_head.csv
       rm -f $d/run_kernel_trace.csv $d/run_memory_copy_trace.csv
       tail -5 $d.log ;;
     *) echo "unknown step $step"; exit 2 ;;

@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdlib>
 #include <new>
 #include <cstdio>
@@ -123,6 +124,7 @@ struct PlanSet {
     int64_t n_data_pk = 0, n_par_pk = 0;  // entries of the fused run's cook lists A (data shards the
                                           // fused framing cook frames) and B (the packets it does not cook)
     int32_t max_fl = 0;                   // largest fec_len of a group with list-A shards
+    int64_t n_left = 0;                   // groups with data shards outside [cfirst, nfr) (k_frame's)
     uint32_t max_src = 0;  // most records of one job (> kFrameLdsSrc: k_frame reads them repeatedly)
     hipEvent_t done = nullptr;
     bool in_flight = false;
@@ -372,6 +374,7 @@ void close_group(rsmi_fenc *E, int k, int m, int fec_len) {
     G.nclean = (uint16_t)std::max((int)cf, fs.first);
     G.nfr = (uint16_t)std::max((int)cf, fs.second);
     if (G.nfr > G.cfirst) E->P->max_fl = std::max(E->P->max_fl, (int32_t)fec_len);
+    if (G.cfirst > 0 || G.nfr < G.nframe) E->P->n_left += 1;
     E->P->jobs.push_back(G);
     E->P->max_src = std::max(E->P->max_src, E->cfg.mode == 0 ? G.nsrc : (uint32_t)G.nframe);
     if (E->cfg.mode == 0) stale_runs(E, slot0, k, fec_len, E->blob_len);
@@ -637,6 +640,7 @@ int rsmi_fenc_plan(rsmi_fenc *E, int64_t n_events, const int32_t *len, const uin
     E->P->recs.clear();
     E->P->n_data_pk = E->P->n_par_pk = 0;
     E->P->max_fl = 0;
+    E->P->n_left = 0;
     E->g_slot0.clear();
     E->g_k.clear();
     E->g_m.clear();
@@ -798,7 +802,33 @@ int prepare_run(rsmi_fenc *E, hipStream_t s) {
     return RSMI_OK;
 }
 
+// RSMI_FENC_TRACE=1: run_dev's host time per stage, one stderr line a call
+// (where a call's latency goes before and between its enqueues).
+struct HostTrace {
+    static bool enabled() {
+        static const bool on = [] {
+            const char *v = std::getenv("RSMI_FENC_TRACE");
+            return v && *v && *v != '0';
+        }();
+        return on;
+    }
+    bool on = enabled();
+    std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+    std::string line;
+    void mark(const char *stage) {
+        if (!on) return;
+        const auto n = std::chrono::steady_clock::now();
+        line += std::string(" ") + stage + "=" +
+                std::to_string(std::chrono::duration_cast<std::chrono::microseconds>(n - t).count());
+        t = n;
+    }
+    ~HostTrace() {
+        if (on && !line.empty()) std::fprintf(stderr, "rsmi_fenc_run host us:%s\n", line.c_str());
+    }
+};
+
 int run_dev(rsmi_fenc *E, uint8_t *slots, int64_t S, void *stream, const CookSpec *ck) {
+    HostTrace ht;
     if (!E || !E->planned) return fail(RSMI_ERR_INVALID, "rsmi_fenc_run_dev without a plan");
     if (E->plan_only) return fail(RSMI_ERR_INVALID, "rsmi_fenc_run_dev on a plan-only encoder");
     if (E->n_slots && (!slots || ((uintptr_t)slots & 15)))
@@ -809,6 +839,7 @@ int run_dev(rsmi_fenc *E, uint8_t *slots, int64_t S, void *stream, const CookSpe
     hipStream_t s = (hipStream_t)stream;
     int rc0 = prepare_run(E, s);
     if (rc0) return rc0;
+    ht.mark("prepare");
     PlanSet &prev = E->ps[E->pcur ^ 1];
     const rsmi::CarryBase carry{{E->dcarry[0], E->dcarry[1]}};
     // cooked runs: the packet list's runs go up with the plan and are expanded
@@ -859,6 +890,7 @@ int run_dev(rsmi_fenc *E, uint8_t *slots, int64_t S, void *stream, const CookSpe
     }
     int rc = grow(&E->dplan, &E->plan_cap, all, false);
     if (rc) return rc;
+    ht.mark("layout");
     hipError_t e = hipSuccess;
     if (gb) e = hipMemcpyAsync(E->dplan + go, E->P->jobs.p, gb, hipMemcpyHostToDevice, s);
     if (e == hipSuccess && sb) e = hipMemcpyAsync(E->dplan + so, E->P->srcs.p, sb, hipMemcpyHostToDevice, s);
@@ -868,6 +900,7 @@ int run_dev(rsmi_fenc *E, uint8_t *slots, int64_t S, void *stream, const CookSpe
         e = hipMemcpyAsync(E->dplan + uo, E->P->shadow_upd.p, ub, hipMemcpyHostToDevice, s);
     if (e == hipSuccess && pb) e = hipMemcpyAsync(E->dplan + po, E->P->pruns.p, pb, hipMemcpyHostToDevice, s);
     const FrameSrc *dsrc = zsrc ? zsrc : reinterpret_cast<const FrameSrc *>(E->dplan + so);
+    ht.mark("uploads");
     if (e == hipSuccess)
         e = rsmi::launch_expand_packets(reinterpret_cast<const rsmi::PacketRun *>(E->dplan + po), (int64_t)nrun,
                                         reinterpret_cast<rsmi_fenc_packet *>(E->dplan + xo),
@@ -879,13 +912,12 @@ int run_dev(rsmi_fenc *E, uint8_t *slots, int64_t S, void *stream, const CookSpe
         e = hipMemcpyAsync(reinterpret_cast<uint32_t *>(E->dplan + jo) + na, E->P->recs.p, (size_t)na * 4,
                            hipMemcpyHostToDevice, s);
     // (fused: k_frame only for the groups' other shards, if there are any)
-    bool frame = !fuse;
-    for (size_t j = 0; j < E->P->jobs.size() && !frame; ++j)
-        frame = E->P->jobs[j].cfirst > 0 || E->P->jobs[j].nfr < E->P->jobs[j].nframe;
+    const bool frame = !fuse || E->P->n_left > 0;
     if (e == hipSuccess && frame)
         e = rsmi::launch_frame(reinterpret_cast<const FrameGroup *>(E->dplan + go), (int64_t)E->P->jobs.size(),
                                dsrc, carry, slots, S, s, fuse);
     if (e != hipSuccess) return fail(RSMI_ERR_HIP, std::string("fenc frame: ") + hipGetErrorString(e));
+    ht.mark(frame ? "expand+frame" : "expand");
     const int64_t *doff = packed ? reinterpret_cast<const int64_t *>(E->dplan + dq) : nullptr;
     const rsmi_fenc_packet *lists = reinterpret_cast<const rsmi_fenc_packet *>(E->dplan + xo);
     if (fuse) {  // do_cook (my_send, packet.cpp:165-168) of list A, framing it on the way
@@ -894,6 +926,7 @@ int run_dev(rsmi_fenc *E, uint8_t *slots, int64_t S, void *stream, const CookSpe
                                 zrec ? zrec : reinterpret_cast<const uint32_t *>(E->dplan + jo) + na};
         rc = rsmi::cook_frame_packets(ck->ctx, slots, S, lists, na, ck->out_len, ck->out, doff, ck->seed, fa, s);
         if (rc) return rc;
+        ht.mark("cook_frame");
     }
     // stale bytes past each blob, before the parity is computed over them
     if (e == hipSuccess)
@@ -906,6 +939,7 @@ int run_dev(rsmi_fenc *E, uint8_t *slots, int64_t S, void *stream, const CookSpe
                              r.len, r.count, stream);
         if (rc) return rc;
     }
+    ht.mark("encode");
     // the blob buffer as this batch leaves it (read by the next batch's stale runs)
     e = rsmi::launch_byte_runs(reinterpret_cast<const rsmi::ByteRun *>(E->dplan + uo),
                                (int64_t)E->P->shadow_upd.size(), slots, S, E->dshadow, s);
@@ -921,6 +955,7 @@ int run_dev(rsmi_fenc *E, uint8_t *slots, int64_t S, void *stream, const CookSpe
     if (nlist > na) {
         rc = rsmi::cook_packets(ck->ctx, slots, S, lists + na, nlist - na, ck->out_len, ck->out, doff, ck->seed, s);
         if (rc) return rc;
+        ht.mark("tail+cook");
     }
     e = hipEventRecord(E->P->done, s);
     if (e != hipSuccess) return fail(RSMI_ERR_HIP, std::string("fenc event: ") + hipGetErrorString(e));
