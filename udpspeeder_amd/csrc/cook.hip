@@ -659,9 +659,17 @@ __global__ __launch_bounds__(kThreads, COOK_OCC) void k_decook(CookArgs a) {
 // the data packets are one kernel.  The <= kFuseRecs records a
 // shard overlaps are staged per packet in LDS.
 constexpr int kScrFuse = kScrCook + 8 * kFuseRecs + 4 * (kFuseRecs + 1) + 12;  // + record addr / off
-// Half rounds (48 pieces, 768 bytes per packet): a round's assembly keeps its
-// pieces' source windows in flight, twice the registers of a plain load.
-constexpr int kPplF = kPpl / 2;
+// Third rounds (32 pieces, 512 bytes per packet): a round's assembly keeps
+// its pieces' source windows in flight, twice the registers of a plain load.
+// 4 pieces per lane fit 125 VGPRs with no spill; 6 spilled 8 and measured
+// 1 % slower, 8 and 12 (fewer waves) 13 and 21 % (profiles/r04/fused_knobs).
+#ifndef COOKF_PPL
+#define COOKF_PPL (kPpl / 3)
+#endif
+#ifndef COOKF_OCC
+#define COOKF_OCC COOK_OCC
+#endif
+constexpr int kPplF = COOKF_PPL;
 constexpr int kRoundF = 16 * kLpp * kPplF;
 
 // acc = Z_{16 qr}(acc) for qr <= N kLpp pieces (shift_pieces for shorter rounds).
@@ -687,7 +695,7 @@ struct LdsRecs {
     }
 };
 
-__global__ __launch_bounds__(kThreads, COOK_OCC) void k_cook_frame(CookArgs a, FuseArgs f) {
+__global__ __launch_bounds__(kThreads, COOKF_OCC) void k_cook_frame(CookArgs a, FuseArgs f) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const bool ck = !(a.flags & RSMI_COOK_NO_CHECKSUM);
     const bool obs = !(a.flags & RSMI_COOK_NO_OBSCURE);
