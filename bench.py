@@ -567,10 +567,10 @@ def frame_cook_config(torch, dev, groups=65536, reps=4):
     return {"datagrams_in": npk, "datagram_len": plen, "groups": groups, "packets_out": nout,
             "run_ms": round(t, 4), "datagrams_in_per_s": round(npk / (t * 1e-3), 1),
             "cooked_packets_per_s": round(nout / (t * 1e-3), 1),
-            "what": "rsmi_fenc_run_cooked_dev: plan upload (groups, records, packet runs) + "
-                    "k_expand_packets + k_frame + k_bs2_20_30 + carry, k_cook of the data packets on "
-                    "a forked stream beside the encoder and of the parity packets after it; "
-                    "device-resident, key on, device-drawn IVs", "lengths_ok": ok}
+            "what": "rsmi_fenc_run_cooked_dev: plan upload (groups, packet runs; source records "
+                    "read in place) + k_expand_packets + k_cook_frame (data packets framed into "
+                    "their slots and cooked in one pass) + k_bs2_20_30 + carry + k_cook of the "
+                    "parity packets; device-resident, key on, device-drawn IVs", "lengths_ok": ok}
 
 
 def collector_config(torch, dev, ncon=200, flushes=12, seed=5):
