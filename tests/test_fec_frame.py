@@ -474,3 +474,87 @@ def test_gpu_collector_200_connections_match_reference(fx, gpu, cook, cook_oracl
     col.close()
     for e in encs:
         e.close()
+
+
+def _tiny_stream(seed, n):
+    """Mode-0 events of 0-6 bytes (and timer flushes): a 20-shard group's
+    blob then holds a few hundred records, so most shards overlap more than the
+    fused framing cook's 8 records (kFuseRecs) and are left to k_frame."""
+    rng = np.random.default_rng(seed)
+    lens = rng.integers(0, 7, n).astype(np.int32)
+    lens[rng.random(n) < 0.004] = -1
+    pay = cook_payloads(seed, 0, n, np.maximum(lens, 0), 8)
+    return lens, [None if lens[i] < 0 else pay[i, :lens[i]].tobytes() for i in range(n)]
+
+
+def test_tiny_records_leave_shards_to_k_frame():
+    """The planner's split for the fused run (no GPU): in a stream of tiny
+    records, runs frame only a prefix of their data shards in list A
+    (nfr < k) -- the case the GPU test below drives through k_frame."""
+    from udpspeeder_amd.fec import FecEncoder
+    lens, _ = _tiny_stream(77, 3000)
+    enc = FecEncoder("20:10", 0, 1250, 200, seq0=9)
+    p = enc.plan_host(lens, np.zeros(len(lens), np.uint64))
+    runs = enc.packet_runs()
+    g = p.groups
+    k_of = {int(s0): int(k) for s0, k in zip(g["slot0"], g["k"])}
+    short = [r for r in runs if int(r["nfr"]) < k_of[int(r["slot"])]]
+    assert len(short) > len(runs) // 2
+    assert all(int(r["ndata"]) <= int(r["nfr"]) for r in runs)
+    enc.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("packed", [False, True])
+def test_gpu_fused_cook_with_k_frame_leftovers(gpu, cook_oracle, packed):
+    """A fused cooked run whose groups' shards overlap more than 8 records: the
+    fused framing cook frames each group's leading shards, k_frame the rest,
+    and every cooked packet equals the oracle's do_cook of the restatement's
+    packet with the device-drawn IV, across batches cut mid-group."""
+    import torch
+    from oracle.cpu import device_ivs
+    from udpspeeder_amd.cook import CookContext
+    from udpspeeder_amd.fec import FecEncoder
+    lens, ev = _tiny_stream(77, 3000)
+    n = len(lens)
+    key = b"tiny key"
+    enc = FecEncoder("20:10", 0, 1250, 200, seq0=9)
+    em = EncodeManager("20:10", 0, 1250, 200, 9)
+    exp = []
+    for e in ev:
+        em.input(e)
+        exp += em.output()
+    ctx = CookContext(key)
+    got, ivs = [], []
+    for bi, (a, b) in enumerate(zip([0, 1234], [1234, n])):
+        offs = np.zeros(b - a, np.uint64)
+        o, chunks = 0, []
+        for i in range(a, b):
+            offs[i - a] = o
+            if ev[i] is not None:
+                chunks.append(ev[i])
+                o += len(ev[i])
+        inbuf = torch.from_numpy(np.frombuffer(b"".join(chunks) + bytes(32), np.uint8).copy()).cuda()
+        p = enc.plan(lens[a:b], offs, inbuf)
+        S = p.slot_stride_min if packed else FecEncoder.slot_stride_for(p.slot_stride_min)
+        slots = torch.full((max(1, p.n_slots) * S,), 0xEE, dtype=torch.uint8, device="cuda")
+        if packed:
+            po, ptot = enc.packed_offsets()
+            out = torch.zeros(max(ptot, 16), dtype=torch.uint8, device="cuda")
+            ol = enc.run_cooked_packed(slots, S, ctx, 50 + bi, out)
+        else:
+            out = torch.zeros(max(1, p.n_slots) * S, dtype=torch.uint8, device="cuda")
+            ol = enc.run_cooked(slots, S, ctx, 50 + bi, out=out)
+        torch.cuda.synchronize()
+        ol = ol.cpu().numpy()[:len(p.packets)]
+        h = out.cpu().numpy()
+        iv, ivl = device_ivs(50 + bi, 0, len(p.packets))
+        for i, (s, ln, _) in enumerate(p.packets):
+            assert ol[i] == ln + 4 + ivl[i] + 1, (bi, i)
+            o = int(po[i]) if packed else s * S + 120
+            got.append(h[o:o + ol[i]].tobytes())
+            ivs.append(iv[i, :ivl[i]].tobytes())
+    assert len(got) == len(exp)
+    bad = [i for i, (g_, e, v) in enumerate(zip(got, exp, ivs)) if g_ != cook_oracle.do_cook(e, v, key)]
+    assert not bad, (len(bad), bad[:5])
+    enc.close()
