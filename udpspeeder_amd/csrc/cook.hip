@@ -312,6 +312,18 @@ __device__ __forceinline__ uint32_t shift_pieces(const uint32_t *T, uint32_t acc
 
 __device__ __forceinline__ int round16(int x) { return (x + 15) & ~15; }
 
+// acc = Z_{16 qr}(acc) for qr <= N kLpp pieces (shift_pieces for shorter rounds).
+template <int N>
+__device__ __forceinline__ uint32_t shift_pieces_n(const uint32_t *T, uint32_t acc, int qr) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        const uint32_t n = zh(T, acc);
+        acc = i < qr / kLpp ? n : acc;
+    }
+    return nib_map(T + kCookLane + 128 * (qr % kLpp), acc);
+}
+
+
 __device__ __forceinline__ void load_tables(uint32_t *lds, const uint32_t *tabs, int words) {
     for (int i = threadIdx.x; i < words / 4; i += kThreads)
         reinterpret_cast<u32x4 *>(lds)[i] = reinterpret_cast<const u32x4 *>(tabs)[i];
@@ -335,12 +347,12 @@ __device__ __forceinline__ int packet_len(const CookArgs &a, int64_t pk) {
     return a.pk ? a.pk[pk].len : a.len[pk];
 }
 
-// The kPpl pieces of round r owned by lane hl: zeros past ext.
-__device__ __forceinline__ void load_round(u32x4 (&d)[kPpl], const uint8_t *pkt, int r, int hl,
-                                           int ext) {
+// The N pieces of round r (N kLpp pieces a packet) owned by lane hl: zeros past ext.
+template <int N>
+__device__ __forceinline__ void load_round(u32x4 (&d)[N], const uint8_t *pkt, int r, int hl, int ext) {
 #pragma unroll
-    for (int p = 0; p < kPpl; ++p) {
-        const int P = r * kRound + 16 * (kLpp * p + hl);
+    for (int p = 0; p < N; ++p) {
+        const int P = r * (16 * kLpp * N) + 16 * (kLpp * p + hl);
         d[p] = P < ext ? ld_piece(pkt + P) : u32x4{0, 0, 0, 0};
     }
 }
@@ -372,6 +384,13 @@ __device__ __forceinline__ u32x4 crc_in_ph(u32x4 v, int P, int n, int ph) {
     }
     return v;
 }
+
+// k_cook's round: COOK_PPL pieces per lane (kPpl: 1536 bytes per packet).
+#ifndef COOK_PPL
+#define COOK_PPL kPpl
+#endif
+constexpr int kPplC = COOK_PPL;
+constexpr int kRoundC = 16 * kLpp * kPplC;
 
 __global__ __launch_bounds__(kThreads, COOK_OCC) void k_cook(CookArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
@@ -409,8 +428,8 @@ __global__ __launch_bounds__(kThreads, COOK_OCC) void k_cook(CookArgs a) {
         uint8_t *oga = opkt - ph;
         // round 0 is read up to the packet's cap (every packet owns cap bytes), so
         // these loads fly together with the length load instead of after it
-        u32x4 cur[kPpl];
-        load_round(cur, pga, 0, hl, have && ((uintptr_t)pkt & 3) == 0 ? min((a.cap + ph) & ~15, kRound) : 0);
+        u32x4 cur[kPplC];
+        load_round(cur, pga, 0, hl, have && ((uintptr_t)pkt & 3) == 0 ? min((a.cap + ph) & ~15, kRoundC) : 0);
         if (have) {
             L = packet_len(a, pk);
             if (obs) ivl = a.iv ? a.iv_len[pk] : 4 + (int)(splitmix(a.seed, (uint64_t)gi, 0) % 29u);
@@ -440,7 +459,7 @@ __global__ __launch_bounds__(kThreads, COOK_OCC) void k_cook(CookArgs a) {
         const uint32_t sstep = ivl ? mod_ivl(16u * kLpp, (uint32_t)ivl, magic) : 0u;
         const int Q = (Lg + 15) >> 4;           // pieces holding payload (crc input)
         const int P0 = Lg & ~15;                // first piece that holds tail bytes
-        const int nrm = wave_max((ext + kRound - 1) / kRound);
+        const int nrm = wave_max((ext + kRoundC - 1) / kRoundC);
         uint32_t acc = 0;
         u32x4 dt = {0, 0, 0, 0};                // this lane's tail piece, if any
         int Pt = -1;
@@ -448,16 +467,16 @@ __global__ __launch_bounds__(kThreads, COOK_OCC) void k_cook(CookArgs a) {
             // rounds past the first (long packets); a packed output's tail may
             // end past the source slot, whose bytes there are never used
             if (r) load_round(cur, pga, r, hl, min(ext, (a.cap + ph) & ~15));
-            const int qr = min(max(Q - 96 * r, 0), 96);
+            const int qr = min(max(Q - kPplC * kLpp * r, 0), kPplC * kLpp);
             // pieces at or past every packet's last crc piece in this round:
             // skip their CRC (a wave-uniform branch per piece slot)
-            const int qr_max = COOK_SKIP ? wave_max(qr) : 96;
+            const int qr_max = COOK_SKIP ? wave_max(qr) : kPplC * kLpp;
             RoundCrc<COOK_2CH != 0> rc;
-            uint32_t ivr = ivl ? mod_ivl((uint32_t)(r * kRound + 16 * hl + 16 * ivl - ph), (uint32_t)ivl, magic)
+            uint32_t ivr = ivl ? mod_ivl((uint32_t)(r * kRoundC + 16 * hl + 16 * ivl - ph), (uint32_t)ivl, magic)
                                : 0u;
 #pragma unroll
-            for (int p = 0; p < kPpl; ++p) {
-                const int P = r * kRound + 16 * (kLpp * p + hl);  // grid offset
+            for (int p = 0; p < kPplC; ++p) {
+                const int P = r * kRoundC + 16 * (kLpp * p + hl);  // grid offset
                 if (ck && kLpp * p < qr_max) rc.add(T, crc_in_ph(cur[p], P, Lg, ph), p, kLpp * p + hl, qr);
                 // wholly payload (the head piece's bytes before the packet are scratch)
                 if (P < ext && P + 16 <= Lg) {  // obscure + xor, store now
@@ -474,7 +493,7 @@ __global__ __launch_bounds__(kThreads, COOK_OCC) void k_cook(CookArgs a) {
             }
             if (ck) {
                 const uint32_t c = rc.finish(T, qr);
-                const uint32_t nacc = (r ? shift_pieces(T, acc, qr) : 0u) ^ c;
+                const uint32_t nacc = (r ? shift_pieces_n<kPplC>(T, acc, qr) : 0u) ^ c;
                 acc = qr > 0 ? nacc : acc;
             }
         }
@@ -671,17 +690,6 @@ constexpr int kScrFuse = kScrCook + 8 * kFuseRecs + 4 * (kFuseRecs + 1) + 12;  /
 #endif
 constexpr int kPplF = COOKF_PPL;
 constexpr int kRoundF = 16 * kLpp * kPplF;
-
-// acc = Z_{16 qr}(acc) for qr <= N kLpp pieces (shift_pieces for shorter rounds).
-template <int N>
-__device__ __forceinline__ uint32_t shift_pieces_n(const uint32_t *T, uint32_t acc, int qr) {
-#pragma unroll
-    for (int i = 0; i < N; ++i) {
-        const uint32_t n = zh(T, acc);
-        acc = i < qr / kLpp ? n : acc;
-    }
-    return nib_map(T + kCookLane + 128 * (qr % kLpp), acc);
-}
 
 // A packet's staged records: blob offsets off[0..n] (off[n] = the end of the
 // last), payload addresses addr[0..n).
