@@ -991,6 +991,7 @@ struct rsmi_fcol {
         HostArr<CarryCopy> carry;
         HostArr<rsmi::ByteRun> stale, upd;
         HostArr<rsmi::PacketRun> pruns;
+        HostArr<uint32_t> recs;  // every manager's list-A records, in list-A order
         hipEvent_t done = nullptr;
         bool in_flight = false;
     } set[2];
@@ -1037,6 +1038,20 @@ int rsmi_fenc_run_many(rsmi_fcol *C, rsmi_fenc *const *enc, int32_t n, uint8_t *
         total_pk += (int64_t)E->P->packets.size();
     }
     if (total_pk > INT32_MAX) return fail(RSMI_ERR_INVALID, "rsmi_fenc_run_many: more than 2^31 packets");
+    // into another buffer, the fused framing cook as in run_dev: lists A and B
+    // of every manager back to back, when every list-A packet fits its bounds
+    int64_t total_a = 0, total_b = 0, n_left = 0;
+    int32_t max_fl = 0;
+    for (int i = 0; i < n; ++i) {
+        total_a += enc[i]->P->n_data_pk;
+        total_b += enc[i]->P->n_par_pk;
+        n_left += enc[i]->P->n_left;
+        max_fl = std::max(max_fl, enc[i]->P->max_fl);
+    }
+    const int64_t cap = S - rsmi::kSlotHeader;
+    const bool fuse = ctx && out && total_pk && total_a > 0 && fuse_enabled() && 8 + max_fl <= RSMI_COOK_MAX_LEN &&
+                      16 + ((max_fl + 15) & ~15) - 8 <= cap && ((8 + max_fl + 4 + 33 + 8 + 15) & ~15) - 8 <= cap;
+    const int64_t nlist = fuse ? total_a + total_b : total_pk;
     if (total_slots && (!slots || ((uintptr_t)slots & 15)))
         return fail(RSMI_ERR_INVALID, "slots_base must be 16-aligned");
     if (ctx && total_pk && !out_len) return fail(RSMI_ERR_INVALID, "rsmi_fenc_run_many: null out_len");
@@ -1111,6 +1126,7 @@ int rsmi_fenc_run_many(rsmi_fcol *C, rsmi_fenc *const *enc, int32_t n, uint8_t *
     }
     // ---- the combined plan, every reference rewritten
     B.jobs.clear(); B.srcs.clear(); B.carry.clear(); B.stale.clear(); B.upd.clear(); B.pruns.clear();
+    B.recs.clear();
     auto resolve = [](const rsmi_fenc *E, uint64_t a) -> uint64_t {
         return (a & kCarryTag) ? (uint64_t)(uintptr_t)(E->dcarry[(a & kCarryBuf1) ? 1 : 0]) + (a & rsmi::kCarryOff)
                                : a;
@@ -1119,7 +1135,7 @@ int rsmi_fenc_run_many(rsmi_fcol *C, rsmi_fenc *const *enc, int32_t n, uint8_t *
         return (l & rsmi::kShadowLoc) ? (rsmi::kAbsLoc | (uint64_t)(uintptr_t)E->dshadow)
                                       : (uint64_t)m[(size_t)l];
     };
-    int64_t pk_base = 0;
+    int64_t pk_base = 0, a_base = 0, b_base = 0;
     for (int i = 0; i < n; ++i) {
         rsmi_fenc *E = enc[i];
         const std::vector<int64_t> &m = smap[(size_t)i];
@@ -1163,10 +1179,16 @@ int rsmi_fenc_run_many(rsmi_fcol *C, rsmi_fenc *const *enc, int32_t n, uint8_t *
                 rsmi::PacketRun r = E->P->pruns[j];
                 r.slot = m[(size_t)r.slot];  // a run lies inside one group (or is one lone slot)
                 r.first += (int32_t)pk_base;
-                r.job += (int32_t)job_base;  // (one cook list, in packet order)
+                r.afirst += (int32_t)a_base;  // (fused: every list A, then every list B;
+                r.bfirst += (int32_t)b_base;  // else one list in packet order)
+                r.job += (int32_t)job_base;
                 B.pruns.push_back(r);
             }
+        if (fuse)  // (a record index is relative to its group's first source)
+            for (size_t j = 0; j < E->P->recs.size(); ++j) B.recs.push_back(E->P->recs[j]);
         pk_base += (int64_t)E->P->packets.size();
+        a_base += E->P->n_data_pk;
+        b_base += E->P->n_par_pk;
     }
     // ---- upload + launches
     uint32_t max_src = 0;
@@ -1175,11 +1197,13 @@ int rsmi_fenc_run_many(rsmi_fcol *C, rsmi_fenc *const *enc, int32_t n, uint8_t *
     const size_t gb = B.jobs.size() * sizeof(FrameGroup), sb = zsrc ? 0 : B.srcs.size() * sizeof(FrameSrc),
                  cb = B.carry.size() * sizeof(CarryCopy), rb = B.stale.size() * sizeof(rsmi::ByteRun),
                  ub = B.upd.size() * sizeof(rsmi::ByteRun), pb = B.pruns.size() * sizeof(rsmi::PacketRun),
-                 xb = ctx ? (size_t)total_pk * sizeof(rsmi_fenc_packet) : 0;
+                 xb = ctx ? (size_t)nlist * sizeof(rsmi_fenc_packet) : 0,
+                 jb = fuse ? (size_t)total_a * 2 * sizeof(int32_t) : 0;
     const size_t go = 0, so = (gb + 255) & ~size_t(255), co = (so + sb + 255) & ~size_t(255),
                  ro = (co + cb + 255) & ~size_t(255), uo = (ro + rb + 255) & ~size_t(255),
-                 po = (uo + ub + 255) & ~size_t(255), xo = (po + pb + 255) & ~size_t(255);
-    int rc = grow(&C->dplan[C->cur], &C->plan_cap[C->cur], xo + xb + 16, false);
+                 po = (uo + ub + 255) & ~size_t(255), xo = (po + pb + 255) & ~size_t(255),
+                 jo = (xo + xb + 255) & ~size_t(255);
+    int rc = grow(&C->dplan[C->cur], &C->plan_cap[C->cur], jo + jb + 16, false);
     if (rc) return rc;
     uint8_t *dp = C->dplan[C->cur];
     hipError_t e = hipSuccess;
@@ -1189,14 +1213,27 @@ int rsmi_fenc_run_many(rsmi_fcol *C, rsmi_fenc *const *enc, int32_t n, uint8_t *
     if (e == hipSuccess && rb) e = hipMemcpyAsync(dp + ro, B.stale.p, rb, hipMemcpyHostToDevice, s);
     if (e == hipSuccess && ub) e = hipMemcpyAsync(dp + uo, B.upd.p, ub, hipMemcpyHostToDevice, s);
     if (e == hipSuccess && pb) e = hipMemcpyAsync(dp + po, B.pruns.p, pb, hipMemcpyHostToDevice, s);
+    const uint32_t *zrec = fuse ? mapped(B.recs) : nullptr;
+    if (e == hipSuccess && fuse && !zrec)
+        e = hipMemcpyAsync(reinterpret_cast<uint32_t *>(dp + jo) + total_a, B.recs.p, (size_t)total_a * 4,
+                           hipMemcpyHostToDevice, s);
+    int32_t *job_a = fuse ? reinterpret_cast<int32_t *>(dp + jo) : nullptr;
+    rsmi_fenc_packet *lists = reinterpret_cast<rsmi_fenc_packet *>(dp + xo);
     if (e == hipSuccess)
         e = rsmi::launch_expand_packets(reinterpret_cast<const rsmi::PacketRun *>(dp + po), (int64_t)B.pruns.size(),
-                                        reinterpret_cast<rsmi_fenc_packet *>(dp + xo),
-                                        reinterpret_cast<rsmi_fenc_packet *>(dp + xo), nullptr, nullptr, s);
+                                        lists, lists + (fuse ? total_a : 0), nullptr, job_a, s,
+                                        reinterpret_cast<const FrameGroup *>(dp + go), slots, S);
     const rsmi::CarryBase none{{nullptr, nullptr}};  // every address is absolute now
-    if (e == hipSuccess)
-        e = rsmi::launch_frame(reinterpret_cast<const FrameGroup *>(dp + go), (int64_t)B.jobs.size(),
-                               zsrc ? zsrc : reinterpret_cast<const FrameSrc *>(dp + so), none, slots, S, s);
+    const FrameSrc *dsrc = zsrc ? zsrc : reinterpret_cast<const FrameSrc *>(dp + so);
+    if (e == hipSuccess && (!fuse || n_left > 0))
+        e = rsmi::launch_frame(reinterpret_cast<const FrameGroup *>(dp + go), (int64_t)B.jobs.size(), dsrc, none,
+                               slots, S, s, fuse);
+    if (e == hipSuccess && fuse) {  // list A framed and cooked in one pass (run_dev)
+        const rsmi::FuseArgs fa{reinterpret_cast<const FrameGroup *>(dp + go), dsrc, none, job_a,
+                                zrec ? zrec : reinterpret_cast<const uint32_t *>(dp + jo) + total_a};
+        rc = rsmi::cook_frame_packets(ctx, slots, S, lists, total_a, out_len, out, nullptr, seed, fa, s);
+        if (rc) return rc;
+    }
     if (e == hipSuccess)
         e = rsmi::launch_byte_runs(reinterpret_cast<const rsmi::ByteRun *>(dp + ro), (int64_t)B.stale.size(),
                                    slots, S, nullptr, s);
@@ -1213,9 +1250,9 @@ int rsmi_fenc_run_many(rsmi_fcol *C, rsmi_fenc *const *enc, int32_t n, uint8_t *
     if (e == hipSuccess)
         e = rsmi::launch_carry(reinterpret_cast<const CarryCopy *>(dp + co), (int64_t)B.carry.size(), none, s);
     if (e != hipSuccess) return fail(RSMI_ERR_HIP, std::string("fcol carry: ") + hipGetErrorString(e));
-    if (ctx && total_pk) {
-        rc = rsmi::cook_packets(ctx, slots, S, reinterpret_cast<const rsmi_fenc_packet *>(dp + xo), total_pk,
-                                out_len, out, nullptr, seed, s);
+    if (ctx && nlist > (fuse ? total_a : 0)) {
+        rc = rsmi::cook_packets(ctx, slots, S, lists + (fuse ? total_a : 0), nlist - (fuse ? total_a : 0), out_len,
+                                out, nullptr, seed, s);
         if (rc) return rc;
     }
     if (hipEventRecord(B.done, s) != hipSuccess) return fail(RSMI_ERR_HIP, "fcol: event");
