@@ -558,3 +558,56 @@ def test_gpu_fused_cook_with_k_frame_leftovers(gpu, cook_oracle, packed):
     bad = [i for i, (g_, e, v) in enumerate(zip(got, exp, ivs)) if g_ != cook_oracle.do_cook(e, v, key)]
     assert not bad, (len(bad), bad[:5])
     enc.close()
+
+
+@pytest.mark.gpu
+def test_gpu_collector_fused_with_k_frame_leftovers(gpu, cook_oracle):
+    """The collector's fused cooked flush over managers whose groups leave
+    shards to k_frame (over 8 records each): every manager's packets equal
+    the restatement's, and every cooked packet de_cooks to them."""
+    import torch
+    from udpspeeder_amd.cook import CookContext
+    from udpspeeder_amd.fec import FecCollector, FecEncoder
+    ncon, key = 8, b"tiny collector"
+    streams = [_tiny_stream(100 + i, 700 + 50 * i) for i in range(ncon)]
+    encs = [FecEncoder("20:10", 0, 1250, 200, seq0=3 + i) for i in range(ncon)]
+    exp = []
+    for i, (_, ev) in enumerate(streams):
+        em = EncodeManager("20:10", 0, 1250, 200, 3 + i)
+        pk = []
+        for e in ev:
+            em.input(e)
+            pk += em.output()
+        exp.append(pk)
+    chunks, offs_all, o = [], [], 0
+    for lens, ev in streams:
+        offs = np.zeros(len(lens), np.uint64)
+        for j, e in enumerate(ev):
+            offs[j] = o
+            if e is not None:
+                chunks.append(e)
+                o += len(e)
+        offs_all.append(offs)
+    inbuf = torch.from_numpy(np.frombuffer(b"".join(chunks) + bytes(32), np.uint8).copy()).cuda()
+    plans = [encs[i].plan(streams[i][0], offs_all[i], inbuf) for i in range(ncon)]
+    S = FecEncoder.slot_stride_for(max(p.slot_stride_min for p in plans))
+    nsl = sum(p.n_slots for p in plans)
+    slots = torch.full((max(1, nsl) * S,), 0xEE, dtype=torch.uint8, device="cuda")
+    out = torch.full_like(slots, 0x11)
+    col = FecCollector()
+    ol = col.run_many(encs, slots, S, cook=CookContext(key), seed=5, out=out)
+    torch.cuda.synchronize()
+    h, hc, olh = slots.cpu().numpy(), out.cpu().numpy(), ol.cpu().numpy()
+    q = 0
+    for i in range(ncon):
+        got = []
+        for s, l, _ in encs[i].packets_now():
+            plain = h[s * S + 120:s * S + 120 + l].tobytes()
+            got.append(plain)
+            st, back, nl = cook_oracle.de_cook(hc[s * S + 120:s * S + 120 + int(olh[q])].tobytes(), key)
+            assert st == 0 and back[:nl] == plain, (i, q)
+            q += 1
+        assert got == exp[i], i
+    col.close()
+    for e in encs:
+        e.close()
