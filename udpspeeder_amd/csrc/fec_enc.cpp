@@ -892,13 +892,14 @@ int run_dev(rsmi_fenc *E, uint8_t *slots, int64_t S, void *stream, const CookSpe
     if (rc) return rc;
     ht.mark("layout");
     hipError_t e = hipSuccess;
+    // (the large copies first, back to back on the copy engine)
     if (gb) e = hipMemcpyAsync(E->dplan + go, E->P->jobs.p, gb, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess && pb) e = hipMemcpyAsync(E->dplan + po, E->P->pruns.p, pb, hipMemcpyHostToDevice, s);
     if (e == hipSuccess && sb) e = hipMemcpyAsync(E->dplan + so, E->P->srcs.p, sb, hipMemcpyHostToDevice, s);
     if (e == hipSuccess && cb) e = hipMemcpyAsync(E->dplan + co, E->P->carry.p, cb, hipMemcpyHostToDevice, s);
     if (e == hipSuccess && rb) e = hipMemcpyAsync(E->dplan + ro, E->P->stale.p, rb, hipMemcpyHostToDevice, s);
     if (e == hipSuccess && ub)
         e = hipMemcpyAsync(E->dplan + uo, E->P->shadow_upd.p, ub, hipMemcpyHostToDevice, s);
-    if (e == hipSuccess && pb) e = hipMemcpyAsync(E->dplan + po, E->P->pruns.p, pb, hipMemcpyHostToDevice, s);
     const FrameSrc *dsrc = zsrc ? zsrc : reinterpret_cast<const FrameSrc *>(E->dplan + so);
     ht.mark("uploads");
     if (e == hipSuccess)
