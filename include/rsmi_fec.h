@@ -185,8 +185,12 @@ int rsmi_fenc_run_cooked_packed_dev(rsmi_fenc *enc, uint8_t *slots_base, int64_t
  * do_cook over all their packets.  The encoders' slots share one slot array:
  * slots_base holds sum(n_slots) slots of slot_stride bytes (slot_stride >=
  * every encoder's slot_stride_min).  Groups are laid out bucketed by code, so
- * afterwards rsmi_fenc_packets / rsmi_fenc_groups of each encoder report slots
- * of the shared array.  With ctx, out_len receives the cooked length of every
+ * afterwards rsmi_fenc_packets / rsmi_fenc_groups / rsmi_fenc_packet_runs of
+ * each encoder report slots of the shared array.  Once the slot layout is
+ * built every listed encoder's plan is consumed, also when a later step
+ * fails: re-plan before running it again (an error before that point --
+ * argument checks, a device mismatch -- leaves the plans intact).  With ctx,
+ * out_len receives the cooked length of every
  * packet, the encoders' packet lists concatenated in the order of enc[]; IVs
  * are drawn from (seed, that concatenated index).  An encoder may appear once
  * per call.  The collector keeps the combined plan's staging (two sets, so a

@@ -52,10 +52,13 @@ int rsmi_udp_recv_batch(int fd, uint8_t *slab, int64_t slot_stride, int64_t slot
  * cook rejected).  to: destination (NULL for a connected socket).  Blocks
  * until the kernel took every datagram (retrying on EAGAIN / ENOBUFS).  A
  * datagram the kernel rejects on its own (ECONNREFUSED after an ICMP
- * port-unreachable, EMSGSIZE) is dropped and the rest still go out, as the
- * reference's per-packet sendto does (packet.cpp:143-162).  Returns the number
- * sent, or RSMI_ERR_INVALID, or RSMI_ERR_IO when datagrams were to be sent and
- * none could be. */
+ * port-unreachable, EMSGSIZE, EINVAL, ...) is dropped and the rest still go
+ * out, as the reference's per-packet sendto does (packet.cpp:143-162).  A
+ * broken socket (EBADF, ENOTSOCK, EFAULT, EDESTADDRREQ, EOPNOTSUPP, EPIPE)
+ * ends the batch.  Returns the number sent (also when a broken socket ended
+ * the batch after some went out: rsmi_last_error then names the errno), or
+ * RSMI_ERR_INVALID, or RSMI_ERR_IO when datagrams were to be sent and none
+ * could be. */
 int rsmi_udp_send_batch(int fd, const uint8_t *slab, int64_t slot_stride, int64_t slot_off,
                         const int64_t *slot, const int32_t *len, int32_t n,
                         const rsmi_udp_addr *to);

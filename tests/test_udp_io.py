@@ -166,3 +166,26 @@ def test_socket_error_stops_the_batch():
         assert time.perf_counter() - t0 < 0.5
     finally:
         tx.close()
+
+
+def test_wrong_family_destination_is_per_datagram():
+    """EINVAL / EAFNOSUPPORT (an IPv6 destination on an IPv4 socket) is a
+    failure of that datagram's address, not of the socket: each datagram is
+    tried and dropped (packet.cpp:143-162 logs and carries on); with none sent
+    the call reports an I/O error naming sendmmsg."""
+    import socket
+    from udpspeeder_amd._lib import RsmiError
+    tx = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+    try:
+        src = io.Slab(8, 64)
+        import ctypes as C
+        import struct
+        to6 = io.rsmi_udp_addr()
+        raw = (struct.pack("=H", socket.AF_INET6) + struct.pack("!H", 9) + bytes(4)
+               + socket.inet_pton(socket.AF_INET6, "::1") + bytes(4))
+        C.memmove(to6.storage, raw, len(raw))
+        to6.len = len(raw)
+        with pytest.raises(RsmiError, match="sendmmsg"):
+            io.send_batch(tx, src, 0, np.full(8, 16, np.int32), to=to6)
+    finally:
+        tx.close()

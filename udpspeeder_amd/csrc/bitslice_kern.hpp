@@ -143,20 +143,27 @@ __device__ __forceinline__ DevIO bs_make_io(uint8_t *base0, int64_t group_stride
 // column}).  Lanes resolve their own group's offset and shard stride, so one
 // wave can mix groups of different lengths; the shard stride varies per lane
 // and goes into the per-lane voffset instead of soffset.
+#ifndef BS_RAG_LD_AUX
+#define BS_RAG_LD_AUX 2  // cache-policy bits of the ragged kernels' loads: nt (round 5: C3 encode
+                         // 0.167-0.169 vs 0.176-0.178 ms default; nt stores as well 0.182-0.183)
+#endif
+#ifndef BS_RAG_ST_AUX
+#define BS_RAG_ST_AUX 0  // ... and of their parity stores
+#endif
 struct RagIO {
     __amdgpu_buffer_rsrc_t rsrc;
     uint32_t o0, o1, ss0, ss1;
     __device__ __forceinline__ void load(int j, uint32_t (&p)[8]) const {
-        const bs_u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rsrc, o0 + j * ss0, 0, 0);
-        const bs_u32x4 y = __builtin_amdgcn_raw_buffer_load_b128(rsrc, o1 + j * ss1, 0, 0);
+        const bs_u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rsrc, o0 + j * ss0, 0, BS_RAG_LD_AUX);
+        const bs_u32x4 y = __builtin_amdgcn_raw_buffer_load_b128(rsrc, o1 + j * ss1, 0, BS_RAG_LD_AUX);
         p[0] = x.x; p[1] = x.y; p[2] = x.z; p[3] = x.w;
         p[4] = y.x; p[5] = y.y; p[6] = y.z; p[7] = y.w;
     }
     __device__ __forceinline__ void store(int j, const uint32_t (&q)[8]) const {
         const bs_u32x4 x = {q[0], q[1], q[2], q[3]};
         const bs_u32x4 y = {q[4], q[5], q[6], q[7]};
-        __builtin_amdgcn_raw_buffer_store_b128(x, rsrc, o0 + j * ss0, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b128(y, rsrc, o1 + j * ss1, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(x, rsrc, o0 + j * ss0, 0, BS_RAG_ST_AUX);
+        __builtin_amdgcn_raw_buffer_store_b128(y, rsrc, o1 + j * ss1, 0, BS_RAG_ST_AUX);
     }
 };
 

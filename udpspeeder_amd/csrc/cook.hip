@@ -88,15 +88,21 @@ typedef u32x4 u32x4_a4 __attribute__((aligned(4)));  // packet pieces: 4-byte al
 #ifndef COOK_NT
 #define COOK_NT 0  // 1: packet loads and stores non-temporal (read and written once)
 #endif
+#ifndef COOK_LD_NT
+#define COOK_LD_NT COOK_NT  // ... the loads alone
+#endif
+#ifndef COOK_ST_NT
+#define COOK_ST_NT COOK_NT  // ... the stores alone
+#endif
 __device__ __forceinline__ u32x4 ld_piece(const uint8_t *p) {
-#if COOK_NT
+#if COOK_LD_NT
     return __builtin_nontemporal_load(reinterpret_cast<const u32x4_a4 *>(p));
 #else
     return *reinterpret_cast<const u32x4_a4 *>(p);
 #endif
 }
 __device__ __forceinline__ void st_piece(uint8_t *p, u32x4 v) {
-#if COOK_NT
+#if COOK_ST_NT
     __builtin_nontemporal_store(v, reinterpret_cast<u32x4_a4 *>(p));
 #else
     *reinterpret_cast<u32x4_a4 *>(p) = v;
@@ -678,6 +684,8 @@ __global__ __launch_bounds__(kThreads, COOK_OCC) void k_decook(CookArgs a) {
 // the data packets are one kernel.  The <= kFuseRecs records a
 // shard overlaps are staged per packet in LDS.
 constexpr int kScrFuse = kScrCook + 8 * kFuseRecs + 4 * (kFuseRecs + 1) + 12;  // + record addr / off
+// k_cook_frame stages a shard's records one lane per record (hl < nrec)
+static_assert(kFuseRecs <= kLpp, "k_cook_frame needs a lane per source record (COOK_LPP >= kFuseRecs)");
 // Third rounds (32 pieces, 512 bytes per packet): a round's assembly keeps
 // its pieces' source windows in flight, twice the registers of a plain load.
 // 4 pieces per lane fit 125 VGPRs with no spill; 6 spilled 8 and measured

@@ -50,7 +50,20 @@ constexpr int kWaves = 4;      // waves per block (one group each)
 #define DEC_RAG_LD_AUX DEC_LD_AUX  // ... of the ragged kernels' survivor loads (TileIO)
 #endif
 #ifndef DEC_ST_AUX
-#define DEC_ST_AUX 0           // cache policy of the rebuilt-row stores
+#define DEC_ST_AUX 16          // cache policy of the uniform kernel's rebuilt-row stores: sc1
+                               // (round 5, scripts/gpu_ab_c2.sh: C2 random 0.389-0.395 vs 0.397-0.403 ms
+                               // with default stores; profiles/r05/c2_store_policy_ab)
+#endif
+#ifndef DEC_ST_AUX_BIG
+#define DEC_ST_AUX_BIG 2       // ... for a group rebuilding >= DEC_ST_BIG_E rows: nt (C2 worst case,
+                               // 5 rows per group: 0.431-0.435 vs 0.449 ms with sc1, 0.465 default)
+#endif
+#ifndef DEC_ST_BIG_E
+#define DEC_ST_BIG_E 5            // (4: C2 random 0.385-0.387 vs 0.381-0.383 ms at 5)
+#endif
+#ifndef DEC_RAG_ST_AUX
+#define DEC_RAG_ST_AUX 16      // cache policy of the ragged kernels' rebuilt-row stores: sc1 (C3 decode
+                               // 0.135-0.136 vs 0.137-0.138 ms default, 0.145-0.148 nt)
 #endif
 constexpr int kRing = DEC_RING;  // survivors in flight per wave
 constexpr int kRows = 10;      // max e handled by the one-wave kernels
@@ -96,6 +109,9 @@ constexpr int kTile = 1280;    // bytes per lane-tile pass (64 x 16 + 64 x 4)
 #endif
 #ifndef DEC_PAIR
 #define DEC_PAIR 0             // uniform kernel: fold survivors in pairs (fewer XORs, more VGPRs)
+#endif
+#ifndef DEC_ORDER
+#define DEC_ORDER 1            // ring loads issued in slot order (precise vmcnt in the survivor loop)
 #endif
 constexpr int kDefer = 0x100;  // internal status: left for k_decode_ragged_big
 #ifndef DEC_TRACE
@@ -374,15 +390,15 @@ struct TileIO {
     // offsets in the VGPR, soffset 0 (see bitslice_kern.hpp DevIO::store)
     __device__ __forceinline__ void store(__amdgpu_buffer_rsrc_t r, uint32_t so, const uint32_t (&y)[W]) const {
         if constexpr (W == 1) {
-            __builtin_amdgcn_raw_buffer_store_b32(y[0], r, v16 + so, 0, DEC_ST_AUX);
+            __builtin_amdgcn_raw_buffer_store_b32(y[0], r, v16 + so, 0, DEC_RAG_ST_AUX);
         } else if constexpr (W == 2) {
             typedef uint32_t u2 __attribute__((ext_vector_type(2)));
             const u2 v = {y[0], y[1]};
-            __builtin_amdgcn_raw_buffer_store_b64(v, r, v16 + so, 0, DEC_ST_AUX);
+            __builtin_amdgcn_raw_buffer_store_b64(v, r, v16 + so, 0, DEC_RAG_ST_AUX);
         } else {
             const u32x4 v = {y[0], y[1], y[2], y[3]};
-            __builtin_amdgcn_raw_buffer_store_b128(v, r, v16 + so, 0, DEC_ST_AUX);
-            if constexpr (W == 5) __builtin_amdgcn_raw_buffer_store_b32(y[4], r, v4 + so, 0, DEC_ST_AUX);
+            __builtin_amdgcn_raw_buffer_store_b128(v, r, v16 + so, 0, DEC_RAG_ST_AUX);
+            if constexpr (W == 5) __builtin_amdgcn_raw_buffer_store_b32(y[4], r, v4 + so, 0, DEC_RAG_ST_AUX);
         }
     }
 };
@@ -505,7 +521,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t group_rsrc(const uint8_t *gbas
 // DEC_LD_AUX / DEC_ST_AUX for HBM; sc0|sc1 (system scope, coherent with the
 // host) when the shards are pinned host memory read over PCIe
 // (rsmi_decode_pinned's zero-copy path).
-template <int LDAUX, int STAUX>
+template <int LDAUX, int STAUX, int STBIG>
 __global__ __launch_bounds__(256, DEC_OCC) void k_decode_fused(UniformArgs a, const uint8_t *present,
                                                       const uint8_t *prows, int32_t *status_out,
                                                       const uint32_t *ptab, const uint8_t *gftab) {
@@ -616,6 +632,14 @@ __global__ __launch_bounds__(256, DEC_OCC) void k_decode_fused(UniformArgs a, co
                 const __amdgpu_buffer_rsrc_t r = DEC_NOMEM ? rsrc0 : (ok ? rsrc : rnull);
                 rq[q] = __builtin_amdgcn_raw_buffer_load_b128(r, v16, DEC_NOMEM ? 0u : so, LDAUX);
                 rd[q] = __builtin_amdgcn_raw_buffer_load_b32(r, v4, DEC_NOMEM ? 0u : so, LDAUX);
+#if DEC_ORDER
+                // issue the ring in slot order: the survivor loop refills
+                // slot 0 first, and the waitcnt pass merges this entry state
+                // with the loop's own; slots issued here in another order make
+                // that merge pessimistic (vmcnt(0) at the top of every ring
+                // cycle, so only one survivor's compute hides each load)
+                __builtin_amdgcn_sched_barrier(0);
+#endif
             }
         };
         start_tile(0);  // the first survivors fly while the matrix is inverted
@@ -731,20 +755,29 @@ __global__ __launch_bounds__(256, DEC_OCC) void k_decode_fused(UniformArgs a, co
                         }
                     }
                 }
+                // the store policy by the group's write share: a group that
+                // rebuilds many rows streams them past the caches (STBIG)
+                auto store_rows = [&](auto aux) {
+                    constexpr int AUX = decltype(aux)::value;
 #pragma unroll
-                for (int r = 0; r < kFPass; ++r) {
-                    if (rb + r < e) {
-                        const uint32_t so = __builtin_amdgcn_readlane(mo_lane, rb + r);
-                        const u32x4 v = {acc[r][0], acc[r][1], acc[r][2], acc[r][3]};
+                    for (int r = 0; r < kFPass; ++r) {
+                        if (rb + r < e) {
+                            const uint32_t so = __builtin_amdgcn_readlane(mo_lane, rb + r);
+                            const u32x4 v = {acc[r][0], acc[r][1], acc[r][2], acc[r][3]};
 #if DEC_ST_SGPR
-                        __builtin_amdgcn_raw_buffer_store_b128(v, rsrc, v16, so, STAUX);
-                        __builtin_amdgcn_raw_buffer_store_b32(acc[r][4], rsrc, v4, so, STAUX);
+                            __builtin_amdgcn_raw_buffer_store_b128(v, rsrc, v16, so, AUX);
+                            __builtin_amdgcn_raw_buffer_store_b32(acc[r][4], rsrc, v4, so, AUX);
 #else
-                        __builtin_amdgcn_raw_buffer_store_b128(v, rsrc, v16 + so, 0, STAUX);
-                        __builtin_amdgcn_raw_buffer_store_b32(acc[r][4], rsrc, v4 + so, 0, STAUX);
+                            __builtin_amdgcn_raw_buffer_store_b128(v, rsrc, v16 + so, 0, AUX);
+                            __builtin_amdgcn_raw_buffer_store_b32(acc[r][4], rsrc, v4 + so, 0, AUX);
 #endif
+                        }
                     }
-                }
+                };
+                if (STAUX != STBIG && e >= DEC_ST_BIG_E)
+                    store_rows(std::integral_constant<int, STBIG>{});
+                else
+                    store_rows(std::integral_constant<int, STAUX>{});
             }
         }
         if (lane == 0 && status_out) status_out[g] = RSMI_DEC_OK;
@@ -1244,10 +1277,10 @@ hipError_t launch_decode_fused(const UniformArgs &a, const uint8_t *present,
     if (blocks > cap) blocks = cap;
     if (blocks < 1) blocks = 1;
     if (host_shards)
-        k_decode_fused<3, 3><<<(unsigned)blocks, 64 * kWaves, lds, s>>>(a, present, parity_rows,
+        k_decode_fused<3, 3, 3><<<(unsigned)blocks, 64 * kWaves, lds, s>>>(a, present, parity_rows,
                                                                       status, ptab, gftab);
     else
-        k_decode_fused<DEC_LD_AUX, DEC_ST_AUX><<<(unsigned)blocks, 64 * kWaves, lds, s>>>(
+        k_decode_fused<DEC_LD_AUX, DEC_ST_AUX, DEC_ST_AUX_BIG><<<(unsigned)blocks, 64 * kWaves, lds, s>>>(
             a, present, parity_rows, status, ptab, gftab);
     return hipGetLastError();
 }

@@ -1101,6 +1101,17 @@ int rsmi_fenc_run_many(rsmi_fcol *C, rsmi_fenc *const *enc, int32_t n, uint8_t *
             next += kv.second.count * kv.second.nn;
         }
     }
+    // From here on the plans' slot references are rewritten in place, so no
+    // encoder may keep its plan past this call, whatever happens below: a
+    // retried run_many (or a run_dev of one of them) would index its own
+    // slot arrays with shared-array slots.  Success clears `planned` anyway.
+    struct Consume {
+        rsmi_fenc *const *enc;
+        int n;
+        ~Consume() {
+            for (int i = 0; i < n; ++i) enc[i]->planned = false;
+        }
+    } consume{enc, n};
     std::vector<std::vector<int64_t>> smap((size_t)n);
     {
         std::map<int, int64_t> fill;
@@ -1175,10 +1186,11 @@ int rsmi_fenc_run_many(rsmi_fcol *C, rsmi_fenc *const *enc, int32_t n, uint8_t *
             rsmi_fenc_packet &p = E->P->packets[j];
             p.slot = m[(size_t)p.slot];  // rsmi_fenc_packets reports the shared array
         }
+        for (size_t j = 0; j < E->P->pruns.size(); ++j)  // rsmi_fenc_packet_runs: shared slots too
+            E->P->pruns[j].slot = m[(size_t)E->P->pruns[j].slot];  // (a run lies inside one group)
         if (ctx)
             for (size_t j = 0; j < E->P->pruns.size(); ++j) {
                 rsmi::PacketRun r = E->P->pruns[j];
-                r.slot = m[(size_t)r.slot];  // a run lies inside one group (or is one lone slot)
                 r.first += (int32_t)pk_base;
                 r.afirst += (int32_t)a_base;  // (fused: every list A, then every list B;
                 r.bfirst += (int32_t)b_base;  // else one list in packet order)

@@ -34,9 +34,15 @@ int io_fail(const char *what) { return fail(RSMI_ERR_IO, std::string(what) + ": 
 
 // sendmmsg errors that belong to one datagram (its destination or its size),
 // after which the next datagram may still go out
-bool per_datagram_error(int en) {
-    return en == ECONNREFUSED || en == EMSGSIZE || en == EHOSTUNREACH || en == ENETUNREACH ||
-           en == EPERM || en == EACCES || en == EHOSTDOWN || en == ENETDOWN;
+// errnos that say the socket itself is unusable: every later datagram would
+// fail the same way.  Anything else (ECONNREFUSED after an ICMP
+// port-unreachable, EMSGSIZE, an unreachable or filtered destination, EINVAL
+// or EAFNOSUPPORT for one bad address, ...) is taken as that datagram's own
+// failure, as the reference's per-packet sendto / send treats every error
+// (packet.cpp:143-162 logs and carries on).
+bool socket_error(int en) {
+    return en == EBADF || en == ENOTSOCK || en == EFAULT || en == EDESTADDRREQ || en == EOPNOTSUPP ||
+           en == EPIPE;
 }
 
 }  // namespace
@@ -171,17 +177,15 @@ int send_all(int fd, int32_t n, const int32_t *len, Addr addr, const rsmi_udp_ad
                     (void)poll(&p, 1, 10);
                     continue;
                 }
-                // msgs[done] failed on its own (ECONNREFUSED after an ICMP
-                // port-unreachable, EMSGSIZE, an unreachable or filtered
-                // destination): drop that one datagram and go on, as the
-                // reference's per-packet sendto/send does (packet.cpp:143-162
-                // logs and carries on).  Anything else is the socket's own
-                // failure (EBADF, ENOTSOCK, EFAULT, EDESTADDRREQ, EPIPE, ...):
-                // every later datagram would fail the same way, so stop now.
+                // msgs[done] failed on its own: drop that one datagram and go
+                // on.  A broken socket stops the batch; what went out before
+                // it is still reported (the error text is kept for
+                // rsmi_last_error).
                 const int en = errno;
-                if (!per_datagram_error(en)) {
+                if (socket_error(en)) {
                     errno = en;
-                    return io_fail("sendmmsg");
+                    const int rc = io_fail("sendmmsg");
+                    return sent > 0 ? sent : rc;
                 }
                 if (!failed) err = en;
                 ++failed;

@@ -118,6 +118,7 @@ class FecEncoder:
         self._keep = (in_buf, (self._keep or (None,))[0])
         self._last_packets = packets
         self._last_nslots = ns.value
+        self._last_smin = smin.value
         return FencPlan(ns.value, smin.value, ret, packets, g)
 
     def _check_slots(self, buf, slot_stride: int, what: str):
@@ -390,12 +391,23 @@ class FecCollector:
         s = stream if stream is not None else torch.cuda.current_stream()
         n_slots = sum(e._last_nslots for e in encoders)
         n_pk = sum(len(e._last_packets) for e in encoders)
+        smin = max((getattr(e, "_last_smin", 0) for e in encoders), default=0)
+        if int(slot_stride) % 16 or int(slot_stride) < smin:
+            raise ValueError(f"slot_stride must be a multiple of 16 >= every encoder's slot_stride_min ({smin})")
         if slots.numel() < n_slots * int(slot_stride):
             raise ValueError(f"slots holds {slots.numel()} bytes; the encoders need {n_slots * slot_stride}")
         if cook is not None and out_len is None:
             out_len = torch.empty(max(n_pk, 1), dtype=torch.int32, device="cuda")
-        if out is not None and out.numel() < n_slots * int(slot_stride):
-            raise ValueError("out is shorter than the shared slot array")
+        elif out_len is not None and (out_len.dtype != torch.int32 or not out_len.is_cuda
+                                      or out_len.numel() < n_pk):
+            # the cook writes out_len[i] for the whole concatenated packet list
+            raise ValueError(f"out_len must be an int32 CUDA tensor of >= {n_pk} entries "
+                             "(one per planned packet of every encoder)")
+        if out is not None:
+            if out.dtype != torch.uint8 or not (out.is_cuda or out.is_pinned()) or out.data_ptr() % 16:
+                raise TypeError("out must be a 16-aligned CUDA or pinned uint8 tensor")
+            if out.numel() < n_slots * int(slot_stride):
+                raise ValueError("out is shorter than the shared slot array")
         arr = (C.c_void_p * max(1, len(encoders)))(*[e._h.value for e in encoders])
         check(lib().rsmi_fenc_run_many(self._h, arr, len(encoders),
                                        slots.data_ptr() if slots.numel() else None, int(slot_stride),
