@@ -451,6 +451,9 @@ def test_gpu_collector_200_connections_match_reference(fx, gpu, cook, cook_oracl
         h = slots.cpu().numpy()
         hc = out.cpu().numpy() if cook else None
         olh = ol.cpu().numpy() if cook else None
+        if cook:  # the collector draws IVs by the concatenated packet index
+            from oracle.cpu import device_ivs
+            ivs, ivls = device_ivs(77 + bi, 0, sum(len(e.packets_now()) for e in encs))
         q = 0
         for ci, c in enumerate(cases):
             pk = encs[ci].packets_now()
@@ -462,6 +465,9 @@ def test_gpu_collector_200_connections_match_reference(fx, gpu, cook, cook_oracl
                     cl = int(olh[q])
                     assert cl > l
                     ck = hc[s * S + 120:s * S + 120 + cl].tobytes()
+                    # byte for byte the oracle's do_cook with this packet's IV
+                    # (a wrong or repeated IV index fails here, not in de_cook)
+                    assert ck == cook_oracle.do_cook(plain, ivs[q, :ivls[q]].tobytes(), b"collector-key"), (ci, q)
                     st, back, nl = cook_oracle.de_cook(ck, b"collector-key")
                     assert st == 0 and back[:nl] == plain, (ci, q)
                 q += 1
@@ -598,15 +604,81 @@ def test_gpu_collector_fused_with_k_frame_leftovers(gpu, cook_oracle):
     ol = col.run_many(encs, slots, S, cook=CookContext(key), seed=5, out=out)
     torch.cuda.synchronize()
     h, hc, olh = slots.cpu().numpy(), out.cpu().numpy(), ol.cpu().numpy()
+    from oracle.cpu import device_ivs
+    ivs, ivls = device_ivs(5, 0, sum(len(e.packets_now()) for e in encs))
     q = 0
     for i in range(ncon):
         got = []
         for s, l, _ in encs[i].packets_now():
             plain = h[s * S + 120:s * S + 120 + l].tobytes()
             got.append(plain)
-            st, back, nl = cook_oracle.de_cook(hc[s * S + 120:s * S + 120 + int(olh[q])].tobytes(), key)
+            ck = hc[s * S + 120:s * S + 120 + int(olh[q])].tobytes()
+            assert ck == cook_oracle.do_cook(plain, ivs[q, :ivls[q]].tobytes(), key), (i, q)
+            st, back, nl = cook_oracle.de_cook(ck, key)
             assert st == 0 and back[:nl] == plain, (i, q)
             q += 1
+        assert got == exp[i], i
+    col.close()
+    for e in encs:
+        e.close()
+
+
+@pytest.mark.gpu
+def test_gpu_collector_failure_after_remap_consumes_plans(gpu, monkeypatch):
+    """rsmi_fenc_run_many rewrites the plans' slot references to the shared
+    array before its uploads and launches; a failure after that point (here
+    the RSMI_DEBUG_FCOL_FAIL hook) leaves no encoder planned, so a retry is a
+    clean "encoder without a plan" error, not an out-of-bounds write.  After
+    re-planning, the same encoders run and produce the reference's packets."""
+    import torch
+    from udpspeeder_amd._lib import RsmiError
+    from udpspeeder_amd.fec import FecCollector, FecEncoder
+    streams = [_tiny_stream(300 + i, 400) for i in range(3)]
+    encs = [FecEncoder("20:10", 0, 1250, 200, seq0=11 + i) for i in range(3)]
+    exp = []
+    for i, (_, ev) in enumerate(streams):
+        em = EncodeManager("20:10", 0, 1250, 200, 11 + i)
+        pk = []
+        for e in ev:
+            em.input(e)
+            pk += em.output()
+        exp.append(pk)
+    chunks, offs_all, o = [], [], 0
+    for lens, ev in streams:
+        offs = np.zeros(len(lens), np.uint64)
+        for j, e in enumerate(ev):
+            offs[j] = o
+            if e is not None:
+                chunks.append(e)
+                o += len(e)
+        offs_all.append(offs)
+    inbuf = torch.from_numpy(np.frombuffer(b"".join(chunks) + bytes(32), np.uint8).copy()).cuda()
+    col = FecCollector()
+
+    def plan_all():
+        ps = [encs[i].plan(streams[i][0], offs_all[i], inbuf) for i in range(3)]
+        S = FecEncoder.slot_stride_for(max(p.slot_stride_min for p in ps))
+        return S, torch.full((max(1, sum(p.n_slots for p in ps)) * S,), 0xEE, dtype=torch.uint8,
+                             device="cuda")
+
+    S, slots = plan_all()
+    monkeypatch.setenv("RSMI_DEBUG_FCOL_FAIL", "1")
+    with pytest.raises(RsmiError, match="injected"):
+        col.run_many(encs, slots, S)
+    monkeypatch.delenv("RSMI_DEBUG_FCOL_FAIL")
+    with pytest.raises(RsmiError, match="without a plan"):
+        col.run_many(encs, slots, S)
+    # the encoders' framing state is untouched by the failed runs: start the
+    # streams again on fresh encoders of the same configuration
+    for e in encs:
+        e.close()
+    encs[:] = [FecEncoder("20:10", 0, 1250, 200, seq0=11 + i) for i in range(3)]
+    S, slots = plan_all()
+    col.run_many(encs, slots, S)
+    torch.cuda.synchronize()
+    h = slots.cpu().numpy()
+    for i in range(3):
+        got = [h[s * S + 120:s * S + 120 + l].tobytes() for s, l, _ in encs[i].packets_now()]
         assert got == exp[i], i
     col.close()
     for e in encs:

@@ -1136,6 +1136,8 @@ int rsmi_fenc_run_many(rsmi_fcol *C, rsmi_fenc *const *enc, int32_t n, uint8_t *
                 if (m[(size_t)sl] < 0) m[(size_t)sl] = lone++;  // mode-1 packets sent ahead of a group
         }
     }
+    // test hook: a failure after the remap (tests/test_fec_frame.py re-plans after it)
+    if (std::getenv("RSMI_DEBUG_FCOL_FAIL")) return fail(RSMI_ERR_INVALID, "rsmi_fenc_run_many: injected failure");
     // ---- the combined plan, every reference rewritten
     B.jobs.clear(); B.srcs.clear(); B.carry.clear(); B.stale.clear(); B.upd.clear(); B.pruns.clear();
     B.recs.clear();
