@@ -273,10 +273,38 @@ int rsmi_decode_pinned(int k, int n, uint8_t *host_shards, int64_t shards_gs,
                        int64_t shard_stride, int len, int64_t ngroups,
                        const uint8_t *present, int32_t *status, int64_t chunk_groups);
 
-/* Which path this thread's last rsmi_decode_pinned took. */
+/* Which path this thread's last rsmi_decode_pinned took (with several
+ * devices: the OR of the paths the ranges took). */
 #define RSMI_PINNED_ZERO_COPY 1
 #define RSMI_PINNED_STAGED 2
 int rsmi_last_decode_pinned_path(void);
+
+/* ---- several GPUs behind the host-memory batch entry points --
+ *
+ * UDPspeeder serves up to max_conn_num = 200 connections from one libev
+ * thread (common.h:112, tunnel_server.cpp:159-196), one FEC manager pair each
+ * (connection.h:244-245).  FEC groups are independent, so a host batch splits
+ * into contiguous group ranges, one per listed device, with no exchange
+ * between them.  After rsmi_set_devices(devs, n) (n >= 1; a device may be
+ * listed more than once), rsmi_encode_pinned and rsmi_decode_pinned run range
+ * i = [G*i/n, G*(i+1)/n) on devs[i], each on its own host thread with its own
+ * HIP streams and pipeline buffers; results land in that range's part of the
+ * caller's host arrays, and the call returns when every range is done (the
+ * first failing range's error is reported, prefixed with its device).  One
+ * such call runs at a time.  n = 0 restores the default: the calling thread's
+ * current device.  rsmi_get_devices returns the list's length and copies up
+ * to cap entries into out (may be NULL).
+ *
+ * For the device-resident collectors (rsmi_fenc_run_many / rsmi_fdec_run_many)
+ * the unit of sharding is the connection: keep one collector per device and
+ * give each the managers of a contiguous range of connections;
+ * rsmi_split_ranges computes such ranges.  bounds[0..parts] receives the cuts
+ * of n items into `parts` contiguous ranges: near-equal counts (cost NULL), or
+ * near-equal summed cost (the cut before part i is the first item whose prefix
+ * sum reaches i/parts of the total), as udpspeeder_amd.shard.balanced_ranges. */
+int rsmi_set_devices(const int32_t *devices, int32_t n);
+int rsmi_get_devices(int32_t *out, int32_t cap);
+int rsmi_split_ranges(int64_t n, const int64_t *cost, int32_t parts, int64_t *bounds);
 
 /* ---- synthetic inputs (bench / tests) ----------------------------------- */
 

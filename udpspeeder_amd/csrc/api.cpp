@@ -7,13 +7,16 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <map>
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "gf256.hpp"
@@ -600,18 +603,23 @@ int host_op(bool decode, int k, int n, uint8_t *base, int64_t gs, int64_t ss, in
 }
 
 // ---- pipelined host <-> device encode / decode (rsmi_*_pinned) ------------
-int encode_pinned(int k, int n, const uint8_t *hd, int64_t dgs, uint8_t *hp, int64_t pgs,
-                  int64_t ss, int len, int64_t ngroups, int64_t chunk) {
+int check_encode_pinned(int k, int n, const uint8_t *hd, int64_t dgs, uint8_t *hp, int64_t pgs,
+                        int64_t ss, int len, int64_t ngroups, int64_t chunk) {
     int rc = check_uniform(k, n, nullptr, 16, ss, len, 0);
     if (rc) return rc;
     if (ngroups < 0 || chunk < 1 || (ngroups && (!hd || (!hp && n > k))) || dgs < k * ss ||
         (n > k && pgs < (n - k) * ss))
         return fail(RSMI_ERR_INVALID, "invalid encode_pinned arguments");
-    if (ngroups == 0 || n == k || len == 0) return RSMI_OK;
-    Device *D = current(&rc);
-    if (!D) return rc;
-    Pipeline &P = D->penc;  // this device's encode pipeline, one call at a time
-    std::lock_guard<std::mutex> lk(P.mu);
+    return RSMI_OK;
+}
+
+// The pipeline on the calling thread's current device (D), with pipeline P:
+// the device's own, or a multi-device worker's (rsmi_set_devices).
+int encode_pinned_on(Device &D, Pipeline &P, int k, int n, const uint8_t *hd, int64_t dgs, uint8_t *hp,
+                     int64_t pgs, int64_t ss, int len, int64_t ngroups, int64_t chunk) {
+    int rc;
+    (void)D;
+    std::lock_guard<std::mutex> lk(P.mu);  // one call at a time per pipeline
     const int64_t dgs_dev = (int64_t)n * ss;
     const size_t need = (size_t)(dgs_dev * chunk);
     if (P.bytes < need) {
@@ -645,10 +653,9 @@ int encode_pinned(int k, int n, const uint8_t *hd, int64_t dgs, uint8_t *hp, int
     return RSMI_OK;
 }
 
-int decode_zero_copy(Device &D, int k, int n, uint8_t *hs_dev, int64_t hgs, int64_t ss, int len,
+int decode_zero_copy(Device &D, Pipeline &P, int k, int n, uint8_t *hs_dev, int64_t hgs, int64_t ss, int len,
                      int64_t ngroups, const uint8_t *present, int32_t *status) {
-    Pipeline &P = D.pzc;  // one call at a time per device
-    std::lock_guard<std::mutex> lk(P.mu);
+    std::lock_guard<std::mutex> lk(P.mu);  // one call at a time per pipeline
     const Code *C;
     int rc;
     {
@@ -762,15 +769,20 @@ uint8_t *mapped_host_range(uint8_t *p, size_t bytes) {
 
 thread_local int g_last_pinned = 0;  // rsmi_last_decode_pinned_path
 
-int decode_pinned(int k, int n, uint8_t *hs, int64_t hgs, int64_t ss, int len, int64_t ngroups,
-                  const uint8_t *present, int32_t *status, int64_t chunk) {
+int check_decode_pinned(int k, int n, uint8_t *hs, int64_t hgs, int64_t ss, int len, int64_t ngroups,
+                        const uint8_t *present, int64_t chunk) {
     int rc = check_uniform(k, n, nullptr, 16, ss, len, 0);
     if (rc) return rc;
     if (ngroups < 0 || chunk < 1 || (ngroups && (!hs || !present)) || hgs < n * ss)
         return fail(RSMI_ERR_INVALID, "invalid decode_pinned arguments");
-    if (ngroups == 0) return RSMI_OK;
-    Device *D = current(&rc);
-    if (!D) return rc;
+    return RSMI_OK;
+}
+
+int decode_pinned_on(Device &Dref, Pipeline &pdec, Pipeline &pzc, int k, int n, uint8_t *hs, int64_t hgs,
+                     int64_t ss, int len, int64_t ngroups, const uint8_t *present, int32_t *status,
+                     int64_t chunk) {
+    int rc;
+    Device *D = &Dref;
     // Zero-copy: shards in pinned host memory are read by the fused decode
     // kernel itself over PCIe -- only the k survivors it selects (lib/rs.cpp:
     // 24-39) -- and it writes only the rebuilt rows back; nothing is staged.
@@ -779,9 +791,9 @@ int decode_pinned(int k, int n, uint8_t *hs, int64_t hgs, int64_t ss, int len, i
         (uintptr_t)hs % 16 == 0)
         hs_dev = mapped_host_range(hs, (size_t)((ngroups - 1) * hgs + (int64_t)n * ss));
     g_last_pinned = hs_dev ? RSMI_PINNED_ZERO_COPY : RSMI_PINNED_STAGED;
-    if (hs_dev) return decode_zero_copy(*D, k, n, hs_dev, hgs, ss, len, ngroups, present, status);
-    Pipeline &P = D->pdec;  // this device's decode pipeline, one call at a time
-    std::lock_guard<std::mutex> lk(P.mu);
+    if (hs_dev) return decode_zero_copy(*D, pzc, k, n, hs_dev, hgs, ss, len, ngroups, present, status);
+    Pipeline &P = pdec;
+    std::lock_guard<std::mutex> lk(P.mu);  // one call at a time per pipeline
     int32_t **dstat = P.dstat;
     uint8_t **dpres = P.dpres;
     int64_t &cap = P.cap;
@@ -848,6 +860,236 @@ int decode_pinned(int k, int n, uint8_t *hs, int64_t hgs, int64_t ss, int len, i
     return RSMI_OK;
 }
 
+// ---- several devices behind the host-memory entry points ------
+//
+// FEC groups are independent, so a host batch splits into contiguous group
+// ranges, one per listed device, with no exchange between them: each range
+// runs the single-device pipeline above on its own host thread, HIP streams
+// and (for the staged paths) device buffers, and its results land in its own
+// part of the caller's host arrays.  Every device has its own PCIe link, so
+// the end-to-end rate of the pinned paths -- PCIe-bound on one device -- adds
+// up across devices.  A device may be listed more than once (two workers,
+// two pipelines on one device: the 1-GPU test of the partition).
+struct Worker {
+    int dev = -1;
+    Pipeline penc, pdec, pzc;  // this worker's own pipelines
+    std::thread th;
+    std::mutex mu;
+    std::condition_variable cv;
+    std::function<void()> task;
+    bool quit = false, busy = false;
+};
+
+struct MultiDev {
+    std::mutex call_mu;  // one multi-device call at a time (the workers have one task slot)
+    std::mutex cfg_mu;
+    std::vector<std::unique_ptr<Worker>> workers;
+};
+
+MultiDev &multi() {
+    static MultiDev *m = new MultiDev();  // never destroyed: workers may outlive static teardown
+    return *m;
+}
+
+void free_pipeline(Pipeline &P) {
+    for (int i = 0; i < Pipeline::kDepth; ++i) {
+        if (P.st[i]) (void)hipStreamDestroy(P.st[i]);
+        if (P.dev[i]) (void)hipFree(P.dev[i]);
+        if (P.dstat[i]) (void)hipFree(P.dstat[i]);
+        if (P.dpres[i]) (void)hipFree(P.dpres[i]);
+        P.st[i] = nullptr;
+        P.dev[i] = nullptr;
+        P.dstat[i] = nullptr;
+        P.dpres[i] = nullptr;
+    }
+    if (P.hpin) (void)hipHostFree(P.hpin);
+    P.hpin = nullptr;
+    P.bytes = P.hpin_bytes = 0;
+    P.cap = 0;
+}
+
+void worker_loop(Worker *W) {
+    (void)hipSetDevice(W->dev);  // the thread's current device for everything it runs
+    for (;;) {
+        std::function<void()> t;
+        {
+            std::unique_lock<std::mutex> lk(W->mu);
+            W->cv.wait(lk, [&] { return W->quit || (W->busy && W->task); });
+            if (W->quit && !W->task) break;
+            t = std::move(W->task);
+            W->task = nullptr;
+        }
+        t();
+        {
+            std::lock_guard<std::mutex> lk(W->mu);
+            W->busy = false;
+        }
+        W->cv.notify_all();
+    }
+    free_pipeline(W->penc);
+    free_pipeline(W->pdec);
+    free_pipeline(W->pzc);
+}
+
+void stop_workers(std::vector<std::unique_ptr<Worker>> &ws) {
+    for (auto &W : ws) {
+        {
+            std::lock_guard<std::mutex> lk(W->mu);
+            W->quit = true;
+        }
+        W->cv.notify_all();
+    }
+    for (auto &W : ws)
+        if (W->th.joinable()) W->th.join();
+    ws.clear();
+}
+
+// Contiguous ranges [bounds[i], bounds[i+1]) of n items over `parts` parts:
+// near-equal counts (cost null), or near-equal summed cost -- the cut before
+// part i is the first item whose prefix sum reaches i/parts of the total
+// (shard.balanced_ranges; C3's ragged groups weigh (k+m)*len).
+void split_ranges(int64_t n, const int64_t *cost, int parts, int64_t *bounds) {
+    bounds[0] = 0;
+    bounds[parts] = n;
+    if (!cost) {
+        for (int i = 1; i < parts; ++i) bounds[i] = (int64_t)((__int128)n * i / parts);
+        return;
+    }
+    std::vector<long double> pre((size_t)n + 1, 0.0L);
+    for (int64_t g = 0; g < n; ++g) pre[(size_t)g + 1] = pre[(size_t)g] + (long double)cost[g];
+    const long double total = pre[(size_t)n];
+    for (int i = 1; i < parts; ++i) {
+        const long double target = total * i / parts;
+        bounds[i] = (int64_t)(std::lower_bound(pre.begin(), pre.end(), target) - pre.begin());
+        if (bounds[i] > n) bounds[i] = n;
+        if (bounds[i] < bounds[i - 1]) bounds[i] = bounds[i - 1];
+    }
+}
+
+// Runs fn(worker, g0, count) for every listed device's range, in parallel, and
+// returns the first failure (its message moved to the calling thread).
+int run_split(int64_t ngroups, const std::function<int(Worker &, int64_t, int64_t)> &fn) {
+    MultiDev &M = multi();
+    std::lock_guard<std::mutex> call(M.call_mu);
+    std::vector<Worker *> ws;
+    {
+        std::lock_guard<std::mutex> lk(M.cfg_mu);
+        for (auto &W : M.workers) ws.push_back(W.get());
+    }
+    const int parts = (int)ws.size();
+    std::vector<int64_t> b((size_t)parts + 1);
+    split_ranges(ngroups, nullptr, parts, b.data());
+    std::vector<int> rcs((size_t)parts, RSMI_OK);
+    std::vector<std::string> errs((size_t)parts);
+    for (int i = 0; i < parts; ++i) {
+        Worker *W = ws[(size_t)i];
+        const int64_t g0 = b[(size_t)i], cnt = b[(size_t)i + 1] - b[(size_t)i];
+        std::lock_guard<std::mutex> lk(W->mu);
+        W->task = [&, W, i, g0, cnt] {
+            rcs[(size_t)i] = cnt > 0 ? fn(*W, g0, cnt) : RSMI_OK;
+            if (rcs[(size_t)i]) errs[(size_t)i] = g_err;  // the worker thread's message
+        };
+        W->busy = true;
+        W->cv.notify_all();
+    }
+    for (Worker *W : ws) {
+        std::unique_lock<std::mutex> lk(W->mu);
+        W->cv.wait(lk, [&] { return !W->busy; });
+    }
+    for (int i = 0; i < parts; ++i)
+        if (rcs[(size_t)i]) {
+            g_err = "device " + std::to_string(ws[(size_t)i]->dev) + ": " + errs[(size_t)i];
+            return rcs[(size_t)i];
+        }
+    return RSMI_OK;
+}
+
+bool multi_active() {
+    MultiDev &M = multi();
+    std::lock_guard<std::mutex> lk(M.cfg_mu);
+    return !M.workers.empty();
+}
+
+int set_devices(const int32_t *devs, int32_t n) {
+    if (n < 0 || n > 64 || (n > 0 && !devs)) return fail(RSMI_ERR_INVALID, "rsmi_set_devices: bad arguments");
+    if (n > 0) {
+        int count = 0;
+        hipError_t e = hipGetDeviceCount(&count);
+        if (e != hipSuccess) return hip_fail(e, "hipGetDeviceCount (no usable GPU?)");
+        for (int i = 0; i < n; ++i)
+            if (devs[i] < 0 || devs[i] >= count)
+                return fail(RSMI_ERR_INVALID, "rsmi_set_devices: device " + std::to_string(devs[i]) +
+                                                  " out of range (" + std::to_string(count) + " devices)");
+    }
+    MultiDev &M = multi();
+    std::lock_guard<std::mutex> call(M.call_mu);  // no call in flight while the pool changes
+    std::vector<std::unique_ptr<Worker>> old;
+    {
+        std::lock_guard<std::mutex> lk(M.cfg_mu);
+        old.swap(M.workers);
+    }
+    stop_workers(old);
+    std::vector<std::unique_ptr<Worker>> fresh;
+    for (int i = 0; i < n; ++i) {
+        fresh.emplace_back(new Worker());
+        fresh.back()->dev = devs[i];
+        fresh.back()->th = std::thread(worker_loop, fresh.back().get());
+    }
+    std::lock_guard<std::mutex> lk(M.cfg_mu);
+    M.workers.swap(fresh);
+    return RSMI_OK;
+}
+
+int get_devices(int32_t *out, int32_t cap) {
+    MultiDev &M = multi();
+    std::lock_guard<std::mutex> lk(M.cfg_mu);
+    const int n = (int)M.workers.size();
+    for (int i = 0; i < n && i < cap && out; ++i) out[i] = M.workers[(size_t)i]->dev;
+    return n;
+}
+
+int encode_pinned(int k, int n, const uint8_t *hd, int64_t dgs, uint8_t *hp, int64_t pgs,
+                  int64_t ss, int len, int64_t ngroups, int64_t chunk) {
+    int rc = check_encode_pinned(k, n, hd, dgs, hp, pgs, ss, len, ngroups, chunk);
+    if (rc) return rc;
+    if (ngroups == 0 || n == k || len == 0) return RSMI_OK;
+    if (multi_active())
+        return run_split(ngroups, [&](Worker &W, int64_t g0, int64_t cnt) {
+            int r;
+            Device *D = current(&r);
+            if (!D) return r;
+            return encode_pinned_on(*D, W.penc, k, n, hd + g0 * dgs, dgs, hp + g0 * pgs, pgs, ss, len, cnt,
+                                    chunk);
+        });
+    Device *D = current(&rc);
+    if (!D) return rc;
+    return encode_pinned_on(*D, D->penc, k, n, hd, dgs, hp, pgs, ss, len, ngroups, chunk);
+}
+
+int decode_pinned(int k, int n, uint8_t *hs, int64_t hgs, int64_t ss, int len, int64_t ngroups,
+                  const uint8_t *present, int32_t *status, int64_t chunk) {
+    int rc = check_decode_pinned(k, n, hs, hgs, ss, len, ngroups, present, chunk);
+    if (rc) return rc;
+    if (ngroups == 0) return RSMI_OK;
+    if (multi_active()) {
+        std::atomic<int> paths{0};
+        rc = run_split(ngroups, [&](Worker &W, int64_t g0, int64_t cnt) {
+            int r;
+            Device *D = current(&r);
+            if (!D) return r;
+            r = decode_pinned_on(*D, W.pdec, W.pzc, k, n, hs + g0 * hgs, hgs, ss, len, cnt, present + g0 * n,
+                                 status ? status + g0 : nullptr, chunk);
+            paths.fetch_or(g_last_pinned);  // (the worker thread's own record)
+            return r;
+        });
+        g_last_pinned = paths.load();  // both bits when the ranges took different paths
+        return rc;
+    }
+    Device *D = current(&rc);
+    if (!D) return rc;
+    return decode_pinned_on(*D, D->pdec, D->pzc, k, n, hs, hgs, ss, len, ngroups, present, status, chunk);
+}
+
 const char *last_error() { return g_err.c_str(); }
 std::atomic<int> &opt_bitslice() { return g_opt_bitslice; }
 
@@ -910,6 +1152,19 @@ int rsmi_prepare_code(int k, int n) { return rsmi::prepare_code(k, n); }
 int rsmi_last_encoder(void) { return rsmi::g_last_enc; }
 
 int rsmi_last_decode_pinned_path(void) { return rsmi::g_last_pinned; }
+
+int rsmi_set_devices(const int32_t *devices, int32_t n) { return rsmi::set_devices(devices, n); }
+
+int rsmi_get_devices(int32_t *out, int32_t cap) { return rsmi::get_devices(out, cap); }
+
+int rsmi_split_ranges(int64_t n, const int64_t *cost, int32_t parts, int64_t *bounds) {
+    if (n < 0 || parts < 1 || !bounds) return rsmi::fail(RSMI_ERR_INVALID, "rsmi_split_ranges: bad arguments");
+    if (cost)
+        for (int64_t g = 0; g < n; ++g)
+            if (cost[g] < 0) return rsmi::fail(RSMI_ERR_INVALID, "rsmi_split_ranges: negative cost");
+    rsmi::split_ranges(n, cost, parts, bounds);
+    return RSMI_OK;
+}
 
 int rsmi_reserve(int k, int n, int64_t ngroups, void *stream) {
     return rsmi::reserve(k, n, ngroups, (hipStream_t)stream);

@@ -461,6 +461,33 @@ def decode_pinned(shards, present, k: int, n: int, length: int, chunk_groups: in
     return st
 
 
+def set_devices(devices) -> None:
+    """rsmi_set_devices: split the host-memory batch entry points
+    (encode_pinned / decode_pinned) over these devices, one contiguous group
+    range each (a device may repeat); [] restores the current device."""
+    d = np.ascontiguousarray(np.asarray(list(devices), np.int32))
+    check(lib().rsmi_set_devices(d.ctypes.data if d.size else None, int(d.size)), "rsmi_set_devices")
+
+
+def get_devices():
+    n = lib().rsmi_get_devices(None, 0)
+    out = np.zeros(max(n, 1), np.int32)
+    lib().rsmi_get_devices(out.ctypes.data, n)
+    return [int(x) for x in out[:n]]
+
+
+def split_ranges(n: int, parts: int, cost=None):
+    """rsmi_split_ranges: [(start, end)] of `parts` contiguous ranges over n
+    items -- near-equal counts, or near-equal summed cost."""
+    b = np.zeros(parts + 1, np.int64)
+    c = None if cost is None else np.ascontiguousarray(np.asarray(cost, np.int64))
+    if c is not None and c.size != n:
+        raise ValueError("cost must have n entries")
+    check(lib().rsmi_split_ranges(int(n), c.ctypes.data if c is not None and c.size else None, int(parts),
+                                  b.ctypes.data), "rsmi_split_ranges")
+    return [(int(b[i]), int(b[i + 1])) for i in range(parts)]
+
+
 def groups_to_device(groups, device="cuda"):
     """Copy a ctypes rsmi_group array to a device uint8 tensor (24 B/group)."""
     import torch
