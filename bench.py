@@ -69,6 +69,10 @@ def parse(argv=None):
     p.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL)")
     p.add_argument("--share-device", action="store_true",
                    help="map every rank to cuda:0 (rehearsing N>1 on a 1-GPU box, gloo only)")
+    p.add_argument("--workload", choices=["c1c2", "c3"], default="c1c2",
+                   help="c1c2 (default): RS(20,10) encode + decode (C1+C2 at N=1, C4 at N>1); c3: "
+                        "the ragged mode-0 mix (k 1..20, -f 1:3,2:4,10:6,20:10, len 64..1250), "
+                        "--total-groups of it split over the ranks by balanced (k+m)*len ranges")
     p.add_argument("--rehearse", action="store_true",
                    help="CPU only: run the launcher / barrier / max-over-ranks / JSON path with a "
                         "numpy stand-in step (tests; never a measurement)")
@@ -117,6 +121,9 @@ def main():
             dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
         else:
             dist.init_process_group(args.backend, rank=rank, world_size=world)
+
+    if args.workload == "c3":
+        return run_c3(args, world, rank, dev, scaling)
 
     if scaling == "weak":
         g0, g1 = shard.weak_range(rank, args.groups)
@@ -175,7 +182,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_extras:
         extras = extra_configs(u, synth, torch, dev, buf, G)
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and not args.no_cpu_baseline:  # after the timed region, every N
         cpu = cpu_baseline(buf, present, G, args.cpu_threads)
     # after the timed region (and after the lines above, which read buf's
     # parity): this rank's bytes against the reference's digests
@@ -243,6 +250,200 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def run_c3(args, world, rank, dev, scaling):
+    """--workload c3: the ragged mode-0 mix (BASELINE configs[3]) as the step.
+    The mix of --total-groups groups (strong) or --groups per rank (weak) is
+    drawn per group id (synth.ragged_mix, so every rank sees the same mix),
+    and ranks own contiguous ranges of near-equal (k+m)*len
+    (shard.balanced_ranges) -- no collective on the data path.  A step is one
+    bucketed encode launch of the rank's groups and one ragged decode of them
+    with min(5, m) erasures each.  After the timed region each rank checks its
+    slice: the parity of 256 sampled groups against the oracle, and that the
+    decode restored every erased row; rank 0 times the reference codec on a
+    bounded sample of its groups (1 thread, one rs_encode2 / rs_decode2 per
+    group, as the reference calls them)."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    import udpspeeder_amd as u
+    from udpspeeder_amd import shard, synth
+
+    table = u.rs_from_str(synth.C3_FEC)
+    ty = [y for _, y in table]
+    if scaling == "weak":
+        g0, g1 = shard.weak_range(rank, args.groups)
+        total = args.groups * world
+    else:
+        total = args.total_groups
+        ka, ma, la = synth.ragged_mix(synth.RAGGED_SEED, 0, total, ty)
+        g0, g1 = shard.balanced_ranges((ka + ma) * la, world)[rank]
+    G = g1 - g0
+    ks, ms_, ls = synth.ragged_mix(synth.RAGGED_SEED, g0, G, ty)
+    groups, nbytes = u.make_groups(ks, ks + ms_, ls)
+    base = torch.zeros(nbytes, dtype=torch.uint8, device=dev)
+    dg = u.rs.groups_to_device(groups, dev)
+    u.rs.fill_ragged(base, dg, G, synth.DATA_SEED, g0=g0)
+    for kk in sorted(set(zip(ks.tolist(), (ks + ms_).tolist()))):
+        u.prepare_code(*kk)
+    plan = u.rs.RaggedPlan(groups)
+    flags = synth.ragged_erasures(synth.ERASE_SEED, g0, ks + ms_, ms_, ERASURES)
+    bits = torch.from_numpy(synth.present_bits(flags).view(np.int32)).to(dev)
+    status = torch.empty(G, dtype=torch.int32, device=dev)
+    stream = torch.cuda.current_stream()
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+
+    def step(i=None):
+        if i is not None:
+            ev[i][0].record(stream)
+        plan.encode(base)
+        if i is not None:
+            ev[i][1].record(stream)
+        plan.decode(base, bits, status=status)
+        if i is not None:
+            ev[i][2].record(stream)
+
+    t_settle = time.perf_counter()
+    while (time.perf_counter() - t_settle) * 1e3 < args.settle_ms:
+        for _ in range(8):
+            step()
+        torch.cuda.synchronize()
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    enc_ms = statistics.mean(a.elapsed_time(b) for a, b, _ in ev)
+    dec_ms = statistics.mean(b.elapsed_time(c) for _, b, c in ev)
+    bad = int((status != 0).sum().item())
+    cpu = None
+    if rank == 0 and not args.no_cpu_baseline:
+        cpu = c3_cpu_baseline(u, base, groups, ks, ms_, ls, flags)
+    ok = None
+    if not args.no_verify:
+        ok = c3_verify(u, synth, torch, base, groups, ks, ms_, ls, g0, plan, bits, status)
+    payload = float((ks * ls).sum())
+    flag = -1.0 if ok is None else float(ok)
+    t = torch.tensor([elapsed, enc_ms, dec_ms, float(bad)] + [flag if r == rank else -1.0 for r in range(world)]
+                     + [payload if r == rank else 0.0 for r in range(world)], dtype=torch.float64,
+                     device=dev if args.backend == "nccl" else "cpu")
+    if world > 1:
+        # max over ranks for the times; per-rank slots for the flags and payloads
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed, enc_ms, dec_ms, bad = float(t[0]), float(t[1]), float(t[2]), int(t[3])
+    parity_ok = [None if float(f) < 0 else bool(f > 0.5) for f in t[4:4 + world]]
+    job_payload = float(t[4 + world:].sum())
+    e = ((flags[:, :20] == 0) & (np.arange(20)[None, :] < ks[:, None])).sum(1)
+    enc_alg = int(((ks + ms_) * ls).sum())
+    dec_alg = int((((e > 0) * ks + e) * ls).sum())
+    roof = {"encode": roofline("encode", "k_bs_ragged: C3 bucketed bit-sliced encode", enc_alg, enc_ms, -1),
+            "decode": roofline("decode", "k_decode_ragged_mix: C3 ragged decode", dec_alg, dec_ms, -1)}
+    dominant = "decode" if dec_ms >= enc_ms else "encode"
+    if rank == 0:
+        print(json.dumps({
+            "metric": METRIC, "value": round(2.0 * job_payload * args.steps / elapsed / 2**30, 2),
+            "unit": "GiB/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+            "scaling": scaling, "vs_baseline": None, "dtype": "u8",
+            "data": "synthetic: SplitMix64 payload bytes, per-group (k, m, len) draws, min(5, m) erasures",
+            "config": {"workload": f"C3: ragged mode-0 mix -f {synth.C3_FEC}, len 64..1250, {total} groups "
+                                   f"over {world} GPU(s) by balanced (k+m)*len ranges, device-resident",
+                       "groups_rank0": G, "global_groups": total,
+                       "parallelism": f"groups sharded over {world} GPU(s), no collective"},
+            "groups_per_s": round(total * args.steps / elapsed, 1),
+            "encode_ms": round(enc_ms, 4), "decode_ms": round(dec_ms, 4), "decode_failures": bad,
+            "parity_ok": parity_ok,
+            "parity_check": "per rank: parity of 256 sampled groups vs the oracle; every erased row "
+                            "restored by the decode",
+            "roofline": roof[dominant], f"roofline_{'encode' if dominant == 'decode' else 'decode'}":
+                roof["encode" if dominant == "decode" else "decode"],
+            "cpu_baseline": cpu}), flush=True)
+    plan.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def c3_verify(u, synth, torch, base, groups, ks, ms_, ls, g0, plan, bits, status):
+    """The rank's C3 slice after the timed loop: 256 sampled groups' parity
+    equal the oracle's (the C restatement of lib/rs.cpp, pinned to the
+    reference's vectors), and a decode of the slice with every erased slot
+    poisoned restores the data rows (the step decoded a codeword)."""
+    import numpy as np
+    from oracle.cpu import Oracle
+    o = Oracle()
+    host = base.cpu().numpy()
+    G = len(ks)
+    rng = np.random.default_rng(g0)
+    ok = True
+    for g in rng.choice(G, min(256, G), replace=False):
+        k, n, ln = int(ks[g]), int(ks[g] + ms_[g]), int(ls[g])
+        off, ss = int(groups[g].offset), int(groups[g].shard_stride)
+        one = np.zeros(n * ss, np.uint8)
+        one[:k * ss] = host[off:off + k * ss]
+        o.encode_batch(k, n, one, n * ss, ss, ln, 1)
+        ok &= bool((one[k * ss:].reshape(n - k, ss)[:, :ln] ==
+                    host[off + k * ss:off + n * ss].reshape(n - k, ss)[:, :ln]).all())
+    data = [host[int(groups[g].offset):int(groups[g].offset) + int(ks[g]) * int(groups[g].shard_stride)].copy()
+            for g in range(G)]
+    flags = synth.ragged_erasures(synth.ERASE_SEED, g0, ks + ms_, ms_, ERASURES)
+    for g in range(G):  # poison the erased slots
+        off, ss = int(groups[g].offset), int(groups[g].shard_stride)
+        for j in np.nonzero(flags[g, :int(ks[g] + ms_[g])] == 0)[0]:
+            host[off + j * ss:off + (j + 1) * ss] = 0xA5
+    base.copy_(torch.from_numpy(host))
+    plan.decode(base, bits, status=status)
+    torch.cuda.synchronize()
+    host = base.cpu().numpy()
+    ok &= int((status != 0).sum().item()) == 0
+    for g in range(G):
+        off, ss, k, ln = int(groups[g].offset), int(groups[g].shard_stride), int(ks[g]), int(ls[g])
+        got = host[off:off + k * ss].reshape(k, ss)[:, :ln]
+        ok &= bool((got == data[g].reshape(k, ss)[:, :ln]).all())
+        if not ok:
+            break
+    return ok
+
+
+def c3_cpu_baseline(u, base, groups, ks, ms_, ls, flags, sample=4096, reps=3):
+    """The reference codec (oracle/_ref: lib/fec.cpp + lib/rs.cpp unmodified)
+    on the first `sample` groups of this rank's C3 slice: one rs_encode2 and
+    one rs_decode2-equivalent call per group (its own k, n, len), 1 thread,
+    median of `reps`; payload GiB/s as the GPU line (k*len per operation)."""
+    import numpy as np
+    from oracle.cpu import Oracle, Reference
+    ref = Reference.available()
+    lib = Reference() if ref else Oracle()
+    host = base.cpu().numpy()
+    S = min(sample, len(ks))
+    spans = [(int(groups[g].offset), int(groups[g].shard_stride), int(ks[g]), int(ks[g] + ms_[g]), int(ls[g]))
+             for g in range(S)]
+    if ref:  # get_code is lazy and not thread-safe: build every code first (lib/rs.cpp:42-55)
+        for k, n in sorted({(k, n) for _, _, k, n, _ in spans}):
+            lib.lib.ref_prewarm(k, n)
+    tot = []
+    for _ in range(reps):
+        bufs = [host[off:off + n * ss].copy() for off, ss, k, n, ln in spans]
+        for b, (off, ss, k, n, ln) in zip(bufs, spans):
+            b[k * ss:] = 0
+        t0 = time.perf_counter()
+        for g, (b, (off, ss, k, n, ln)) in enumerate(zip(bufs, spans)):
+            lib.encode_batch(k, n, b, n * ss, ss, ln, 1)
+            lib.decode_batch(k, n, b, n * ss, ss, ln, 1, np.ascontiguousarray(flags[g, :n]).reshape(1, n))
+        tot.append(time.perf_counter() - t0)
+    pay = float(sum(k * ln for _, _, k, _, ln in spans))
+    return {"value": round(2.0 * pay / statistics.median(tot) / 2**30, 3), "unit": "GiB/s", "cores": 1,
+            "kind": "reference" if ref else "port",
+            "sample": f"first {S} groups of rank 0's C3 slice, one encode + one decode call per group "
+                      f"(Python loop over ctypes calls included), median of {reps}"}
 
 
 def verify_slice(u, synth, torch, buf, present, g0, G):

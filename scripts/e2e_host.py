@@ -11,6 +11,11 @@ import udpspeeder_amd as u
 k, n, ln, G, S = 20, 30, 1250, 65536, 1280
 m = n - k
 dev = torch.device("cuda:0")
+# E2E_DEVICES="0,0": the host entry points split over that device list
+# (rsmi_set_devices; one worker thread, streams and pipelines per entry)
+DEVS = [int(x) for x in os.environ.get("E2E_DEVICES", "").split(",") if x != ""]
+if DEVS:
+    u.rs.set_devices(DEVS)
 data = torch.empty((G, k, S), dtype=torch.uint8).pin_memory()
 par = torch.empty((G, m, S), dtype=torch.uint8).pin_memory()
 tmp = torch.empty((G, n, S), dtype=torch.uint8, device=dev)
@@ -39,6 +44,7 @@ t0 = time.perf_counter(); data.copy_(dd, non_blocking=True); torch.cuda.synchron
 d2h = data.numel() / (time.perf_counter() - t0) / 1e9
 res["raw_h2d_GBps"] = h2d
 res["raw_d2h_GBps"] = d2h
+res["devices"] = u.rs.get_devices() or "current"
 print(json.dumps(res, indent=1))
 
 # ---- end-to-end decode.  Pinned shards: zero-copy -- the fused decode kernel
