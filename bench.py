@@ -886,18 +886,28 @@ def dropin_latency(u, calls=300):
 
 
 def dropin_latency_both(u):
-    """The drop-in per-call latency through the one-kernel path (default:
-    pinned staging read over PCIe by one kernel, completion flag polled) and
-    through the staged copy path (H2D, kernel, D2H, stream sync)."""
+    """The drop-in per-call latency through the default path -- the group
+    posted to the resident one-group server (RSMI_OPT_ONE_SERVER: 16
+    workgroups polling a doorbell in pinned host memory, no launch per call),
+    which reads the pinned staging over PCIe and raises per-workgroup flags --
+    and, beside it, the same kernel launched per call and the staged copy
+    path (H2D, kernel, D2H, stream sync)."""
     L = u.lib()
     prev = L.rsmi_set_option(3, 1)
+    prev_srv = L.rsmi_set_option(5, 20000)
     try:
         one = dropin_latency(u)
+        L.rsmi_set_option(5, 0)
+        launched = dropin_latency(u)
         L.rsmi_set_option(3, 0)
         staged = dropin_latency(u)
     finally:
         L.rsmi_set_option(3, prev)
-    one["what"] += ": one kernel reads pinned staging over PCIe, flag polled (oneshot.hip)"
+        L.rsmi_set_option(5, prev_srv)
+    one["what"] += (": posted to the resident server (oneshot.hip k_one_server), which reads pinned staging "
+                    "over PCIe; per-workgroup flags polled")
+    one["launch_per_call"] = {"rs_encode2": launched["rs_encode2"], "rs_decode2": launched["rs_decode2"],
+                              "what": "the same multi-workgroup kernel launched per call (k_one_multi)"}
     one["staged_copy_path"] = {"rs_encode2": staged["rs_encode2"], "rs_decode2": staged["rs_decode2"],
                                "what": "pinned staging, H2D, kernel, D2H, stream sync"}
     return one

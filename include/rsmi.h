@@ -79,6 +79,19 @@ const char *rsmi_last_error(void);
  * records one workgroup stages at n (tests force small caps to exercise plans
  * of many workgroup rounds).  Read when a plan is created. */
 #define RSMI_OPT_CLS_REC_CAP 4
+/* RSMI_OPT_ONE_SERVER: idle timeout in microseconds of the resident
+ * one-group server (default 20000; 0 turns it off and stops a running one).
+ * With it on, a single-group host call (RSMI_OPT_ONE_GROUP) posts its group
+ * to a one-workgroup kernel that stays resident on the device between calls
+ * and polls a doorbell in pinned host memory -- no kernel launch on the
+ * per-call path (UDPspeeder calls rs_decode2 once per group, synchronously,
+ * fec_manager.cpp:632,710).  The server ends after that long without a call
+ * (or 10 s in any case) and is relaunched by the next call.  While it runs it
+ * holds one CU and its stream's hardware queue: device-wide synchronisation
+ * (hipDeviceSynchronize, torch.cuda.synchronize) waits for it to go idle,
+ * and work on a stream that shares that hardware queue waits as well -- a
+ * process that mixes drop-in calls with its own GPU work may prefer 0. */
+#define RSMI_OPT_ONE_SERVER 5
 int rsmi_set_option(int option, int value);
 
 /* Host copy of fec_new(k,n)'s n x k systematic encoding matrix (row-major),

@@ -1,0 +1,101 @@
+"""The resident one-group server (RSMI_OPT_ONE_SERVER, oneshot.hip
+k_one_server): the level-1 drop-in's single-group calls posted to a kernel
+that stays on the device and polls a doorbell, bit-exact with the oracle
+across relaunches (idle timeout, explicit stop), codes and shapes; its exit
+bound keeps device-wide synchronisation finite."""
+import time
+
+import numpy as np
+import pytest
+
+OPT_ONE_GROUP, OPT_SERVER = 3, 5
+
+
+def _roundtrip(u, oracle, rng, k, n, ln):
+    rows = rng.integers(0, 256, (n, ln), dtype=np.uint8)
+    data = [bytearray(rows[j].tobytes()) for j in range(n)]
+    u.rs_encode2(k, n, data, ln)
+    ref = np.zeros((n, ln), np.uint8)
+    ref[:k] = rows[:k]
+    oracle.encode_batch(k, n, ref.reshape(-1), 0, ln, ln, 1)
+    for j in range(n):
+        assert bytes(data[j]) == ref[j].tobytes(), ("encode", k, n, ln, j)
+    # decode a non-codeword (random parity): the survivors used are pinned
+    e = min(k, n - k, 5)
+    er = [int(x) for x in rng.choice(n, e, replace=False)]
+    present = np.ones(n, np.uint8)
+    present[er] = 0
+    buf = np.ascontiguousarray(rows.copy())
+    st_ref = oracle.decode_batch(k, n, buf.reshape(-1), 0, ln, ln, 1, present[None, :])
+    arr = [bytearray(rows[j].tobytes()) for j in range(n)]
+    ptrs = [arr[j] if present[j] else None for j in range(n)]
+    rc = u.rs_decode2(k, n, ptrs, ln)
+    assert rc == int(st_ref[0])
+    for j in range(k):
+        assert bytes(ptrs[j]) == buf[j].tobytes(), ("decode", k, n, ln, j)
+
+
+@pytest.mark.gpu
+def test_server_calls_relaunch_and_stop(gpu, oracle):
+    import torch
+    import udpspeeder_amd as u
+    L = u.lib()
+    prev1 = L.rsmi_set_option(OPT_ONE_GROUP, 1)
+    prev = L.rsmi_set_option(OPT_SERVER, 3000)  # 3 ms idle: relaunches happen below
+    try:
+        rng = np.random.default_rng(9)
+        shapes = [(20, 30, 1250), (3, 6, 3), (10, 16, 900), (1, 2, 1), (20, 30, 17)]
+        for i in range(60):  # back to back: one server takes them all
+            _roundtrip(u, oracle, rng, *shapes[i % len(shapes)])
+        for _ in range(3):  # idle past the timeout: the server ends, the next call relaunches it
+            time.sleep(0.02)
+            _roundtrip(u, oracle, rng, 20, 30, 1250)
+        # device-wide synchronisation returns once the server has gone idle
+        t0 = time.perf_counter()
+        torch.cuda.synchronize()
+        assert time.perf_counter() - t0 < 1.0
+        # switched off: a running server is stopped, calls launch per call
+        _roundtrip(u, oracle, rng, 20, 30, 1250)
+        assert L.rsmi_set_option(OPT_SERVER, 0) == 3000
+        _roundtrip(u, oracle, rng, 20, 30, 1250)
+        L.rsmi_set_option(OPT_SERVER, 3000)
+        _roundtrip(u, oracle, rng, 20, 30, 1250)
+    finally:
+        L.rsmi_set_option(OPT_SERVER, prev)
+        L.rsmi_set_option(OPT_ONE_GROUP, prev1)
+
+
+@pytest.mark.gpu
+def test_server_latency_beats_launch_per_call(gpu):
+    """The point of the server: a single-group rs_decode2 without a kernel
+    launch on its path.  Median of 200 calls each way (a loose bound -- the
+    bench reports the numbers)."""
+    import ctypes as C
+    import statistics
+    import udpspeeder_amd as u
+    L = u.lib()
+    k, n, ln = 20, 30, 1250
+    rows = np.random.default_rng(3).integers(0, 256, (n, ln), dtype=np.uint8)
+    dec = L.compat["rs_decode2"]
+    erased = {1, 4, 9, 22, 27}
+
+    def med():
+        ts = []
+        for i in range(220):
+            ptrs = (C.c_void_p * n)(*[None if j in erased else rows[j].ctypes.data for j in range(n)])
+            t0 = time.perf_counter()
+            assert dec(k, n, ptrs, ln) == 0
+            ts.append(time.perf_counter() - t0)
+        return statistics.median(ts[20:]) * 1e6
+
+    prev1 = L.rsmi_set_option(OPT_ONE_GROUP, 1)
+    prev = L.rsmi_set_option(OPT_SERVER, 20000)
+    try:
+        t_srv = med()
+        L.rsmi_set_option(OPT_SERVER, 0)
+        t_launch = med()
+    finally:
+        L.rsmi_set_option(OPT_SERVER, prev)
+        L.rsmi_set_option(OPT_ONE_GROUP, prev1)
+    print(f"rs_decode2 median: server {t_srv:.1f} us, launch per call {t_launch:.1f} us")
+    assert t_srv < t_launch

@@ -29,6 +29,7 @@ namespace {
 thread_local std::string g_err;
 thread_local int g_last_enc = RSMI_ENC_NONE;  // rsmi_last_encoder
 std::atomic<int> g_opt_oneshot{1};              // RSMI_OPT_ONE_GROUP
+std::atomic<int> g_opt_server{-1};              // RSMI_OPT_ONE_SERVER: idle us (-1: not read yet)
 std::atomic<int> g_opt_bitslice{1};
 std::atomic<int> g_opt_fused{1};
 
@@ -98,6 +99,11 @@ struct Device {
     uint8_t *one_pin = nullptr, *one_dev = nullptr;  // host / device address of the staging
     size_t one_bytes = 0;
     uint32_t one_seq = 0;
+    // the resident one-group server (oneshot.hip k_one_server), guarded by one_mu
+    OneSrvCtl *srv_pin = nullptr, *srv_dev = nullptr;
+    OneSrvDev *srv_dv = nullptr;  // device memory of the server's stop / exit words
+    uint32_t srv_gen = 0;
+    bool srv_running = false;
 };
 
 std::mutex g_devs_mu;
@@ -432,6 +438,76 @@ int host_buffers(Device &D, size_t bytes, int64_t ngroups) {
 }
 }  // namespace
 
+// ---- the resident one-group server --------------------------------------------
+int server_idle_us() {
+    int v = g_opt_server.load();
+    if (v < 0) {  // first use: RSMI_ONE_SERVER_IDLE_US overrides the default (0 = off)
+        const char *env = getenv("RSMI_ONE_SERVER_IDLE_US");
+        v = env ? std::max(0, atoi(env)) : 20000;
+        int expect = -1;
+        if (!g_opt_server.compare_exchange_strong(expect, v)) v = g_opt_server.load();
+    }
+    return v;
+}
+
+std::mutex g_srv_list_mu;
+std::vector<Device *> g_srv_devs;  // devices whose server may be running
+
+void stop_servers_at_exit() {
+    std::lock_guard<std::mutex> lk(g_srv_list_mu);
+    for (Device *D : g_srv_devs)
+        if (D->srv_pin) reinterpret_cast<volatile uint32_t *>(&D->srv_pin->quit)[0] = 1u;
+}
+
+// caller holds D.one_mu
+int launch_server(Device &D, uint32_t done0, uint32_t idle_us) {
+    if (!D.srv_pin) {
+        void *hp = nullptr, *dp = nullptr;
+        RSMI_HIP(hipHostMalloc(&hp, sizeof(OneSrvCtl), hipHostMallocDefault), "hipHostMalloc(server)");
+        RSMI_HIP(hipHostGetDevicePointer(&dp, hp, 0), "hipHostGetDevicePointer(server)");
+        std::memset(hp, 0, sizeof(OneSrvCtl));
+        RSMI_HIP(hipMalloc(&D.srv_dv, sizeof(OneSrvDev)), "hipMalloc(server)");
+        D.srv_pin = static_cast<OneSrvCtl *>(hp);
+        D.srv_dev = static_cast<OneSrvCtl *>(dp);
+        std::lock_guard<std::mutex> lk(g_srv_list_mu);
+        if (g_srv_devs.empty()) std::atexit(stop_servers_at_exit);
+        g_srv_devs.push_back(&D);
+    }
+    reinterpret_cast<volatile uint32_t *>(&D.srv_pin->quit)[0] = 0u;
+    const uint32_t gen = ++D.srv_gen;
+    hipError_t e = launch_one_server(D.srv_dev, D.srv_dv, D.ptab, D.gftab, gen, done0, idle_us, 10000u,
+                                     D.one_stream);
+    if (e != hipSuccess) return hip_fail(e, "one-group server launch");
+    D.srv_running = true;
+    return RSMI_OK;
+}
+
+// caller holds D.one_mu; the job's inputs are in staging.  Every word of the
+// job block carries the seq beside its dword of OneArgs (OneSrvCtl).
+int post_to_server(Device &D, const OneArgs &a, uint32_t idle_us) {
+    if (!D.srv_pin || !D.srv_running) {
+        int rc = launch_server(D, a.seq - 1, idle_us);
+        if (rc) return rc;
+    }
+    uint32_t w[kOneJobWords] = {};
+    static_assert(sizeof(OneArgs) <= sizeof(w), "OneArgs fits the job block");
+    std::memcpy(w, &a, sizeof(OneArgs));
+    std::atomic_thread_fence(std::memory_order_release);  // the inputs before any job word
+    volatile uint64_t *job = D.srv_pin->job;
+    for (int i = 0; i < kOneJobWords; ++i) job[i] = ((uint64_t)a.seq << 32) | w[i];
+    return RSMI_OK;
+}
+
+// Stop a running server and wait for it (RSMI_OPT_ONE_SERVER 0, tests).
+int stop_server(Device &D) {
+    std::lock_guard<std::mutex> lk(D.one_mu);
+    if (!D.srv_pin || !D.srv_running) return RSMI_OK;
+    reinterpret_cast<volatile uint32_t *>(&D.srv_pin->quit)[0] = 1u;
+    RSMI_HIP(hipStreamSynchronize(D.one_stream), "stop one-group server");
+    D.srv_running = false;
+    return RSMI_OK;
+}
+
 // One group, host buffers, one kernel (oneshot.hip): the shards the kernel
 // needs are copied into pinned staging, the kernel reads them over PCIe,
 // writes the output rows back into staging and raises a flag this thread
@@ -451,7 +527,7 @@ int one_group_op(Device &D, bool decode, int k, int n, uint8_t *const *ptrs, uin
     std::lock_guard<std::mutex> lk(D.one_mu);
     const int m = n - k;
     const size_t in_bytes = (size_t)n * ss, out_bytes = (size_t)(decode ? k : m) * ss;
-    const size_t need = in_bytes + out_bytes + 64;
+    const size_t need = in_bytes + out_bytes + 128;
     if (!D.one_stream)
         RSMI_HIP(hipStreamCreateWithFlags(&D.one_stream, hipStreamNonBlocking), "hipStreamCreate(one)");
     if (D.one_bytes < need) {
@@ -467,8 +543,22 @@ int one_group_op(Device &D, bool decode, int k, int n, uint8_t *const *ptrs, uin
         std::memset(D.one_pin, 0, cap);
     }
     uint8_t *in = D.one_pin, *rows = D.one_pin + in_bytes;
-    uint8_t *tail = D.one_pin + D.one_bytes - 64;  // status | flag
-    volatile uint32_t *flag = reinterpret_cast<volatile uint32_t *>(tail + 32);
+    uint8_t *tail = D.one_pin + D.one_bytes - 128;  // status | pad | flags[kOneSrvWgs]
+    int rows_out = m;  // encode: the parity rows; decode: the missing data rows
+    if (decode) {
+        rows_out = 0;
+        for (int j = 0; j < k; ++j) rows_out += present[j] ? 0 : 1;
+    }
+    const bool multi = one_multi_ok(k, n, len, ss > 0 ? ss : 16, rows_out);
+    const int idle_us = multi ? server_idle_us() : 0;
+    if (!multi && D.srv_running) {  // the single-workgroup kernel queues on the server's stream
+        reinterpret_cast<volatile uint32_t *>(&D.srv_pin->quit)[0] = 1u;
+        RSMI_HIP(hipStreamSynchronize(D.one_stream), "stop one-group server");
+        D.srv_running = false;
+    }
+    volatile uint32_t *flags = idle_us > 0 ? D.srv_pin ? D.srv_pin->flags : nullptr
+                                           : reinterpret_cast<volatile uint32_t *>(tail + 64);
+    const int nflags = multi ? kOneSrvWgs : 1;
     OneArgs a{};
     a.in = D.one_dev;
     a.out = D.one_dev + in_bytes;
@@ -476,7 +566,7 @@ int one_group_op(Device &D, bool decode, int k, int n, uint8_t *const *ptrs, uin
     a.ptab = D.ptab;
     a.gftab = D.gftab;
     a.status = reinterpret_cast<int32_t *>(D.one_dev + (tail - D.one_pin));
-    a.flag = reinterpret_cast<uint32_t *>(D.one_dev + (tail + 32 - D.one_pin));
+    a.flag = reinterpret_cast<uint32_t *>(D.one_dev + (tail + 64 - D.one_pin));
     a.seq = ++D.one_seq;
     a.k = k;
     a.n = n;
@@ -495,16 +585,37 @@ int one_group_op(Device &D, bool decode, int k, int n, uint8_t *const *ptrs, uin
         for (int j = 0; j < k; ++j) std::memcpy(in + (size_t)j * ss, ptrs[j], (size_t)len);
     }
     std::atomic_thread_fence(std::memory_order_release);
-    hipError_t e = launch_one_group(a, D.one_stream);
-    if (e != hipSuccess) return hip_fail(e, "one-group kernel launch");
-    // spin on the flag; a kernel that never raises it surfaces its error
-    // through the stream after a bound
+    if (idle_us > 0) {
+        rc = post_to_server(D, a, (uint32_t)idle_us);
+        if (rc) return rc;
+        flags = D.srv_pin->flags;
+    } else {
+        hipError_t e = multi ? launch_one_multi(a, D.one_stream) : launch_one_group(a, D.one_stream);
+        if (e != hipSuccess) return hip_fail(e, "one-group kernel launch");
+    }
+    // spin on the completion words (one per workgroup of the multi-workgroup
+    // kernels); a kernel that never raises them surfaces its error through the
+    // stream after a bound.  With the server: a server that ended (idle or
+    // lifetime) before it ran this job is relaunched, and the new one takes
+    // the pending job.
+    auto all_done = [&] {
+        for (int i = 0; i < nflags; ++i)
+            if (flags[i] != a.seq) return false;
+        return true;
+    };
     const auto t0 = std::chrono::steady_clock::now();
-    while (*flag != a.seq) {
+    while (!all_done()) {
         __builtin_ia32_pause();
+        if (idle_us > 0 && reinterpret_cast<volatile uint32_t *>(&D.srv_pin->exit_gen)[0] == D.srv_gen) {
+            if (all_done()) break;  // it finished this job, then went idle
+            rc = launch_server(D, a.seq - 1, (uint32_t)idle_us);
+            if (rc) return rc;
+        }
         if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) {
+            if (idle_us > 0) reinterpret_cast<volatile uint32_t *>(&D.srv_pin->quit)[0] = 1u;
             RSMI_HIP(hipStreamSynchronize(D.one_stream), "one-group kernel");
-            if (*flag != a.seq) return fail(RSMI_ERR_HIP, "one-group kernel did not complete");
+            D.srv_running = false;
+            if (!all_done()) return fail(RSMI_ERR_HIP, "one-group kernel did not complete");
         }
     }
     std::atomic_thread_fence(std::memory_order_acquire);
@@ -1107,6 +1218,29 @@ int rsmi_set_option(int option, int value) {
     if (option == RSMI_OPT_FUSED_DECODE) return rsmi::g_opt_fused.exchange(value ? 1 : 0);
     if (option == RSMI_OPT_ONE_GROUP) return rsmi::g_opt_oneshot.exchange(value ? 1 : 0);
     if (option == RSMI_OPT_CLS_REC_CAP) return rsmi::g_opt_cls_cap.exchange(value > 0 ? value : 0);
+    if (option == RSMI_OPT_ONE_SERVER) {
+        const int prev = rsmi::server_idle_us();
+        rsmi::g_opt_server.store(value > 0 ? value : 0);
+        if (value <= 0) {  // stop every running server (the next calls launch per call)
+            std::vector<rsmi::Device *> ds;
+            {
+                std::lock_guard<std::mutex> lk(rsmi::g_srv_list_mu);
+                ds = rsmi::g_srv_devs;
+            }
+            int cur = -1;
+            (void)hipGetDevice(&cur);
+            for (rsmi::Device *D : ds) {
+                (void)hipSetDevice(D->id);
+                const int rc = rsmi::stop_server(*D);
+                if (rc) {
+                    (void)hipSetDevice(cur);
+                    return rc;
+                }
+            }
+            if (cur >= 0) (void)hipSetDevice(cur);
+        }
+        return prev;
+    }
     rsmi::set_error("unknown option");
     return RSMI_ERR_INVALID;
 }
@@ -1152,6 +1286,7 @@ int rsmi_prepare_code(int k, int n) { return rsmi::prepare_code(k, n); }
 int rsmi_last_encoder(void) { return rsmi::g_last_enc; }
 
 int rsmi_last_decode_pinned_path(void) { return rsmi::g_last_pinned; }
+
 
 int rsmi_set_devices(const int32_t *devices, int32_t n) { return rsmi::set_devices(devices, n); }
 

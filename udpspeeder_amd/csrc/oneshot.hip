@@ -50,16 +50,31 @@ __device__ __forceinline__ uint32_t gmul_t(uint4 t, uint32_t t2, uint32_t x) {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-__global__ __launch_bounds__(kOneThreads) void k_one_group(OneArgs a) {
-    __shared__ uint4 s01[256];
-    __shared__ uint32_t s2[256];
-    __shared__ uint8_t lexp[512], llog[256], linv[256];
-    __shared__ uint8_t sel[256], miss[256];
-    __shared__ uint4 ct01[kCoefMax];  // coefficient (r, j)'s split table at r * k + j
-    __shared__ uint32_t ct2[kCoefMax];
-    __shared__ uint8_t aug[kAugMax];
-    __shared__ __attribute__((aligned(16))) uint8_t xs[kSurvLds];  // survivor j at j * lpad
-    __shared__ int s_e, s_st;
+#include "lagrange.hpp"
+
+// The workgroup's LDS (one group's tables, survivors and coefficients).
+struct OneSmem {
+    uint4 s01[256];
+    uint32_t s2[256];
+    uint8_t lexp[512], llog[256], linv[256];
+    uint8_t sel[256], miss[256];
+    uint4 ct01[kCoefMax];  // coefficient (r, j)'s split table at r * k + j
+    uint32_t ct2[kCoefMax];
+    uint8_t aug[kAugMax];
+    __attribute__((aligned(16))) uint8_t xs[kSurvLds];  // survivor j at j * lpad
+    int s_e, s_st;
+};
+
+// One group in one workgroup (codes and shapes the multi-workgroup form below
+// does not take).
+__device__ __forceinline__ void one_body(const OneArgs &a, OneSmem &S) {
+    uint4 *s01 = S.s01;
+    uint32_t *s2 = S.s2;
+    uint8_t *lexp = S.lexp, *llog = S.llog, *linv = S.linv, *sel = S.sel, *miss = S.miss;
+    uint4 *ct01 = S.ct01;
+    uint32_t *ct2 = S.ct2;
+    uint8_t *aug = S.aug, *xs = S.xs;
+    int &s_e = S.s_e, &s_st = S.s_st;
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int k = a.k, n = a.n, len = a.len;
@@ -275,7 +290,293 @@ __global__ __launch_bounds__(kOneThreads) void k_one_group(OneArgs a) {
     }
 }
 
+__global__ __launch_bounds__(kOneThreads) void k_one_group(OneArgs a) {
+    __shared__ OneSmem S;
+    one_body(a, S);
+}
+
+// ---- the multi-workgroup form: per-call launch or resident server --------------
+// k_one_group runs a whole group in ONE workgroup: at the clocks a nearly idle
+// GPU runs (one group per call), its serial chain -- survivors over PCIe,
+// Gauss-Jordan in one wave, a 20-survivor MAC per thread -- took ~15 us of
+// the ~19 us call (profiles/r05/dropin).  Here kOneSrvWgs workgroups split the
+// group's 16-byte pieces (columns): each one selects the survivors, computes
+// the coefficients (Lagrange form, lagrange.hpp; the code's rows for the
+// encode), loads only its pieces of the survivors, splits the MAC over its
+// four waves by survivor and stores its pieces of the output rows, then raises
+// its own completion word (flags[wg] = seq).  No workgroup waits for another.
+constexpr int kMwThreads = 256;
+constexpr int kMwCoef = 640;     // e x k coefficients (e <= 10, k <= 64)
+constexpr int kMwSurv = 16384;   // k x pieces-per-workgroup x 16 bytes
+constexpr int kMwOut = 1024;     // e x dwords-per-workgroup outputs
+
+struct MwSmem {
+    __attribute__((aligned(16))) uint8_t ltab[kLTabBytes];  // LTables image
+    uint4 s01[256];                                         // split tables by value (encode)
+    uint32_t s2[256];
+    uint4 ct01[kMwCoef];  // coefficient (r, j) at r * k + j
+    uint32_t ct2[kMwCoef];
+    __attribute__((aligned(16))) uint8_t xs[kMwSurv];  // survivor j's pieces at j * pw * 16
+    uint32_t part[4 * kMwOut];                          // per-wave partial sums
+    uint8_t sel[64], miss[16];
+    uint32_t args[32];
+    int e, st;
+    uint32_t cmd, seq;
+};
+
+__device__ __forceinline__ void mw_tables(MwSmem &S, const uint32_t *ptab, const uint8_t *gftab) {
+    const uint4 *src = reinterpret_cast<const uint4 *>(gftab + kGfLtabOff);
+    for (int i = threadIdx.x; i < kLTabBytes / 16; i += kMwThreads)
+        reinterpret_cast<uint4 *>(S.ltab)[i] = src[i];
+    for (int i = threadIdx.x; i < 256; i += kMwThreads) {
+        S.s01[i] = reinterpret_cast<const uint4 *>(ptab + i * kPtabDwords)[0];
+        S.s2[i] = ptab[i * kPtabDwords + 4];
+    }
+}
+
+// The pieces [p0, p0 + pw) of workgroup wg (of nwg) among the group's P.
+__device__ __forceinline__ void mw_span(int P, int wg, int nwg, int &p0, int &pw) {
+    const int per = (P + nwg - 1) / nwg;
+    p0 = wg * per;
+    pw = p0 >= P ? 0 : (P - p0 < per ? P - p0 : per);
+}
+
+// One workgroup's share of one group (a: the job), then flags[wg] = seq.
+__device__ __forceinline__ void mw_body(const OneArgs &a, MwSmem &S, int wg, int nwg, uint32_t *flags) {
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int k = a.k, n = a.n, len = a.len;
+    const uint32_t ss = (uint32_t)a.ss;
+    const int lpad = (len + 15) & ~15;
+    const int P = lpad >> 4;
+    int p0, pw;
+    mw_span(P, wg, nwg, p0, pw);
+    // ---- survivors (the first k present, lib/rs.cpp:24-39) or the data shards
+    if (wv == 0) {
+        const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+        int cnt = 0, e = 0;
+        if (a.encode) {
+            if (lane < k) S.sel[lane] = (uint8_t)lane;
+            cnt = k;
+            e = n - k;
+        } else {
+            for (int b = 0; b < n && cnt < k; b += 64) {
+                const int idx = b + lane;
+                const bool f = idx < n && ((a.present[idx >> 5] >> (idx & 31)) & 1u);
+                const uint64_t mk = __ballot(f);
+                const int rank = cnt + __popcll(mk & lt);
+                if (f && rank < k) S.sel[rank] = (uint8_t)idx;
+                cnt += __popcll(mk);
+            }
+            if (cnt >= k) {  // k <= 64: one window of data indices
+                const bool ms = lane < k && !((a.present[lane >> 5] >> (lane & 31)) & 1u);
+                const uint64_t mk = __ballot(ms);
+                if (ms) S.miss[__popcll(mk & lt)] = (uint8_t)lane;
+                e = __popcll(mk);
+            }
+        }
+        if (lane == 0) {
+            S.e = e;
+            S.st = cnt < k ? RSMI_DEC_TOO_FEW : RSMI_DEC_OK;
+        }
+    }
+    __syncthreads();
+    const int e = S.e;
+    const bool work = S.st == RSMI_DEC_OK && e > 0 && pw > 0;
+    if (work) {
+        // ---- this workgroup's survivor pieces, all in flight at once
+        const auto in = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(a.in), 0, (int)(n * ss), 0x00020000);
+        const int items = k * pw;  // <= kMwSurv / 16 = 1024
+        u32x4 v[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int t = tid + q * kMwThreads;
+            if (t < items) {
+                const int j = t / pw, c = t - j * pw;
+                v[q] = __builtin_amdgcn_raw_buffer_load_b128(in, (uint32_t)(p0 + c) * 16u + (uint32_t)S.sel[j] * ss,
+                                                             0u, kAux);
+            }
+        }
+        // ---- coefficients while the loads fly
+        if (a.encode) {
+            for (int t = tid; t < e * k; t += kMwThreads) {
+                const uint8_t c = a.rows[t];  // parity row r = t / k, column j = t % k
+                S.ct01[t] = S.s01[c];
+                S.ct2[t] = S.s2[c];
+            }
+        } else if (wv == 0) {
+            const LTables LT{reinterpret_cast<const uint4 *>(S.ltab), reinterpret_cast<const uint32_t *>(S.ltab + 4096),
+                             S.ltab + 5120, S.ltab + 5376};
+            const uint32_t xs = LT.px[lane < k ? S.sel[lane] : 0u];
+            const uint32_t B = lagrange_b(k, xs, LT);
+            for (int rb = 0; rb < e; rb += 5) {
+                const uint32_t xm = lane + rb < e ? (uint32_t)LT.px[S.miss[lane + rb]] : 0u;
+                lagrange_rows<5>(k, e - rb < 5 ? e - rb : 5, xs, B, xm, LT, lane, [&](int r, uint32_t lv) {
+                    S.ct01[(rb + r) * k + lane] = LT.t01[lv];
+                    S.ct2[(rb + r) * k + lane] = LT.t2[lv];
+                });
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int t = tid + q * kMwThreads;
+            if (t < items) *reinterpret_cast<u32x4 *>(S.xs + t * 16) = v[q];  // survivor j at j * pw pieces
+        }
+    }
+    __syncthreads();
+    const int D = 4 * pw;  // output dwords of each row in this workgroup
+    const int O = e * D;
+    if (work) {
+        // ---- MAC: wave wv takes survivors wv, wv + 4, ...; lane o an output (row, dword)
+        for (int o = lane; o < O; o += 64) {
+            const int r = o / D, d = o - r * D;
+            uint32_t acc = 0;
+            for (int j = wv; j < k; j += 4) {
+                const uint32_t x = *reinterpret_cast<const uint32_t *>(S.xs + (j * pw) * 16 + d * 4);
+                const uint4 t = S.ct01[r * k + j];
+                const uint32_t t2 = S.ct2[r * k + j];
+                acc ^= xor3(__builtin_amdgcn_perm(t.y, t.x, x & 0x07070707u),
+                            __builtin_amdgcn_perm(t.w, t.z, (x >> 3) & 0x07070707u),
+                            __builtin_amdgcn_perm(t2, t2, (x >> 6) & 0x03030303u));
+            }
+            S.part[wv * O + o] = acc;
+        }
+    }
+    __syncthreads();
+    if (work) {
+        const auto out = __builtin_amdgcn_make_buffer_rsrc(a.out, 0, (int)(e * ss), 0x00020000);
+        for (int o = tid; o < O; o += kMwThreads) {
+            const int r = o / D, d = o - r * D;
+            const uint32_t val = S.part[o] ^ S.part[O + o] ^ S.part[2 * O + o] ^ S.part[3 * O + o];
+            __builtin_amdgcn_raw_buffer_store_b32(val, out, (uint32_t)r * ss + (uint32_t)(p0 * 16 + d * 4), 0, kAux);
+        }
+    }
+    // ---- completion: this workgroup's rows (and the status), then its flag
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+        if (wg == 0) __hip_atomic_store(a.status, (int32_t)S.st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(flags + wg, a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+__global__ __launch_bounds__(kMwThreads) void k_one_multi(OneArgs a) {
+    __shared__ MwSmem S;
+    mw_tables(S, a.ptab, a.gftab);
+    __syncthreads();
+    mw_body(a, S, (int)blockIdx.x, (int)gridDim.x, a.flag);
+}
+
+// ---- the resident server: no launch on the per-call path -----------------------
+// kOneSrvWgs workgroups stay on the device and poll the job block in pinned
+// host memory (OneSrvCtl::job: every dword of the job's OneArgs paired with
+// the job's seq in one 8-byte word, written after the job's inputs; a wave
+// whose lanes all read the same new seq has read the whole job).  Each
+// workgroup runs its pieces of the job (mw_body) and raises flags[wg].
+// Workgroup 0 decides when the server ends -- ctl->quit from the host, no job
+// for idle_ticks of the 100 MHz s_memrealtime clock, or life_ticks in any case
+// -- and tells the others through dv->stop (device memory); the last one out
+// writes the generation to ctl->exit_gen, which tells the host to launch a new
+// server for the next job (a job that workgroups saw in part before they
+// stopped is run again whole by the next server: a job's outputs depend only
+// on its inputs).
+__device__ __forceinline__ uint32_t sys_load(const uint32_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ uint64_t sys_load64(const uint64_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ __launch_bounds__(kMwThreads) void k_one_server(OneSrvCtl *ctl, OneSrvDev *dv, const uint32_t *ptab,
+                                                           const uint8_t *gftab, uint32_t gen, uint32_t done0,
+                                                           uint64_t idle_ticks, uint64_t life_ticks) {
+    __shared__ MwSmem S;
+    static_assert(sizeof(OneArgs) <= 4 * kOneJobWords && sizeof(OneArgs) % 4 == 0, "OneArgs fits the job block");
+    const int tid = threadIdx.x, lane = tid & 63, wg = (int)blockIdx.x;
+    mw_tables(S, ptab, gftab);
+    uint32_t done = done0;
+    const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+    uint64_t t_last = t_start;
+    for (;;) {
+        if (tid < 64) {
+            uint32_t cmd = 0, seq = 0, w = 0;
+            for (;;) {
+                const uint64_t jw = lane < kOneJobWords ? sys_load64(&ctl->job[lane]) : 0ull;
+                w = (uint32_t)jw;
+                const uint32_t js = (uint32_t)(jw >> 32);
+                const uint32_t s0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)js);
+                const bool torn = __ballot(lane < kOneJobWords && js != s0) != 0;  // host mid-write
+                if (!torn && s0 != done) { cmd = 1; seq = s0; break; }
+                if (wg == 0) {
+                    const uint32_t q = sys_load(&ctl->quit);
+                    const uint64_t now = __builtin_amdgcn_s_memrealtime();
+                    if (q || now - t_last > idle_ticks || now - t_start > life_ticks) {
+                        if (lane == 0) __hip_atomic_store(&dv->stop, gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        break;
+                    }
+                } else if (__hip_atomic_load(&dv->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gen) {
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(4);
+            }
+            if (lane < kOneJobWords) S.args[lane] = w;
+            if (lane == 0) {
+                S.cmd = cmd;
+                S.seq = seq;
+            }
+        }
+        __syncthreads();
+        if (S.cmd != 1) break;
+        // system-scope acquire (buffer_inv sc0 sc1): without it, survivor loads
+        // of staging lines an earlier job read came back stale (a launched
+        // kernel gets this invalidate from its dispatch)
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+        OneArgs a;
+        {
+            uint32_t w[kOneJobWords];
+#pragma unroll
+            for (int i = 0; i < kOneJobWords; ++i) w[i] = S.args[i];
+            __builtin_memcpy(&a, w, sizeof(OneArgs));
+        }
+        a.seq = S.seq;
+        mw_body(a, S, wg, (int)gridDim.x, ctl->flags);
+        done = a.seq;
+        t_last = __builtin_amdgcn_s_memrealtime();
+        __syncthreads();  // S.args / S.cmd are rewritten by the next poll
+    }
+    if (tid == 0) {
+        const uint32_t out = __hip_atomic_fetch_add(&dv->exited, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        if (out + 1 == gridDim.x) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+            __hip_atomic_store(&ctl->exit_gen, gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+}
+
 }  // namespace
+
+hipError_t launch_one_server(OneSrvCtl *ctl_dev, OneSrvDev *dv, const uint32_t *ptab, const uint8_t *gftab,
+                             uint32_t gen, uint32_t done0, uint32_t idle_us, uint32_t life_ms, hipStream_t s) {
+    hipError_t e = hipMemsetAsync(dv, 0, sizeof(OneSrvDev), s);
+    if (e != hipSuccess) return e;
+    k_one_server<<<kOneSrvWgs, kMwThreads, 0, s>>>(ctl_dev, dv, ptab, gftab, gen, done0, (uint64_t)idle_us * 100u,
+                                                   (uint64_t)life_ms * 100000u);
+    return hipGetLastError();
+}
+
+bool one_multi_ok(int k, int n, int len, int ss, int e) {  // e: the output rows of this call
+    const int P = ((len + 15) & ~15) >> 4;
+    const int pw = (P + kOneSrvWgs - 1) / kOneSrvWgs;
+    return k >= 1 && k <= 64 && n > k && n <= 256 && e <= 10 && len >= 0 && ss >= ((len + 15) & ~15) &&
+           ss % 16 == 0 && k * pw * 16 <= kMwSurv && e * 4 * pw <= kMwOut && e * k <= kMwCoef &&
+           (int64_t)n * ss < (int64_t(1) << 31);
+}
+
+hipError_t launch_one_multi(const OneArgs &a, hipStream_t s) {
+    k_one_multi<<<kOneSrvWgs, kMwThreads, 0, s>>>(a);
+    return hipGetLastError();
+}
 
 bool one_group_ok(int k, int n, int len, int ss, bool encode) {
     const int m = n - k;

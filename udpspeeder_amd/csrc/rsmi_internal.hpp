@@ -173,6 +173,29 @@ struct OneArgs {
 };
 bool one_group_ok(int k, int n, int len, int ss, bool encode);
 hipError_t launch_one_group(const OneArgs &a, hipStream_t s);
+// The multi-workgroup one-group kernels (oneshot.hip): kOneSrvWgs workgroups
+// split the group's 16-byte pieces; each raises its own completion word.
+constexpr int kOneSrvWgs = 16;
+bool one_multi_ok(int k, int n, int len, int ss, int rows);  // rows: output rows of the call
+hipError_t launch_one_multi(const OneArgs &a, hipStream_t s);  // a.flag: kOneSrvWgs words
+// The resident server's control block (pinned, device-mapped).  job[i]:
+// dword i of the job's OneArgs in the low half, the job's seq in the high
+// half -- one aligned 8-byte store each, written after the job's inputs, so a
+// wave whose every lane reads the new seq has read the whole job and its
+// inputs are visible; quit stops the server; the kernel writes its generation
+// to exit_gen when it ends and flags[wg] = seq when workgroup wg has finished
+// a job.
+constexpr int kOneJobWords = 30;
+struct OneSrvCtl {
+    uint64_t job[32];
+    uint32_t quit, exit_gen, pad[14];
+    uint32_t flags[kOneSrvWgs];
+};
+struct OneSrvDev {  // device memory: workgroup 0's stop decision, the exit count
+    uint32_t stop, exited, pad[2];
+};
+hipError_t launch_one_server(OneSrvCtl *ctl_dev, OneSrvDev *dv, const uint32_t *ptab, const uint8_t *gftab,
+                             uint32_t gen, uint32_t done0, uint32_t idle_us, uint32_t life_ms, hipStream_t s);
 
 // ---- packet cook / de_cook (cook.hip, cook_host.cpp) -------------------------------
 // A packet is walked by kCookLpp lanes of a wave (8: eight packets per wave;
