@@ -783,7 +783,9 @@ def collector_config(torch, dev, ncon=200, flushes=12, seed=5):
     the byte work: framing + encode + do_cook into device memory, either as
     ONE collector launch set or as 200 rsmi_fenc_run_cooked_dev calls.
     Reports the GPU time of the run part (HIP events, per flush, median) and
-    the wall time of the whole flush including the host planning."""
+    the wall time of the whole flush including the host planning: the
+    collector plans every manager in one native call (rsmi_fenc_plan_many, a
+    pool of host threads), the per-connection mode one FecEncoder.plan each."""
     import numpy as np
     from udpspeeder_amd.cook import CookContext
     from udpspeeder_amd.fec import FecCollector, FecEncoder
@@ -795,7 +797,7 @@ def collector_config(torch, dev, ncon=200, flushes=12, seed=5):
         col = FecCollector() if mode == "collector" else None
         S = FecEncoder.slot_stride_for(1250)
         slots = out = None
-        gpu_ms, wall_ms, npk_tot, nev_tot = [], [], 0, 0
+        gpu_ms, wall_ms, plan_ms, npk_tot, nev_tot = [], [], [], 0, 0
         r2 = np.random.default_rng(seed)  # the same traffic for both modes
         for f in range(flushes):
             nper = r2.integers(64, 257, ncon)
@@ -804,14 +806,25 @@ def collector_config(torch, dev, ncon=200, flushes=12, seed=5):
             inbuf = torch.randint(0, 256, (tot + 64,), dtype=torch.uint8, device=dev)
             torch.cuda.synchronize()
             t0 = time.perf_counter()
-            o, plans = 0, []
-            for ci in range(ncon):
-                l = lens[ci]
-                offs = np.concatenate([[0], np.cumsum(np.maximum(l, 0))[:-1]]).astype(np.uint64) + np.uint64(o)
-                o += int(np.maximum(l, 0).sum())
-                plans.append(encs[ci].plan(l, offs, inbuf))
-            nsl = sum(p.n_slots for p in plans)
-            npk = sum(len(p.packets) for p in plans)
+            if mode == "collector":  # every manager planned by one native call (host threads)
+                flat = np.concatenate(lens)
+                offs_flat = np.zeros(flat.size, np.uint64)
+                np.cumsum(np.maximum(flat[:-1], 0), out=offs_flat[1:])
+                cuts = np.cumsum([0] + [len(l) for l in lens])
+                ns_, npk_, _ = col.plan_many(encs, [flat[cuts[i]:cuts[i + 1]] for i in range(ncon)],
+                                             [offs_flat[cuts[i]:cuts[i + 1]] for i in range(ncon)], inbuf)
+                nsl, npk = int(ns_.sum()), int(npk_.sum())
+                plans = [type("P", (), {"n_slots": int(x)}) for x in ns_]
+            else:
+                o, plans = 0, []
+                for ci in range(ncon):
+                    l = lens[ci]
+                    offs = np.concatenate([[0], np.cumsum(np.maximum(l, 0))[:-1]]).astype(np.uint64) + np.uint64(o)
+                    o += int(np.maximum(l, 0).sum())
+                    plans.append(encs[ci].plan(l, offs, inbuf))
+                nsl = sum(p.n_slots for p in plans)
+                npk = sum(len(p.packets) for p in plans)
+            t_plan = time.perf_counter()
             if slots is None or slots.numel() < nsl * S:
                 slots = torch.empty(max(nsl, 1) * S * 2, dtype=torch.uint8, device=dev)
                 out = torch.empty_like(slots)
@@ -833,6 +846,7 @@ def collector_config(torch, dev, ncon=200, flushes=12, seed=5):
             if f >= 2:  # the first flushes pay allocations and run-time compiles
                 gpu_ms.append(e0.elapsed_time(e1))
                 wall_ms.append((t1 - t0) * 1e3)
+                plan_ms.append((t_plan - t0) * 1e3)
                 npk_tot += npk
                 nev_tot += sum(len(l) for l in lens)
             del inbuf
@@ -842,6 +856,7 @@ def collector_config(torch, dev, ncon=200, flushes=12, seed=5):
             col.close()
         res[mode] = {"run_ms_per_flush": round(statistics.median(gpu_ms), 4),
                      "flush_wall_ms": round(statistics.median(wall_ms), 3),
+                     "plan_ms": round(statistics.median(plan_ms), 3),
                      "cooked_packets_per_s_run": round(npk_tot / (sum(gpu_ms) * 1e-3), 1),
                      "packets_per_flush": round(npk_tot / len(gpu_ms), 1)}
     ctx.close()

@@ -197,6 +197,15 @@ int rsmi_fenc_run_cooked_packed_dev(rsmi_fenc *enc, uint8_t *slots_base, int64_t
  * call may be planned while the previous one runs). */
 typedef struct rsmi_fcol rsmi_fcol;
 int rsmi_fcol_create(rsmi_fcol **out);
+/* Plan n encoders at once: encoder i takes events ev0[i] .. ev0[i+1]-1 of the
+ * concatenated len / in_off / ret arrays (offsets into the one in_base), as
+ * rsmi_fenc_plan would, on up to nthreads host threads (0: 8); n_slots,
+ * n_packets and slot_stride_min (may be NULL) receive each encoder's values.
+ * Every encoder is planned; the first failure is returned. */
+int rsmi_fenc_plan_many(rsmi_fenc *const *enc, int32_t n, const int64_t *ev0, const int32_t *len,
+                        const uint64_t *in_off, const uint8_t *in_base, int32_t *ret,
+                        int64_t *n_slots, int64_t *n_packets, int32_t *slot_stride_min,
+                        int32_t nthreads);
 void rsmi_fcol_destroy(rsmi_fcol *col);
 int rsmi_fenc_run_many(rsmi_fcol *col, rsmi_fenc *const *enc, int32_t n, uint8_t *slots_base,
                        int64_t slot_stride, const struct rsmi_cook_ctx *ctx, uint64_t seed,

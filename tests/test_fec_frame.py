@@ -402,8 +402,8 @@ def test_gpu_frames_cooked_match_reference(fx, gpu, cook_oracle, name, nbatch, h
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("cook", [False, True])
-def test_gpu_collector_200_connections_match_reference(fx, gpu, cook, cook_oracle):
+@pytest.mark.parametrize("cook,native_plan", [(False, False), (True, False), (True, True)])
+def test_gpu_collector_200_connections_match_reference(fx, gpu, cook, native_plan, cook_oracle):
     """The cross-connection collector (rsmi_fenc_run_many): 200 managers --
     max_conn_num, common.h:112, one per connection (connection.h:244-245) --
     each fed its own golden event stream (case i % 10, cut into 3 batches at
@@ -420,11 +420,11 @@ def test_gpu_collector_200_connections_match_reference(fx, gpu, cook, cook_oracl
     encs = [FecEncoder(c["rs"], c["mode"], c["mtu"], c["ql"], seq0=c["seq0"]) for c in cases]
     rng = np.random.default_rng(200)
     cuts = []
+    col = FecCollector()
     for c in cases:
         n = len(c["lens"])
         a, b = sorted(rng.integers(1, n, 2))
         cuts.append([0, int(a), int(b), n])
-    col = FecCollector()
     ctx = CookContext(b"collector-key") if cook else None
     got = [[] for _ in range(ncon)]
     for bi in range(3):
@@ -439,11 +439,17 @@ def test_gpu_collector_200_connections_match_reference(fx, gpu, cook, cook_oracl
                     o += len(c["ev"][i])
             offs_all.append(offs)
         inbuf = torch.from_numpy(np.frombuffer(b"".join(chunks) + bytes(32), np.uint8).copy()).cuda()
-        plans = [encs[ci].plan(c["lens"][cuts[ci][bi]:cuts[ci][bi + 1]], offs_all[ci], inbuf)
-                 for ci, c in enumerate(cases)]
-        # one stride for the shared array: every encoder's minimum, plus do_cook's tail
-        S = FecEncoder.slot_stride_for(max(p.slot_stride_min for p in plans) - 128)
-        nsl = sum(p.n_slots for p in plans)
+        if native_plan:  # every manager in one rsmi_fenc_plan_many call (host threads)
+            ns_, _, sm_ = col.plan_many(encs, [c["lens"][cuts[ci][bi]:cuts[ci][bi + 1]]
+                                               for ci, c in enumerate(cases)], offs_all, inbuf)
+            S = FecEncoder.slot_stride_for(int(sm_.max()) - 128)
+            nsl = int(ns_.sum())
+        else:
+            plans = [encs[ci].plan(c["lens"][cuts[ci][bi]:cuts[ci][bi + 1]], offs_all[ci], inbuf)
+                     for ci, c in enumerate(cases)]
+            # one stride for the shared array: every encoder's minimum, plus do_cook's tail
+            S = FecEncoder.slot_stride_for(max(p.slot_stride_min for p in plans) - 128)
+            nsl = sum(p.n_slots for p in plans)
         slots = torch.full((max(1, nsl) * S,), 0xEE, dtype=torch.uint8, device="cuda")
         out = torch.full_like(slots, 0x11) if cook else None
         ol = col.run_many(encs, slots, S, cook=ctx, seed=77 + bi, out=out)
@@ -682,4 +688,42 @@ def test_gpu_collector_failure_after_remap_consumes_plans(gpu, monkeypatch):
         assert got == exp[i], i
     col.close()
     for e in encs:
+        e.close()
+
+
+def test_plan_many_equals_one_plan_each(fx):
+    """rsmi_fenc_plan_many (every manager planned on a pool of host threads)
+    makes exactly the decisions of one rsmi_fenc_plan per manager: the same
+    input() returns, packet lists, groups and slot counts, over three batches
+    of 60 managers' golden streams (plan-only encoders, no GPU)."""
+    from udpspeeder_amd.fec import FecCollector, FecEncoder
+    ncon = 60
+    cases = [_case(fx, NAMES[i % len(NAMES)]) for i in range(ncon)]
+    a = [FecEncoder(c["rs"], c["mode"], c["mtu"], c["ql"], seq0=c["seq0"]) for c in cases]
+    b = [FecEncoder(c["rs"], c["mode"], c["mtu"], c["ql"], seq0=c["seq0"]) for c in cases]
+    col = FecCollector()
+    rng = np.random.default_rng(60)
+    cuts = []
+    for c in cases:
+        n = len(c["lens"])
+        x, y = sorted(rng.integers(1, n, 2))
+        cuts.append([0, int(x), int(y), n])
+    for bi in range(3):
+        lens = [c["lens"][cuts[i][bi]:cuts[i][bi + 1]] for i, c in enumerate(cases)]
+        offs = [np.zeros(len(l), np.uint64) for l in lens]
+        ns, npk, sm = col.plan_many(a, lens, offs, None, nthreads=4)
+        ret_all = col.last_ret
+        q = 0
+        for i in range(ncon):
+            p = b[i].plan_host(lens[i], offs[i])
+            assert (ns[i], npk[i], sm[i]) == (p.n_slots, len(p.packets), p.slot_stride_min), (bi, i)
+            assert np.array_equal(ret_all[q:q + len(lens[i])], p.ret), (bi, i)
+            q += len(lens[i])
+            assert np.array_equal(a[i].packets_now(), p.packets), (bi, i)
+            ga = a[i].groups_now() if hasattr(a[i], "groups_now") else None
+            if ga is not None:
+                for key in p.groups:
+                    assert np.array_equal(ga[key], p.groups[key]), (bi, i, key)
+    col.close()
+    for e in a + b:
         e.close()

@@ -22,6 +22,7 @@
 
 namespace rsmi {
 void set_error(const std::string &m);
+const char *last_error();
 }
 
 using rsmi::CarryCopy;
@@ -966,6 +967,44 @@ int run_dev(rsmi_fenc *E, uint8_t *slots, int64_t S, void *stream, const CookSpe
 }
 
 }  // namespace
+
+// ---- many managers planned at once -------------------------------------------
+// A flush plans every connection's manager on its own state; they share
+// nothing, so rsmi_fenc_plan_many runs rsmi_fenc_plan for each on a pool of
+// host threads (host_pool.cpp).  The first failing manager's error is
+// reported; the others are planned regardless.
+extern "C" int rsmi_fenc_plan_many(rsmi_fenc *const *enc, int32_t n, const int64_t *ev0, const int32_t *len,
+                                   const uint64_t *in_off, const uint8_t *in_base, int32_t *ret,
+                                   int64_t *n_slots, int64_t *n_packets, int32_t *slot_stride_min,
+                                   int32_t nthreads) {
+    if (n < 0 || (n && (!enc || !ev0)) || (n && ev0[n] > ev0[0] && !len))
+        return fail(RSMI_ERR_INVALID, "rsmi_fenc_plan_many: bad arguments");
+    for (int i = 0; i < n; ++i) {
+        if (!enc[i] || ev0[i + 1] < ev0[i]) return fail(RSMI_ERR_INVALID, "rsmi_fenc_plan_many: bad encoder or range");
+        for (int j = 0; j < i; ++j)
+            if (enc[j] == enc[i]) return fail(RSMI_ERR_INVALID, "rsmi_fenc_plan_many: an encoder listed twice");
+    }
+    std::vector<int> rcs((size_t)n, RSMI_OK);
+    std::vector<std::string> errs((size_t)n);
+    rsmi::host_parallel_for(n, nthreads > 0 ? nthreads : 8, [&](int i) {
+        const int64_t a = ev0[i], cnt = ev0[i + 1] - ev0[i];
+        int64_t ns = 0, np = 0;
+        int32_t sm = 0;
+        const int rc = rsmi_fenc_plan(enc[i], cnt, len ? len + a : nullptr, in_off ? in_off + a : nullptr, in_base,
+                                      ret ? ret + a : nullptr, &ns, &np, &sm);
+        rcs[(size_t)i] = rc;
+        if (rc) {
+            errs[(size_t)i] = rsmi::last_error();
+            return;
+        }
+        if (n_slots) n_slots[i] = ns;
+        if (n_packets) n_packets[i] = np;
+        if (slot_stride_min) slot_stride_min[i] = sm;
+    });
+    for (int i = 0; i < n; ++i)
+        if (rcs[(size_t)i]) return fail(rcs[(size_t)i], "encoder " + std::to_string(i) + ": " + errs[(size_t)i]);
+    return RSMI_OK;
+}
 
 // ---- the collector: many managers' planned batches as one launch set --------
 //

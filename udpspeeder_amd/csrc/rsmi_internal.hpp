@@ -3,6 +3,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <functional>
+
 #include <cstdint>
 #include <string>
 #include <utility>
@@ -392,5 +394,9 @@ int cook_frame_packets(const rsmi_cook_ctx *ctx, uint8_t *slots, int64_t S, cons
                        int64_t npk, int32_t *out_len, uint8_t *dst, const int64_t *dst_off, uint64_t seed,
                        const FuseArgs &f, hipStream_t s);
 hipError_t launch_cook_frame(const CookArgs &a, const FuseArgs &f, int max_blocks, hipStream_t s);
+
+// host_pool.cpp: fn(0..n-1) over up to nthreads host threads (the caller
+// included); returns when every item is done.
+void host_parallel_for(int n, int nthreads, const std::function<void(int)> &fn);
 
 }  // namespace rsmi

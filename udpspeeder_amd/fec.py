@@ -119,6 +119,7 @@ class FecEncoder:
         self._last_packets = packets
         self._last_nslots = ns.value
         self._last_smin = smin.value
+        self._last_npk = npk.value
         return FencPlan(ns.value, smin.value, ret, packets, g)
 
     def _check_slots(self, buf, slot_stride: int, what: str):
@@ -154,7 +155,7 @@ class FecEncoder:
         lengths, one per planned packet (-1: did not fit)."""
         import torch
         s = stream if stream is not None else torch.cuda.current_stream()
-        npk = len(self._last_packets) if getattr(self, "_last_packets", None) is not None else None
+        npk = getattr(self, "_last_npk", None)
         if out_len is None:
             out_len = torch.empty(max(npk or 0, 1), dtype=torch.int32, device="cuda")
         elif out_len.dtype != torch.int32 or not out_len.is_cuda or out_len.numel() < (npk or 0):
@@ -231,10 +232,11 @@ class FecEncoder:
     def packets_now(self):
         """The last plan's packet list as it stands now (after
         FecCollector.run_many: slots of the shared slot array)."""
-        pk = (rsmi_fenc_packet * max(1, len(self._last_packets)))()
+        npk = self._last_npk
+        pk = (rsmi_fenc_packet * max(1, npk))()
         check(lib().rsmi_fenc_packets(self._h, pk), "rsmi_fenc_packets")
         dt = np.dtype([("slot", np.int64), ("len", np.int32), ("event", np.int32)])
-        return np.frombuffer(bytes(pk), dt)[:len(self._last_packets)].copy()
+        return np.frombuffer(bytes(pk), dt)[:npk].copy()
 
     @staticmethod
     def slot_stride_for(fec_len_max: int) -> int:
@@ -381,6 +383,34 @@ class FecCollector:
         except Exception:
             pass
 
+    def plan_many(self, encoders, lens, offsets, in_buf, nthreads: int = 8):
+        """rsmi_fenc_plan_many: plan every encoder's batch (lens[i], offsets[i]
+        into the one in_buf) on up to nthreads host threads.  Returns the
+        per-encoder (n_slots, n_packets, slot_stride_min) arrays; the
+        encoders' packet lists are read with packets_now() after the run."""
+        n = len(encoders)
+        counts = np.array([len(l) for l in lens], np.int64)
+        ev0 = np.zeros(n + 1, np.int64)
+        np.cumsum(counts, out=ev0[1:])
+        L = np.ascontiguousarray(np.concatenate(lens) if n else np.zeros(0), np.int32)
+        O = np.ascontiguousarray(np.concatenate(offsets) if n else np.zeros(0), np.uint64)
+        ret = np.zeros(max(1, L.size), np.int32)
+        ns = np.zeros(max(1, n), np.int64)
+        npk = np.zeros(max(1, n), np.int64)
+        smin = np.zeros(max(1, n), np.int32)
+        arr = (C.c_void_p * max(1, n))(*[e._h.value for e in encoders])
+        base = in_buf if isinstance(in_buf, int) else (in_buf.data_ptr() if in_buf is not None else None)
+        check(lib().rsmi_fenc_plan_many(arr, n, ev0.ctypes.data, L.ctypes.data if L.size else None,
+                                        O.ctypes.data if O.size else None, base or None, ret.ctypes.data,
+                                        ns.ctypes.data, npk.ctypes.data, smin.ctypes.data, int(nthreads)),
+              "rsmi_fenc_plan_many")
+        for i, e in enumerate(encoders):
+            e._last_nslots, e._last_npk, e._last_smin = int(ns[i]), int(npk[i]), int(smin[i])
+            e._last_packets = None
+            e._keep = (in_buf, (e._keep or (None,))[0])
+        self.last_ret = ret[:L.size]
+        return ns[:n], npk[:n], smin[:n]
+
     def run_many(self, encoders, slots, slot_stride: int, cook=None, seed: int = 0, out=None,
                  out_len=None, stream=None):
         """Frame + encode (+ do_cook into `out`, None: in place) every encoder's
@@ -390,7 +420,7 @@ class FecCollector:
         import torch
         s = stream if stream is not None else torch.cuda.current_stream()
         n_slots = sum(e._last_nslots for e in encoders)
-        n_pk = sum(len(e._last_packets) for e in encoders)
+        n_pk = sum(e._last_npk for e in encoders)
         smin = max((getattr(e, "_last_smin", 0) for e in encoders), default=0)
         if int(slot_stride) % 16 or int(slot_stride) < smin:
             raise ValueError(f"slot_stride must be a multiple of 16 >= every encoder's slot_stride_min ({smin})")
