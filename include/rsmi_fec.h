@@ -262,11 +262,15 @@ int rsmi_fdec_run_dev(rsmi_fdec *dec, void *stream);
 
 /* The receive-side collector (see rsmi_fenc_run_many): n planned decoders'
  * batches in one launch set -- one gather into a staging area shared across
- * decoders and bucketed by (k, n), one decode per code, one pass packing each
- * decoder's rows to copy back, one moving their carries -- then each
- * decoder's rows to its own pinned buffer.  Afterwards each decoder's
- * rsmi_fdec_outputs works as after rsmi_fdec_run_dev.  The collector keeps
- * the shared staging; a call waits for its previous call. */
+ * decoders and bucketed by (k, n), one decode per code, one pass packing
+ * every decoder's rows back to back, one moving their carries -- then one
+ * copy of all the rows into the collector's pinned buffer.  Afterwards each
+ * decoder's rsmi_fdec_outputs works as after rsmi_fdec_run_dev; the output
+ * pointers into decoded rows point into that buffer, which the collector
+ * keeps per set of two (calls alternate): they stay valid until the
+ * decoder's next plan, the collector's second-next call or its destruction,
+ * whichever comes first.  The collector keeps the shared staging; a call
+ * waits for its previous call. */
 typedef struct rsmi_fdcol rsmi_fdcol;
 int rsmi_fdcol_create(rsmi_fdcol **out);
 void rsmi_fdcol_destroy(rsmi_fdcol *col);

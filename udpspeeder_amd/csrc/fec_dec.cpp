@@ -224,8 +224,15 @@ struct Batch {
     bool planned = false, ran = false, resolved = false;
     uint8_t *hmeta = nullptr, *hblob = nullptr;  // pinned: upload source, rows copied back
     size_t hmeta_cap = 0, hblob_cap = 0;
+    // a collector run: the rows came back into the collector's pinned buffer
+    // (one copy for every decoder), and its event stands for this batch's
+    const uint8_t *hblob_view = nullptr;
+    std::shared_ptr<rsmi::SharedEv> ext;
+    hipStream_t stream = nullptr;
     hipEvent_t done = nullptr;
     bool in_flight = false;
+    hipEvent_t ev() const { return ext ? ext->ev : done; }
+    const uint8_t *rows_back() const { return hblob_view ? hblob_view : hblob; }
 };
 
 struct rsmi_fdec {
@@ -257,8 +264,9 @@ namespace {
 
 int wait_batch(Batch &X) {
     if (X.in_flight) {
-        hipError_t e = hipEventSynchronize(X.done);
+        hipError_t e = hipEventSynchronize(X.ev());
         X.in_flight = false;
+        X.ext.reset();
         if (e != hipSuccess) return fail(RSMI_ERR_HIP, std::string("fdec wait: ") + hipGetErrorString(e));
     }
     return RSMI_OK;
@@ -436,7 +444,7 @@ void resolve_outputs(const Batch &X, size_t b, size_t e, Spill &sp, std::vector<
         const Job &J = X.jobs[(size_t)o.job];
         const RowRef *rr = X.rows.data() + J.rows0;
         auto row = [&](int i) -> const uint8_t * {
-            return rr[i].host ? rr[i].host : X.hblob + rr[i].d2h;
+            return rr[i].host ? rr[i].host : X.rows_back() + rr[i].d2h;
         };
         const int64_t L = J.len;
         const int64_t cur = (int64_t)J.k * L;  // the blob: the k data rows back to back
@@ -693,7 +701,7 @@ int bind_dec(rsmi_fdec *D, hipStream_t s) {
         return fail(RSMI_ERR_INVALID, "rsmi_fdec_run_dev on another device than the decoder's");
     }
     Batch &prev = D->bat[D->bi ^ 1];
-    if (prev.in_flight && hipStreamWaitEvent(s, prev.done, 0) != hipSuccess)
+    if (prev.in_flight && prev.stream != s && hipStreamWaitEvent(s, prev.ev(), 0) != hipSuccess)
         return fail(RSMI_ERR_HIP, "fdec: hipStreamWaitEvent");
     return RSMI_OK;
 }
@@ -770,6 +778,9 @@ int rsmi_fdec_run_dev(rsmi_fdec *D, void *stream) {
     if (e == hipSuccess && D->B->d2h_bytes)
         e = hipMemcpyAsync(D->B->hblob, D->dblob, (size_t)D->B->d2h_bytes, hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipEventRecord(D->B->done, s);
+    D->B->ext.reset();
+    D->B->hblob_view = nullptr;
+    D->B->stream = s;
     if (e != hipSuccess) return fail(RSMI_ERR_HIP, std::string("fdec run: ") + hipGetErrorString(e));
     D->B->in_flight = true;
     D->B->planned = false;
@@ -861,9 +872,13 @@ struct rsmi_fdcol {
     size_t status_cap = 0;
     uint8_t *hmeta[2] = {nullptr, nullptr};
     size_t hmeta_cap[2] = {0, 0};
-    hipEvent_t done[2] = {nullptr, nullptr};
+    std::shared_ptr<rsmi::SharedEv> done[2];  // also the decoders' batches' event (Batch::ext)
     bool in_flight[2] = {false, false};
     int cur = 0;
+    // every decoder's rows, packed on the device and copied back in one piece
+    // (per set: a decoder's outputs point into the set it ran in)
+    uint8_t *dback = nullptr, *hback[2] = {nullptr, nullptr};
+    size_t dback_cap = 0, hback_cap[2] = {0, 0};
 };
 
 extern "C" {
@@ -877,11 +892,12 @@ int rsmi_fdcol_create(rsmi_fdcol **out) {
 void rsmi_fdcol_destroy(rsmi_fdcol *C) {
     if (!C) return;
     for (int i = 0; i < 2; ++i) {
-        if (C->in_flight[i]) (void)hipEventSynchronize(C->done[i]);
-        if (C->done[i]) (void)hipEventDestroy(C->done[i]);
+        if (C->in_flight[i] && C->done[i]) (void)hipEventSynchronize(C->done[i]->ev);
+        C->done[i].reset();  // (destroyed once no decoder's batch holds it)
         if (C->hmeta[i]) (void)hipHostFree(C->hmeta[i]);
+        if (C->hback[i]) (void)hipHostFree(C->hback[i]);
     }
-    for (uint8_t *p : {C->dstage, C->dmeta}) if (p) (void)hipFree(p);
+    for (uint8_t *p : {C->dstage, C->dmeta, C->dback}) if (p) (void)hipFree(p);
     if (C->dstatus) (void)hipFree(C->dstatus);
     delete C;
 }
@@ -899,9 +915,11 @@ int rsmi_fdec_run_many(rsmi_fdcol *C, rsmi_fdec *const *dec, int32_t n, void *st
     int cur;
     if (hipGetDevice(&cur) != hipSuccess) return fail(RSMI_ERR_HIP, "fdcol: no usable GPU");
     if (C->device < 0) {
-        for (auto &ev : C->done)
-            if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess)
+        for (auto &ev : C->done) {
+            ev = std::make_shared<rsmi::SharedEv>();
+            if (hipEventCreateWithFlags(&ev->ev, hipEventDisableTiming) != hipSuccess)
                 return fail(RSMI_ERR_HIP, "fdcol: hipEventCreate");
+        }
         C->device = cur;
     } else if (C->device != cur) {
         return fail(RSMI_ERR_INVALID, "rsmi_fdec_run_many on another device than the collector's");
@@ -909,7 +927,7 @@ int rsmi_fdec_run_many(rsmi_fdcol *C, rsmi_fdec *const *dec, int32_t n, void *st
     // the shared staging / metadata buffers are rewritten: after the last call
     for (int i = 0; i < 2; ++i)
         if (C->in_flight[i]) {
-            if (hipEventSynchronize(C->done[i]) != hipSuccess) return fail(RSMI_ERR_HIP, "fdcol: wait");
+            if (hipEventSynchronize(C->done[i]->ev) != hipSuccess) return fail(RSMI_ERR_HIP, "fdcol: wait");
             C->in_flight[i] = false;
         }
     for (int i = 0; i < n; ++i) {
@@ -922,10 +940,11 @@ int rsmi_fdec_run_many(rsmi_fdcol *C, rsmi_fdec *const *dec, int32_t n, void *st
             if (rc) return rc;
         }
         rc = dev_grow(&D->dcarry, &D->dcarry_cap, (size_t)D->buff_num * kRingBytes);
-        if (!rc) rc = dev_grow(&D->dblob, &D->blob_cap, (size_t)D->B->d2h_bytes + 16);
-        if (!rc) rc = host_grow(&D->B->hblob, &D->B->hblob_cap, (size_t)D->B->d2h_bytes + 16);
         if (rc) return rc;
     }
+    // every decoder's rows back to back in the collector's buffers
+    std::vector<int64_t> boff((size_t)n + 1, 0);
+    for (int i = 0; i < n; ++i) boff[(size_t)i + 1] = boff[(size_t)i] + ((dec[i]->B->d2h_bytes + 255) & ~int64_t(255));
     // ---- shared buckets: (k, n) across decoders, rows appended decoder by decoder
     struct CB {
         int k, nn, len = 0;
@@ -954,6 +973,8 @@ int rsmi_fdec_run_many(rsmi_fdcol *C, rsmi_fdec *const *dec, int32_t n, void *st
     }
     int rc = dev_grow(&C->dstage, &C->stage_cap, (size_t)so + 16);
     if (!rc) rc = dev_grow(&C->dstatus, &C->status_cap, (size_t)max_rows * 4 + 16);
+    if (!rc)  // (the previous calls' copies out of it were waited for above)
+        rc = dev_grow(&C->dback, &C->dback_cap, (size_t)boff[(size_t)n] + 16);
     if (rc) return rc;
     std::vector<GatherCopy> gathers;
     std::vector<uint8_t> present((size_t)po, 0);
@@ -985,8 +1006,8 @@ int rsmi_fdec_run_many(rsmi_fdcol *C, rsmi_fdec *const *dec, int32_t n, void *st
         int64_t ro = 0;
         for (const auto &jr : X.d2h_rows) {
             const Job &J = X.jobs[(size_t)jr.first];
-            packs.push_back(CarryCopy{shard_at(D, (size_t)i, J, jr.second), (uint64_t)(uintptr_t)(D->dblob + ro),
-                                      (uint32_t)J.len, 0});
+            packs.push_back(CarryCopy{shard_at(D, (size_t)i, J, jr.second),
+                                      (uint64_t)(uintptr_t)(C->dback + boff[(size_t)i] + ro), (uint32_t)J.len, 0});
             ro += (J.len + 15) & ~15;
         }
         for (const CarryCopy &cc : X.carries)
@@ -999,6 +1020,7 @@ int rsmi_fdec_run_many(rsmi_fdcol *C, rsmi_fdec *const *dec, int32_t n, void *st
     C->cur ^= 1;
     rc = dev_grow(&C->dmeta, &C->meta_cap, all);
     if (!rc) rc = host_grow(&C->hmeta[C->cur], &C->hmeta_cap[C->cur], all);
+    if (!rc) rc = host_grow(&C->hback[C->cur], &C->hback_cap[C->cur], (size_t)boff[(size_t)n] + 16);
     if (rc) return rc;
     uint8_t *hm = C->hmeta[C->cur];
     if (gb) std::memcpy(hm + go, gathers.data(), gb);
@@ -1022,17 +1044,16 @@ int rsmi_fdec_run_many(rsmi_fdcol *C, rsmi_fdec *const *dec, int32_t n, void *st
     if (e == hipSuccess)
         e = rsmi::launch_carry(reinterpret_cast<const CarryCopy *>(C->dmeta + co), (int64_t)carries.size(), none,
                                s);
-    for (int i = 0; e == hipSuccess && i < n; ++i) {
-        rsmi_fdec *D = dec[i];
-        if (D->B->d2h_bytes)
-            e = hipMemcpyAsync(D->B->hblob, D->dblob, (size_t)D->B->d2h_bytes, hipMemcpyDeviceToHost, s);
-    }
-    if (e == hipSuccess) e = hipEventRecord(C->done[C->cur], s);
-    for (int i = 0; e == hipSuccess && i < n; ++i) e = hipEventRecord(dec[i]->B->done, s);
+    if (e == hipSuccess && boff[(size_t)n])  // one copy for every decoder's rows
+        e = hipMemcpyAsync(C->hback[C->cur], C->dback, (size_t)boff[(size_t)n], hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipEventRecord(C->done[C->cur]->ev, s);
     if (e != hipSuccess) return fail(RSMI_ERR_HIP, std::string("fdcol run: ") + hipGetErrorString(e));
     C->in_flight[C->cur] = true;
-    for (int i = 0; i < n; ++i) {
+    for (int i = 0; i < n; ++i) {  // one event for all (a record per decoder cost ~5 us each)
         rsmi_fdec *D = dec[i];
+        D->B->hblob_view = C->hback[C->cur] + boff[(size_t)i];
+        D->B->ext = C->done[C->cur];
+        D->B->stream = s;
         D->B->in_flight = true;
         D->B->planned = false;
         D->B->ran = true;

@@ -14,6 +14,7 @@
 #include <cstdio>
 #include <cstring>
 #include <map>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -129,6 +130,12 @@ struct PlanSet {
     uint32_t max_src = 0;  // most records of one job (> kFrameLdsSrc: k_frame reads them repeatedly)
     hipEvent_t done = nullptr;
     bool in_flight = false;
+    // run by a collector: its event stands for this set's (one record per
+    // flush instead of one per manager), and the stream it ran on (a run on
+    // the same stream needs no cross-stream wait)
+    std::shared_ptr<rsmi::SharedEv> ext;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev() const { return ext ? ext->ev : done; }
 };
 
 }  // namespace
@@ -219,9 +226,10 @@ const T *mapped(const HostArr<T> &a) {
 
 int wait_set(PlanSet &B) {
     if (B.in_flight) {
-        hipError_t e = hipEventSynchronize(B.done);
+        hipError_t e = hipEventSynchronize(B.ev());
         if (e != hipSuccess) return fail(RSMI_ERR_HIP, std::string("fenc wait: ") + hipGetErrorString(e));
         B.in_flight = false;
+        B.ext.reset();
     }
     return RSMI_OK;
 }
@@ -784,7 +792,7 @@ int prepare_run(rsmi_fenc *E, hipStream_t s) {
         return fail(RSMI_ERR_INVALID, "rsmi_fenc_run_dev on another device than the encoder's");
     }
     PlanSet &prev = E->ps[E->pcur ^ 1];
-    if (prev.in_flight && hipStreamWaitEvent(s, prev.done, 0) != hipSuccess)
+    if (prev.in_flight && prev.stream != s && hipStreamWaitEvent(s, prev.ev(), 0) != hipSuccess)
         return fail(RSMI_ERR_HIP, "fenc: hipStreamWaitEvent");
     // growing a shared device buffer frees the old one: not under the previous batch
     const bool grows = E->carry_need > E->carry_cap[E->carry_cur] || !E->dshadow;
@@ -961,6 +969,8 @@ int run_dev(rsmi_fenc *E, uint8_t *slots, int64_t S, void *stream, const CookSpe
     }
     e = hipEventRecord(E->P->done, s);
     if (e != hipSuccess) return fail(RSMI_ERR_HIP, std::string("fenc event: ") + hipGetErrorString(e));
+    E->P->ext.reset();
+    E->P->stream = s;
     E->P->in_flight = true;
     E->planned = false;
     return RSMI_OK;
@@ -1032,7 +1042,7 @@ struct rsmi_fcol {
         HostArr<rsmi::ByteRun> stale, upd;
         HostArr<rsmi::PacketRun> pruns;
         HostArr<uint32_t> recs;  // every manager's list-A records, in list-A order
-        hipEvent_t done = nullptr;
+        std::shared_ptr<rsmi::SharedEv> done;  // also the managers' plan sets' event (PlanSet::ext)
         bool in_flight = false;
     } set[2];
     int cur = 0;
@@ -1052,8 +1062,8 @@ int rsmi_fcol_create(rsmi_fcol **out) {
 void rsmi_fcol_destroy(rsmi_fcol *C) {
     if (!C) return;
     for (auto &B : C->set) {
-        if (B.in_flight) (void)hipEventSynchronize(B.done);
-        if (B.done) (void)hipEventDestroy(B.done);
+        if (B.in_flight && B.done) (void)hipEventSynchronize(B.done->ev);
+        B.done.reset();  // (destroyed once no manager's plan set holds it)
     }
     for (int i = 0; i < 2; ++i)
         if (C->dplan[i]) (void)hipFree(C->dplan[i]);
@@ -1100,9 +1110,11 @@ int rsmi_fenc_run_many(rsmi_fcol *C, rsmi_fenc *const *enc, int32_t n, uint8_t *
     int cur;
     if (hipGetDevice(&cur) != hipSuccess) return fail(RSMI_ERR_HIP, "fcol: no usable GPU");
     if (C->device < 0) {
-        for (auto &B : C->set)
-            if (hipEventCreateWithFlags(&B.done, hipEventDisableTiming) != hipSuccess)
+        for (auto &B : C->set) {
+            B.done = std::make_shared<rsmi::SharedEv>();
+            if (hipEventCreateWithFlags(&B.done->ev, hipEventDisableTiming) != hipSuccess)
                 return fail(RSMI_ERR_HIP, "fcol: hipEventCreate");
+        }
         C->device = cur;
     } else if (C->device != cur) {
         return fail(RSMI_ERR_INVALID, "rsmi_fenc_run_many on another device than the collector's");
@@ -1115,7 +1127,7 @@ int rsmi_fenc_run_many(rsmi_fcol *C, rsmi_fenc *const *enc, int32_t n, uint8_t *
     C->cur ^= 1;
     rsmi_fcol::Set &B = C->set[C->cur];
     if (B.in_flight) {
-        if (hipEventSynchronize(B.done) != hipSuccess) return fail(RSMI_ERR_HIP, "fcol: wait");
+        if (hipEventSynchronize(B.done->ev) != hipSuccess) return fail(RSMI_ERR_HIP, "fcol: wait");
         B.in_flight = false;
     }
     // ---- slot layout: every group bucketed by code, then the lone mode-1 slots
@@ -1309,11 +1321,12 @@ int rsmi_fenc_run_many(rsmi_fcol *C, rsmi_fenc *const *enc, int32_t n, uint8_t *
                                 out, nullptr, seed, s);
         if (rc) return rc;
     }
-    if (hipEventRecord(B.done, s) != hipSuccess) return fail(RSMI_ERR_HIP, "fcol: event");
+    if (hipEventRecord(B.done->ev, s) != hipSuccess) return fail(RSMI_ERR_HIP, "fcol: event");
     B.in_flight = true;
-    for (int i = 0; i < n; ++i) {
+    for (int i = 0; i < n; ++i) {  // one event for all (a record per manager cost ~5 us each)
         rsmi_fenc *E = enc[i];
-        if (hipEventRecord(E->P->done, s) != hipSuccess) return fail(RSMI_ERR_HIP, "fenc event");
+        E->P->ext = B.done;
+        E->P->stream = s;
         E->P->in_flight = true;
         E->planned = false;
     }

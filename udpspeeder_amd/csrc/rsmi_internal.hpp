@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <functional>
+#include <memory>
 
 #include <cstdint>
 #include <string>
@@ -398,5 +399,15 @@ hipError_t launch_cook_frame(const CookArgs &a, const FuseArgs &f, int max_block
 // host_pool.cpp: fn(0..n-1) over up to nthreads host threads (the caller
 // included); returns when every item is done.
 void host_parallel_for(int n, int nthreads, const std::function<void(int)> &fn);
+
+// An event several plan sets / batches may wait on: a collector's
+// (rsmi_fenc_run_many, rsmi_fdec_run_many), which every manager it ran holds
+// until its own next run -- one record per flush instead of one per manager.
+struct SharedEv {
+    hipEvent_t ev = nullptr;
+    ~SharedEv() {
+        if (ev) (void)hipEventDestroy(ev);
+    }
+};
 
 }  // namespace rsmi
