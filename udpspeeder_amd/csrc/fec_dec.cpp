@@ -25,6 +25,7 @@
 #include <memory>
 #include <new>
 #include <string>
+#include <deque>
 #include <unordered_map>
 #include <thread>
 #include <vector>
@@ -38,6 +39,7 @@ void set_error(const std::string &m);
 
 using rsmi::GatherCopy;
 using rsmi::CarryCopy;
+using rsmi::JoinCopy;
 
 namespace {
 
@@ -56,6 +58,82 @@ constexpr int kRingBytes = (kBufLen + 15) & ~15; // carry bytes per ring slot
 uint32_t rd_u32(const uint8_t *p) { return (uint32_t)p[0] << 24 | (uint32_t)p[1] << 16 | (uint32_t)p[2] << 8 | p[3]; }
 uint32_t rd_u16(const uint8_t *p) { return (uint32_t)p[0] << 8 | p[1]; }
 
+// seq -> V: open addressing, linear probing, backward-shift erase (no
+// tombstones), at most half full.  The planner's maps only find, insert and
+// erase (nothing iterates them), so a flat table replaces the reference's
+// node-based std::unordered_map without a change in behaviour, at one probe
+// per lookup and no allocation per group.
+template <class V>
+struct SeqMap {
+    struct Ent {
+        uint32_t key, used;
+        V val;
+    };
+    std::vector<Ent> t;
+    size_t mask = 0, n = 0;
+    uint64_t edits = 0;  // inserts + erases: a cached lookup holds while this is unchanged
+    explicit SeqMap(size_t cap = 64) { rehash(cap); }
+    size_t home(uint32_t k) const { return (size_t)((k * 0x9E3779B1u) ^ (k >> 16)) & mask; }
+    void rehash(size_t cap) {
+        size_t c = 16;
+        while (c < cap) c <<= 1;
+        std::vector<Ent> old(c, Ent{0, 0, V{}});
+        old.swap(t);
+        mask = c - 1;
+        for (const Ent &e : old)
+            if (e.used) {
+                size_t i = home(e.key);
+                while (t[i].used) i = (i + 1) & mask;
+                t[i] = e;
+            }
+    }
+    V *find(uint32_t k) {
+        for (size_t i = home(k);; i = (i + 1) & mask) {
+            if (!t[i].used) return nullptr;
+            if (t[i].key == k) return &t[i].val;
+        }
+    }
+    // the slot for k; inserted (value v0) if absent
+    V &get(uint32_t k, const V &v0, bool *inserted = nullptr) {
+        size_t i = home(k);
+        for (; t[i].used; i = (i + 1) & mask)
+            if (t[i].key == k) {
+                if (inserted) *inserted = false;
+                return t[i].val;
+            }
+        if (2 * (n + 1) > t.size()) {
+            rehash(2 * t.size());
+            return get(k, v0, inserted);
+        }
+        t[i] = Ent{k, 1, v0};
+        ++n;
+        ++edits;
+        if (inserted) *inserted = true;
+        return t[i].val;
+    }
+    bool erase(uint32_t k) {
+        size_t i = home(k);
+        for (;; i = (i + 1) & mask) {
+            if (!t[i].used) return false;
+            if (t[i].key == k) break;
+        }
+        // shift back the run after i: an entry moves into the hole unless its
+        // home lies cyclically in (hole, its slot]
+        for (size_t j = (i + 1) & mask; t[j].used; j = (j + 1) & mask) {
+            const size_t h = home(t[j].key);
+            const bool stays = i <= j ? (h > i && h <= j) : (h > i || h <= j);
+            if (!stays) {
+                t[i] = t[j];
+                i = j;
+            }
+        }
+        t[i].used = 0;
+        --n;
+        ++edits;
+        return true;
+    }
+};
+
 // anti_replay_t (fec_manager.h:187-235)
 struct AntiReplay {
     struct Info {
@@ -63,15 +141,14 @@ struct AntiReplay {
         uint32_t index;
     };
     std::vector<int64_t> buf = std::vector<int64_t>(kAntiReplaySize, -1);
-    std::unordered_map<uint32_t, Info> mp;
+    SeqMap<Info> mp{(size_t)kAntiReplaySize * 3};
     uint32_t index = 0;
-    AntiReplay() { mp.reserve(kAntiReplaySize * 3); }
     bool valid(uint32_t seq, int64_t now) {
-        auto it = mp.find(seq);
-        if (it == mp.end()) return true;
-        if (now - it->second.time > kAntiReplayTimeout) {
-            buf[it->second.index] = -1;
-            mp.erase(it);
+        Info *it = mp.find(seq);
+        if (!it) return true;
+        if (now - it->time > kAntiReplayTimeout) {
+            buf[it->index] = -1;
+            mp.erase(seq);
             return true;
         }
         return false;
@@ -80,7 +157,7 @@ struct AntiReplay {
         if (!valid(seq, now)) return;
         if (buf[index] != -1) mp.erase((uint32_t)buf[index]);
         buf[index] = seq;
-        mp[seq] = Info{now, index};
+        mp.get(seq, Info{}) = Info{now, index};
         if (++index == kAntiReplaySize) index = 0;
     }
 };
@@ -138,7 +215,8 @@ struct Job {  // one group decoded in this batch
     int32_t event;
     int bucket;
     int64_t row;        // group row in its bucket's staging
-    int64_t rows0;      // its k RowRefs in rsmi_fdec::rows
+    int64_t rows0;      // mode 1: its k RowRefs in rsmi_fdec::rows
+    int64_t lin = -1;   // mode 0: its blob (the k data rows joined on the device), in the rows copied back
 };
 
 struct Bucket {
@@ -156,7 +234,7 @@ struct Out {
 template <class T>
 int dev_grow(T **p, size_t *cap, size_t need) {
     if (need <= *cap) return RSMI_OK;
-    size_t c = std::max(need, *cap * 2);
+    size_t c = std::max(need + need / 4, *cap * 2);  // headroom: batch sizes wander
     c = (c + 4095) & ~size_t(4095);
     if (*p) (void)hipFree(*p);
     *p = nullptr;
@@ -168,7 +246,7 @@ int dev_grow(T **p, size_t *cap, size_t need) {
 
 int host_grow(uint8_t **p, size_t *cap, size_t need) {
     if (need <= *cap) return RSMI_OK;
-    size_t c = std::max(need, *cap * 2);
+    size_t c = std::max(need + need / 4, *cap * 2);  // headroom: batch sizes wander
     c = (c + 4095) & ~size_t(4095);
     if (*p) (void)hipHostFree(*p);
     *p = nullptr;
@@ -214,7 +292,7 @@ struct Batch {
     std::vector<Out> outs;
     std::vector<uint8_t> present;  // all buckets' present flags
     std::vector<RowRef> rows;      // k per job
-    std::vector<std::pair<int64_t, int>> d2h_rows;  // (job, row) copied back, in d2h order
+    std::vector<std::pair<int64_t, int>> d2h_rows;  // (job, row; -1: the joined blob) copied back, in d2h order
     // outputs that straddle two rows are copied into bump-allocated chunks, one
     // arena per resolver thread, kept from batch to batch (fresh pages would cost
     // a fault per 4 KiB)
@@ -235,10 +313,31 @@ struct Batch {
     const uint8_t *rows_back() const { return hblob_view ? hblob_view : hblob; }
 };
 
+struct EvictMemo {  // the last ring eviction (input_packet)
+    bool valid = false;
+    uint32_t seq = 0;
+    int64_t now = 0;
+    uint64_t ar_edits = 0, mp_edits = 0;
+};
+
+struct SeqMemo {  // the last packet's anti-replay check and group (input_packet)
+    Group *gp = nullptr;
+    uint32_t seq = 0;
+    int64_t now = 0;
+    uint64_t ar_edits = 0, mp_edits = 0;
+};
+
 struct rsmi_fdec {
     int buff_num = 2000;
+    EvictMemo evict_memo;
+    SeqMemo seq_memo;
+    std::vector<std::pair<int, int>> sel;  // plan_decode's survivors
     AntiReplay ar;
-    std::unordered_map<uint32_t, Group> mp;
+    // fec_decode_manager_t::mp (fec_manager.h:388): seq -> a group in the slab
+    // (stable addresses; freed groups keep their map's storage for reuse)
+    SeqMap<uint32_t> mp;
+    std::deque<Group> groups;
+    std::vector<uint32_t> free_groups;
     std::vector<RingEnt> ring;
     int index = 0;
     bool plan_only = false;
@@ -257,7 +356,34 @@ struct rsmi_fdec {
     int32_t *dstatus = nullptr;
     size_t status_cap = 0;
 
-    Group &group(uint32_t seq) { return mp[seq]; }  // operator[] inserts, as the reference
+    Group &group(uint32_t seq) {  // inserts, as the reference's operator[]
+        bool fresh;
+        uint32_t &gi = mp.get(seq, 0u, &fresh);
+        if (fresh) {
+            if (free_groups.empty()) {
+                gi = (uint32_t)groups.size();
+                groups.emplace_back();
+            } else {
+                gi = free_groups.back();
+                free_groups.pop_back();
+                Group &g = groups[gi];
+                g.type = g.data_num = g.red = g.len = -1;
+                g.fec_done = 0;
+                g.gm.v.clear();
+            }
+        }
+        return groups[gi];
+    }
+    Group *find_group(uint32_t seq) {
+        uint32_t *gi = mp.find(seq);
+        return gi ? &groups[*gi] : nullptr;
+    }
+    void erase_group(uint32_t seq) {
+        uint32_t *gi = mp.find(seq);
+        if (!gi) return;
+        free_groups.push_back(*gi);
+        mp.erase(seq);
+    }
 };
 
 namespace {
@@ -295,7 +421,8 @@ void plan_decode(rsmi_fdec *D, uint32_t seq, Group &g, int type, int inner, int 
     }
     g.fec_done = 1;
     // rs_decode2's survivors: the first k present indices below n (rs.cpp:24-39)
-    std::vector<std::pair<int, int>> sel;
+    std::vector<std::pair<int, int>> &sel = D->sel;  // scratch, kept between groups
+    sel.clear();
     bool bad = false;
     for (auto &kv : g.gm) {
         if (kv.first >= n) bad = true;
@@ -330,10 +457,13 @@ void plan_decode(rsmi_fdec *D, uint32_t seq, Group &g, int type, int inner, int 
     J.bucket = b;
     J.row = B.rows++;
     J.rows0 = (int64_t)D->B->rows.size();
-    // data rows the host will read: the received packet when this batch's host
-    // buffer holds it, else the decoded (or carried) row, copied back
+    // mode 0: the blob comes back whole, its k data rows joined on the device
+    // (records straddle rows); mode 1: the rows the host reads are the received
+    // packet when this batch's host buffer holds it, else the decoded (or
+    // carried) row, copied back
     const int64_t job = (int64_t)D->B->jobs.size();
-    for (int i = 0; i < k; ++i) {
+    if (type == 0) D->B->d2h_rows.emplace_back(job, -1);
+    for (int i = 0; i < k && type != 0; ++i) {
         auto f = g.gm.find(i);
         const RingEnt *r = f != g.gm.end() ? &D->ring[(size_t)f->second] : nullptr;
         if (r && r->host && r->in_batch) {
@@ -371,8 +501,17 @@ int input_packet(rsmi_fdec *D, const uint8_t *s, int len, uint64_t dsrc, int32_t
     }
     if (type == 0 && data_num == 0) return -1;
     if (data_num + red >= RSMI_FEC_MAX_PACKETS) return -1;
-    if (!D->ar.valid(seq, now)) return 0;
-    Group *gp = &D->group(seq);  // operator[]: inserts, as the reference's mp[seq]
+    // packets of one group mostly arrive together: the last lookup holds while
+    // neither map changed and the clock stands still (a valid seq stays valid)
+    SeqMemo &sm = D->seq_memo;
+    Group *gp;
+    if (sm.gp && sm.seq == seq && sm.now == now && sm.ar_edits == D->ar.mp.edits && sm.mp_edits == D->mp.edits) {
+        gp = sm.gp;
+    } else {
+        if (!D->ar.valid(seq, now)) return 0;
+        gp = &D->group(seq);  // inserts, as the reference's mp[seq]
+        sm = SeqMemo{gp, seq, now, D->ar.mp.edits, D->mp.edits};
+    }
     {
         Group &g = *gp;
         if (g.fec_done) return -1;
@@ -392,9 +531,15 @@ int input_packet(rsmi_fdec *D, const uint8_t *s, int len, uint64_t dsrc, int32_t
     RingEnt &slot = D->ring[(size_t)D->index];
     if (slot.used) {  // ring reuse evicts the slot's group (:554-576)
         const uint32_t tmp_seq = slot.seq;
-        D->ar.set_invalid(tmp_seq, now);
-        auto it = D->mp.find(tmp_seq);
-        if (it != D->mp.end()) D->mp.erase(it);  // other groups' references stay valid
+        // consecutive slots mostly hold one group: evicting it again is a no-op
+        // while neither map changed since and the clock stands still
+        EvictMemo &em = D->evict_memo;
+        if (!(em.valid && em.seq == tmp_seq && em.now == now && em.ar_edits == D->ar.mp.edits &&
+              em.mp_edits == D->mp.edits)) {
+            D->ar.set_invalid(tmp_seq, now);
+            D->erase_group(tmp_seq);  // other groups' references stay valid
+            em = EvictMemo{true, tmp_seq, now, D->ar.mp.edits, D->mp.edits};
+        }
         if (tmp_seq == seq) return -1;
     }
     slot.used = true;
@@ -431,9 +576,9 @@ int input_packet(rsmi_fdec *D, const uint8_t *s, int len, uint64_t dsrc, int32_t
     return 0;
 }
 
-// Output records of outs[b, e) (fec_manager.cpp:97-129 and :713-755), read from
-// the rows the host holds and the rows copied back; records that straddle two
-// rows are copied into sp.
+// Output records of outs[b, e) (fec_manager.cpp:97-129 and :713-755): mode 0
+// from the group's blob, copied back whole; mode 1 from the rows the host holds
+// and the rows copied back.
 void resolve_outputs(const Batch &X, size_t b, size_t e, Spill &sp, std::vector<Out> &res) {
     for (size_t oi = b; oi < e; ++oi) {
         const Out &o = X.outs[oi];
@@ -442,42 +587,30 @@ void resolve_outputs(const Batch &X, size_t b, size_t e, Spill &sp, std::vector<
             continue;
         }
         const Job &J = X.jobs[(size_t)o.job];
-        const RowRef *rr = X.rows.data() + J.rows0;
-        auto row = [&](int i) -> const uint8_t * {
-            return rr[i].host ? rr[i].host : X.rows_back() + rr[i].d2h;
-        };
         const int64_t L = J.len;
-        const int64_t cur = (int64_t)J.k * L;  // the blob: the k data rows back to back
-        // n bytes of the blob at pos: a pointer into one row, or a spilled copy
-        auto span = [&](int64_t pos, int64_t n) -> const uint8_t * {
-            const int64_t r = pos / L, o0 = pos - r * L;
-            if (o0 + n <= L) return row((int)r) + o0;
-            uint8_t *buf = sp.alloc((size_t)n);
-            for (int64_t c = 0; c < n;) {
-                const int64_t rr2 = (pos + c) / L, oo = pos + c - rr2 * L;
-                const int64_t t = std::min(n - c, L - oo);
-                std::memcpy(buf + c, row((int)rr2) + oo, (size_t)t);
-                c += t;
-            }
-            return buf;
-        };
         if (J.type == 0) {  // blob_decode_t::output (fec_manager.cpp:97-129)
+            const uint8_t *blob = X.rows_back() + J.lin;
+            const int64_t cur = (int64_t)J.k * L;  // the k data rows back to back
             if (cur < 4) continue;
-            const uint32_t cnt = rd_u32(span(0, 4));
+            const uint32_t cnt = rd_u32(blob);
             if (cnt > (uint32_t)kMaxBlobPackets) continue;
             int64_t pos = 4;
             const size_t mark = res.size();
             bool ok = true;
             for (uint32_t i = 0; i < cnt; ++i) {
                 if (pos + 2 > cur) { ok = false; break; }
-                const int l = (int)rd_u16(span(pos, 2));
+                const int l = (int)rd_u16(blob + pos);
                 pos += 2;
                 if (pos + l > cur) { ok = false; break; }
-                res.push_back(Out{o.event, o.job, l ? span(pos, l) : row(0), l});
+                res.push_back(Out{o.event, o.job, blob + (l ? pos : 0), l});
                 pos += l;
             }
             if (!ok) res.resize(mark);
         } else {  // mode 1 (:713-755): every data row's u16 <= max_data_len, then the missed rows
+            const RowRef *rr = X.rows.data() + J.rows0;
+            auto row = [&](int i) -> const uint8_t * {
+                return rr[i].host ? rr[i].host : X.rows_back() + rr[i].d2h;
+            };
             bool ok = true;
             for (int i = 0; i < J.k; ++i)
                 if ((int)rd_u16(row(i)) > kMaxDataLen) ok = false;
@@ -583,7 +716,7 @@ int rsmi_fdec_create(int32_t buff_num, rsmi_fdec **out) {
     rsmi_fdec *D = new rsmi_fdec();
     if (buff_num) D->buff_num = buff_num;
     D->ring.assign((size_t)D->buff_num, RingEnt{});
-    D->mp.reserve((size_t)D->buff_num * 3);
+    D->mp.rehash((size_t)D->buff_num * 4);
     *out = D;
     return RSMI_OK;
 }
@@ -630,7 +763,15 @@ int rsmi_fdec_plan(rsmi_fdec *D, int64_t n, const int32_t *len, const uint64_t *
     for (Spill &sp : D->B->spills) sp.reset();  // the chunks are reused
     D->B->staging_bytes = D->B->d2h_bytes = 0;
     D->B->host_base = host_base;
+    static const bool prof = env_int("RSMI_FDEC_PROFILE", 0) != 0;
+    const auto t0 = std::chrono::steady_clock::now();
+    // The headers are cold (a batch of packets is megabytes, read once): fetch
+    // kAhead packets ahead, so their misses overlap instead of costing one
+    // memory latency each.  mode 1 also reads the payload's u16 (bytes 8-9).
+    constexpr int64_t kAhead = 16;
+    for (int64_t i = 0; i < std::min(n, kAhead); ++i) __builtin_prefetch(host_base + off[i]);
     for (int64_t i = 0; i < n; ++i) {
+        if (i + kAhead < n) __builtin_prefetch(host_base + off[i + kAhead]);
         int r;
         if (len[i] < 0 || len[i] + 100 >= kBufLen) {
             r = -1;  // the reference asserts len + 100 < buf_len (:471)
@@ -640,6 +781,7 @@ int rsmi_fdec_plan(rsmi_fdec *D, int64_t n, const int32_t *len, const uint64_t *
         }
         if (ret) ret[i] = r;
     }
+    const auto t1 = std::chrono::steady_clock::now();
     // staging layout per bucket: rows x n shards x stride, present flags rows x n
     int64_t so = 0, po = 0;
     for (Bucket &B : D->B->buckets) {
@@ -661,22 +803,35 @@ int rsmi_fdec_plan(rsmi_fdec *D, int64_t n, const int32_t *len, const uint64_t *
         G.dst_len = (uint32_t)B.stride;
         D->B->present[(size_t)(B.present_off + J.row * B.n + idx)] = 1;
     }
+    const auto t2 = std::chrono::steady_clock::now();
     // live shards of the batch move to the carry area, at their ring slot (:587)
     for (int sidx = 0; sidx < D->buff_num; ++sidx) {
         RingEnt &r = D->ring[(size_t)sidx];
         if (!r.used || !r.in_batch) continue;
         r.in_batch = false;
-        auto it = D->mp.find(r.seq);
-        const bool live = it != D->mp.end() && !it->second.fec_done;
+        const Group *g = D->find_group(r.seq);
+        const bool live = g && !g->fec_done;
         const uint64_t dst = rsmi::kCarryTag | (uint64_t)sidx * kRingBytes;
         if (live && r.len > 0) D->B->carries.push_back(CarryCopy{r.src, dst, (uint32_t)r.len, 0});
         r.src = dst;
         r.host = nullptr;
     }
-    for (auto &jr : D->B->d2h_rows) {  // byte offsets of the rows copied back
-        const Job &J = D->B->jobs[(size_t)jr.first];
-        D->B->rows[(size_t)(J.rows0 + jr.second)].d2h = D->B->d2h_bytes;
-        D->B->d2h_bytes += (J.len + 15) & ~15;
+    for (auto &jr : D->B->d2h_rows) {  // byte offsets of the rows and blobs copied back
+        Job &J = D->B->jobs[(size_t)jr.first];
+        if (jr.second < 0) {
+            J.lin = D->B->d2h_bytes;
+            D->B->d2h_bytes += ((int64_t)J.k * J.len + 15) & ~int64_t(15);
+        } else {
+            D->B->rows[(size_t)(J.rows0 + jr.second)].d2h = D->B->d2h_bytes;
+            D->B->d2h_bytes += (J.len + 15) & ~15;
+        }
+    }
+    if (prof) {
+        const auto t3 = std::chrono::steady_clock::now();
+        fprintf(stderr, "fdec plan: packets %.3f ms, gathers %.3f ms, carries %.3f ms (%lld packets, %zu jobs)\n",
+                std::chrono::duration<double, std::milli>(t1 - t0).count(),
+                std::chrono::duration<double, std::milli>(t2 - t1).count(),
+                std::chrono::duration<double, std::milli>(t3 - t2).count(), (long long)n, D->B->jobs.size());
     }
     D->B->planned = true;
     D->B->ran = D->B->resolved = false;
@@ -713,6 +868,8 @@ int rsmi_fdec_run_dev(rsmi_fdec *D, void *stream) {
     if (!D || !D->B->planned) return fail(RSMI_ERR_INVALID, "rsmi_fdec_run_dev without a plan");
     if (D->plan_only) return fail(RSMI_ERR_INVALID, "rsmi_fdec_run_dev on a plan-only decoder");
     hipStream_t s = (hipStream_t)stream;
+    static const bool prof = env_int("RSMI_FDEC_PROFILE", 0) != 0;
+    const auto t0 = std::chrono::steady_clock::now();
     int rc0 = bind_dec(D, s);
     if (rc0) return rc0;
     Batch &prev = D->bat[D->bi ^ 1];
@@ -729,18 +886,20 @@ int rsmi_fdec_run_dev(rsmi_fdec *D, void *stream) {
     if (!rc) rc = host_grow(&D->B->hblob, &D->B->hblob_cap, (size_t)D->B->d2h_bytes + 16);
     if (!rc) rc = dev_grow(&D->dstatus, &D->status_cap, (size_t)max_rows * 4 + 16);
     if (rc) return rc;
+    const auto ta = std::chrono::steady_clock::now();
     // metadata: gathers | present | row copies back | carries, one upload
-    std::vector<CarryCopy> packs(D->B->d2h_rows.size());
-    int64_t ro = 0;
+    std::vector<JoinCopy> packs(D->B->d2h_rows.size());
     for (size_t j = 0; j < D->B->d2h_rows.size(); ++j) {
+        const int i = D->B->d2h_rows[j].second;
         const Job &J = D->B->jobs[(size_t)D->B->d2h_rows[j].first];
         const Bucket &B = D->B->buckets[(size_t)J.bucket];
-        const uint8_t *row = D->dstage + B.staging_off + (J.row * B.n + D->B->d2h_rows[j].second) * B.stride;
-        packs[j] = CarryCopy{(uint64_t)(uintptr_t)row, (uint64_t)(uintptr_t)(D->dblob + ro), (uint32_t)J.len, 0};
-        ro += (J.len + 15) & ~15;
+        const uint8_t *row = D->dstage + B.staging_off + (J.row * B.n + std::max(i, 0)) * B.stride;
+        const int64_t at = i < 0 ? J.lin : D->B->rows[(size_t)(J.rows0 + i)].d2h;
+        packs[j] = JoinCopy{(uint64_t)(uintptr_t)row, (uint64_t)(uintptr_t)(D->dblob + at), (uint32_t)J.len,
+                            i < 0 ? (uint32_t)J.k : 1u, (uint32_t)B.stride, 0};
     }
     const size_t gb = D->B->gathers.size() * sizeof(GatherCopy), pb = D->B->present.size(),
-                 kb = packs.size() * sizeof(CarryCopy), cb = D->B->carries.size() * sizeof(CarryCopy);
+                 kb = packs.size() * sizeof(JoinCopy), cb = D->B->carries.size() * sizeof(CarryCopy);
     const size_t go = 0, po = (gb + 255) & ~size_t(255), ko = (po + pb + 255) & ~size_t(255),
                  co = (ko + kb + 255) & ~size_t(255), all = co + cb + 16;
     if (all > D->meta_cap) {
@@ -750,6 +909,7 @@ int rsmi_fdec_run_dev(rsmi_fdec *D, void *stream) {
     rc = dev_grow(&D->dmeta, &D->meta_cap, all);
     if (!rc) rc = host_grow(&D->B->hmeta, &D->B->hmeta_cap, all);
     if (rc) return rc;
+    const auto tb = std::chrono::steady_clock::now();
     GatherCopy *hg = reinterpret_cast<GatherCopy *>(D->B->hmeta + go);
     for (size_t i = 0; i < D->B->gathers.size(); ++i) {
         hg[i] = D->B->gathers[i];
@@ -759,7 +919,9 @@ int rsmi_fdec_run_dev(rsmi_fdec *D, void *stream) {
     if (kb) std::memcpy(D->B->hmeta + ko, packs.data(), kb);
     if (cb) std::memcpy(D->B->hmeta + co, D->B->carries.data(), cb);
     const rsmi::CarryBase carry{{D->dcarry, D->dcarry}};
+    const auto t1 = std::chrono::steady_clock::now();
     hipError_t e = hipMemcpyAsync(D->dmeta, D->B->hmeta, all, hipMemcpyHostToDevice, s);
+    const auto t2 = std::chrono::steady_clock::now();
     if (e == hipSuccess)
         e = rsmi::launch_gather(reinterpret_cast<const GatherCopy *>(D->dmeta + go),
                                 (int64_t)D->B->gathers.size(), carry, s);
@@ -770,14 +932,22 @@ int rsmi_fdec_run_dev(rsmi_fdec *D, void *stream) {
                              B.len, B.rows, D->dmeta + po + B.present_off, D->dstatus, stream);
         if (rc) return rc;
     }
-    e = rsmi::launch_carry(reinterpret_cast<const CarryCopy *>(D->dmeta + ko), (int64_t)packs.size(),
-                           carry, s);
+    e = rsmi::launch_join(reinterpret_cast<const JoinCopy *>(D->dmeta + ko), (int64_t)packs.size(), s);
     if (e == hipSuccess)
         e = rsmi::launch_carry(reinterpret_cast<const CarryCopy *>(D->dmeta + co),
                                (int64_t)D->B->carries.size(), carry, s);
+    const auto t3 = std::chrono::steady_clock::now();
     if (e == hipSuccess && D->B->d2h_bytes)
         e = hipMemcpyAsync(D->B->hblob, D->dblob, (size_t)D->B->d2h_bytes, hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipEventRecord(D->B->done, s);
+    if (prof) {
+        const auto t4 = std::chrono::steady_clock::now();
+        auto ms = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+            return std::chrono::duration<double, std::milli>(b - a).count();
+        };
+        fprintf(stderr, "fdec run: buffers %.3f ms, packs %.3f ms, meta %.3f ms, upload %.3f ms, kernels %.3f ms, copy back %.3f ms (%zu B up, %lld B back)\n",
+                ms(t0, ta), ms(ta, tb), ms(tb, t1), ms(t1, t2), ms(t2, t3), ms(t3, t4), all, (long long)D->B->d2h_bytes);
+    }
     D->B->ext.reset();
     D->B->hblob_view = nullptr;
     D->B->stream = s;
@@ -978,7 +1148,8 @@ int rsmi_fdec_run_many(rsmi_fdcol *C, rsmi_fdec *const *dec, int32_t n, void *st
     if (rc) return rc;
     std::vector<GatherCopy> gathers;
     std::vector<uint8_t> present((size_t)po, 0);
-    std::vector<CarryCopy> packs, carries;
+    std::vector<JoinCopy> packs;
+    std::vector<CarryCopy> carries;
     auto resolve = [](const rsmi_fdec *D, uint64_t a) -> uint64_t {
         return (a & rsmi::kCarryTag) ? (uint64_t)(uintptr_t)D->dcarry + (a & rsmi::kCarryOff) : a;
     };
@@ -1003,18 +1174,20 @@ int rsmi_fdec_run_many(rsmi_fdcol *C, rsmi_fdec *const *dec, int32_t n, void *st
             gathers.push_back(G);
             present[(size_t)(c.poff + (rowbase[(size_t)i][(size_t)J.bucket] + J.row) * c.nn + idx)] = 1;
         }
-        int64_t ro = 0;
         for (const auto &jr : X.d2h_rows) {
             const Job &J = X.jobs[(size_t)jr.first];
-            packs.push_back(CarryCopy{shard_at(D, (size_t)i, J, jr.second),
-                                      (uint64_t)(uintptr_t)(C->dback + boff[(size_t)i] + ro), (uint32_t)J.len, 0});
-            ro += (J.len + 15) & ~15;
+            const Bucket &B = X.buckets[(size_t)J.bucket];
+            const int64_t at = jr.second < 0 ? J.lin : X.rows[(size_t)(J.rows0 + jr.second)].d2h;
+            packs.push_back(JoinCopy{shard_at(D, (size_t)i, J, std::max(jr.second, 0)),
+                                     (uint64_t)(uintptr_t)(C->dback + boff[(size_t)i] + at), (uint32_t)J.len,
+                                     jr.second < 0 ? (uint32_t)J.k : 1u,
+                                     (uint32_t)cbs[B.k * 257 + B.n].stride, 0});
         }
         for (const CarryCopy &cc : X.carries)
             carries.push_back(CarryCopy{resolve(D, cc.src), resolve(D, cc.dst), cc.len, 0});
     }
     const size_t gb = gathers.size() * sizeof(GatherCopy), pb = present.size(),
-                 kb = packs.size() * sizeof(CarryCopy), cb = carries.size() * sizeof(CarryCopy);
+                 kb = packs.size() * sizeof(JoinCopy), cb = carries.size() * sizeof(CarryCopy);
     const size_t go = 0, pof = (gb + 255) & ~size_t(255), ko = (pof + pb + 255) & ~size_t(255),
                  co = (ko + kb + 255) & ~size_t(255), all = co + cb + 16;
     C->cur ^= 1;
@@ -1040,7 +1213,7 @@ int rsmi_fdec_run_many(rsmi_fdcol *C, rsmi_fdec *const *dec, int32_t n, void *st
                              C->dmeta + pof + c.poff, C->dstatus, stream);
         if (rc) return rc;
     }
-    e = rsmi::launch_carry(reinterpret_cast<const CarryCopy *>(C->dmeta + ko), (int64_t)packs.size(), none, s);
+    e = rsmi::launch_join(reinterpret_cast<const JoinCopy *>(C->dmeta + ko), (int64_t)packs.size(), s);
     if (e == hipSuccess)
         e = rsmi::launch_carry(reinterpret_cast<const CarryCopy *>(C->dmeta + co), (int64_t)carries.size(), none,
                                s);

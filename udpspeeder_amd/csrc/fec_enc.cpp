@@ -236,7 +236,7 @@ int wait_set(PlanSet &B) {
 
 int grow(uint8_t **p, size_t *cap, size_t need, bool pinned) {
     if (need <= *cap) return RSMI_OK;
-    size_t c = std::max(need, *cap * 2);
+    size_t c = std::max(need + need / 4, *cap * 2);  // headroom: batch sizes wander
     c = (c + 4095) & ~size_t(4095);
     if (*p) (void)(pinned ? hipHostFree(*p) : hipFree(*p));
     *p = nullptr;

@@ -242,6 +242,34 @@ __global__ __launch_bounds__(kThreads) void k_carry(const CarryCopy *jobs, int64
     }
 }
 
+// Rows copied back (fec_dec.cpp): one wave per job, a 16-byte output piece
+// per lane; a piece that crosses a row end takes the next row's head as a
+// second window (a third and more only when len < 16).
+__global__ __launch_bounds__(kThreads) void k_join(const JoinCopy *jobs, int64_t njobs) {
+    const int lane = threadIdx.x & 63;
+    const int64_t w0 = (int64_t)blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
+    for (int64_t w = w0; w < njobs; w += (int64_t)gridDim.x * (kThreads / 64)) {
+        const JoinCopy J = jobs[w];
+        const uint8_t *src = reinterpret_cast<const uint8_t *>(J.src);
+        uint8_t *dst = reinterpret_cast<uint8_t *>(J.dst);
+        const uint32_t L = J.len, total = J.k * J.len;
+        for (uint32_t b = 16 * lane; b < total; b += 16 * 64) {
+            const uint32_t end = min(b + 16, total);
+            uint32_t r = b / L, o = b - r * L, pos = b;
+            u32x4 acc = {0, 0, 0, 0};
+            while (pos < end) {
+                const uint32_t n = min(end - pos, L - o);
+                const int lo = (int)(pos - b), hi = lo + (int)n;
+                acc |= keep(window(src + (int64_t)r * J.stride + o, lo, hi), lo, hi);
+                pos += n;
+                ++r;
+                o = 0;
+            }
+            *reinterpret_cast<u32x4 *>(dst + b) = acc;
+        }
+    }
+}
+
 // Received shard -> decode staging, zero-filled to dst_len: one wave per shard.
 __global__ __launch_bounds__(kThreads) void k_gather(const GatherCopy *jobs, int64_t njobs,
                                                       CarryBase carry) {
@@ -359,6 +387,14 @@ hipError_t launch_frame(const FrameGroup *groups, int64_t ngroups, const FrameSr
     const int64_t blocks = ngroups < 65536 ? ngroups : 65536;
     k_frame<<<(unsigned)blocks, kFThreads, 0, s>>>(groups, ngroups, srcs, carry, slots, slot_stride,
                                                    skip_clean ? 1 : 0);
+    return hipGetLastError();
+}
+
+hipError_t launch_join(const JoinCopy *jobs, int64_t njobs, hipStream_t s) {
+    if (njobs <= 0) return hipSuccess;
+    int64_t blocks = (njobs + kThreads / 64 - 1) / (kThreads / 64);
+    if (blocks > 8192) blocks = 8192;
+    k_join<<<(unsigned)blocks, kThreads, 0, s>>>(jobs, njobs);
     return hipGetLastError();
 }
 

@@ -336,6 +336,15 @@ struct GatherCopy {
     uint32_t len, dst_len;
 };
 hipError_t launch_gather(const GatherCopy *jobs, int64_t njobs, CarryBase carry, hipStream_t s);
+// Receive side, rows copied back: rows src, src + stride, ... (k of them, len
+// bytes each) joined back to back at dst (16-aligned, room for
+// round_up(k * len, 16)).  A mode-0 group's k data rows become its blob in one
+// piece, so no record straddles two rows on the host; k = 1 copies one row.
+struct JoinCopy {
+    uint64_t src, dst;  // device addresses
+    uint32_t len, k, stride, pad;
+};
+hipError_t launch_join(const JoinCopy *jobs, int64_t njobs, hipStream_t s);
 // Mode-0 stale bytes (fec_enc.cpp): a byte run between shard rows of the
 // batch's slots and the encoder's device copy of blob_encode_t's buffer.  A
 // location is a slot index (byte slots + slot*stride + kSlotShard + off) or,
