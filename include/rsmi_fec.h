@@ -256,6 +256,17 @@ int rsmi_fdec_plan(rsmi_fdec *dec, int64_t n, const int32_t *len, const uint64_t
                    const uint8_t *host_base, const uint8_t *dev_base, int64_t now_ms,
                    int32_t *ret, int64_t *n_decodes);
 
+/* rsmi_fdec_plan for n decoders at once, on up to nthreads host threads (a
+ * server's per-connection managers share nothing).  Decoder i takes packets
+ * pk0[i] .. pk0[i+1]-1 of len / off, relative to host_base[i] and (dev_base
+ * NULL or dev_base[i] NULL: plan-only) dev_base[i]; ret[pk0[i] + j] and
+ * n_decodes[i] (may be NULL) as rsmi_fdec_plan's.  Every decoder is planned;
+ * the first failure is returned. */
+int rsmi_fdec_plan_many(rsmi_fdec *const *dec, int32_t n, const int64_t *pk0, const int32_t *len,
+                        const uint64_t *off, const uint8_t *const *host_base,
+                        const uint8_t *const *dev_base, int64_t now_ms, int32_t *ret,
+                        int64_t *n_decodes, int32_t nthreads);
+
 /* Gather, decode, pack and copy back the planned groups on `stream`
  * (asynchronous; dev_base must stay valid until it completes). */
 int rsmi_fdec_run_dev(rsmi_fdec *dec, void *stream);

@@ -96,6 +96,29 @@ def test_planner_ret_matches_reference(fx, name, nbatch):
     dec.close()
 
 
+@pytest.mark.parametrize("nthreads", [1, 4])
+def test_planner_plan_many_matches_reference(fx, nthreads):
+    """rsmi_fdec_plan_many (every decoder planned on a pool of host threads):
+    each decoder's return codes over 3 batches equal the reference's."""
+    from udpspeeder_amd.fec import FecDecodeCollector, FecDecoder
+    cases = [_case(fx, NAMES[i % len(NAMES)]) for i in range(2 * len(NAMES))]
+    packed = [_pack(c["chan"]) for c in cases]
+    decs = [FecDecoder() for _ in cases]
+    col = FecDecodeCollector()
+    ret = [[] for _ in cases]
+    for bi in range(3):
+        cuts = [np.linspace(0, len(p[1]), 4).astype(int)[bi:bi + 2] for p in packed]
+        plans = col.plan_many(decs, [p[0] for p in packed], [p[1][a:b] for p, (a, b) in zip(packed, cuts)],
+                              [p[2][a:b] for p, (a, b) in zip(packed, cuts)], nthreads=nthreads)
+        for i, pl in enumerate(plans):
+            ret[i] += list(pl.ret)
+    for i, c in enumerate(cases):
+        assert ret[i] == c["ret"], i
+    col.close()
+    for d in decs:
+        d.close()
+
+
 def _long_run(mode, rs, seed, n=6000, lmax=900):
     rng = np.random.default_rng(seed)
     em = EncodeManager(rs, mode, 1250, 200, seed)
@@ -258,7 +281,8 @@ def test_gpu_per_call_interface(gpu):
 
 
 @pytest.mark.gpu
-def test_gpu_decode_collector_200_connections_match_reference(fx, gpu):
+@pytest.mark.parametrize("native_plan", [False, True])
+def test_gpu_decode_collector_200_connections_match_reference(fx, gpu, native_plan):
     """The receive-side collector (rsmi_fdec_run_many): 200 decoders, one per
     connection (connection.h:244-245, max_conn_num = 200, common.h:112), each
     fed its own golden channel (case i % len(DEC_CASES), cut into 3 batches at its own
@@ -282,10 +306,17 @@ def test_gpu_decode_collector_200_connections_match_reference(fx, gpu):
     ret = [[] for _ in range(ncon)]
     out = [[] for _ in range(ncon)]
     for bi in range(3):
-        for ci in range(ncon):
-            host, lens, offs = packed[ci]
-            a, b = cuts[ci][bi], cuts[ci][bi + 1]
-            ret[ci] += list(decs[ci].plan(host, lens[a:b], offs[a:b], devs[ci]).ret)
+        if native_plan:  # rsmi_fdec_plan_many: all 200 planned on host threads
+            sl = [slice(cuts[ci][bi], cuts[ci][bi + 1]) for ci in range(ncon)]
+            plans = col.plan_many(decs, [p[0] for p in packed], [p[1][s] for p, s in zip(packed, sl)],
+                                  [p[2][s] for p, s in zip(packed, sl)], devs)
+            for ci in range(ncon):
+                ret[ci] += list(plans[ci].ret)
+        else:
+            for ci in range(ncon):
+                host, lens, offs = packed[ci]
+                a, b = cuts[ci][bi], cuts[ci][bi + 1]
+                ret[ci] += list(decs[ci].plan(host, lens[a:b], offs[a:b], devs[ci]).ret)
         col.run_many(decs)
         for ci in range(ncon):
             a = cuts[ci][bi]

@@ -145,6 +145,7 @@ def _bind(lib: C.CDLL) -> C.CDLL:
         "rsmi_fcol_destroy": ([vp], None),
         "rsmi_fenc_run_many": ([vp, vp, C.c_int32, vp, i64, vp, C.c_uint64, vp, vp, vp], i32),
         "rsmi_fenc_plan_many": ([vp, i32, vp, vp, vp, vp, vp, vp, vp, vp, i32], i32),
+        "rsmi_fdec_plan_many": ([vp, i32, vp, vp, vp, vp, vp, i64, vp, vp, i32], i32),
         "rsmi_fdcol_create": ([vp], i32),
         "rsmi_fdcol_destroy": ([vp], None),
         "rsmi_fdec_run_many": ([vp, vp, C.c_int32, vp], i32),

@@ -35,6 +35,7 @@
 
 namespace rsmi {
 void set_error(const std::string &m);
+const char *last_error();
 }
 
 using rsmi::GatherCopy;
@@ -863,6 +864,39 @@ int bind_dec(rsmi_fdec *D, hipStream_t s) {
 }  // namespace
 
 extern "C" {
+
+// The managers of a server's connections share nothing (connection.h:244-245),
+// so rsmi_fdec_plan_many runs rsmi_fdec_plan for each on the pool of host
+// threads (host_pool.cpp), as rsmi_fenc_plan_many does on the send side.
+int rsmi_fdec_plan_many(rsmi_fdec *const *dec, int32_t n, const int64_t *pk0, const int32_t *len,
+                        const uint64_t *off, const uint8_t *const *host_base,
+                        const uint8_t *const *dev_base, int64_t now_ms, int32_t *ret,
+                        int64_t *n_decodes, int32_t nthreads) {
+    if (n < 0 || (n && (!dec || !pk0 || !host_base)))
+        return fail(RSMI_ERR_INVALID, "rsmi_fdec_plan_many: bad arguments");
+    for (int i = 0; i < n; ++i) {
+        if (!dec[i] || pk0[i + 1] < pk0[i]) return fail(RSMI_ERR_INVALID, "rsmi_fdec_plan_many: bad decoder or range");
+        for (int j = 0; j < i; ++j)
+            if (dec[j] == dec[i]) return fail(RSMI_ERR_INVALID, "rsmi_fdec_plan_many: a decoder listed twice");
+    }
+    std::vector<int> rcs((size_t)n, RSMI_OK);
+    std::vector<std::string> errs((size_t)n);
+    rsmi::host_parallel_for(n, nthreads > 0 ? nthreads : 8, [&](int i) {
+        const int64_t a = pk0[i], cnt = pk0[i + 1] - pk0[i];
+        int64_t nd = 0;
+        const int rc = rsmi_fdec_plan(dec[i], cnt, len ? len + a : nullptr, off ? off + a : nullptr, host_base[i],
+                                      dev_base ? dev_base[i] : nullptr, now_ms, ret ? ret + a : nullptr, &nd);
+        rcs[(size_t)i] = rc;
+        if (rc) {
+            errs[(size_t)i] = rsmi::last_error();
+            return;
+        }
+        if (n_decodes) n_decodes[i] = nd;
+    });
+    for (int i = 0; i < n; ++i)
+        if (rcs[(size_t)i]) return fail(rcs[(size_t)i], "decoder " + std::to_string(i) + ": " + errs[(size_t)i]);
+    return RSMI_OK;
+}
 
 int rsmi_fdec_run_dev(rsmi_fdec *D, void *stream) {
     if (!D || !D->B->planned) return fail(RSMI_ERR_INVALID, "rsmi_fdec_run_dev without a plan");

@@ -469,6 +469,35 @@ class FecDecodeCollector:
         except Exception:
             pass
 
+    def plan_many(self, decoders, host_bufs, lens, offsets, dev_bufs=None, now_ms: int = 0,
+                  nthreads: int = 8):
+        """rsmi_fdec_plan_many: FecDecoder.plan for every decoder (packets
+        lens[i] / offsets[i] into host_bufs[i] and dev_bufs[i]; dev_bufs None:
+        plan only) on up to nthreads host threads.  Returns the per-decoder
+        FdecPlan list."""
+        n = len(decoders)
+        counts = np.array([len(l) for l in lens], np.int64)
+        pk0 = np.zeros(n + 1, np.int64)
+        np.cumsum(counts, out=pk0[1:])
+        L = np.ascontiguousarray(np.concatenate(lens) if n else np.zeros(0), np.int32)
+        O = np.ascontiguousarray(np.concatenate(offsets) if n else np.zeros(0), np.uint64)
+        ret = np.zeros(max(1, L.size), np.int32)
+        nd = np.zeros(max(1, n), np.int64)
+        arr = (C.c_void_p * max(1, n))(*[d._h.value for d in decoders])
+        hb = (C.c_void_p * max(1, n))(*[h.ctypes.data for h in host_bufs])
+        db = None
+        if dev_bufs is not None:
+            db = (C.c_void_p * max(1, n))(*[(d.data_ptr() if d is not None else None) for d in dev_bufs])
+        check(lib().rsmi_fdec_plan_many(arr, n, pk0.ctypes.data, L.ctypes.data if L.size else None,
+                                        O.ctypes.data if O.size else None, hb, db, int(now_ms),
+                                        ret.ctypes.data, nd.ctypes.data, int(nthreads)), "rsmi_fdec_plan_many")
+        plans = []
+        for i, d in enumerate(decoders):
+            dv = dev_bufs[i] if dev_bufs is not None else None
+            d._keep = ((host_bufs[i], dv), (d._keep or (None,))[0])
+            plans.append(FdecPlan(ret[pk0[i]:pk0[i + 1]].copy(), int(nd[i])))
+        return plans
+
     def run_many(self, decoders, stream=None):
         import torch
         s = stream if stream is not None else torch.cuda.current_stream()
