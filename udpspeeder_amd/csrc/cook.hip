@@ -67,6 +67,11 @@ constexpr int kPpl = 96 / kLpp;         // pieces per lane per round
 #ifndef COOK_SB
 #define COOK_SB 1  // scheduling fence every COOK_SB pieces (0: none), bounds registers
 #endif
+#ifndef COOK_DEFER
+#define COOK_DEFER 0  // k_cook, bit 0: a piece's key-stream load issued before its CRC;
+                      // bit 1: the round's stores after the round (in vmcnt, a store made
+                      // the next piece's key-stream load wait for it)
+#endif
 constexpr int kThreads = kLpp == 32 ? 512 : 256;  // LDS (tables per block) bounds residency
 constexpr int kRound = 1536;            // 96 pieces per packet per round
 constexpr int kScrCook = 144;           // per-packet LDS: iv2[64] | overlay[64] | misc[16]
@@ -483,12 +488,21 @@ __global__ __launch_bounds__(kThreads, COOK_OCC) void k_cook(CookArgs a) {
 #pragma unroll
             for (int p = 0; p < kPplC; ++p) {
                 const int P = r * kRoundC + 16 * (kLpp * p + hl);  // grid offset
-                if (ck && kLpp * p < qr_max) rc.add(T, crc_in_ph(cur[p], P, Lg, ph), p, kLpp * p + hl, qr);
                 // wholly payload (the head piece's bytes before the packet are scratch)
-                if (P < ext && P + 16 <= Lg) {  // obscure + xor, store now
-                    u32x4 m = ks_piece(a, P - ph);
+                const bool whole = P < ext && P + 16 <= Lg;
+                u32x4 m = {0, 0, 0, 0};
+                if ((COOK_DEFER & 1) && whole) {  // the key stream's load flies during the CRC
+                    m = ks_piece(a, P - ph);
                     if (ivl) m ^= iv_window_at(iv2w, ivr);
-                    st_piece(oga + P, cur[p] ^ m);
+                }
+                if (ck && kLpp * p < qr_max) rc.add(T, crc_in_ph(cur[p], P, Lg, ph), p, kLpp * p + hl, qr);
+                if (whole) {  // obscure + xor
+                    if (!(COOK_DEFER & 1)) {
+                        m = ks_piece(a, P - ph);
+                        if (ivl) m ^= iv_window_at(iv2w, ivr);
+                    }
+                    if (COOK_DEFER & 2) cur[p] ^= m;  // stored after the round
+                    else st_piece(oga + P, cur[p] ^ m);
                 } else if (P < ext && P >= P0) {
                     dt = cur[p];
                     Pt = P;
@@ -496,6 +510,13 @@ __global__ __launch_bounds__(kThreads, COOK_OCC) void k_cook(CookArgs a) {
                 if (ivl) ivr = iv_step(ivr, sstep, (uint32_t)ivl);
                 if (COOK_SB && p % COOK_SB == COOK_SB - 1)
                     __builtin_amdgcn_sched_barrier(0);  // COOK_SB pieces' lookups at a time
+            }
+            if (COOK_DEFER & 2) {
+#pragma unroll
+                for (int p = 0; p < kPplC; ++p) {
+                    const int P = r * kRoundC + 16 * (kLpp * p + hl);
+                    if (P < ext && P + 16 <= Lg) st_piece(oga + P, cur[p]);
+                }
             }
             if (ck) {
                 const uint32_t c = rc.finish(T, qr);
