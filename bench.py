@@ -44,6 +44,22 @@ C4_GROUPS = 1 << 20
 SETTLE_EXTRA_MS = 150.0  # untimed calls before each other_configs measurement (clock ramp)
 TRAFFIC = {"encode": os.path.join(ROOT, "profiles", "traffic.json"),
            "decode": os.path.join(ROOT, "profiles", "traffic_decode.json")}
+# The sources a kernel's counters depend on: a traffic JSON carries their
+# digest from the counter pass (scripts/pmc_traffic.py), and roofline() reports
+# its bytes only while the sources are unchanged.
+KERNEL_SOURCES = {"encode": ["udpspeeder_amd/csrc/bitslice.hip", "udpspeeder_amd/csrc/bitslice_kern.hpp",
+                             "udpspeeder_amd/csrc/gen_bitslice.py"],
+                  "decode": ["udpspeeder_amd/csrc/decode.hip", "udpspeeder_amd/csrc/lagrange.hpp"]}
+
+
+def kernel_source_sha(which):
+    import hashlib
+    h = hashlib.sha256()
+    for rel in KERNEL_SOURCES[which]:
+        h.update(rel.encode() + b"\0")
+        with open(os.path.join(ROOT, rel), "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()
 
 
 def parse(argv=None):
@@ -484,19 +500,23 @@ def verify_slice(u, synth, torch, buf, present, g0, G):
 
 def roofline(which, kernel, alg_bytes, ms, G):
     achieved = alg_bytes / (ms * 1e-3) / 1e9
-    traffic = None
+    traffic, note = None, "no counter pass for this kernel and size"
     path = TRAFFIC[which]
     if os.path.exists(path):
         try:
             tj = json.load(open(path))
-            # only counters of the kernel this build launches
+            # only counters of the kernel this build launches, from its current sources
             if tj.get("groups") == G and kernel.split(":")[0] == tj.get("kernel"):
-                traffic = tj.get("hbm_bytes_per_launch")
+                if tj.get("source_sha256") == kernel_source_sha(which):
+                    traffic = tj.get("hbm_bytes_per_launch")
+                    note = f"PMC pass {os.path.relpath(path, ROOT)} (sources unchanged since)"
+                else:
+                    note = "stale: the kernel's sources changed since the counter pass"
         except (OSError, ValueError):
             traffic = None
     return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": kernel,
-            "alg_bytes_per_launch": int(alg_bytes), "avg_launch_ms": round(ms, 4)}
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": note,
+            "kernel": kernel, "alg_bytes_per_launch": int(alg_bytes), "avg_launch_ms": round(ms, 4)}
 
 
 def rehearse(args, world, rank, scaling):

@@ -10,7 +10,7 @@ export PMC_SETS="FETCH_SIZE;WRITE_SIZE;SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_I
 bash scripts/pmc_passes.sh pmc5_codec k_bs2_20_30 k_decode_fused -- scripts/ab_encode.py
 O=gpurun_out/pmc5_codec
 python scripts/pmc_traffic.py $O/p1/run_counter_collection.csv $O/p2/run_counter_collection.csv \
-    k_bs2_20_30 65536 2457600000 > $O/traffic.json
+    k_bs2_20_30 65536 2457600000 encode > $O/traffic.json
 python - <<'PY' > $O/alg_decode.txt
 import sys; sys.path.insert(0, ".")
 from udpspeeder_amd import synth
@@ -19,7 +19,7 @@ e = (p[:, :20] == 0).sum(1)
 print(int(((e > 0) * 20 * 1250).sum() + (e * 1250).sum()))
 PY
 python scripts/pmc_traffic.py $O/p1/run_counter_collection.csv $O/p2/run_counter_collection.csv \
-    k_decode_fused 65536 $(cat $O/alg_decode.txt) > $O/traffic_decode.json
+    k_decode_fused 65536 $(cat $O/alg_decode.txt) decode > $O/traffic_decode.json
 cat $O/traffic.json $O/traffic_decode.json
 bash scripts/pmc_passes.sh pmc5_cook k_cook k_decook -- scripts/bench_cook.py
 bash scripts/pmc_passes.sh pmc5_c3 k_bs_ragged k_decode_ragged_mix -- scripts/bench_c3.py

@@ -47,3 +47,21 @@ def test_world_size_mismatch_is_an_error():
     p = _run(["--gpus", "8", "--rehearse"], {"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
     assert p.returncode != 0 and "WORLD_SIZE=1" in p.stderr
     assert not [l for l in p.stdout.splitlines() if l.startswith("{")]
+
+
+def test_roofline_traffic_only_from_current_sources(tmp_path, monkeypatch):
+    """roofline.traffic comes from a counter pass only while the kernel's
+    sources still hash to the digest stamped into it; otherwise it is null and
+    marked stale."""
+    sys.path.insert(0, ROOT)
+    import bench
+    for which, kern in (("encode", "k_bs2_20_30"), ("decode", "k_decode_fused")):
+        tj = {"kernel": kern, "groups": 65536, "hbm_bytes_per_launch": 123.0,
+              "source_sha256": bench.kernel_source_sha(which)}
+        p = tmp_path / f"{which}.json"
+        p.write_text(json.dumps(tj))
+        monkeypatch.setitem(bench.TRAFFIC, which, str(p))
+        assert bench.roofline(which, kern + ": x", 1e9, 0.5, 65536)["traffic"] == 123.0
+        p.write_text(json.dumps(dict(tj, source_sha256="0" * 64)))
+        r = bench.roofline(which, kern + ": x", 1e9, 0.5, 65536)
+        assert r["traffic"] is None and r["traffic_source"].startswith("stale")
