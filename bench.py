@@ -914,10 +914,22 @@ def dropin_latency(u, calls=300):
         td.append(time.perf_counter() - t0)
         if rc:
             raise SystemExit("dropin_latency: rs_decode2 failed")
-    return {"rs_encode2": round(statistics.median(te[20:]) * 1e6, 1),
-            "rs_decode2": round(statistics.median(td[20:]) * 1e6, 1),
+    # the same calls timed in C (rsmi_dropin_latency), the harness of the
+    # reference's per-call figure (cpu_baseline.single_thread): no ctypes
+    # dispatch or interpreter time in the number
+    L = u.lib()
+    pres = np.ones(n, np.uint8)
+    pres[erased] = 0
+    ce, cd = C.c_double(), C.c_double()
+    if L.rsmi_dropin_latency(0, K, n, LEN, None, calls, C.byref(ce)) or \
+            L.rsmi_dropin_latency(1, K, n, LEN, pres.ctypes.data, calls, C.byref(cd)):
+        raise SystemExit("dropin_latency: rsmi_dropin_latency failed")
+    return {"rs_encode2": round(ce.value, 1), "rs_decode2": round(cd.value, 1),
             "calls": calls, "what": "one RS(20,10) 1250-B group per call, host buffers, "
-                                    "synchronous"}
+                                    "synchronous; median, timed in C like the reference's per-call figure",
+            "python_ctypes": {"rs_encode2": round(statistics.median(te[20:]) * 1e6, 1),
+                              "rs_decode2": round(statistics.median(td[20:]) * 1e6, 1),
+                              "what": "the same calls from Python through ctypes"}}
 
 
 def dropin_latency_both(u):

@@ -80,19 +80,28 @@ const char *rsmi_last_error(void);
  * of many workgroup rounds).  Read when a plan is created. */
 #define RSMI_OPT_CLS_REC_CAP 4
 /* RSMI_OPT_ONE_SERVER: idle timeout in microseconds of the resident
- * one-group server (default 20000; 0 turns it off and stops a running one).
- * With it on, a single-group host call (RSMI_OPT_ONE_GROUP) posts its group
- * to a one-workgroup kernel that stays resident on the device between calls
- * and polls a doorbell in pinned host memory -- no kernel launch on the
- * per-call path (UDPspeeder calls rs_decode2 once per group, synchronously,
- * fec_manager.cpp:632,710).  The server ends after that long without a call
- * (or 10 s in any case) and is relaunched by the next call.  While it runs it
- * holds one CU and its stream's hardware queue: device-wide synchronisation
+ * one-group server (default 20000, or RSMI_ONE_SERVER_IDLE_US; 0 turns it off
+ * and stops a running one).  With it on, a single-group host call
+ * (RSMI_OPT_ONE_GROUP) posts its group to a 16-workgroup kernel that stays
+ * resident on the device between calls and polls a doorbell in pinned host
+ * memory -- no kernel launch on the per-call path (UDPspeeder calls
+ * rs_decode2 once per group, synchronously, fec_manager.cpp:632,710).  The
+ * server ends after that long without a call (or 10 s in any case) and is
+ * relaunched by the next call.  While it runs it holds 16 CUs' worth of
+ * workgroups and its stream's hardware queue: device-wide synchronisation
  * (hipDeviceSynchronize, torch.cuda.synchronize) waits for it to go idle,
  * and work on a stream that shares that hardware queue waits as well -- a
  * process that mixes drop-in calls with its own GPU work may prefer 0. */
 #define RSMI_OPT_ONE_SERVER 5
+
 int rsmi_set_option(int option, int value);
+
+/* Median wall time in microseconds of one drop-in rs_encode2 (decode 0) or
+ * rs_decode2 (decode 1; rows with present[j] == 0 erased) call on host
+ * buffers, k / n / len, over `calls` calls after 20 untimed ones, timed in C
+ * (the harness the reference's per-call figure is timed with). */
+int rsmi_dropin_latency(int decode, int k, int n, int len, const uint8_t *present, int calls,
+                        double *median_us);
 
 /* Host copy of fec_new(k,n)'s n x k systematic encoding matrix (row-major),
  * lib/fec.cpp:665-720.  Valid: 1 <= k <= n <= 256. */

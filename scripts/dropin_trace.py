@@ -33,6 +33,12 @@ def med(calls=400):
         te.append(time.perf_counter() - t0)
     out = {"rs_decode2_us": round(statistics.median(td[20:]) * 1e6, 2),
            "rs_encode2_us": round(statistics.median(te[20:]) * 1e6, 2)}
+    pres = np.ones(n, np.uint8)
+    pres[list(erased)] = 0
+    cd, ce = C.c_double(), C.c_double()
+    assert L.rsmi_dropin_latency(1, k, n, ln, pres.ctypes.data, calls, C.byref(cd)) == 0
+    assert L.rsmi_dropin_latency(0, k, n, ln, None, calls, C.byref(ce)) == 0
+    out["c_timed"] = {"rs_decode2_us": round(cd.value, 2), "rs_encode2_us": round(ce.value, 2)}
     return out
 
 

@@ -99,3 +99,20 @@ def test_server_latency_beats_launch_per_call(gpu):
         L.rsmi_set_option(OPT_ONE_GROUP, prev1)
     print(f"rs_decode2 median: server {t_srv:.1f} us, launch per call {t_launch:.1f} us")
     assert t_srv < t_launch
+
+
+@pytest.mark.gpu
+def test_c_timed_latency_helper(gpu):
+    """rsmi_dropin_latency (the bench's C-timed per-call figure) runs both
+    calls through the default path and reports a plausible median."""
+    import ctypes as C
+    import udpspeeder_amd as u
+    L = u.lib()
+    k, n, ln = 20, 30, 1250
+    pres = np.ones(n, np.uint8)
+    pres[[1, 4, 9, 22, 27]] = 0
+    d, e = C.c_double(), C.c_double()
+    assert L.rsmi_dropin_latency(1, k, n, ln, pres.ctypes.data, 50, C.byref(d)) == 0
+    assert L.rsmi_dropin_latency(0, k, n, ln, None, 50, C.byref(e)) == 0
+    assert 0 < d.value < 1000 and 0 < e.value < 1000
+    assert L.rsmi_dropin_latency(1, k, n, ln, None, 50, C.byref(d)) != 0  # decode needs present

@@ -86,6 +86,7 @@ def _bind(lib: C.CDLL) -> C.CDLL:
     sig = {
         "rsmi_version": ([], i32),
         "rsmi_set_option": ([i32, i32], i32),
+        "rsmi_dropin_latency": ([i32, i32, i32, i32, vp, i32, vp], i32),
         "rsmi_init": ([], i32),
         "rsmi_last_error": ([], C.c_char_p),
         "rsmi_get_matrix": ([i32, i32, vp], i32),

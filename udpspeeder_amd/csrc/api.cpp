@@ -459,11 +459,23 @@ void stop_servers_at_exit() {
         if (D->srv_pin) reinterpret_cast<volatile uint32_t *>(&D->srv_pin->quit)[0] = 1u;
 }
 
+// Pinned memory of the one-group path (staging, server control block):
+// RSMI_ONE_HOSTMEM = 0 hipHostMallocDefault, 1 coherent, 2 uncached (A/B knob).
+unsigned one_hostmem_flags() {
+    static const unsigned f = [] {
+        const char *e = getenv("RSMI_ONE_HOSTMEM");
+        const int v = e ? atoi(e) : 0;
+        return v == 1 ? (unsigned)hipHostMallocCoherent : v == 2 ? (unsigned)hipHostMallocUncached
+                                                                 : (unsigned)hipHostMallocDefault;
+    }();
+    return f;
+}
+
 // caller holds D.one_mu
 int launch_server(Device &D, uint32_t done0, uint32_t idle_us) {
     if (!D.srv_pin) {
         void *hp = nullptr, *dp = nullptr;
-        RSMI_HIP(hipHostMalloc(&hp, sizeof(OneSrvCtl), hipHostMallocDefault), "hipHostMalloc(server)");
+        RSMI_HIP(hipHostMalloc(&hp, sizeof(OneSrvCtl), one_hostmem_flags()), "hipHostMalloc(server)");
         RSMI_HIP(hipHostGetDevicePointer(&dp, hp, 0), "hipHostGetDevicePointer(server)");
         std::memset(hp, 0, sizeof(OneSrvCtl));
         RSMI_HIP(hipMalloc(&D.srv_dv, sizeof(OneSrvDev)), "hipMalloc(server)");
@@ -535,7 +547,7 @@ int one_group_op(Device &D, bool decode, int k, int n, uint8_t *const *ptrs, uin
         D.one_pin = D.one_dev = nullptr;
         D.one_bytes = 0;
         const size_t cap = std::max<size_t>(need, 64 * 1024);
-        RSMI_HIP(hipHostMalloc(&D.one_pin, cap, hipHostMallocDefault), "hipHostMalloc(one)");
+        RSMI_HIP(hipHostMalloc(&D.one_pin, cap, one_hostmem_flags()), "hipHostMalloc(one)");
         void *dp = nullptr;
         RSMI_HIP(hipHostGetDevicePointer(&dp, D.one_pin, 0), "hipHostGetDevicePointer(one)");
         D.one_dev = static_cast<uint8_t *>(dp);

@@ -7,6 +7,8 @@
 // (pinned staging -> HIP kernels -> copy back).  Per-call cost is therefore
 // PCIe-latency-bound; fec_manager-scale throughput comes from the batched
 // rsmi_* API.  There is no CPU fallback.
+#include <algorithm>
+#include <chrono>
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
@@ -200,4 +202,41 @@ int rs_decode2(int k, int n, char *data[], int size) {
     void *code = get_code(k, n);
     if (!code) return 1;
     return rs_decode(code, data, size);
+}
+
+// Per-call latency of the drop-in, timed in C as the reference's per-call
+// figure is (bench.py cpu_baseline times lib/rs.cpp's calls in a C loop), so
+// the two numbers carry the same harness: `calls` calls after 20 untimed ones,
+// each on fresh pointer arrays built outside the timed region; decode erases
+// the rows whose present[j] is 0.  *median_us receives the median.
+extern "C" int rsmi_dropin_latency(int decode, int k, int n, int len, const uint8_t *present, int calls,
+                                   double *median_us) {
+    if (k < 1 || n <= k || n > 256 || len < 0 || calls < 1 || !median_us || (decode && !present))
+        return RSMI_ERR_INVALID;
+    std::vector<std::vector<char>> rows((size_t)n, std::vector<char>((size_t)len + 1));
+    uint64_t x = 0x9E3779B97F4A7C15ull;
+    for (auto &r : rows)
+        for (char &c : r) {
+            x ^= x << 13; x ^= x >> 7; x ^= x << 17;
+            c = (char)x;
+        }
+    std::vector<char *> ptrs((size_t)n);
+    for (int j = 0; j < n; ++j) ptrs[(size_t)j] = rows[(size_t)j].data();
+    if (decode) rs_encode2(k, n, ptrs.data(), len);  // a codeword: every call rebuilds the same rows
+    std::vector<double> t;
+    t.reserve((size_t)calls);
+    for (int i = 0; i < calls + 20; ++i) {
+        for (int j = 0; j < n; ++j) ptrs[(size_t)j] = (decode && !present[j]) ? nullptr : rows[(size_t)j].data();
+        const auto t0 = std::chrono::steady_clock::now();
+        if (decode) {
+            if (rs_decode2(k, n, ptrs.data(), len) != 0) return RSMI_ERR_HIP;
+        } else {
+            rs_encode2(k, n, ptrs.data(), len);
+        }
+        const auto t1 = std::chrono::steady_clock::now();
+        if (i >= 20) t.push_back(std::chrono::duration<double, std::micro>(t1 - t0).count());
+    }
+    std::nth_element(t.begin(), t.begin() + (ptrdiff_t)(t.size() / 2), t.end());
+    *median_us = t[t.size() / 2];
+    return RSMI_OK;
 }

@@ -481,6 +481,12 @@ __global__ __launch_bounds__(kMwThreads) void k_one_multi(OneArgs a) {
 // server for the next job (a job that workgroups saw in part before they
 // stopped is run again whole by the next server: a job's outputs depend only
 // on its inputs).
+#ifndef SRV_PIPE
+#define SRV_PIPE 1  // k_one_server: 4 = four job polls in flight per wave, 1 = one round trip per poll
+#endif
+#ifndef SRV_GAP
+#define SRV_GAP 4  // s_sleep units (64 clocks each) between two polls
+#endif
 __device__ __forceinline__ uint32_t sys_load(const uint32_t *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -501,6 +507,60 @@ __global__ __launch_bounds__(kMwThreads) void k_one_server(OneSrvCtl *ctl, OneSr
     for (;;) {
         if (tid < 64) {
             uint32_t cmd = 0, seq = 0, w = 0;
+#if SRV_PIPE > 1
+            // four polls in flight, one issued every SRV_GAP sleep: a job is seen
+            // about one PCIe round trip after it lands, not up to two.  Lanes
+            // 0..29 read the job words, 30-31 the quit word, 32-63 workgroup 0's
+            // stop word (no exec mask and no other load in the loop, so every
+            // wait is for one poll and the rest stay in flight)
+            const uint64_t *pa = lane < kOneJobWords ? &ctl->job[lane]
+                                 : lane < 32       ? reinterpret_cast<const uint64_t *>(&ctl->quit)
+                                                   : reinterpret_cast<const uint64_t *>(&dv->stop);
+            bool stop = false;
+            auto check = [&](uint64_t jw) -> bool {
+                w = (uint32_t)jw;
+                const uint32_t js = (uint32_t)(jw >> 32);
+                const uint32_t s0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)js);
+                const bool torn = __ballot(lane < kOneJobWords && js != s0) != 0;  // host mid-write
+                if (!torn && s0 != done) {
+                    cmd = 1;
+                    seq = s0;
+                    return true;
+                }
+                if (wg == 0) {
+                    const uint32_t q = (uint32_t)__builtin_amdgcn_readlane((int)w, 30);
+                    const uint64_t now = __builtin_amdgcn_s_memrealtime();
+                    if (q || now - t_last > idle_ticks || now - t_start > life_ticks) {
+                        if (lane == 0) __hip_atomic_store(&dv->stop, gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                        stop = true;
+                        return true;
+                    }
+                } else if ((uint32_t)__builtin_amdgcn_readlane((int)w, 32) == gen) {
+                    stop = true;
+                    return true;
+                }
+                return false;
+            };
+            uint64_t r0 = sys_load64(pa);
+            __builtin_amdgcn_s_sleep(SRV_GAP);
+            uint64_t r1 = sys_load64(pa);
+            __builtin_amdgcn_s_sleep(SRV_GAP);
+            uint64_t r2 = sys_load64(pa);
+            __builtin_amdgcn_s_sleep(SRV_GAP);
+            uint64_t r3 = sys_load64(pa);
+#define SRV_STEP(R)                             \
+    if (check(R)) break;                        \
+    __builtin_amdgcn_s_sleep(SRV_GAP);          \
+    R = sys_load64(pa);
+            for (;;) {
+                SRV_STEP(r0)
+                SRV_STEP(r1)
+                SRV_STEP(r2)
+                SRV_STEP(r3)
+            }
+#undef SRV_STEP
+            (void)stop;
+#else
             for (;;) {
                 const uint64_t jw = lane < kOneJobWords ? sys_load64(&ctl->job[lane]) : 0ull;
                 w = (uint32_t)jw;
@@ -518,8 +578,9 @@ __global__ __launch_bounds__(kMwThreads) void k_one_server(OneSrvCtl *ctl, OneSr
                 } else if (__hip_atomic_load(&dv->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gen) {
                     break;
                 }
-                __builtin_amdgcn_s_sleep(4);
+                __builtin_amdgcn_s_sleep(SRV_GAP);
             }
+#endif
             if (lane < kOneJobWords) S.args[lane] = w;
             if (lane == 0) {
                 S.cmd = cmd;
