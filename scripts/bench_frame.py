@@ -59,6 +59,7 @@ def main():
     ap.add_argument("--fec", default="20:10")
     ap.add_argument("--cpu-sample", type=int, default=100000, help="0 = no CPU baseline")
     ap.add_argument("--cook", default="", choices=["", "dev", "host", "sep"])
+    ap.add_argument("--cook-flags", type=int, default=0, help="RSMI_COOK_NO_* flags (measurement: 1 = no CRC)")
     args = ap.parse_args()
     plen = args.len or (1200 if args.mode == 0 else 1250)
     npk = args.groups * 20
@@ -73,7 +74,7 @@ def main():
     ctx = None
     if args.cook:
         from udpspeeder_amd.cook import CookContext
-        ctx = CookContext(b"passwd123")
+        ctx = CookContext(b"passwd123", args.cook_flags)
     for rep in range(args.reps + 1):
         t0 = time.perf_counter()
         p = enc.plan(lens, offs, inbuf)

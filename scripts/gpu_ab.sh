@@ -14,6 +14,7 @@ for i in 1 2 3; do
     for b in $benches; do
       args=""
       [ "$b" = cook ] && args="--cpu-sample 0 --iters 20"
+      [ "$b" = frame ] && args="--cook dev --cpu-sample 0"
       if [ "$lib" = default ]; then
         echo -n "default $b: "; timeout -k 10 150 python -u scripts/bench_$b.py $args | tr '\n' ' ' || exit 1
       else

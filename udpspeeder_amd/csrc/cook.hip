@@ -717,6 +717,13 @@ static_assert(kFuseRecs <= kLpp, "k_cook_frame needs a lane per source record (C
 #ifndef COOKF_OCC
 #define COOKF_OCC COOK_OCC
 #endif
+#ifndef COOKF_PROBE
+#define COOKF_PROBE 0  // measurement only (wrong output): 1 no plain slot stores, 2 no cooked
+                       // stores, 4 no source loads (zeros)
+#endif
+#ifndef COOKF_ONE_CHAIN
+#define COOKF_ONE_CHAIN 1  // k_cook_frame: one Horner chain per lane across its rounds
+#endif
 constexpr int kPplF = COOKF_PPL;
 constexpr int kRoundF = 16 * kLpp * kPplF;
 
@@ -821,6 +828,13 @@ __global__ __launch_bounds__(kThreads, COOKF_OCC) void k_cook_frame(CookArgs a, 
         uint32_t acc = 0;
         u32x4 dt = {0, 0, 0, 0};
         int Pt = -1;
+#if COOKF_ONE_CHAIN
+        // a lane's pieces in every round continue one arithmetic sequence (slot
+        // s = r kPplF + p, step 16 kLpp), so its Horner chain runs across the
+        // rounds and is finished once: no per-round lane maps, swizzles and
+        // Z_{16 qr} shifts (for a 1.2 KB packet, 72 of a lane's ~270 lookups)
+        RoundCrc<false> rcx;
+#endif
         for (int r = 0; r < nrm; ++r) {
             // ---- frame: the round's pieces from the staged records
             u32x4 cur[kPplF];
@@ -841,7 +855,8 @@ __global__ __launch_bounds__(kThreads, COOKF_OCC) void k_cook_frame(CookArgs a, 
                 }
             }
 #pragma unroll
-            for (int p = 0; p < kPplF; ++p) cur[p] = fpiece::window(A[p], 0, 16);
+            for (int p = 0; p < kPplF; ++p)
+                cur[p] = (COOKF_PROBE & 4) ? u32x4{0, 0, 0, 0} : fpiece::window(A[p], 0, 16);
 #pragma unroll
             for (int p = 0; p < kPplF; ++p) {
                 const int P = r * kRoundF + 16 * (kLpp * p + hl);
@@ -856,22 +871,33 @@ __global__ __launch_bounds__(kThreads, COOKF_OCC) void k_cook_frame(CookArgs a, 
                     for (uint32_t u = 1; u < nrec; ++u) t = roff[u] <= bb ? u : t;
                     cur[p] = fpiece::stream_piece(rv, t, nrec, (int64_t)b, (int64_t)slen, m0, G.nsrc);
                 }
-                if (P < pext && ok) st_piece(pga + P, cur[p]);  // the plain packet, for the encoder
+                if (P < pext && ok && !(COOKF_PROBE & 1)) st_piece(pga + P, cur[p]);  // the plain packet, for the encoder
             }
             // ---- cook (k_cook's round, one Horner chain)
             const int qr = min(max(Q - kPplF * kLpp * r, 0), kPplF * kLpp);
             const int qr_max = COOK_SKIP ? wave_max(qr) : kPplF * kLpp;
+#if COOKF_ONE_CHAIN
+            RoundCrc<false> &rc = rcx;
+#else
             RoundCrc<false> rc;
+#endif
             uint32_t ivr = ivl ? mod_ivl((uint32_t)(r * kRoundF + 16 * hl + 16 * ivl - ph), (uint32_t)ivl, magic)
                                : 0u;
 #pragma unroll
             for (int p = 0; p < kPplF; ++p) {
                 const int P = r * kRoundF + 16 * (kLpp * p + hl);
+#if COOKF_ONE_CHAIN
+                if (ck && kLpp * p < qr_max) {
+                    const int sl = r * kPplF + p;  // the lane's slot over all rounds
+                    rc.add(T, crc_in_ph(cur[p], P, Lg, ph), sl, kLpp * sl + hl, Q);
+                }
+#else
                 if (ck && kLpp * p < qr_max) rc.add(T, crc_in_ph(cur[p], P, Lg, ph), p, kLpp * p + hl, qr);
+#endif
                 if (P < ext && P + 16 <= Lg) {
                     u32x4 m = ks_piece(a, P - ph);
                     if (ivl) m ^= iv_window_at(iv2w, ivr);
-                    st_piece(oga + P, cur[p] ^ m);
+                    if (!(COOKF_PROBE & 2)) st_piece(oga + P, cur[p] ^ m);
                 } else if (P < ext && P >= P0) {
                     dt = cur[p];
                     Pt = P;
@@ -879,12 +905,17 @@ __global__ __launch_bounds__(kThreads, COOKF_OCC) void k_cook_frame(CookArgs a, 
                 if (ivl) ivr = iv_step(ivr, sstep, (uint32_t)ivl);
                 if (COOK_SB && p % COOK_SB == COOK_SB - 1) __builtin_amdgcn_sched_barrier(0);
             }
+#if !COOKF_ONE_CHAIN
             if (ck) {
                 const uint32_t c = rc.finish(T, qr);
                 const uint32_t nacc = (r ? shift_pieces_n<kPplF>(T, acc, qr) : 0u) ^ c;
                 acc = qr > 0 ? nacc : acc;
             }
+#endif
         }
+#if COOKF_ONE_CHAIN
+        if (ck) acc = rcx.finish(T, Q);
+#endif
         uint32_t crc = 0;
         if (ck && L > 0 && cookit) crc = ~unshift(T, acc, (uint32_t)(16 * Q - Lg));
         if (cookit) {
