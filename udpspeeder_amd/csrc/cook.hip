@@ -67,12 +67,18 @@ constexpr int kPpl = 96 / kLpp;         // pieces per lane per round
 #ifndef COOK_SB
 #define COOK_SB 1  // scheduling fence every COOK_SB pieces (0: none), bounds registers
 #endif
+#ifndef COOK_ONE_CHAIN
+#define COOK_ONE_CHAIN 1  // k_cook: one Horner chain (pair) per lane across rounds, finished once
+#endif
 #ifndef COOK_DEFER
 #define COOK_DEFER 0  // k_cook, bit 0: a piece's key-stream load issued before its CRC;
                       // bit 1: the round's stores after the round (in vmcnt, a store made
                       // the next piece's key-stream load wait for it)
 #endif
-constexpr int kThreads = kLpp == 32 ? 512 : 256;  // LDS (tables per block) bounds residency
+#ifndef COOK_THREADS
+#define COOK_THREADS (kLpp == 32 ? 512 : 256)
+#endif
+constexpr int kThreads = COOK_THREADS;  // LDS (tables per block) bounds residency
 constexpr int kRound = 1536;            // 96 pieces per packet per round
 constexpr int kScrCook = 144;           // per-packet LDS: iv2[64] | overlay[64] | misc[16]
 constexpr int kScrDecook = 304;         // iv2[288] (iv_len up to 255) | misc[16]
@@ -474,6 +480,9 @@ __global__ __launch_bounds__(kThreads, COOK_OCC) void k_cook(CookArgs a) {
         uint32_t acc = 0;
         u32x4 dt = {0, 0, 0, 0};                // this lane's tail piece, if any
         int Pt = -1;
+#if COOK_ONE_CHAIN
+        RoundCrc<COOK_2CH != 0> rcx;  // slot s = r kPplC + p over all rounds (see k_cook_frame)
+#endif
         for (int r = 0; r < nrm; ++r) {
             // rounds past the first (long packets); a packed output's tail may
             // end past the source slot, whose bytes there are never used
@@ -482,7 +491,11 @@ __global__ __launch_bounds__(kThreads, COOK_OCC) void k_cook(CookArgs a) {
             // pieces at or past every packet's last crc piece in this round:
             // skip their CRC (a wave-uniform branch per piece slot)
             const int qr_max = COOK_SKIP ? wave_max(qr) : kPplC * kLpp;
+#if COOK_ONE_CHAIN
+            RoundCrc<COOK_2CH != 0> &rc = rcx;
+#else
             RoundCrc<COOK_2CH != 0> rc;
+#endif
             uint32_t ivr = ivl ? mod_ivl((uint32_t)(r * kRoundC + 16 * hl + 16 * ivl - ph), (uint32_t)ivl, magic)
                                : 0u;
 #pragma unroll
@@ -495,7 +508,14 @@ __global__ __launch_bounds__(kThreads, COOK_OCC) void k_cook(CookArgs a) {
                     m = ks_piece(a, P - ph);
                     if (ivl) m ^= iv_window_at(iv2w, ivr);
                 }
+#if COOK_ONE_CHAIN
+                if (ck && kLpp * p < qr_max) {
+                    const int sl = r * kPplC + p;
+                    rc.add(T, crc_in_ph(cur[p], P, Lg, ph), sl, kLpp * sl + hl, Q);
+                }
+#else
                 if (ck && kLpp * p < qr_max) rc.add(T, crc_in_ph(cur[p], P, Lg, ph), p, kLpp * p + hl, qr);
+#endif
                 if (whole) {  // obscure + xor
                     if (!(COOK_DEFER & 1)) {
                         m = ks_piece(a, P - ph);
@@ -518,12 +538,17 @@ __global__ __launch_bounds__(kThreads, COOK_OCC) void k_cook(CookArgs a) {
                     if (P < ext && P + 16 <= Lg) st_piece(oga + P, cur[p]);
                 }
             }
+#if !COOK_ONE_CHAIN
             if (ck) {
                 const uint32_t c = rc.finish(T, qr);
                 const uint32_t nacc = (r ? shift_pieces_n<kPplC>(T, acc, qr) : 0u) ^ c;
                 acc = qr > 0 ? nacc : acc;
             }
+#endif
         }
+#if COOK_ONE_CHAIN
+        if (ck) acc = rcx.finish(T, Q);
+#endif
         CT(2);
         uint32_t crc = 0;
         if (ck && L > 0) crc = ~unshift(T, acc, (uint32_t)(16 * Q - Lg));
