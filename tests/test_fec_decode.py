@@ -143,6 +143,27 @@ def test_oracle_matches_live_reference_with_ring_evictions(mode, rs):
     assert ret == list(r_ret) and ev == list(r_ev) and out == r_out
 
 
+@pytest.mark.parametrize("mode,rs,seed", [(0, "20:10", 41), (1, "1:3,2:4,10:6,20:10", 42), (0, "1:3,2:4,10:6,20:10", 43)])
+def test_planner_long_runs_with_evictions_match_oracle(mode, rs, seed):
+    """librsmi.so's planner without a GPU on 6,000-event runs with loss,
+    duplicates, swaps, delays past the 2,000-slot ring (evictions), replays,
+    truncations and garbage, cut into uneven batches: every input() return
+    value equals the restatement's (pinned to the live reference above).
+    Exercises the planner's flat maps and its memoised lookups and evictions
+    (fec_dec.cpp SeqMap / SeqMemo / EvictMemo) where groups interleave."""
+    from udpspeeder_amd.fec import FecDecoder
+    chan = _long_run(mode, rs, seed)
+    ret, _, _ = _oracle_run(chan)
+    host, lens, offs = _pack(chan)
+    dec = FecDecoder()
+    cuts = [0, 1, 700, 701, 2900, 4321, len(chan)]
+    got = []
+    for a, b in zip(cuts[:-1], cuts[1:]):
+        got += list(dec.plan(host, lens[a:b], offs[a:b]).ret)
+    assert got == ret
+    dec.close()
+
+
 def test_planner_anti_replay_timeout_matches_oracle():
     """anti_replay_timeout (120 s): replays older than it are accepted again."""
     from udpspeeder_amd.fec import FecDecoder
