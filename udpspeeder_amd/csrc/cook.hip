@@ -20,8 +20,10 @@
 //   * h is shifted to the end of the round's data by Z_{16k}, k = pieces after
 //     the lane's last piece (always 0..kLpp-1: kLpp nibble-table maps), and the
 //     packet's kLpp lanes XOR-reduce with ds_swizzle;
-//   * rounds chain as acc = Z_{16 Q_r}(acc) ^ round, Z_{16 Q_r} being
-//     Z_{16 kLpp} applied Q_r/kLpp times and one lane map;
+//   * a lane's pieces in successive rounds continue the same arithmetic
+//     sequence (step 16 kLpp), so its Horner chain runs across rounds and is
+//     shifted and reduced once per packet (COOK_ONE_CHAIN / COOKF_ONE_CHAIN;
+//     the older form chained rounds as acc = Z_{16 Q_r}(acc) ^ round);
 //   * the < 16 bytes of zero padding are removed with Z_{-z} (two nibble maps).
 // crc32h's init ~0 is folded in by complementing the first 4 bytes of the
 // padded message, its final ~ at the end.
