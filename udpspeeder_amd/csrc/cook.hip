@@ -746,7 +746,7 @@ static_assert(kFuseRecs <= kLpp, "k_cook_frame needs a lane per source record (C
 #endif
 #ifndef COOKF_PROBE
 #define COOKF_PROBE 0  // measurement only (wrong output): 1 no plain slot stores, 2 no cooked
-                       // stores, 4 no source loads (zeros)
+                       // stores, 4 no source loads (zeros), 8 no plain header piece
 #endif
 #ifndef COOKF_ONE_CHAIN
 #define COOKF_ONE_CHAIN 1  // k_cook_frame: one Horner chain per lane across its rounds
@@ -898,7 +898,8 @@ __global__ __launch_bounds__(kThreads, COOKF_OCC) void k_cook_frame(CookArgs a, 
                     for (uint32_t u = 1; u < nrec; ++u) t = roff[u] <= bb ? u : t;
                     cur[p] = fpiece::stream_piece(rv, t, nrec, (int64_t)b, (int64_t)slen, m0, G.nsrc);
                 }
-                if (P < pext && ok && !(COOKF_PROBE & 1)) st_piece(pga + P, cur[p]);  // the plain packet, for the encoder
+                if (P < pext && ok && !(COOKF_PROBE & 1) && !((COOKF_PROBE & 8) && P == 0))
+                    st_piece(pga + P, cur[p]);  // the plain packet, for the encoder
             }
             // ---- cook (k_cook's round, one Horner chain)
             const int qr = min(max(Q - kPplF * kLpp * r, 0), kPplF * kLpp);
