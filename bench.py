@@ -155,6 +155,7 @@ def main():
     u.fill_data(buf, K, LEN, synth.DATA_SEED, g0=g0)
     present = torch.from_numpy(synth.erasure_present(synth.ERASE_SEED, g0, G, n, ERASURES)).to(dev)
     status = torch.empty(G, dtype=torch.int32, device=dev)
+    smap = torch.empty((G, K), dtype=torch.uint8, device=dev)  # rs_decode's data[] permutation
     stream = torch.cuda.current_stream()
     u.reserve(K, n, G, stream)
 
@@ -166,7 +167,11 @@ def main():
         u.encode(buf, K, n, LEN, stream=stream)
         if i is not None:
             ev[i][1].record(stream)
-        u.decode(buf, present, K, n, LEN, status=status, stream=stream)
+        # the reference's placement (lib/fec.cpp:872-877): rebuilt rows over
+        # the parity survivors, data[] permutation into smap; the next step's
+        # encode rewrites the parity from the untouched data slots
+        u.decode(buf, present, K, n, LEN, status=status, stream=stream, placement="reference",
+                 slot_map=smap)
         if i is not None:
             ev[i][2].record(stream)
 
@@ -194,6 +199,16 @@ def main():
     enc_ms = statistics.mean(a.elapsed_time(b) for a, b, _ in ev)
     dec_ms = statistics.mean(b.elapsed_time(c) for _, b, c in ev)
     bad = int((status != 0).sum().item())
+    # the last timed decode's output, read through its slot map (the pointer
+    # permutation rs_decode2 leaves in data[]): the rows it rebuilt over the
+    # parity survivors equal the data they replace (e <= 5: the erased data
+    # slots were never written, so they still hold the data)
+    timed_ok = all(bool(torch.equal(u.reference_rows(buf[c:c + 65536], smap[c:c + 65536])[:, :, :LEN],
+                                    buf[c:c + 65536, :K, :LEN])) for c in range(0, G, 65536))
+    # ... and the parity those survivors held comes back with one more encode
+    # (untimed), for the lines below and the parity digest
+    u.encode(buf, K, n, LEN, stream=stream)
+    torch.cuda.synchronize()
     extras = None
     if rank == 0 and world == 1 and not args.no_extras:
         extras = extra_configs(u, synth, torch, dev, buf, G)
@@ -204,7 +219,9 @@ def main():
     # parity): this rank's bytes against the reference's digests
     check = None if args.no_verify else verify_slice(u, synth, torch, buf, present, g0, G)
     ok_flags = [-1.0] * world
-    ok_flags[rank] = -1.0 if check is None or check.get("ok") is None else float(check["ok"])
+    ok_flags[rank] = -1.0 if check is None or check.get("ok") is None else float(check["ok"] and timed_ok)
+    if check is not None:
+        check["timed_decode_rows_match"] = timed_ok
     parity_ok = [None if f < 0 else bool(f) for f in ok_flags]
     if world > 1:
         # max over ranks: the job is as slow as its slowest GPU; every rank's
@@ -466,7 +483,9 @@ def verify_slice(u, synth, torch, buf, present, g0, G):
     """This rank's bytes, checked after the timed region against digests the
     real reference produced (tests/golden/full_hashes.json, c4_rank_slices
     ranges, made by oracle/gen_golden.py --c4) for exactly this group range:
-    * parity: the timed loop's encode output (the parity rows now in buf);
+    * parity: the timed loop's encode kernel's output (rerun once after the
+      loop: its last decode wrote rows over the parity survivors, as
+      rs_decode2 does);
     * decode: the rank's slice refilled as the non-codeword input (data from
       DATA_SEED, parity from DATA_SEED ^ 0xFFFF), every erased slot poisoned,
       one decode through the same call as the step, the k data rows compared
@@ -488,12 +507,19 @@ def verify_slice(u, synth, torch, buf, present, g0, G):
     u.fill_data(buf, K, LEN, F["seed"], g0=g0)
     u.fill_data(buf[:, K:], M, LEN, F["parity_seed"], g0=g0)
     buf.masked_fill_((present == 0).unsqueeze(-1), 0xA5)  # erased slots hold junk
-    st = u.decode(buf, present, K, n, LEN)
+    smap = torch.empty((G, K), dtype=torch.uint8, device=buf.device)
+    st = u.decode(buf, present, K, n, LEN, placement="reference", slot_map=smap)
     fails = int((st != 0).sum().item())
-    dat = synth.hashes_digest(synth.group_hashes_dev(buf[:, :K, :LEN]))
-    ok = par == R["parity_gsum"] and dat == R["data_out_gsum"] and fails == 0
+    # the data rows read through the slot map, in data[] order (the pointer
+    # permutation rs_decode leaves the caller), and the map itself against the
+    # host closed form on a sample of groups
+    map_ok = all((smap[g].cpu().numpy() == u.ref_slot_map(K, n, present[g].cpu().numpy())).all()
+                 for g in range(0, G, max(1, G // 64)))
+    dat = synth.hashes_digest(synth.group_hashes_dev(u.reference_rows(buf, smap)[:, :, :LEN]))
+    ok = par == R["parity_gsum"] and dat == R["data_out_gsum"] and fails == 0 and map_ok
     return {"ok": ok, "range": [g0, g0 + G], "parity_match": par == R["parity_gsum"],
-            "decode_match": dat == R["data_out_gsum"], "decode_failures": fails,
+            "decode_match": dat == R["data_out_gsum"], "slot_map_match": map_ok,
+            "decode_failures": fails,
             "check_s": round(time.perf_counter() - t0, 2),
             "what": "reference digests of this rank's encode parity and non-codeword decode"}
 
@@ -597,7 +623,9 @@ def extra_configs(u, synth, torch, dev, buf, G):
     pres = torch.from_numpy(synth.erasure_present(synth.ERASE_SEED + 1, 0, G, n, ERASURES,
                                                   limit=K)).to(dev)
     st = torch.empty(G, dtype=torch.int32, device=dev)
-    ms = _time_ms(torch, lambda: u.decode(buf, pres, K, n, LEN, status=st))
+    sm = torch.empty((G, K), dtype=torch.uint8, device=dev)
+    ms = _time_ms(torch, lambda: u.decode(buf, pres, K, n, LEN, status=st, placement="reference",
+                                          slot_map=sm))
     alg = G * (K + ERASURES) * LEN
     out["c2_worst_5_data_erasures"] = {
         "decode_ms": round(ms, 4), "groups": G,
@@ -605,6 +633,7 @@ def extra_configs(u, synth, torch, dev, buf, G):
         "alg_GBps": round(alg / (ms * 1e-3) / 1e9, 1),
         "roofline_frac": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
         "failures": int((st != 0).sum().item())}
+    u.encode(buf, K, n, LEN)  # the parity those decodes wrote rows over, back for the lines below
     out.update(c3_configs(u, synth, torch, dev, G))
     out["c4_one_gpu"] = c4_one_gpu(u, synth, torch, dev)
     out["rtc_f10_5_encode"] = rtc_config(u, synth, torch, dev)
@@ -693,11 +722,12 @@ def c4_one_gpu(u, synth, torch, dev, steps=5):
     u.fill_data(b, K, LEN, synth.DATA_SEED)
     p = torch.from_numpy(synth.erasure_present(synth.ERASE_SEED, 0, Gc, n, ERASURES)).to(dev)
     st = torch.empty(Gc, dtype=torch.int32, device=dev)
+    sm = torch.empty((Gc, K), dtype=torch.uint8, device=dev)
     u.reserve(K, n, Gc)
 
     def step():
         u.encode(b, K, n, LEN)
-        u.decode(b, p, K, n, LEN, status=st)
+        u.decode(b, p, K, n, LEN, status=st, placement="reference", slot_map=sm)
     ms = _time_ms(torch, step, reps=steps, warm=1)
     r = {"groups": Gc, "ms_per_step": round(ms, 3),
          "GiBps": round(2.0 * Gc * K * LEN / (ms * 1e-3) / 2**30, 1),

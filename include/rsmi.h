@@ -86,15 +86,29 @@ const char *rsmi_last_error(void);
  * resident on the device between calls and polls a doorbell in pinned host
  * memory -- no kernel launch on the per-call path (UDPspeeder calls
  * rs_decode2 once per group, synchronously, fec_manager.cpp:632,710).  The
- * server ends after that long without a call (or 10 s in any case) and is
- * relaunched by the next call.  While it runs it holds 16 CUs' worth of
- * workgroups and its stream's hardware queue: device-wide synchronisation
- * (hipDeviceSynchronize, torch.cuda.synchronize) waits for it to go idle,
- * and work on a stream that shares that hardware queue waits as well -- a
- * process that mixes drop-in calls with its own GPU work may prefer 0. */
+ * server ends after that long without a call, or after its lifetime
+ * (RSMI_OPT_ONE_SERVER_LIFE) under steady traffic, and is relaunched by the
+ * next call.  While it runs it holds 16 CUs' worth of workgroups and its
+ * stream's hardware queue: device-wide synchronisation (hipDeviceSynchronize,
+ * torch.cuda.synchronize) waits for it to end -- at most one lifetime -- and
+ * work on a stream that shares that hardware queue waits as well.  A process
+ * that mixes drop-in calls with its own GPU work calls rsmi_quiesce() before
+ * a device-wide sync (no wait at all), or sets 0. */
 #define RSMI_OPT_ONE_SERVER 5
+/* RSMI_OPT_ONE_SERVER_LIFE: the resident server's lifetime cap in
+ * milliseconds (default 8, the reference's per-group latency budget
+ * fec_manager.h:30, or RSMI_ONE_SERVER_LIFE_MS; >= 1).  Bounds how long a
+ * device-wide synchronisation can wait for it under steady traffic; each
+ * relaunch costs the call that makes it one kernel launch. */
+#define RSMI_OPT_ONE_SERVER_LIFE 6
 
 int rsmi_set_option(int option, int value);
+
+/* Stop the resident one-group server on every device and wait for it to end
+ * (the next drop-in call relaunches it).  Call before a device-wide
+ * synchronisation, or before work that must not share the server's hardware
+ * queue, from any thread. */
+int rsmi_quiesce(void);
 
 /* Median wall time in microseconds of one drop-in rs_encode2 (decode 0) or
  * rs_decode2 (decode 1; rows with present[j] == 0 erased) call on host
@@ -200,6 +214,29 @@ int rsmi_encode_dev(int k, int n, uint8_t *base, int64_t group_stride,
 int rsmi_decode_dev(int k, int n, uint8_t *base, int64_t group_stride,
                     int64_t shard_stride, int len, int64_t ngroups,
                     const uint8_t *present, int32_t *status, void *stream);
+
+/* rs_decode2 with the reference's placement (lib/fec.cpp:838-882): each
+ * rebuilt data row i is written over the parity survivor that fec_decode's
+ * shuffle (fec.cpp:755-788) leaves in data[i] -- the buffer rs_decode2's
+ * caller finds behind data[i] afterwards (fec.cpp:872-877, lib/rs.h:36-38).
+ * Data survivors stay in place.  slot_map (DEVICE uint8[ngroups*k], may be
+ * NULL) receives per group the slot now holding data row i, i.e. the pointer
+ * permutation rs_decode leaves in data[0..k-1] (0xFF for an erased row of a
+ * group with fewer than k shards).  Erased data slots are scratch (the
+ * fused kernel writes them only for groups rebuilding more than 5 rows, the
+ * two-kernel path always).  Same arguments, stream
+ * semantics and status codes as rsmi_decode_dev.  The parity survivors are
+ * read before they are overwritten, so a repeat call on the same buffer
+ * decodes different input. */
+int rsmi_decode_dev_ref(int k, int n, uint8_t *base, int64_t group_stride,
+                        int64_t shard_stride, int len, int64_t ngroups,
+                        const uint8_t *present, int32_t *status, uint8_t *slot_map,
+                        void *stream);
+
+/* Host computation of one group's reference slot map (as rsmi_decode_dev_ref
+ * writes it) from present[n]; slot_map receives k entries.  Returns the
+ * number of missing data rows, -1 for too few shards, RSMI_ERR_INVALID. */
+int rsmi_ref_slot_map(int k, int n, const uint8_t *present, uint8_t *slot_map);
 
 /* ---- ragged batches (mode 0 mix: each group its own k, n, len) ---------- */
 

@@ -210,6 +210,10 @@ void rsmi_fcol_destroy(rsmi_fcol *col);
 int rsmi_fenc_run_many(rsmi_fcol *col, rsmi_fenc *const *enc, int32_t n, uint8_t *slots_base,
                        int64_t slot_stride, const struct rsmi_cook_ctx *ctx, uint64_t seed,
                        uint8_t *out, int32_t *out_len, void *stream);
+/* Test hook: on != 0 makes every rsmi_fenc_run_many fail right after it has
+ * consumed its encoders' plans (tests/test_fec_frame.py); returns the
+ * previous setting. */
+int rsmi_debug_fcol_fail(int on);
 
 /* ---- receive side: fec_decode_manager_t ------------------
  *

@@ -8,7 +8,7 @@ import time
 import numpy as np
 import pytest
 
-OPT_ONE_GROUP, OPT_SERVER = 3, 5
+OPT_ONE_GROUP, OPT_SERVER, OPT_SERVER_LIFE = 3, 5, 6
 
 
 def _roundtrip(u, oracle, rng, k, n, ln):
@@ -116,3 +116,76 @@ def test_c_timed_latency_helper(gpu):
     assert L.rsmi_dropin_latency(0, k, n, ln, None, 50, C.byref(e)) == 0
     assert 0 < d.value < 1000 and 0 < e.value < 1000
     assert L.rsmi_dropin_latency(1, k, n, ln, None, 50, C.byref(d)) != 0  # decode needs present
+
+
+@pytest.mark.gpu
+def test_server_bounded_sync_under_steady_traffic(gpu):
+    """Steady drop-in traffic (one rs_decode2 every ~2 ms for 1 s from one
+    thread) while another thread runs torch.cuda.synchronize(): the server's
+    lifetime cap (RSMI_OPT_ONE_SERVER_LIFE, default 8 ms) bounds every sync,
+    where a server kept busy by the traffic would otherwise hold it until its
+    idle timeout never comes.  rsmi_quiesce() makes the wait disappear."""
+    import ctypes as C
+    import threading
+    import torch
+    import udpspeeder_amd as u
+    L = u.lib()
+    k, n, ln = 20, 30, 1250
+    rows = np.random.default_rng(5).integers(0, 256, (n, ln), dtype=np.uint8)
+    dec = L.compat["rs_decode2"]
+    erased = {0, 3, 11, 24, 29}
+    prev1 = L.rsmi_set_option(OPT_ONE_GROUP, 1)
+    prev = L.rsmi_set_option(OPT_SERVER, 20000)
+    assert L.rsmi_set_option(OPT_SERVER_LIFE, 8) >= 1
+    stop = threading.Event()
+    errors, calls = [], [0]
+
+    def traffic():
+        t_end = time.perf_counter() + 1.0
+        while time.perf_counter() < t_end:
+            ptrs = (C.c_void_p * n)(*[None if j in erased else rows[j].ctypes.data for j in range(n)])
+            if dec(k, n, ptrs, ln) != 0:
+                errors.append("rs_decode2 failed")
+                break
+            calls[0] += 1
+            time.sleep(0.002)
+        stop.set()
+
+    waits, qwaits = [], []
+    try:
+        th = threading.Thread(target=traffic)
+        th.start()
+        time.sleep(0.05)
+        while not stop.is_set():
+            t0 = time.perf_counter()
+            torch.cuda.synchronize()
+            waits.append(time.perf_counter() - t0)
+            t0 = time.perf_counter()
+            assert L.rsmi_quiesce() == 0
+            torch.cuda.synchronize()
+            qwaits.append(time.perf_counter() - t0)
+            time.sleep(0.01)
+        th.join()
+    finally:
+        L.rsmi_set_option(OPT_SERVER, prev)
+        L.rsmi_set_option(OPT_ONE_GROUP, prev1)
+    assert not errors
+    assert calls[0] > 100 and len(waits) > 10
+    print(f"{calls[0]} calls; sync wait max {max(waits) * 1e3:.1f} ms, "
+          f"after rsmi_quiesce max {max(qwaits) * 1e3:.1f} ms")
+    # the lifetime (8 ms) plus scheduling slack; was up to 10 s
+    assert max(waits) < 0.1
+    assert max(qwaits) < 0.1
+
+
+@pytest.mark.gpu
+def test_server_lifetime_option(gpu):
+    import udpspeeder_amd as u
+    L = u.lib()
+    prev = L.rsmi_set_option(OPT_SERVER_LIFE, 5)
+    try:
+        assert L.rsmi_set_option(OPT_SERVER_LIFE, 8) == 5
+        assert L.rsmi_set_option(OPT_SERVER_LIFE, 0) < 0  # invalid: the lifetime stays
+        assert L.rsmi_set_option(OPT_SERVER_LIFE, 8) == 8
+    finally:
+        L.rsmi_set_option(OPT_SERVER_LIFE, prev)

@@ -633,7 +633,7 @@ def test_gpu_collector_fused_with_k_frame_leftovers(gpu, cook_oracle):
 def test_gpu_collector_failure_after_remap_consumes_plans(gpu, monkeypatch):
     """rsmi_fenc_run_many rewrites the plans' slot references to the shared
     array before its uploads and launches; a failure after that point (here
-    the RSMI_DEBUG_FCOL_FAIL hook) leaves no encoder planned, so a retry is a
+    the rsmi_debug_fcol_fail hook) leaves no encoder planned, so a retry is a
     clean "encoder without a plan" error, not an out-of-bounds write.  After
     re-planning, the same encoders run and produce the reference's packets."""
     import torch
@@ -668,10 +668,13 @@ def test_gpu_collector_failure_after_remap_consumes_plans(gpu, monkeypatch):
                              device="cuda")
 
     S, slots = plan_all()
-    monkeypatch.setenv("RSMI_DEBUG_FCOL_FAIL", "1")
-    with pytest.raises(RsmiError, match="injected"):
-        col.run_many(encs, slots, S)
-    monkeypatch.delenv("RSMI_DEBUG_FCOL_FAIL")
+    from udpspeeder_amd import lib
+    lib().rsmi_debug_fcol_fail(1)
+    try:
+        with pytest.raises(RsmiError, match="injected"):
+            col.run_many(encs, slots, S)
+    finally:
+        lib().rsmi_debug_fcol_fail(0)
     with pytest.raises(RsmiError, match="without a plan"):
         col.run_many(encs, slots, S)
     # the encoders' framing state is untouched by the failed runs: start the

@@ -88,6 +88,7 @@ def _bind(lib: C.CDLL) -> C.CDLL:
         "rsmi_set_option": ([i32, i32], i32),
         "rsmi_dropin_latency": ([i32, i32, i32, i32, vp, i32, vp], i32),
         "rsmi_init": ([], i32),
+        "rsmi_quiesce": ([], i32),
         "rsmi_last_error": ([], C.c_char_p),
         "rsmi_get_matrix": ([i32, i32, vp], i32),
         "rsmi_decode_matrix": ([i32, i32, vp, vp, vp, vp], i32),
@@ -103,6 +104,8 @@ def _bind(lib: C.CDLL) -> C.CDLL:
         "rsmi_bitslice_split_source": ([i32, i32, C.c_char_p, i64], i64),
         "rsmi_encode_dev": ([i32, i32, vp, i64, i64, i32, i64, vp], i32),
         "rsmi_decode_dev": ([i32, i32, vp, i64, i64, i32, i64, vp, vp, vp], i32),
+        "rsmi_decode_dev_ref": ([i32, i32, vp, i64, i64, i32, i64, vp, vp, vp, vp], i32),
+        "rsmi_ref_slot_map": ([i32, i32, vp, vp], i32),
         "rsmi_encode_ragged": ([vp, i64, vp, vp], i32),
         "rsmi_encode_ragged_dev": ([vp, i64, vp, vp], i32),
         "rsmi_encode_host": ([i32, i32, vp, i64, i64, i32, i64], i32),
@@ -144,6 +147,7 @@ def _bind(lib: C.CDLL) -> C.CDLL:
         "rsmi_fenc_run_cooked_packed_dev": ([vp, vp, i64, vp, C.c_uint64, vp, i64, vp, vp], i32),
         "rsmi_fcol_create": ([vp], i32),
         "rsmi_fcol_destroy": ([vp], None),
+        "rsmi_debug_fcol_fail": ([i32], i32),
         "rsmi_fenc_run_many": ([vp, vp, C.c_int32, vp, i64, vp, C.c_uint64, vp, vp, vp], i32),
         "rsmi_fenc_plan_many": ([vp, i32, vp, vp, vp, vp, vp, vp, vp, vp, i32], i32),
         "rsmi_fdec_plan_many": ([vp, i32, vp, vp, vp, vp, vp, i64, vp, vp, i32], i32),

@@ -30,6 +30,7 @@ thread_local std::string g_err;
 thread_local int g_last_enc = RSMI_ENC_NONE;  // rsmi_last_encoder
 std::atomic<int> g_opt_oneshot{1};              // RSMI_OPT_ONE_GROUP
 std::atomic<int> g_opt_server{-1};              // RSMI_OPT_ONE_SERVER: idle us (-1: not read yet)
+std::atomic<int> g_opt_server_life{-1};         // RSMI_OPT_ONE_SERVER_LIFE: ms (-1: not read yet)
 std::atomic<int> g_opt_bitslice{1};
 std::atomic<int> g_opt_fused{1};
 
@@ -280,7 +281,8 @@ int encode_dev(int k, int n, uint8_t *base, int64_t gs, int64_t ss, int len, int
 }
 
 int decode_dev(int k, int n, uint8_t *base, int64_t gs, int64_t ss, int len, int64_t ngroups,
-               const uint8_t *present, int32_t *status, hipStream_t s) {
+               const uint8_t *present, int32_t *status, hipStream_t s, bool ref = false,
+               uint8_t *slot_map = nullptr) {
     int rc = check_uniform(k, n, base, gs, ss, len, ngroups);
     if (rc) return rc;
     if (ngroups > 0 && !present) return fail(RSMI_ERR_INVALID, "null present");
@@ -302,7 +304,8 @@ int decode_dev(int k, int n, uint8_t *base, int64_t gs, int64_t ss, int len, int
     int W;
     UniformArgs a = make_args(k, n, base, gs, ss, len, ngroups, &W);
     if (fused) {
-        hipError_t e = launch_decode_fused(a, present, C->dev_rows, status, D->ptab, D->gftab, s);
+        hipError_t e = launch_decode_fused(a, present, C->dev_rows, status, D->ptab, D->gftab, s,
+                                           false, ref, slot_map);
         if (e != hipSuccess) return hip_fail(e, "fused decode launch");
         return RSMI_OK;
     }
@@ -311,6 +314,10 @@ int decode_dev(int k, int n, uint8_t *base, int64_t gs, int64_t ss, int len, int
     if (n > k && len > 0) {
         e = launch_decode_apply(a, W, plans, D->ptab, s);
         if (e != hipSuccess) return hip_fail(e, "decode apply launch");
+    }
+    if (ref) {
+        e = launch_decode_ref_move(a, plans, present, slot_map, s);
+        if (e != hipSuccess) return hip_fail(e, "decode placement launch");
     }
     return RSMI_OK;
 }
@@ -450,6 +457,21 @@ int server_idle_us() {
     return v;
 }
 
+// The server's lifetime cap (relaunched by the next call after it): the
+// reference's own latency budget, fec_manager.h:30 (timeout = 8 ms), so a
+// device-wide synchronisation waits at most about that long for it even under
+// steady traffic.
+int server_life_ms() {
+    int v = g_opt_server_life.load();
+    if (v < 0) {
+        const char *env = getenv("RSMI_ONE_SERVER_LIFE_MS");
+        v = env ? std::max(1, atoi(env)) : 8;
+        int expect = -1;
+        if (!g_opt_server_life.compare_exchange_strong(expect, v)) v = g_opt_server_life.load();
+    }
+    return v;
+}
+
 std::mutex g_srv_list_mu;
 std::vector<Device *> g_srv_devs;  // devices whose server may be running
 
@@ -487,8 +509,8 @@ int launch_server(Device &D, uint32_t done0, uint32_t idle_us) {
     }
     reinterpret_cast<volatile uint32_t *>(&D.srv_pin->quit)[0] = 0u;
     const uint32_t gen = ++D.srv_gen;
-    hipError_t e = launch_one_server(D.srv_dev, D.srv_dv, D.ptab, D.gftab, gen, done0, idle_us, 10000u,
-                                     D.one_stream);
+    hipError_t e = launch_one_server(D.srv_dev, D.srv_dv, D.ptab, D.gftab, gen, done0, idle_us,
+                                     (uint32_t)server_life_ms(), D.one_stream);
     if (e != hipSuccess) return hip_fail(e, "one-group server launch");
     D.srv_running = true;
     return RSMI_OK;
@@ -510,14 +532,38 @@ int post_to_server(Device &D, const OneArgs &a, uint32_t idle_us) {
     return RSMI_OK;
 }
 
-// Stop a running server and wait for it (RSMI_OPT_ONE_SERVER 0, tests).
-int stop_server(Device &D) {
-    std::lock_guard<std::mutex> lk(D.one_mu);
+// caller holds D.one_mu: stop a running server and wait for it to end
+int stop_server_locked(Device &D) {
     if (!D.srv_pin || !D.srv_running) return RSMI_OK;
     reinterpret_cast<volatile uint32_t *>(&D.srv_pin->quit)[0] = 1u;
     RSMI_HIP(hipStreamSynchronize(D.one_stream), "stop one-group server");
     D.srv_running = false;
     return RSMI_OK;
+}
+
+// Stop a running server and wait for it (RSMI_OPT_ONE_SERVER 0, rsmi_quiesce).
+int stop_server(Device &D) {
+    std::lock_guard<std::mutex> lk(D.one_mu);
+    return stop_server_locked(D);
+}
+
+// Every device's server stopped (the next drop-in call relaunches its own).
+int stop_all_servers() {
+    std::vector<Device *> ds;
+    {
+        std::lock_guard<std::mutex> lk(g_srv_list_mu);
+        ds = g_srv_devs;
+    }
+    int cur = -1;
+    (void)hipGetDevice(&cur);
+    int rc = RSMI_OK;
+    for (Device *D : ds) {
+        (void)hipSetDevice(D->id);
+        rc = stop_server(*D);
+        if (rc) break;
+    }
+    if (cur >= 0) (void)hipSetDevice(cur);
+    return rc;
 }
 
 // One group, host buffers, one kernel (oneshot.hip): the shards the kernel
@@ -543,6 +589,10 @@ int one_group_op(Device &D, bool decode, int k, int n, uint8_t *const *ptrs, uin
     if (!D.one_stream)
         RSMI_HIP(hipStreamCreateWithFlags(&D.one_stream, hipStreamNonBlocking), "hipStreamCreate(one)");
     if (D.one_bytes < need) {
+        // a resident server still polls this staging, and CLR's hipHostFree
+        // waits for every stream: stop it first (relaunched by the post below)
+        rc = stop_server_locked(D);
+        if (rc) return rc;
         if (D.one_pin) (void)hipHostFree(D.one_pin);
         D.one_pin = D.one_dev = nullptr;
         D.one_bytes = 0;
@@ -564,9 +614,8 @@ int one_group_op(Device &D, bool decode, int k, int n, uint8_t *const *ptrs, uin
     const bool multi = one_multi_ok(k, n, len, ss > 0 ? ss : 16, rows_out);
     const int idle_us = multi ? server_idle_us() : 0;
     if (!multi && D.srv_running) {  // the single-workgroup kernel queues on the server's stream
-        reinterpret_cast<volatile uint32_t *>(&D.srv_pin->quit)[0] = 1u;
-        RSMI_HIP(hipStreamSynchronize(D.one_stream), "stop one-group server");
-        D.srv_running = false;
+        rc = stop_server_locked(D);
+        if (rc) return rc;
     }
     volatile uint32_t *flags = idle_us > 0 ? D.srv_pin ? D.srv_pin->flags : nullptr
                                            : reinterpret_cast<volatile uint32_t *>(tail + 64);
@@ -1072,6 +1121,7 @@ void stop_workers(std::vector<std::unique_ptr<Worker>> &ws) {
 // part i is the first item whose prefix sum reaches i/parts of the total
 // (shard.balanced_ranges; C3's ragged groups weigh (k+m)*len).
 void split_ranges(int64_t n, const int64_t *cost, int parts, int64_t *bounds) {
+    if (parts < 1) return;  // (callers reject parts < 1)
     bounds[0] = 0;
     bounds[parts] = n;
     if (!cost) {
@@ -1089,9 +1139,16 @@ void split_ranges(int64_t n, const int64_t *cost, int parts, int64_t *bounds) {
     }
 }
 
+// run_split's answer when no device list is set: the caller runs the call on
+// its own current device.  Decided under call_mu, so a concurrent
+// rsmi_set_devices(.., 0) cannot turn a split call into a silent no-op.
+constexpr int kNoWorkers = 1;
+
 // Runs fn(worker, g0, count) for every listed device's range, in parallel, and
-// returns the first failure (its message moved to the calling thread).
-int run_split(int64_t ngroups, const std::function<int(Worker &, int64_t, int64_t)> &fn) {
+// returns the first failure (its message moved to the calling thread), or
+// kNoWorkers.  cost (may be null): per-group weights the ranges balance.
+int run_split(int64_t ngroups, const std::function<int(Worker &, int64_t, int64_t)> &fn,
+              const int64_t *cost = nullptr) {
     MultiDev &M = multi();
     std::lock_guard<std::mutex> call(M.call_mu);
     std::vector<Worker *> ws;
@@ -1100,8 +1157,9 @@ int run_split(int64_t ngroups, const std::function<int(Worker &, int64_t, int64_
         for (auto &W : M.workers) ws.push_back(W.get());
     }
     const int parts = (int)ws.size();
+    if (parts < 1) return kNoWorkers;
     std::vector<int64_t> b((size_t)parts + 1);
-    split_ranges(ngroups, nullptr, parts, b.data());
+    split_ranges(ngroups, cost, parts, b.data());
     std::vector<int> rcs((size_t)parts, RSMI_OK);
     std::vector<std::string> errs((size_t)parts);
     for (int i = 0; i < parts; ++i) {
@@ -1125,12 +1183,6 @@ int run_split(int64_t ngroups, const std::function<int(Worker &, int64_t, int64_
             return rcs[(size_t)i];
         }
     return RSMI_OK;
-}
-
-bool multi_active() {
-    MultiDev &M = multi();
-    std::lock_guard<std::mutex> lk(M.cfg_mu);
-    return !M.workers.empty();
 }
 
 int set_devices(const int32_t *devs, int32_t n) {
@@ -1176,14 +1228,14 @@ int encode_pinned(int k, int n, const uint8_t *hd, int64_t dgs, uint8_t *hp, int
     int rc = check_encode_pinned(k, n, hd, dgs, hp, pgs, ss, len, ngroups, chunk);
     if (rc) return rc;
     if (ngroups == 0 || n == k || len == 0) return RSMI_OK;
-    if (multi_active())
-        return run_split(ngroups, [&](Worker &W, int64_t g0, int64_t cnt) {
-            int r;
-            Device *D = current(&r);
-            if (!D) return r;
-            return encode_pinned_on(*D, W.penc, k, n, hd + g0 * dgs, dgs, hp + g0 * pgs, pgs, ss, len, cnt,
-                                    chunk);
-        });
+    rc = run_split(ngroups, [&](Worker &W, int64_t g0, int64_t cnt) {
+        int r;
+        Device *D = current(&r);
+        if (!D) return r;
+        return encode_pinned_on(*D, W.penc, k, n, hd + g0 * dgs, dgs, hp + g0 * pgs, pgs, ss, len, cnt,
+                                chunk);
+    });
+    if (rc != kNoWorkers) return rc;
     Device *D = current(&rc);
     if (!D) return rc;
     return encode_pinned_on(*D, D->penc, k, n, hd, dgs, hp, pgs, ss, len, ngroups, chunk);
@@ -1194,7 +1246,7 @@ int decode_pinned(int k, int n, uint8_t *hs, int64_t hgs, int64_t ss, int len, i
     int rc = check_decode_pinned(k, n, hs, hgs, ss, len, ngroups, present, chunk);
     if (rc) return rc;
     if (ngroups == 0) return RSMI_OK;
-    if (multi_active()) {
+    {
         std::atomic<int> paths{0};
         rc = run_split(ngroups, [&](Worker &W, int64_t g0, int64_t cnt) {
             int r;
@@ -1205,8 +1257,10 @@ int decode_pinned(int k, int n, uint8_t *hs, int64_t hgs, int64_t ss, int len, i
             paths.fetch_or(g_last_pinned);  // (the worker thread's own record)
             return r;
         });
-        g_last_pinned = paths.load();  // both bits when the ranges took different paths
-        return rc;
+        if (rc != kNoWorkers) {
+            g_last_pinned = paths.load();  // both bits when the ranges took different paths
+            return rc;
+        }
     }
     Device *D = current(&rc);
     if (!D) return rc;
@@ -1234,28 +1288,25 @@ int rsmi_set_option(int option, int value) {
         const int prev = rsmi::server_idle_us();
         rsmi::g_opt_server.store(value > 0 ? value : 0);
         if (value <= 0) {  // stop every running server (the next calls launch per call)
-            std::vector<rsmi::Device *> ds;
-            {
-                std::lock_guard<std::mutex> lk(rsmi::g_srv_list_mu);
-                ds = rsmi::g_srv_devs;
-            }
-            int cur = -1;
-            (void)hipGetDevice(&cur);
-            for (rsmi::Device *D : ds) {
-                (void)hipSetDevice(D->id);
-                const int rc = rsmi::stop_server(*D);
-                if (rc) {
-                    (void)hipSetDevice(cur);
-                    return rc;
-                }
-            }
-            if (cur >= 0) (void)hipSetDevice(cur);
+            const int rc = rsmi::stop_all_servers();
+            if (rc) return rc;
         }
+        return prev;
+    }
+    if (option == RSMI_OPT_ONE_SERVER_LIFE) {
+        const int prev = rsmi::server_life_ms();
+        if (value < 1) {
+            rsmi::set_error("RSMI_OPT_ONE_SERVER_LIFE: lifetime must be >= 1 ms");
+            return RSMI_ERR_INVALID;
+        }
+        rsmi::g_opt_server_life.store(value);
         return prev;
     }
     rsmi::set_error("unknown option");
     return RSMI_ERR_INVALID;
 }
+
+int rsmi_quiesce(void) { return rsmi::stop_all_servers(); }
 
 int rsmi_init(void) {
     int rc;
@@ -1326,6 +1377,30 @@ int rsmi_decode_dev(int k, int n, uint8_t *base, int64_t gs, int64_t ss, int len
                     int64_t ngroups, const uint8_t *present, int32_t *status, void *stream) {
     return rsmi::decode_dev(k, n, base, gs, ss, len, ngroups, present, status,
                             (hipStream_t)stream);
+}
+
+int rsmi_decode_dev_ref(int k, int n, uint8_t *base, int64_t gs, int64_t ss, int len,
+                        int64_t ngroups, const uint8_t *present, int32_t *status,
+                        uint8_t *slot_map, void *stream) {
+    return rsmi::decode_dev(k, n, base, gs, ss, len, ngroups, present, status,
+                            (hipStream_t)stream, true, slot_map);
+}
+
+int rsmi_ref_slot_map(int k, int n, const uint8_t *present, uint8_t *slot_map) {
+    if (k < 1 || n < k || n > 256 || !present || !slot_map)
+        return rsmi::fail(RSMI_ERR_INVALID, "invalid rsmi_ref_slot_map arguments");
+    uint8_t sel[256];
+    int cnt = 0, e = 0;
+    for (int j = 0; j < n && cnt < k; ++j)
+        if (present[j]) sel[cnt++] = (uint8_t)j;
+    if (cnt < k) {
+        for (int i = 0; i < k; ++i) slot_map[i] = present[i] ? (uint8_t)i : (uint8_t)0xFF;
+        return -1;
+    }
+    for (int i = 0; i < k; ++i) e += !present[i];
+    for (int i = 0; i < k; ++i)
+        slot_map[i] = present[i] ? (uint8_t)i : (uint8_t)rsmi::ref_slot_of(k, e, sel, i);
+    return e;
 }
 
 int rsmi_encode_ragged(const rsmi_group *groups, int64_t ngroups, uint8_t *base, void *stream) {

@@ -61,6 +61,14 @@ constexpr int kWaves = 4;      // waves per block (one group each)
 #ifndef DEC_ST_BIG_E
 #define DEC_ST_BIG_E 5            // (4: C2 random 0.385-0.387 vs 0.381-0.383 ms at 5)
 #endif
+#ifndef DEC_REF_ST_AUX
+#define DEC_REF_ST_AUX 0       // store policy of the reference-placement rows (over the parity survivors
+                               // just read): default (dec4_probe "last survivors' slots": 0.348-0.352 ms,
+                               // against 0.354-0.359 with sc0|sc1)
+#endif
+#ifndef DEC_REF_ST_AUX_BIG
+#define DEC_REF_ST_AUX_BIG DEC_REF_ST_AUX
+#endif
 #ifndef DEC_RAG_ST_AUX
 #define DEC_RAG_ST_AUX 16      // cache policy of the ragged kernels' rebuilt-row stores: sc1 (C3 decode
                                // 0.135-0.136 vs 0.137-0.138 ms default, 0.145-0.148 nt)
@@ -412,10 +420,15 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t group_rsrc(const uint8_t *gbas
 // DEC_LD_AUX / DEC_ST_AUX for HBM; sc0|sc1 (system scope, coherent with the
 // host) when the shards are pinned host memory read over PCIe
 // (rsmi_decode_pinned's zero-copy path).
-template <int LDAUX, int STAUX, int STBIG>
+// REF: the reference's placement (rsmi_decode_dev_ref): rebuilt data row i
+// goes over the parity survivor fec_decode's shuffle leaves in data[i]
+// (fec.cpp:755-788, 872-877), and slot_map (may be null) receives, per group,
+// the slot now holding each data row.
+template <int LDAUX, int STAUX, int STBIG, int REF>
 __global__ __launch_bounds__(256, DEC_OCC) void k_decode_fused(UniformArgs a, const uint8_t *present,
                                                       const uint8_t *prows, int32_t *status_out,
-                                                      const uint32_t *ptab, const uint8_t *gftab) {
+                                                      const uint32_t *ptab, const uint8_t *gftab,
+                                                      uint8_t *slot_map) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int k = a.k, n = a.n;
     (void)prows;
@@ -481,7 +494,32 @@ __global__ __launch_bounds__(256, DEC_OCC) void k_decode_fused(UniformArgs a, co
         wave_sync();
         if (st != RSMI_DEC_OK || e == 0) {
             if (lane == 0 && status_out) status_out[g] = st;
+            // nothing moves: data row i stays in slot i (0xFF: erased, too few)
+            if (REF && slot_map && lane < k) slot_map[g * k + lane] = pf ? (uint8_t)lane : (uint8_t)0xFF;
             continue;
+        }
+        // REF: the slot rebuilt row r (lane r) goes to.  fec_decode packs the
+        // k survivors sel[] (ascending: s = k - e data shards, then parity)
+        // and its shuffle moves each data survivor home, swapping the
+        // displaced packet into the vacated position; position x < s
+        // therefore passes its final occupant along the chain
+        // x -> sel[x] -> ... (strictly increasing) to the first position >= s,
+        // which still holds its parity packet: row miss[r] ends in that
+        // packet's buffer (pinned against decode_small.npz's ptr_out).
+        uint32_t ref_slot = 0;
+        if (REF) {
+            if (lane < e) {
+                int x = L.miss[lane];
+                const int s = k - e;
+                while (x < s) x = L.sel[x];
+                ref_slot = L.sel[x];
+            }
+            if (slot_map) {
+                uint8_t *tmp = L.miss + 128;  // scratch: the slice's miss[] holds e <= 10 entries
+                if (lane < e) tmp[L.miss[lane]] = (uint8_t)ref_slot;
+                wave_sync();
+                if (lane < k) slot_map[g * k + lane] = pf ? (uint8_t)lane : tmp[lane];
+            }
         }
 
 #if DEC_TRACE
@@ -505,6 +543,7 @@ __global__ __launch_bounds__(256, DEC_OCC) void k_decode_fused(UniformArgs a, co
         const uint32_t sel_lane = lane < k ? (uint32_t)L.sel[lane] : 0u;
         const uint32_t so_lane = sel_lane * ss;
         const uint32_t mo_lane = (lane < e ? (uint32_t)L.miss[lane] : 0u) * ss;
+        const uint32_t ref_lane = ref_slot * ss;
         typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
         u32x4 rq[kRing];
         uint32_t rd[kRing];
@@ -648,12 +687,16 @@ __global__ __launch_bounds__(256, DEC_OCC) void k_decode_fused(UniformArgs a, co
                 }
                 // the store policy by the group's write share: a group that
                 // rebuilds many rows streams them past the caches (STBIG)
+                // REF: the last pass writes over the parity survivors (every
+                // read of this tile is behind it); earlier passes park their
+                // rows in their own (erased) slots, moved after the last pass
+                const uint32_t dst_lane = (REF && rb + kFPass >= e) ? ref_lane : mo_lane;
                 auto store_rows = [&](auto aux) {
                     constexpr int AUX = decltype(aux)::value;
 #pragma unroll
                     for (int r = 0; r < kFPass; ++r) {
                         if (rb + r < e) {
-                            const uint32_t so = __builtin_amdgcn_readlane(mo_lane, rb + r);
+                            const uint32_t so = __builtin_amdgcn_readlane(dst_lane, rb + r);
                             const u32x4 v = {acc[r][0], acc[r][1], acc[r][2], acc[r][3]};
 #if DEC_ST_SGPR
                             __builtin_amdgcn_raw_buffer_store_b128(v, rsrc, v16, so, AUX);
@@ -669,6 +712,27 @@ __global__ __launch_bounds__(256, DEC_OCC) void k_decode_fused(UniformArgs a, co
                     store_rows(std::integral_constant<int, STBIG>{});
                 else
                     store_rows(std::integral_constant<int, STAUX>{});
+            }
+        }
+        if (REF && e > kFPass) {
+            // rows of the earlier passes: own slot -> their parity survivor
+            // (each lane moves the bytes it stored; the fences order the
+            // stores before the loads, which bypass the CU cache)
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            const int moved = (e - 1) / kFPass * kFPass;
+            for (int toff = 0; toff < a.len; toff += kTile) {
+                const int tlen = lpad - toff;
+                const uint32_t c16 = (16 * lane < tlen) ? (uint32_t)(toff + 16 * lane) : 0x80000000u;
+                const uint32_t c4 = (1024 + 4 * lane < tlen) ? (uint32_t)(toff + 1024 + 4 * lane) : 0x80000000u;
+                for (int r = 0; r < moved; ++r) {
+                    const uint32_t src = __builtin_amdgcn_readlane(mo_lane, r);
+                    const uint32_t dst = __builtin_amdgcn_readlane(ref_lane, r);
+                    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, c16, src, 1);
+                    const uint32_t d = __builtin_amdgcn_raw_buffer_load_b32(rsrc, c4, src, 1);
+                    __builtin_amdgcn_raw_buffer_store_b128(v, rsrc, c16 + dst, 0, STAUX);
+                    __builtin_amdgcn_raw_buffer_store_b32(d, rsrc, c4 + dst, 0, STAUX);
+                }
             }
         }
         if (lane == 0 && status_out) status_out[g] = RSMI_DEC_OK;
@@ -1161,18 +1225,21 @@ bool decode_fused_ok(int k, int n, int64_t group_stride, int64_t shard_stride, i
 hipError_t launch_decode_fused(const UniformArgs &a, const uint8_t *present,
                                const uint8_t *parity_rows, int32_t *status,
                                const uint32_t *ptab, const uint8_t *gftab, hipStream_t s,
-                               bool host_shards) {
+                               bool host_shards, bool ref, uint8_t *slot_map) {
     const size_t lds = kLTabBytes + (size_t)kWaves * wave_lds_bytes(a.k);
     int64_t blocks = (a.ngroups + kWaves - 1) / kWaves;
     const int64_t cap = 256 * DEC_GRID_PER_CU;
     if (blocks > cap) blocks = cap;
     if (blocks < 1) blocks = 1;
     if (host_shards)
-        k_decode_fused<3, 3, 3><<<(unsigned)blocks, 64 * kWaves, lds, s>>>(a, present, parity_rows,
-                                                                      status, ptab, gftab);
+        k_decode_fused<3, 3, 3, 0><<<(unsigned)blocks, 64 * kWaves, lds, s>>>(a, present, parity_rows,
+                                                                         status, ptab, gftab, nullptr);
+    else if (ref)
+        k_decode_fused<DEC_LD_AUX, DEC_REF_ST_AUX, DEC_REF_ST_AUX_BIG, 1>
+            <<<(unsigned)blocks, 64 * kWaves, lds, s>>>(a, present, parity_rows, status, ptab, gftab, slot_map);
     else
-        k_decode_fused<DEC_LD_AUX, DEC_ST_AUX, DEC_ST_AUX_BIG><<<(unsigned)blocks, 64 * kWaves, lds, s>>>(
-            a, present, parity_rows, status, ptab, gftab);
+        k_decode_fused<DEC_LD_AUX, DEC_ST_AUX, DEC_ST_AUX_BIG, 0><<<(unsigned)blocks, 64 * kWaves, lds, s>>>(
+            a, present, parity_rows, status, ptab, gftab, nullptr);
     return hipGetLastError();
 }
 

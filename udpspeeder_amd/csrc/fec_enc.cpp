@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdlib>
 #include <new>
@@ -1051,7 +1052,13 @@ struct rsmi_fcol {
     size_t plan_cap[2] = {0, 0};
 };
 
+namespace {
+std::atomic<int> g_fcol_fail{0};  // rsmi_debug_fcol_fail (tests only)
+}  // namespace
+
 extern "C" {
+
+int rsmi_debug_fcol_fail(int on) { return g_fcol_fail.exchange(on ? 1 : 0); }
 
 int rsmi_fcol_create(rsmi_fcol **out) {
     if (!out) return fail(RSMI_ERR_INVALID, "null out");
@@ -1188,7 +1195,8 @@ int rsmi_fenc_run_many(rsmi_fcol *C, rsmi_fenc *const *enc, int32_t n, uint8_t *
         }
     }
     // test hook: a failure after the remap (tests/test_fec_frame.py re-plans after it)
-    if (std::getenv("RSMI_DEBUG_FCOL_FAIL")) return fail(RSMI_ERR_INVALID, "rsmi_fenc_run_many: injected failure");
+    if (g_fcol_fail.load(std::memory_order_relaxed))
+        return fail(RSMI_ERR_INVALID, "rsmi_fenc_run_many: injected failure");
     // ---- the combined plan, every reference rewritten
     B.jobs.clear(); B.srcs.clear(); B.carry.clear(); B.stale.clear(); B.upd.clear(); B.pruns.clear();
     B.recs.clear();

@@ -261,6 +261,38 @@ __global__ __launch_bounds__(64) void k_decode_plan(UniformArgs a, const uint8_t
     }
 }
 
+// ---- the reference's placement after a two-kernel decode --------------------
+// k_decode_apply rebuilt each missing data row in its own slot; fec_decode
+// leaves it in the buffer of the parity survivor its shuffle moves into data[i]
+// (fec.cpp:755-788, 872-877; ref_slot_of).  One wave per group moves the rows
+// there (16-byte pieces up to round_up(len, 16), inside the slot padding) and
+// writes the group's slot map (0xFF: an erased row of a group with too few).
+__global__ __launch_bounds__(64) void k_decode_ref_move(UniformArgs a, const uint8_t *plans,
+                                                        const uint8_t *present, uint8_t *slot_map) {
+    const int k = a.k, m = a.n - a.k, lane = threadIdx.x;
+    const PlanLayout L(k, k < m ? k : m);
+    const int pieces = (a.len + 15) >> 4;
+    for (int64_t g = blockIdx.x; g < a.ngroups; g += gridDim.x) {
+        const uint8_t *plan = plans + g * L.stride;
+        const int st = *reinterpret_cast<const int32_t *>(plan);
+        const int e = st == RSMI_DEC_OK ? plan[4] : 0;
+        const uint8_t *sel = plan + 8, *miss = plan + 8 + k;
+        uint8_t *gb = a.base + g * a.group_stride;
+        for (int r = 0; r < e; ++r) {
+            const uint4 *src = reinterpret_cast<const uint4 *>(gb + miss[r] * a.shard_stride);
+            uint4 *dst = reinterpret_cast<uint4 *>(gb + ref_slot_of(k, e, sel, miss[r]) * a.shard_stride);
+            for (int p = lane; p < pieces; p += 64) dst[p] = src[p];
+        }
+        if (slot_map) {
+            for (int i = lane; i < k; i += 64) {
+                uint8_t v = present[g * a.n + i] ? (uint8_t)i : (uint8_t)0xFF;
+                if (v == 0xFF && e > 0) v = (uint8_t)ref_slot_of(k, e, sel, i);
+                slot_map[g * k + i] = v;
+            }
+        }
+    }
+}
+
 // ---- ragged encode: one wavefront per group, tile width chosen per group ----
 __global__ __launch_bounds__(256) void k_encode_ragged(const rsmi_group *groups, int64_t ngroups,
                                                        uint8_t *base, const uint64_t *code_dir,
@@ -394,6 +426,14 @@ hipError_t launch_decode_apply(const UniformArgs &a, int W, const uint8_t *plans
         case 4: k_decode_apply<4><<<grid, 256, 0, s>>>(a, plans, ptab); break;
         default: k_decode_apply<5><<<grid, 256, 0, s>>>(a, plans, ptab); break;
     }
+    return hipGetLastError();
+}
+
+hipError_t launch_decode_ref_move(const UniformArgs &a, const uint8_t *plans, const uint8_t *present,
+                                  uint8_t *slot_map, hipStream_t s) {
+    int64_t grid = a.ngroups < 256 * 16 ? a.ngroups : 256 * 16;
+    if (grid < 1) grid = 1;
+    k_decode_ref_move<<<(int)grid, 64, 0, s>>>(a, plans, present, slot_map);
     return hipGetLastError();
 }
 

@@ -49,6 +49,10 @@ hipError_t launch_decode_apply(const UniformArgs &a, int W, const uint8_t *plans
                                const uint32_t *ptab, hipStream_t s);
 hipError_t launch_encode_ragged(const rsmi_group *groups, int64_t ngroups, uint8_t *base,
                                 const uint64_t *code_dir, const uint32_t *ptab, hipStream_t s);
+// After plan + apply: rebuilt rows to the reference's slots, and the slot map
+// (rsmi_decode_dev_ref); present is the call's [ngroups][n] flags.
+hipError_t launch_decode_ref_move(const UniformArgs &a, const uint8_t *plans, const uint8_t *present,
+                                  uint8_t *slot_map, hipStream_t s);
 hipError_t launch_fill_data(int k, int len, uint8_t *base, int64_t group_stride,
                             int64_t shard_stride, int64_t g0, int64_t ngroups, uint64_t seed,
                             hipStream_t s);
@@ -63,7 +67,16 @@ bool decode_fused_ok(int k, int n, int64_t group_stride, int64_t shard_stride, i
 hipError_t launch_decode_fused(const UniformArgs &a, const uint8_t *present,
                                const uint8_t *parity_rows, int32_t *status,
                                const uint32_t *ptab, const uint8_t *gftab, hipStream_t s,
-                               bool host_shards = false);
+                               bool host_shards = false, bool ref = false,
+                               uint8_t *slot_map = nullptr);
+// The reference's placement of a group's rebuilt rows (fec.cpp:755-788,
+// 872-877): slot of the parity survivor that ends in data[i] for each missing
+// data row i, given sel (the k survivors, ascending) and the missing rows.
+__host__ __device__ inline int ref_slot_of(int k, int e, const uint8_t *sel, int miss_row) {
+    int x = miss_row;
+    while (x < k - e) x = sel[x];
+    return sel[x];
+}
 
 // Ragged decode (decode.hip): one-wave-per-group kernel, then the
 // workgroup-per-group kernel for the groups it defers.

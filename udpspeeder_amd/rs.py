@@ -236,10 +236,17 @@ def encode(shards, k: int, n: int, length: Optional[int] = None, stream=None) ->
 
 
 def decode(shards, present, k: int, n: int, length: Optional[int] = None, status=None,
-           stream=None):
+           stream=None, placement: str = "own", slot_map=None):
     """rs_decode2 on every group: ``present`` [G, n] uint8 CUDA (nonzero =
-    received).  Missing data rows are rebuilt in their own slot.  Returns the
-    int32 [G] status tensor (0 ok, -1 too few shards, 1 singular)."""
+    received).  Returns the int32 [G] status tensor (0 ok, -1 too few shards,
+    1 singular).
+
+    ``placement="own"`` (default) rebuilds each missing data row in its own
+    slot.  ``placement="reference"`` writes it where fec_decode does
+    (lib/fec.cpp:872-877): over the parity survivor its shuffle moves into
+    data[i] (rsmi_decode_dev_ref); ``slot_map`` (uint8 [G, k] CUDA, optional)
+    then receives the slot holding each data row (reference_rows reads
+    through it)."""
     import torch
     G, gs, ss, S = _shard_geometry(shards, n)
     _check_dev(present, "present", torch.uint8)
@@ -247,9 +254,47 @@ def decode(shards, present, k: int, n: int, length: Optional[int] = None, status
         raise ValueError("present must be a contiguous [G, n] uint8 tensor on the shards' device")
     status = _status_out(status, G, shards.device)
     L = S if length is None else int(length)
-    check(lib().rsmi_decode_dev(k, n, shards.data_ptr(), gs, ss, L, G, present.data_ptr(),
-                                status.data_ptr(), _stream_handle(stream)), "rsmi_decode_dev")
+    if placement == "own":
+        if slot_map is not None:
+            raise ValueError("slot_map needs placement='reference'")
+        check(lib().rsmi_decode_dev(k, n, shards.data_ptr(), gs, ss, L, G, present.data_ptr(),
+                                    status.data_ptr(), _stream_handle(stream)), "rsmi_decode_dev")
+    elif placement == "reference":
+        mp = None
+        if slot_map is not None:
+            _check_dev(slot_map, "slot_map", torch.uint8)
+            if tuple(slot_map.shape) != (G, k) or not slot_map.is_contiguous() or \
+                    slot_map.device != shards.device:
+                raise ValueError("slot_map must be a contiguous [G, k] uint8 tensor on the shards' device")
+            mp = slot_map.data_ptr()
+        check(lib().rsmi_decode_dev_ref(k, n, shards.data_ptr(), gs, ss, L, G, present.data_ptr(),
+                                        status.data_ptr(), mp, _stream_handle(stream)),
+              "rsmi_decode_dev_ref")
+    else:
+        raise ValueError(f"placement must be 'own' or 'reference', not {placement!r}")
     return status
+
+
+def reference_rows(shards, slot_map):
+    """The k data rows of every group after a reference-placement decode, in
+    data[] order: shards[g, slot_map[g, i]] (a [G, k, S] gather, on the
+    device)."""
+    import torch
+    G = shards.shape[0]
+    gi = torch.arange(G, device=shards.device).unsqueeze(1)
+    return shards[gi, slot_map.long()]
+
+
+def ref_slot_map(k: int, n: int, present) -> np.ndarray:
+    """Host slot map of one group (rsmi_ref_slot_map): the slot holding data
+    row i after rs_decode2, the permutation fec_decode's shuffle leaves in
+    data[0..k-1] (0xFF: erased row of a group with too few shards)."""
+    pres = np.ascontiguousarray(np.asarray(present, np.uint8).reshape(-1)[:n])
+    out = np.zeros(k, np.uint8)
+    rc = lib().rsmi_ref_slot_map(k, n, pres.ctypes.data, out.ctypes.data)
+    if rc < -1:
+        raise RsmiError(f"rsmi_ref_slot_map failed ({rc})")
+    return out
 
 
 def make_groups(ks: Iterable[int], ns: Iterable[int], lens: Iterable[int],
