@@ -294,6 +294,18 @@ int rsmi_decode_ragged_dev(const rsmi_group *dev_groups, int64_t ngroups, uint8_
  * and returns once it has completed. */
 int rsmi_decode_ragged(const rsmi_group *groups, int64_t ngroups, uint8_t *base,
                        const uint32_t *present_bits, int32_t *status, void *stream);
+/* The ragged decodes with the reference's placement (as rsmi_decode_dev_ref):
+ * rebuilt data rows over the parity survivors fec_decode's shuffle leaves in
+ * data[i]; slot_map (DEVICE, may be NULL) receives group g's k entries at
+ * slot_map + g * map_stride (entries i >= map_stride are not written), 0xFF
+ * for an erased row of a group not decoded; groups with status
+ * RSMI_DEC_UNSUPPORTED get no map.  Erased data slots are scratch. */
+int rsmi_decode_ragged_plan_ref(const rsmi_ragged_plan *plan, uint8_t *base,
+                                const uint32_t *present_bits, int32_t *status,
+                                uint8_t *slot_map, int32_t map_stride, void *stream);
+int rsmi_decode_ragged_dev_ref(const rsmi_group *dev_groups, int64_t ngroups, uint8_t *base,
+                               const uint32_t *present_bits, int32_t *status, int kmax,
+                               uint8_t *slot_map, int32_t map_stride, void *stream);
 void rsmi_ragged_plan_destroy(rsmi_ragged_plan *plan);
 
 /* ---- host-memory convenience (pinned staging + H2D/D2H on an internal

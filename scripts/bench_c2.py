@@ -33,13 +33,19 @@ def time_ms(fn, reps=30, settle_ms=300.0):
 
 
 out = {}
+smap = torch.empty((G, K), dtype=torch.uint8, device="cuda")
 for name, lim in (("c2_random", 0), ("c2_worst", K)):
     pres = torch.from_numpy(synth.erasure_present(synth.ERASE_SEED + (1 if lim else 0), 0, G, N, 5,
                                                   limit=lim)).to("cuda")
     st = torch.empty(G, dtype=torch.int32, device="cuda")
-    ms = time_ms(lambda: u.decode(buf, pres, K, N, LEN, status=st))
     e = (pres[:, :K] == 0).sum(1).cpu()
     alg = int(((e > 0) * K * LEN).sum() + (e * LEN).sum())
-    assert int((st != 0).sum()) == 0
-    out[name] = {"decode_ms": round(ms, 4), "frac": round(alg / (ms * 1e-3) / 8e12, 4)}
+    for place in ("own", "ref"):
+        if place == "own":
+            ms = time_ms(lambda: u.decode(buf, pres, K, N, LEN, status=st))
+        else:  # the reference's placement (over the parity survivors; the bytes read change, not the work)
+            ms = time_ms(lambda: u.decode(buf, pres, K, N, LEN, status=st, placement="reference", slot_map=smap))
+            u.encode(buf, K, N, LEN)
+        assert int((st != 0).sum()) == 0
+        out[f"{name}_{place}"] = {"decode_ms": round(ms, 4), "frac": round(alg / (ms * 1e-3) / 8e12, 4)}
 print(json.dumps(out))

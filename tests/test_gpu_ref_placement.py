@@ -166,3 +166,114 @@ def test_ref_placement_roundtrip_repeated(gpu):
         st = u.decode(t, pres, k, n, ln, placement="reference", slot_map=smap)
         assert int((st != 0).sum().item()) == 0
         assert torch.equal(u.reference_rows(t, smap)[:, :, :ln], orig)
+
+
+# ---------------------------------------------------------------- ragged
+def _ragged_ref_check(u, oracle, groups, host, flags, out, st, smap, stride):
+    """Every group against the oracle: status, the slot map (host closed form,
+    entries < stride), the bytes behind each data[i], and every slot that is
+    neither a destination nor an erased data slot left as it was."""
+    for i in range(len(groups)):
+        d = groups[i]
+        n, k, S = d.n, d.k, d.shard_stride
+        seg = host[d.offset:d.offset + n * S].copy()
+        ost = oracle.decode_batch(k, n, seg, 0, S, d.len, 1, flags[i:i + 1, :n])
+        assert st[i] == ost[0], (i, k, n)
+        if st[i] not in (0, -1):
+            continue
+        exp_map = u.ref_slot_map(k, n, flags[i, :n])
+        kk = min(k, stride)
+        assert (smap[i, :kk] == exp_map[:kk]).all(), (i, k, n)
+        got = out[d.offset:d.offset + n * S].reshape(n, S)
+        org = host[d.offset:d.offset + n * S].reshape(n, S)
+        if st[i] == 0:
+            exp = seg.reshape(n, S)
+            for j in range(k):
+                assert (got[exp_map[j], :d.len] == exp[j, :d.len]).all(), (i, k, n, j)
+        dst = set(int(x) for x in exp_map) - set(range(k)) if st[i] == 0 else set()
+        for j in range(n):
+            if j in dst or (j < k and not flags[i, j]):
+                continue
+            assert (got[j] == org[j]).all(), (i, j)
+        pad = pad_end(d.len, S)
+        assert (got[:, pad:] == org[:, pad:]).all(), i
+
+
+@pytest.mark.parametrize("form", ["plan", "dev"])
+def test_ref_ragged_many_codes_vs_oracle(gpu, oracle, form):
+    """Ragged reference-placement decode over ~200 codes: e up to 10 (row
+    blocks of 5: the earlier blocks parked and moved), k up to 60 (k > 32:
+    the workgroup kernel), lengths 1..3000 (several tiles), too-few groups;
+    slot maps with a stride smaller than some k."""
+    import torch
+    import udpspeeder_amd as u
+    from udpspeeder_amd import synth
+    rng = np.random.default_rng(606)
+    G = 500
+    ks = rng.integers(1, 61, G)
+    ms = rng.integers(1, 21, G)
+    ls = rng.integers(1, 3000, G)
+    ls[:4] = [1, 16, 1280, 1281]
+    groups, total = u.make_groups(ks, ks + ms, ls)
+    host = rng.integers(0, 256, total, dtype=np.uint8)
+    flags = np.zeros((G, 256), np.uint8)
+    for i in range(G):
+        n, m = int(ks[i] + ms[i]), int(ms[i])
+        flags[i, :n] = 1
+        flags[i, rng.choice(n, min(int(rng.integers(0, 12)), n), replace=False)] = 0
+    for c in set(zip(ks.tolist(), (ks + ms).tolist())):
+        u.prepare_code(*c)
+    base = upload(host, gpu)
+    bits = torch.from_numpy(synth.present_bits(flags).view(np.int32)).to(gpu)
+    stride = 48
+    smap = torch.full((G, stride), 0xEE, dtype=torch.uint8, device=gpu)
+    if form == "plan":
+        plan = u.rs.RaggedPlan(groups, wait_codes=False)
+        st = plan.decode(base, bits, placement="reference", slot_map=smap)
+        torch.cuda.synchronize()
+        plan.close()
+    else:
+        from udpspeeder_amd._lib import check
+        st = torch.empty(G, dtype=torch.int32, device=gpu)
+        dg = u.rs.groups_to_device(groups, gpu)
+        check(u.lib().rsmi_decode_ragged_dev_ref(dg.data_ptr(), G, base.data_ptr(), bits.data_ptr(),
+                                                 st.data_ptr(), 60, smap.data_ptr(), stride, None),
+              "rsmi_decode_ragged_dev_ref")
+    _ragged_ref_check(u, oracle, groups, host, flags, base.cpu().numpy(), st.cpu().numpy(),
+                      smap.cpu().numpy(), stride)
+
+
+def test_ref_ragged_c3_full_sha(gpu, golden):
+    """C3 decode at full size through a plan with the reference's placement:
+    the rows read through the slot map hash to the reference's digest."""
+    import torch
+    import udpspeeder_amd as u
+    from udpspeeder_amd import synth
+    F = golden.full["c3_ragged_decode"]
+    table = u.rs_from_str(F["fec"])
+    ks, ms, ls = synth.ragged_mix(F["ragged_seed"], 0, F["groups"], [y for _, y in table])
+    groups, total = u.make_groups(ks, ks + ms, ls)
+    base = torch.zeros(total, dtype=torch.uint8, device=gpu)
+    u.rs.fill_ragged(base, u.rs.groups_to_device(groups, gpu), len(groups), DATA_SEED)
+    par, _ = u.make_groups(np.maximum(ms, 1), np.maximum(ms, 1), ls)
+    for i in range(len(groups)):
+        par[i].offset = groups[i].offset + groups[i].k * groups[i].shard_stride
+        par[i].shard_stride = groups[i].shard_stride
+    u.rs.fill_ragged(base, u.rs.groups_to_device(par, gpu), len(groups), F["parity_seed"])
+    flags = synth.ragged_erasures(F["erase_seed"], 0, ks + ms, ms, F["erasures"])
+    bits = torch.from_numpy(synth.present_bits(flags).view(np.int32)).to(gpu)
+    plan = u.rs.RaggedPlan(groups)
+    G = len(groups)
+    smap = torch.empty((G, 20), dtype=torch.uint8, device=gpu)
+    st = plan.decode(base, bits, placement="reference", slot_map=smap)
+    torch.cuda.synchronize()
+    plan.close()
+    assert int((st != 0).sum()) == 0
+    out = base.cpu().numpy()
+    m = smap.cpu().numpy()
+    h = hashlib.sha256()
+    for i in range(G):
+        d = groups[i]
+        rows = out[d.offset:d.offset + d.n * d.shard_stride].reshape(d.n, d.shard_stride)
+        h.update(rows[m[i, :d.k].astype(np.int64), :d.len].tobytes())
+    assert h.hexdigest() == F["data_out_sha256"]

@@ -117,6 +117,8 @@ def _bind(lib: C.CDLL) -> C.CDLL:
         "rsmi_ragged_plan_uses_bitslice": ([vp], i32),
         "rsmi_ragged_plan_destroy": ([vp], None),
         "rsmi_decode_ragged_plan": ([vp, vp, vp, vp, vp], i32),
+        "rsmi_decode_ragged_plan_ref": ([vp, vp, vp, vp, vp, i32, vp], i32),
+        "rsmi_decode_ragged_dev_ref": ([vp, i64, vp, vp, vp, i32, vp, i32, vp], i32),
         "rsmi_decode_ragged_dev": ([vp, i64, vp, vp, vp, i32, vp], i32),
         "rsmi_decode_ragged": ([vp, i64, vp, vp, vp, vp], i32),
         "rsmi_encode_pinned": ([i32, i32, vp, i64, vp, i64, i64, i32, i64, i64], i32),

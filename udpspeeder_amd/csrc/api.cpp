@@ -358,7 +358,8 @@ int encode_ragged_dev(const rsmi_group *dg, int64_t ngroups, uint8_t *base, hipS
 }
 
 int decode_ragged_dev(const rsmi_group *dg, int64_t ngroups, uint8_t *base,
-                      const uint32_t *present_bits, int32_t *status, int kmax, hipStream_t s) {
+                      const uint32_t *present_bits, int32_t *status, int kmax, hipStream_t s,
+                      RefOut ro = RefOut{nullptr, 0, 0}) {
     if (ngroups < 0) return fail(RSMI_ERR_INVALID, "negative ngroups");
     if (ngroups == 0) return RSMI_OK;
     if (!dg || !base || !present_bits || !status)
@@ -368,7 +369,7 @@ int decode_ragged_dev(const rsmi_group *dg, int64_t ngroups, uint8_t *base,
     Device *D = current(&rc);
     if (!D) return rc;
     hipError_t e = launch_decode_ragged(dg, ngroups, base, present_bits, status, kmax,
-                                        D->code_dir, D->ptab, D->gftab, s);
+                                        D->code_dir, D->ptab, D->gftab, s, ro);
     if (e != hipSuccess) return hip_fail(e, "ragged decode launch");
     return RSMI_OK;
 }
@@ -391,7 +392,7 @@ int decode_ragged_cls_dev(const rsmi_group *dg, int64_t ngroups, const ClsLaunch
     // class kernels take any e in row blocks); without one, no big launch
     if (e == hipSuccess && C.need_big)
         e = launch_decode_ragged_big(dg, ngroups, base, present_bits, status, D->code_dir, D->ptab,
-                                     D->gftab, s, C.defer, C.epoch);
+                                     D->gftab, s, C.defer, C.epoch, C.ref);
     if (e != hipSuccess) return hip_fail(e, "ragged decode launch");
     return RSMI_OK;
 }
@@ -1417,6 +1418,14 @@ int rsmi_encode_ragged(const rsmi_group *groups, int64_t ngroups, uint8_t *base,
         return RSMI_ERR_HIP;
     }
     return RSMI_OK;
+}
+
+int rsmi_decode_ragged_dev_ref(const rsmi_group *groups, int64_t ngroups, uint8_t *base,
+                               const uint32_t *present_bits, int32_t *status, int kmax,
+                               uint8_t *slot_map, int32_t map_stride, void *stream) {
+    if (slot_map && map_stride < 1) return rsmi::fail(RSMI_ERR_INVALID, "map_stride < 1");
+    return rsmi::decode_ragged_dev(groups, ngroups, base, present_bits, status, kmax, (hipStream_t)stream,
+                                   rsmi::RefOut{slot_map, map_stride, 1});
 }
 
 int rsmi_decode_ragged_dev(const rsmi_group *groups, int64_t ngroups, uint8_t *base,

@@ -751,6 +751,10 @@ static_assert(kFuseRecs <= kLpp, "k_cook_frame needs a lane per source record (C
 #ifndef COOKF_ONE_CHAIN
 #define COOKF_ONE_CHAIN 1  // k_cook_frame: one Horner chain per lane across its rounds
 #endif
+#ifndef COOKF_LINE
+#define COOKF_LINE 1  // k_cook_frame: lane pieces on the 128-byte line grid of the slot
+#endif
+static_assert(!COOKF_LINE || COOKF_ONE_CHAIN, "COOKF_LINE shifts the pieces of the one-chain fold only");
 constexpr int kPplF = COOKF_PPL;
 constexpr int kRoundF = 16 * kLpp * kPplF;
 
@@ -799,6 +803,14 @@ __global__ __launch_bounds__(kThreads, COOKF_OCC) void k_cook_frame(CookArgs a, 
         const int ph = (int)((uintptr_t)pkt & 15);
         uint8_t *pga = pkt - ph;
         uint8_t *oga = opkt - ph;
+        // COOKF_LINE: the lanes' piece grid starts on the 128-byte line that
+        // holds the packet's first grid piece (the slot start: that piece is
+        // 112 B in), `lead` pieces before it, which no lane touches -- so one
+        // store instruction writes whole lines of the plain slot (and of a
+        // slot-layout output), where the packet's own grid made every line
+        // two stores of different rounds (1.24x the plain stream's bytes,
+        // profiles/r05/cook_frame_probes)
+        const int lead = COOKF_LINE ? (int)(((uintptr_t)pga & 127) >> 4) : 0;
         const uint32_t i = (uint32_t)(slot - (int64_t)G.slot0);  // shard index in its group
         const bool m0 = G.mode == 0;
         const uint32_t fl = G.fec_len;
@@ -851,7 +863,7 @@ __global__ __launch_bounds__(kThreads, COOKF_OCC) void k_cook_frame(CookArgs a, 
         const uint32_t sstep = ivl ? mod_ivl(16u * kLpp, (uint32_t)ivl, magic) : 0u;
         const int Q = cookit ? (Lg + 15) >> 4 : 0;
         const int P0 = Lg & ~15;
-        const int nrm = wave_max((xall + kRoundF - 1) / kRoundF);
+        const int nrm = wave_max((xall + 16 * lead + kRoundF - 1) / kRoundF);
         uint32_t acc = 0;
         u32x4 dt = {0, 0, 0, 0};
         int Pt = -1;
@@ -869,7 +881,7 @@ __global__ __launch_bounds__(kThreads, COOKF_OCC) void k_cook_frame(CookArgs a, 
             const uint8_t *A[kPplF];
 #pragma unroll
             for (int p = 0; p < kPplF; ++p) {
-                const int P = r * kRoundF + 16 * (kLpp * p + hl);
+                const int P = r * kRoundF + 16 * (kLpp * p + hl - lead);
                 A[p] = reinterpret_cast<const uint8_t *>(raddr);  // readable dummy
                 if (P > 0 && P < xall) {
                     const uint32_t b = sbase + (uint32_t)(P - 16);
@@ -886,10 +898,10 @@ __global__ __launch_bounds__(kThreads, COOKF_OCC) void k_cook_frame(CookArgs a, 
                 cur[p] = (COOKF_PROBE & 4) ? u32x4{0, 0, 0, 0} : fpiece::window(A[p], 0, 16);
 #pragma unroll
             for (int p = 0; p < kPplF; ++p) {
-                const int P = r * kRoundF + 16 * (kLpp * p + hl);
+                const int P = r * kRoundF + 16 * (kLpp * p + hl - lead);
                 if (P == 0) {
                     cur[p] = u32x4{0u, 0u, __builtin_bswap32(G.seq), w1};
-                } else if (P >= xall) {
+                } else if (P >= xall || P < 0) {
                     cur[p] = u32x4{0u, 0u, 0u, 0u};
                 } else if (slow & (1 << p)) {
                     const uint32_t b = sbase + (uint32_t)(P - 16);
@@ -898,31 +910,33 @@ __global__ __launch_bounds__(kThreads, COOKF_OCC) void k_cook_frame(CookArgs a, 
                     for (uint32_t u = 1; u < nrec; ++u) t = roff[u] <= bb ? u : t;
                     cur[p] = fpiece::stream_piece(rv, t, nrec, (int64_t)b, (int64_t)slen, m0, G.nsrc);
                 }
-                if (P < pext && ok && !(COOKF_PROBE & 1) && !((COOKF_PROBE & 8) && P == 0))
+                if (P >= 0 && P < pext && ok && !(COOKF_PROBE & 1) && !((COOKF_PROBE & 8) && P == 0))
                     st_piece(pga + P, cur[p]);  // the plain packet, for the encoder
             }
             // ---- cook (k_cook's round, one Horner chain)
-            const int qr = min(max(Q - kPplF * kLpp * r, 0), kPplF * kLpp);
+            // (lead: round r's slot p holds pieces kLpp (r kPplF + p) + hl - lead)
+            const int qr = min(max(Q + lead - kPplF * kLpp * r, 0), kPplF * kLpp);
             const int qr_max = COOK_SKIP ? wave_max(qr) : kPplF * kLpp;
 #if COOKF_ONE_CHAIN
             RoundCrc<false> &rc = rcx;
 #else
             RoundCrc<false> rc;
 #endif
-            uint32_t ivr = ivl ? mod_ivl((uint32_t)(r * kRoundF + 16 * hl + 16 * ivl - ph), (uint32_t)ivl, magic)
+            uint32_t ivr = ivl ? mod_ivl((uint32_t)(r * kRoundF + 16 * (hl - lead) + 128 * ivl - ph), (uint32_t)ivl,
+                                         magic)
                                : 0u;
 #pragma unroll
             for (int p = 0; p < kPplF; ++p) {
-                const int P = r * kRoundF + 16 * (kLpp * p + hl);
+                const int P = r * kRoundF + 16 * (kLpp * p + hl - lead);
 #if COOKF_ONE_CHAIN
-                if (ck && kLpp * p < qr_max) {
+                if (ck && kLpp * p < qr_max && P >= 0) {
                     const int sl = r * kPplF + p;  // the lane's slot over all rounds
-                    rc.add(T, crc_in_ph(cur[p], P, Lg, ph), sl, kLpp * sl + hl, Q);
+                    rc.add(T, crc_in_ph(cur[p], P, Lg, ph), sl, kLpp * sl + hl - lead, Q);
                 }
 #else
                 if (ck && kLpp * p < qr_max) rc.add(T, crc_in_ph(cur[p], P, Lg, ph), p, kLpp * p + hl, qr);
 #endif
-                if (P < ext && P + 16 <= Lg) {
+                if (P >= 0 && P < ext && P + 16 <= Lg) {
                     u32x4 m = ks_piece(a, P - ph);
                     if (ivl) m ^= iv_window_at(iv2w, ivr);
                     if (!(COOKF_PROBE & 2)) st_piece(oga + P, cur[p] ^ m);

@@ -62,12 +62,14 @@ constexpr int kWaves = 4;      // waves per block (one group each)
 #define DEC_ST_BIG_E 5            // (4: C2 random 0.385-0.387 vs 0.381-0.383 ms at 5)
 #endif
 #ifndef DEC_REF_ST_AUX
-#define DEC_REF_ST_AUX 0       // store policy of the reference-placement rows (over the parity survivors
-                               // just read): default (dec4_probe "last survivors' slots": 0.348-0.352 ms,
-                               // against 0.354-0.359 with sc0|sc1)
+#define DEC_REF_ST_AUX 16      // store policy of the reference-placement rows (over the parity survivors
+                               // just read): sc1 as for own slots (round 6, profiles/r06/c2_place_ab.txt:
+                               // C2 random 0.3768-0.3789 ms vs own slots 0.3775-0.3783; default policy
+                               // 0.380-0.383, nt 0.398; the pattern probe's "last survivors' slots" gain
+                               // does not carry over to the kernel)
 #endif
 #ifndef DEC_REF_ST_AUX_BIG
-#define DEC_REF_ST_AUX_BIG DEC_REF_ST_AUX
+#define DEC_REF_ST_AUX_BIG 2
 #endif
 #ifndef DEC_RAG_ST_AUX
 #define DEC_RAG_ST_AUX 16      // cache policy of the ragged kernels' rebuilt-row stores: sc1 (C3 decode
@@ -807,6 +809,45 @@ struct NoHook {
     __device__ void operator()() const {}
 };
 
+// The reference's placement (RefOut.on; rsmi_decode_dev_ref's rule, ref_slot_of
+// over the slice's sel[]): the slot of the parity survivor fec_decode's
+// shuffle leaves in data[row].
+__device__ __forceinline__ int ref_slot_lds(const uint8_t *sel, int k, int e, int row) {
+    int x = row;
+    while (x < k - e) x = sel[x];
+    return sel[x];
+}
+
+// A group's slot map (lanes i < k <= 64): i for a present data row, its
+// reference slot for a rebuilt one, 0xFF for an erased row of a group that
+// was not decoded.
+template <class Flag>
+__device__ __forceinline__ void write_slot_map(const RefOut &ro, int64_t g, int k, int e, bool decoded,
+                                               Flag flag, const WaveLds &L, int lane) {
+    if (!ro.map || lane >= k || lane >= ro.stride) return;
+    const bool p = flag(0, lane);
+    ro.map[g * ro.stride + lane] =
+        p ? (uint8_t)lane : decoded ? (uint8_t)ref_slot_lds(L.sel, k, e, lane) : (uint8_t)0xFF;
+}
+
+// Move rows [0, nrows) of the group from their own (erased) slots to their
+// reference slots: 16-byte pieces over the padded length, the stores ordered
+// before the loads, which read past the CU cache (other lanes wrote them).
+__device__ __forceinline__ void ref_move_rows(__amdgpu_buffer_rsrc_t rsrc, const WaveLds &L, int k, int e,
+                                              int nrows, uint32_t ss, int lpad, int lane) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    for (int r = 0; r < nrows; ++r) {
+        const int row = L.miss[r];
+        const uint32_t src = (uint32_t)row * ss;
+        const uint32_t dst = (uint32_t)__builtin_amdgcn_readfirstlane(ref_slot_lds(L.sel, k, e, row)) * ss;
+        for (int p = 16 * lane; p < lpad; p += 1024) {
+            const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (uint32_t)p, src, 1);
+            __builtin_amdgcn_raw_buffer_store_b128(v, rsrc, (uint32_t)p + dst, 0, DEC_RAG_ST_AUX);
+        }
+    }
+}
+
 // after_select() runs once, right after the survivor selection (the class
 // kernels fetch the next group's present words there).
 // Rows rb0 .. rb0 + NR - 1 of the group's missing data rows (the slice holds
@@ -818,7 +859,8 @@ __device__ __forceinline__ bool ragged_group_run(const GroupDesc &D, Flag flag, 
                                                  int32_t *status_out, const RagTables &T,
                                                  const WaveLds &L, int kmax, int lane,
                                                  DeferMark dm = DeferMark{nullptr, 0},
-                                                 Hook after_select = Hook{}, int rb0 = 0) {
+                                                 Hook after_select = Hook{}, int rb0 = 0,
+                                                 RefOut ro = RefOut{nullptr, 0, 0}) {
     const int64_t g = D.g;
     const int k = D.k, n = D.n, len = D.len;
     const uint32_t ss = D.ss;
@@ -841,6 +883,7 @@ __device__ __forceinline__ bool ragged_group_run(const GroupDesc &D, Flag flag, 
 #endif
     if (cnt < k || e == 0) {
         if (lane == 0) status_out[g] = cnt < k ? RSMI_DEC_TOO_FEW : RSMI_DEC_OK;
+        if (ro.on) write_slot_map(ro, g, k, e, false, flag, L, lane);
         return false;
     }
     if (k > kmax || (uint64_t)n * ss >= 0x80000000ull) {
@@ -864,14 +907,23 @@ __device__ __forceinline__ bool ragged_group_run(const GroupDesc &D, Flag flag, 
         // rows rb0 .. rb0 + nb0 - 1 of the e missing ones (lane d: row rb0 + d)
         const uint32_t miss_lane = lane + rb0 < e ? (uint32_t)L.miss[lane + rb0] : 0u;
         B.so_lane = sel_lane * ss;
-        B.mo_lane = miss_lane * ss;
         const int nb0 = e - rb0 < NR ? e - rb0 : NR;
+        // the reference's placement: the group's last pass of kPass rows (the
+        // last block's, B.run makes kPass-row passes per tile) writes over
+        // the parity survivors -- every read of the tile is behind its stores
+        // -- and the rows before it park in their own slots, moved after it
+        const bool last = rb0 + NR >= e;
+        const int lastpass = (nb0 - 1) / kPass * kPass;  // its first row, relative to rb0
+        B.mo_lane = (ro.on && last && lane >= lastpass && lane + rb0 < e
+                         ? (uint32_t)ref_slot_lds(L.sel, k, e, (int)miss_lane) : miss_lane) * ss;
         if (len > 0) B.start_tile(0, lane);  // the first survivors fly while the coefficients form
         lagrange_coefs<NR>(k, nb0, sel_lane, miss_lane, L, T, lane);  // distinct points: never singular
 #if DEC_TRACE
         const uint64_t tr2 = trace_now();
 #endif
         if (len > 0) B.run(L, lane, 0, nb0);
+        if (ro.on && last && rb0 + lastpass > 0 && len > 0)
+            ref_move_rows(B.rsrc, L, k, e, rb0 + lastpass, ss, lpad, lane);
         const int st = RSMI_DEC_OK;
 #if DEC_TRACE
         const uint64_t tr3 = trace_now();
@@ -895,6 +947,7 @@ __device__ __forceinline__ bool ragged_group_run(const GroupDesc &D, Flag flag, 
     }
     if (rb0 + NR < e) return true;  // more rows: the status waits for the last block
     if (lane == 0) status_out[g] = st;
+    if (ro.on) write_slot_map(ro, g, k, e, true, flag, L, lane);
     return false;
 }
 
@@ -904,7 +957,7 @@ template <int WC, int NR>
 __device__ __forceinline__ void ragged_group(int64_t g, const rsmi_group &d, uint32_t w8,
                                              uint8_t *base, int32_t *status_out,
                                              const uint64_t *code_dir, const RagTables &T,
-                                             const WaveLds &L, int kmax, int lane) {
+                                             const WaveLds &L, int kmax, int lane, RefOut ro) {
     GroupDesc D;
     D.g = g;
     D.k = __builtin_amdgcn_readfirstlane(d.k);
@@ -925,7 +978,7 @@ __device__ __forceinline__ void ragged_group(int64_t g, const rsmi_group &d, uin
                 const uint32_t hi = __builtin_amdgcn_readlane(w8, ((b >> 5) + 1) & 7);
                 return ((((idx & 32) ? hi : lo) >> (idx & 31)) & 1u) != 0;
             },
-            base, status_out, T, L, kmax, lane, DeferMark{nullptr, 0}, NoHook{}, rb0);
+            base, status_out, T, L, kmax, lane, DeferMark{nullptr, 0}, NoHook{}, rb0, ro);
         wave_sync();  // the LDS slice is rewritten by the next block or group
         if (!more) break;
     }
@@ -936,7 +989,7 @@ __device__ __forceinline__ void ragged_group(int64_t g, const rsmi_group &d, uin
 __global__ __launch_bounds__(256, DEC_RAG_OCC) void k_decode_ragged(
     const rsmi_group *__restrict__ groups, int64_t ngroups, uint8_t *base,
     const uint32_t *__restrict__ present, int32_t *status_out, const uint64_t *__restrict__ code_dir,
-    const uint32_t *ptab, const uint8_t *gftab, int kmax) {
+    const uint32_t *ptab, const uint8_t *gftab, int kmax, RefOut ro) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const RagTables T = load_rag_tables(smem, ptab, gftab);
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -951,7 +1004,7 @@ __global__ __launch_bounds__(256, DEC_RAG_OCC) void k_decode_ragged(
         asm volatile("" : "+v"(lane));
         const rsmi_group d = groups[g];
         ragged_group<0, kRows>(g, d, present[g * 8 + (lane & 7)], base, status_out, code_dir, T, L,
-                               kmax, lane);
+                               kmax, lane, ro);
         wave_sync();  // the LDS slice is rewritten by the next group
     }
 }
@@ -972,7 +1025,7 @@ template <int W>
 __device__ __forceinline__ void cls_block(const uint32_t *__restrict__ rec, uint32_t i0, uint32_t cnt,
                                           int maxb, uint8_t *base, const uint32_t *__restrict__ present,
                                           int32_t *status_out, const uint32_t *ptab, const uint8_t *gftab,
-                                          int kmax, DeferMark dm, int b) {
+                                          int kmax, DeferMark dm, int b, RefOut ro) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
 #if DEC_TRACE
     const uint64_t tk0 = trace_now();
@@ -1034,7 +1087,7 @@ __device__ __forceinline__ void cls_block(const uint32_t *__restrict__ rec, uint
                     const uint32_t hi = __builtin_amdgcn_readlane(pw, ((bb >> 5) + 1) & 7);
                     return ((((idx & 32) ? hi : lo) >> (idx & 31)) & 1u) != 0;
                 },
-                base, status_out, T, L, kmax, lane_g, dm, NoHook{}, rb0);
+                base, status_out, T, L, kmax, lane_g, dm, NoHook{}, rb0, ro);
             wave_sync();  // the LDS slice is rewritten by the next block or group
             if (!more) break;
         }
@@ -1045,10 +1098,11 @@ template <int W, int OCC>
 __global__ __launch_bounds__(64 * kClsWaves, OCC) void k_decode_ragged_cls(
     const uint32_t *__restrict__ rec, const uint32_t *__restrict__ wst, int nb, int maxb, uint8_t *base,
     const uint32_t *__restrict__ present, int32_t *status_out, const uint32_t *ptab,
-    const uint8_t *gftab, int kmax, DeferMark dm) {
+    const uint8_t *gftab, int kmax, DeferMark dm, RefOut ro) {
     const int b = blockIdx.x;
     if (b >= nb) return;  // (whole block: before any barrier)
-    cls_block<W>(rec, wst[b], wst[b + 1] - wst[b], maxb, base, present, status_out, ptab, gftab, kmax, dm, b);
+    cls_block<W>(rec, wst[b], wst[b + 1] - wst[b], maxb, base, present, status_out, ptab, gftab, kmax, dm, b,
+                 ro);
 }
 
 // Several classes in one launch (DEC_MIX): the grid is the classes' workgroups
@@ -1063,13 +1117,13 @@ template <int OCC, int CMASK>
 __global__ __launch_bounds__(64 * kClsWaves, OCC) void k_decode_ragged_mix(
     const uint32_t *__restrict__ rec, MixGrid M, int maxb, uint8_t *base,
     const uint32_t *__restrict__ present, int32_t *status_out, const uint32_t *ptab,
-    const uint8_t *gftab, int kmax, DeferMark dm) {
+    const uint8_t *gftab, int kmax, DeferMark dm, RefOut ro) {
     int b = blockIdx.x;
 #define RSMI_MIX_CLASS(c, W)                                                                        \
     if (CMASK & (1 << c)) {                                                                         \
         if (b < M.nb[c]) {                                                                          \
             cls_block<W>(rec, M.wst[c][b], M.wst[c][b + 1] - M.wst[c][b], maxb, base, present,      \
-                         status_out, ptab, gftab, kmax, dm, b);                                     \
+                         status_out, ptab, gftab, kmax, dm, b, ro);                                 \
             return;                                                                                 \
         }                                                                                           \
         b -= M.nb[c];                                                                               \
@@ -1091,7 +1145,7 @@ constexpr int kBigRows = 8;
 __global__ __launch_bounds__(256) void k_decode_ragged_big(
     const rsmi_group *groups, int64_t ngroups, uint8_t *base, const uint32_t *present,
     int32_t *status_out, const uint64_t *code_dir, const uint32_t *ptab, const uint8_t *gftab,
-    const uint32_t *defer_word, uint32_t epoch) {
+    const uint32_t *defer_word, uint32_t epoch, RefOut ro) {
     // plans: nothing to do unless a class kernel marked a deferral this call
     if (defer_word && (uint32_t)__builtin_amdgcn_readfirstlane(*defer_word) < epoch) return;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -1206,6 +1260,30 @@ __global__ __launch_bounds__(256) void k_decode_ragged_big(
                                 *reinterpret_cast<uint32_t *>(gb + miss[rb + r] * ss + 4 * w) = acc[r];
                     }
                 }
+                if (ro.on) {
+                    // the reference's placement: every row from its own slot
+                    // to the parity survivor fec_decode's shuffle picks (all
+                    // reads of the survivors are behind the barrier)
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                    __syncthreads();
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                    const int pieces = (len + 15) >> 4;
+                    for (int t = tid; t < e * pieces; t += 256) {
+                        const int r = t / pieces, p = t - r * pieces;
+                        const int dst = ref_slot_lds(sel, k, e, miss[r]);
+                        *reinterpret_cast<u32x4 *>(gb + dst * ss + 16 * p) =
+                            __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(gb + miss[r] * ss + 16 * p));
+                    }
+                }
+            }
+            if (ro.on && ro.map) {
+                const uint32_t *pw8 = present + g * 8;
+                for (int i = tid; i < k && i < ro.stride; i += 256) {
+                    const bool p = (pw8[i >> 5] >> (i & 31)) & 1u;
+                    ro.map[g * ro.stride + i] = p ? (uint8_t)i
+                                              : st == RSMI_DEC_OK ? (uint8_t)ref_slot_lds(sel, k, e, i)
+                                                                  : (uint8_t)0xFF;
+                }
             }
             if (tid == 0) status_out[g] = st;
             __syncthreads();  // sel / miss / aug are rewritten by the next group
@@ -1243,27 +1321,22 @@ hipError_t launch_decode_fused(const UniformArgs &a, const uint8_t *present,
     return hipGetLastError();
 }
 
-hipError_t launch_decode_ragged_big(const rsmi_group *groups, int64_t ngroups, uint8_t *base,
-                                    const uint32_t *present_bits, int32_t *status,
-                                    const uint64_t *code_dir, const uint32_t *ptab,
-                                    const uint8_t *gftab, hipStream_t s, const uint32_t *defer_word,
-                                    uint32_t epoch);
 
 hipError_t launch_decode_ragged(const rsmi_group *groups, int64_t ngroups, uint8_t *base,
                                 const uint32_t *present_bits, int32_t *status, int kmax,
                                 const uint64_t *code_dir, const uint32_t *ptab,
-                                const uint8_t *gftab, hipStream_t s) {
+                                const uint8_t *gftab, hipStream_t s, RefOut ro) {
     if (ngroups <= 0) return hipSuccess;
     kmax = kmax < 1 ? 1 : (kmax > 32 ? 32 : kmax);  // larger k: the workgroup kernel
     const size_t lds = kRagTabBytes + (size_t)kWaves * rag_lds_bytes(kmax, kRows);
     int64_t blocks = (ngroups + kWaves - 1) / kWaves;
     if (blocks > 256 * 8) blocks = 256 * 8;
     k_decode_ragged<<<(unsigned)blocks, 64 * kWaves, lds, s>>>(groups, ngroups, base, present_bits,
-                                                              status, code_dir, ptab, gftab, kmax);
+                                                              status, code_dir, ptab, gftab, kmax, ro);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     return launch_decode_ragged_big(groups, ngroups, base, present_bits, status, code_dir, ptab,
-                                    gftab, s);
+                                    gftab, s, nullptr, 0, ro);
 }
 
 // tables | wave slices | records | present words | counter
@@ -1289,7 +1362,7 @@ hipError_t launch_decode_ragged_cls(const rsmi_group *groups, const ClsLaunch &C
         const size_t lds = cls_lds_bytes(kmax, C.maxb[c]);
         kern<<<(unsigned)nb, 64 * kClsWaves, lds, cs[c]>>>(C.rec, C.wst[c], nb, C.maxb[c], base,
                                                         present_bits, status, ptab, gftab, kmax,
-                                                        DeferMark{C.defer, C.epoch});
+                                                        DeferMark{C.defer, C.epoch}, C.ref);
         return hipGetLastError();
     };
     // classes in one launch: CMASK's classes, OCC waves per SIMD
@@ -1304,7 +1377,7 @@ hipError_t launch_decode_ragged_cls(const rsmi_group *groups, const ClsLaunch &C
         }
         if (nb <= 0) return hipSuccess;
         kern<<<(unsigned)nb, 64 * kClsWaves, cls_lds_bytes(kmax, maxb), cs[3]>>>(
-            C.rec, M, maxb, base, present_bits, status, ptab, gftab, kmax, DeferMark{C.defer, C.epoch});
+            C.rec, M, maxb, base, present_bits, status, ptab, gftab, kmax, DeferMark{C.defer, C.epoch}, C.ref);
         return hipGetLastError();
     };
     hipError_t e = hipSuccess;
@@ -1321,14 +1394,14 @@ hipError_t launch_decode_ragged_big(const rsmi_group *groups, int64_t ngroups, u
                                     const uint32_t *present_bits, int32_t *status,
                                     const uint64_t *code_dir, const uint32_t *ptab,
                                     const uint8_t *gftab, hipStream_t s, const uint32_t *defer_word,
-                                    uint32_t epoch) {
+                                    uint32_t epoch, RefOut ro) {
     // one block per CU at most: when nothing was deferred (the usual case
     // for plans) every block only reads the mark and leaves, and 1,024 of
     // them cost 5 us of launch and drain per decode call (C3, rocprofv3)
     int64_t bb = (ngroups + 255) / 256;
     if (bb > 256) bb = 256;
     k_decode_ragged_big<<<(unsigned)bb, 256, kTabBytes + 512 + kBigAug, s>>>(
-        groups, ngroups, base, present_bits, status, code_dir, ptab, gftab, defer_word, epoch);
+        groups, ngroups, base, present_bits, status, code_dir, ptab, gftab, defer_word, epoch, ro);
     return hipGetLastError();
 }
 

@@ -35,7 +35,7 @@ const uint8_t *device_code_rows(int k, int n);
 void set_error(const std::string &m);
 uint64_t *device_code_dir(int *rc);
 int decode_ragged_dev(const rsmi_group *dg, int64_t ngroups, uint8_t *base,
-                      const uint32_t *present_bits, int32_t *status, int kmax, hipStream_t s);
+                      const uint32_t *present_bits, int32_t *status, int kmax, hipStream_t s, RefOut ro);
 int decode_ragged_cls_dev(const rsmi_group *dg, int64_t ngroups, const ClsLaunch &C, uint8_t *base,
                           const uint32_t *present_bits, int32_t *status, int kmax, hipStream_t s);
 const uint32_t *device_ptab(int *rc);
@@ -346,9 +346,9 @@ extern "C" int rsmi_encode_ragged_plan(const rsmi_ragged_plan *P, uint8_t *base,
     return RSMI_OK;
 }
 
-extern "C" int rsmi_decode_ragged_plan(const rsmi_ragged_plan *P, uint8_t *base,
-                                       const uint32_t *present_bits, int32_t *status,
-                                       void *stream) {
+namespace {
+int decode_plan_call(const rsmi_ragged_plan *P, uint8_t *base, const uint32_t *present_bits, int32_t *status,
+                     rsmi::RefOut ro, void *stream) {
     if (!P) return fail(RSMI_ERR_INVALID, "null plan");
     if (RSMI_DEC_CLASSES) {
         rsmi::ClsLaunch C = P->cls;
@@ -356,11 +356,26 @@ extern "C" int rsmi_decode_ragged_plan(const rsmi_ragged_plan *P, uint8_t *base,
         // after this one deferred (graph replays keep their captured mark and
         // may scan needlessly; never the reverse)
         C.epoch = const_cast<rsmi_ragged_plan *>(P)->epoch.fetch_add(1) + 1;
+        C.ref = ro;
         return rsmi::decode_ragged_cls_dev(P->d_groups, P->ngroups, C, base, present_bits, status,
                                            P->kmax, (hipStream_t)stream);
     }
     return rsmi::decode_ragged_dev(P->d_groups, P->ngroups, base, present_bits, status, P->kmax,
-                                   (hipStream_t)stream);
+                                   (hipStream_t)stream, ro);
+}
+}  // namespace
+
+extern "C" int rsmi_decode_ragged_plan(const rsmi_ragged_plan *P, uint8_t *base,
+                                       const uint32_t *present_bits, int32_t *status,
+                                       void *stream) {
+    return decode_plan_call(P, base, present_bits, status, rsmi::RefOut{nullptr, 0, 0}, stream);
+}
+
+extern "C" int rsmi_decode_ragged_plan_ref(const rsmi_ragged_plan *P, uint8_t *base,
+                                           const uint32_t *present_bits, int32_t *status,
+                                           uint8_t *slot_map, int32_t map_stride, void *stream) {
+    if (slot_map && map_stride < 1) return fail(RSMI_ERR_INVALID, "map_stride < 1");
+    return decode_plan_call(P, base, present_bits, status, rsmi::RefOut{slot_map, map_stride, 1}, stream);
 }
 
 extern "C" int rsmi_ragged_plan_uses_bitslice(const rsmi_ragged_plan *P) {

@@ -39,6 +39,16 @@ struct UniformArgs {
     int64_t ngroups;
 };
 
+// Ragged decodes with the reference's placement (rsmi_decode_ragged_*_ref):
+// on = 1 writes rebuilt rows over the parity survivors fec_decode's shuffle
+// picks (ref_slot_of); map (device, may be null) receives group g's slot map
+// at map + g * stride (entries i < min(k, stride)).
+struct RefOut {
+    uint8_t *map;
+    int32_t stride;
+    int32_t on;
+};
+
 // Host-side launchers implemented in kernels.hip; return hipError_t.
 hipError_t launch_encode_generic(const UniformArgs &a, int W, const uint8_t *parity_rows,
                                  const uint32_t *ptab, hipStream_t s);
@@ -83,7 +93,7 @@ __host__ __device__ inline int ref_slot_of(int k, int e, const uint8_t *sel, int
 hipError_t launch_decode_ragged(const rsmi_group *groups, int64_t ngroups, uint8_t *base,
                                 const uint32_t *present_bits, int32_t *status, int kmax,
                                 const uint64_t *code_dir, const uint32_t *ptab,
-                                const uint8_t *gftab, hipStream_t s);
+                                const uint8_t *gftab, hipStream_t s, RefOut ro = RefOut{nullptr, 0, 0});
 // Tile width of a ragged group (lane dwords: 1, 2, 4 or 5): the narrowest
 // that covers its padded length in one pass, else 1280-byte tiles.  Lane
 // pieces of 4, 8 or 16 bytes divide the padded length (a multiple of 16).
@@ -115,6 +125,7 @@ struct ClsLaunch {
     uint32_t epoch;          // this call's mark (plans count calls)
     int need_big;            // the plan holds groups the class kernels defer (k > 32, or
                              // slots spanning >= 2 GiB): launch the big kernel after them
+    RefOut ref;              // placement of this call's rows (set per call)
 };
 // The (k,n) code's parity rows on the current device (nullptr: not resident).
 const uint8_t *device_code_rows(int k, int n);
@@ -132,7 +143,8 @@ hipError_t launch_decode_ragged_big(const rsmi_group *groups, int64_t ngroups, u
                                     const uint32_t *present_bits, int32_t *status,
                                     const uint64_t *code_dir, const uint32_t *ptab,
                                     const uint8_t *gftab, hipStream_t s,
-                                    const uint32_t *defer_word = nullptr, uint32_t epoch = 0);
+                                    const uint32_t *defer_word = nullptr, uint32_t epoch = 0,
+                                    RefOut ro = RefOut{nullptr, 0, 0});
 
 // Bit-sliced encode kernels specialised at build time for hot (k,n) codes
 // (gen_bitslice.py -> gen/bitslice_codes.inc), or compiled at run time

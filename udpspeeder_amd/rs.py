@@ -351,16 +351,37 @@ class RaggedPlan:
         check(lib().rsmi_encode_ragged_plan(self._h, base.data_ptr(), _stream_handle(stream)),
               "rsmi_encode_ragged_plan")
 
-    def decode(self, base, present_bits, status=None, stream=None):
+    def decode(self, base, present_bits, status=None, stream=None, placement: str = "own",
+               slot_map=None):
         """rs_decode2 on every group of the plan's layout; ``present_bits`` an
         int32 [G, 8] CUDA tensor of 256-bit masks (synth.present_bits).
+        ``placement="reference"`` writes rebuilt rows where fec_decode does
+        (rsmi_decode_ragged_plan_ref); ``slot_map`` (uint8 [G, S] CUDA,
+        optional) then receives each group's first min(k, S) slot-map entries.
         Returns the int32 [G] status tensor."""
+        import torch
         _check_dev(base, "base")
         _present_bits(present_bits, self.ngroups, base.device)
         status = _status_out(status, self.ngroups, base.device)
-        check(lib().rsmi_decode_ragged_plan(self._h, base.data_ptr(), present_bits.data_ptr(),
-                                            status.data_ptr(), _stream_handle(stream)),
-              "rsmi_decode_ragged_plan")
+        if placement == "own":
+            if slot_map is not None:
+                raise ValueError("slot_map needs placement='reference'")
+            check(lib().rsmi_decode_ragged_plan(self._h, base.data_ptr(), present_bits.data_ptr(),
+                                                status.data_ptr(), _stream_handle(stream)),
+                  "rsmi_decode_ragged_plan")
+        elif placement == "reference":
+            mp, ms = None, 0
+            if slot_map is not None:
+                _check_dev(slot_map, "slot_map", torch.uint8)
+                if slot_map.dim() != 2 or slot_map.shape[0] != self.ngroups or \
+                        not slot_map.is_contiguous() or slot_map.device != base.device:
+                    raise ValueError("slot_map must be a contiguous [G, S] uint8 tensor on the base's device")
+                mp, ms = slot_map.data_ptr(), slot_map.shape[1]
+            check(lib().rsmi_decode_ragged_plan_ref(self._h, base.data_ptr(), present_bits.data_ptr(),
+                                                    status.data_ptr(), mp, ms, _stream_handle(stream)),
+                  "rsmi_decode_ragged_plan_ref")
+        else:
+            raise ValueError(f"placement must be 'own' or 'reference', not {placement!r}")
         return status
 
     def close(self) -> None:
