@@ -350,6 +350,20 @@ int rsmi_decode_pinned(int k, int n, uint8_t *host_shards, int64_t shards_gs,
 #define RSMI_PINNED_STAGED 2
 int rsmi_last_decode_pinned_path(void);
 
+/* Ragged batches in host memory (the mode-0 mix as it leaves the sockets):
+ * groups[] (HOST) describe the batch at host_base (offsets relative to it,
+ * ascending and non-overlapping, 16-aligned); chunks of chunk_groups groups
+ * flow H2D (their contiguous byte span) -> ragged encode (parity rows
+ * written) or decode (rebuilt data rows in their own slots; present_bits HOST
+ * uint32[ngroups * 8] as rsmi_decode_ragged_plan's, status HOST int32[ngroups],
+ * may be NULL) -> span D2H on three streams.  Host memory should be pinned.
+ * With a device list (rsmi_set_devices) the groups split into contiguous
+ * ranges of near-equal summed n * len, one per listed device.  Synchronous. */
+int rsmi_encode_ragged_pinned(const rsmi_group *groups, int64_t ngroups, uint8_t *host_base,
+                              int64_t chunk_groups);
+int rsmi_decode_ragged_pinned(const rsmi_group *groups, int64_t ngroups, uint8_t *host_base,
+                              const uint32_t *present_bits, int32_t *status, int64_t chunk_groups);
+
 /* ---- several GPUs behind the host-memory batch entry points --
  *
  * UDPspeeder serves up to max_conn_num = 200 connections from one libev
@@ -358,7 +372,8 @@ int rsmi_last_decode_pinned_path(void);
  * into contiguous group ranges, one per listed device, with no exchange
  * between them.  After rsmi_set_devices(devs, n) (n >= 1; a device may be
  * listed more than once), rsmi_encode_pinned and rsmi_decode_pinned run range
- * i = [G*i/n, G*(i+1)/n) on devs[i], each on its own host thread with its own
+ * i = [G*i/n, G*(i+1)/n) on devs[i] (the ragged host entries: ranges of
+ * near-equal summed n * len), each on its own host thread with its own
  * HIP streams and pipeline buffers; results land in that range's part of the
  * caller's host arrays, and the call returns when every range is done (the
  * first failing range's error is reported, prefixed with its device).  One

@@ -1,4 +1,5 @@
-"""A/B timing of the RS(20,10) C1 encode (and decode) for the library named by RSMI_LIB."""
+"""A/B timing of the RS(20,10) C1 encode (and the C2 decode, reference placement: bench.py's
+step) for the library named by RSMI_LIB."""
 import os, sys, statistics
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
@@ -9,10 +10,11 @@ t = torch.empty((G, n, 1280), dtype=torch.uint8, device="cuda")
 u.fill_data(t, k, ln, 5)
 pres = torch.from_numpy(synth.erasure_present(synth.ERASE_SEED, 0, G, n, 5)).cuda()
 st = torch.empty(G, dtype=torch.int32, device="cuda")
+sm = torch.empty((G, k), dtype=torch.uint8, device="cuda")
 enc, dec = [], []
 for i in range(40):
     a, b, c = (torch.cuda.Event(enable_timing=True) for _ in range(3))
-    a.record(); u.encode(t, k, n, ln); b.record(); u.decode(t, pres, k, n, ln, status=st); c.record()
+    a.record(); u.encode(t, k, n, ln); b.record(); u.decode(t, pres, k, n, ln, status=st, placement="reference", slot_map=sm); c.record()
     torch.cuda.synchronize()
     if i >= 5:
         enc.append(a.elapsed_time(b)); dec.append(b.elapsed_time(c))

@@ -49,3 +49,9 @@ assert int((st != 0).sum()) == 0 and torch.equal(base, clean)
 e = ((flags[:, :20] == 0) & (np.arange(20)[None, :] < ks[:, None])).sum(1)
 dalg = int(((ks + e) * ls).sum())
 print(json.dumps({"c3_decode_ms": td, "alg_GBps": dalg / (td * 1e-3) / 1e9, "frac": dalg / (td * 1e-3) / 8e12}))
+# the reference's placement (rebuilt rows over the parity survivors): the parity
+# slots change, so each timed call decodes a different input -- same work
+sm = torch.empty((G, 20), dtype=torch.uint8, device="cuda")
+tr = time_ms(lambda: plan.decode(base, bits, status=st, placement="reference", slot_map=sm))
+base.copy_(clean)
+print(json.dumps({"c3_decode_ref_ms": tr, "frac": dalg / (tr * 1e-3) / 8e12}))

@@ -78,3 +78,44 @@ for name, buf, chunk in (("zero_copy_pinned", shards, 4096), ("staged_pageable",
 assert torch.equal(shards[:, :k, :ln], tmp[:, :k, :ln].cpu())
 assert (pageable[:, :k, :ln] == tmp[:, :k, :ln].cpu().numpy()).all()
 print(json.dumps({"decode_e2e": dres}, indent=1))
+
+# ---- end-to-end C3 (the mode-0 mix) through the ragged host entries: each
+# chunk's contiguous span H2D, ragged encode / decode, span D2H; with
+# E2E_DEVICES the groups split by summed n * len (rsmi_encode_ragged_pinned)
+table = u.rs_from_str(synth.C3_FEC)
+ks, ms_, ls = synth.ragged_mix(synth.RAGGED_SEED, 0, G, [y for _, y in table])
+groups, total = u.make_groups(ks, ks + ms_, ls)
+rb = torch.zeros(total, dtype=torch.uint8).pin_memory()
+dtmp = torch.zeros(total, dtype=torch.uint8, device=dev)
+u.rs.fill_ragged(dtmp, u.rs.groups_to_device(groups, dev), G, synth.DATA_SEED)
+rb.copy_(dtmp)
+payload = float((ks * ls).sum())
+span = float(((ks + ms_) * np.array([g.shard_stride for g in groups])).sum())
+flags = synth.ragged_erasures(synth.ERASE_SEED, 0, ks + ms_, ms_, 5)
+bits = synth.present_bits(flags)
+rres = {"groups": G, "payload_bytes": payload, "span_bytes_each_way": span}
+for chunk in (4096, 16384):
+    for op in ("encode", "decode"):
+        fn = ((lambda: u.rs.encode_ragged_pinned(rb, groups, chunk_groups=chunk)) if op == "encode" else
+              (lambda: u.rs.decode_ragged_pinned(rb, groups, bits, chunk_groups=chunk)))
+        fn()
+        ts = []
+        for _ in range(5):
+            t0 = time.perf_counter()
+            fn()
+            ts.append(time.perf_counter() - t0)
+        t = sorted(ts)[len(ts) // 2]
+        rres[f"{op}_chunk{chunk}"] = {"s": t, "payload_GiBps": payload / t / 2**30,
+                                      "pcie_GBps_both_ways": 2 * span / t / 1e9}
+# the encode's parity against the device path
+plan = u.rs.RaggedPlan(groups)
+plan.encode(dtmp)
+torch.cuda.synchronize()
+plan.close()
+hb, db = rb.numpy(), dtmp.cpu().numpy()
+for g in range(0, G, 31):  # payload bytes of every row (the pad bytes may differ between encoders)
+    d = groups[g]
+    rows = lambda x: x[d.offset:d.offset + d.n * d.shard_stride].reshape(d.n, d.shard_stride)[:, :d.len]
+    assert (rows(hb) == rows(db)).all(), g
+rres["devices"] = u.rs.get_devices() or "current"
+print(json.dumps({"c3_ragged_e2e": rres}, indent=1))

@@ -7,7 +7,7 @@ R=$PWD
 O=$R/gpurun_out/traffic
 PMC_SETS="FETCH_SIZE;WRITE_SIZE" bash scripts/pmc_passes.sh traffic k_bs2_20_30 k_decode_fused -- scripts/ab_encode.py > /dev/null
 python scripts/pmc_traffic.py $O/p1/run_counter_collection.csv $O/p2/run_counter_collection.csv \
-    k_bs2_20_30 65536 2457600000 > $O/traffic_encode.json
+    k_bs2_20_30 65536 2457600000 encode > $O/traffic_encode.json
 python - <<'PY' > $O/alg_decode.txt
 import sys; sys.path.insert(0, ".")
 from udpspeeder_amd import synth
@@ -16,5 +16,5 @@ e = (p[:, :20] == 0).sum(1)
 print(int(((e > 0) * 20 * 1250).sum() + (e * 1250).sum()))
 PY
 python scripts/pmc_traffic.py $O/p1/run_counter_collection.csv $O/p2/run_counter_collection.csv \
-    k_decode_fused 65536 $(cat $O/alg_decode.txt) > $O/traffic_decode.json
+    k_decode_fused 65536 $(cat $O/alg_decode.txt) decode > $O/traffic_decode.json
 cat $O/traffic_encode.json $O/traffic_decode.json

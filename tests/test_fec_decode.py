@@ -350,3 +350,65 @@ def test_gpu_decode_collector_200_connections_match_reference(fx, gpu, native_pl
     col.close()
     for d in decs:
         d.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("devices", [[0, 0], [0, 0, 0]])
+def test_gpu_decode_collectors_split_over_device_list(fx, gpu, devices):
+    """The receive side sharded by connection (include/rsmi.h: one
+    collector per device, each the decoders of a contiguous connection range
+    from rsmi_split_ranges balanced by bytes received): 200 connections over
+    the device list [0, 0] ([0, 0, 0]) -- one collector and one host thread per
+    entry, every thread on its device -- run concurrently per flush; every
+    connection's return codes, output events and bytes equal the reference's."""
+    import threading
+    import torch
+    import udpspeeder_amd as u
+    from udpspeeder_amd.fec import FecDecodeCollector, FecDecoder
+    ncon = 200
+    cases = [_case(fx, NAMES[i % len(NAMES)]) for i in range(ncon)]
+    packed = [_pack(c["chan"]) for c in cases]
+    devs_t = [torch.from_numpy(h).cuda(devices[0]) for h, _, _ in packed]
+    ranges = u.rs.split_ranges(ncon, len(devices), [int(p[1].sum()) for p in packed])
+    decs = [FecDecoder() for _ in range(ncon)]
+    cols = [FecDecodeCollector() for _ in devices]
+    rng = np.random.default_rng(19)
+    cuts = []
+    for c in cases:
+        a, b = sorted(rng.integers(1, len(c["chan"]), 2))
+        cuts.append([0, int(a), int(b), len(c["chan"])])
+    ret = [[] for _ in range(ncon)]
+    out = [[] for _ in range(ncon)]
+    errs = []
+
+    def shard(r, bi):
+        try:
+            torch.cuda.set_device(devices[r])
+            lo, hi = ranges[r]
+            for ci in range(lo, hi):
+                host, lens, offs = packed[ci]
+                a, b = cuts[ci][bi], cuts[ci][bi + 1]
+                ret[ci] += list(decs[ci].plan(host, lens[a:b], offs[a:b], devs_t[ci]).ret)
+            if hi > lo:
+                cols[r].run_many(decs[lo:hi])
+            for ci in range(lo, hi):
+                a = cuts[ci][bi]
+                out[ci] += [(bts, e + a) for bts, e in decs[ci].outputs()]
+        except Exception as e:  # noqa: BLE001
+            errs.append(e)
+
+    for bi in range(3):
+        ths = [threading.Thread(target=shard, args=(r, bi)) for r in range(len(devices))]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join()
+        assert not errs, errs
+    for ci, c in enumerate(cases):
+        assert ret[ci] == c["ret"], ci
+        assert [e for _, e in out[ci]] == c["out_event"], ci
+        assert hashlib.sha256(b"".join(b for b, _ in out[ci])).digest() == c["sha"], ci
+    for col in cols:
+        col.close()
+    for d in decs:
+        d.close()

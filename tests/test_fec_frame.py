@@ -730,3 +730,82 @@ def test_plan_many_equals_one_plan_each(fx):
     col.close()
     for e in a + b:
         e.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("devices", [[0, 0], [0, 0, 0]])
+def test_gpu_collectors_split_over_device_list(fx, gpu, devices):
+    """The send side sharded by connection (include/rsmi.h: one
+    collector per device, each the managers of a contiguous connection range
+    from rsmi_split_ranges balanced by bytes sent): 200 connections over the
+    device list [0, 0] ([0, 0, 0]) -- one collector, slot array and host thread
+    per entry, every thread on its device -- run concurrently per flush;
+    every connection's packets equal the reference's."""
+    import threading
+    import torch
+    import udpspeeder_amd as u
+    from udpspeeder_amd.fec import FecCollector, FecEncoder
+    ncon = 200
+    cases = [_case(fx, NAMES[i % len(NAMES)]) for i in range(ncon)]
+    encs = [FecEncoder(c["rs"], c["mode"], c["mtu"], c["ql"], seq0=c["seq0"]) for c in cases]
+    ranges = u.rs.split_ranges(ncon, len(devices),
+                               [int(np.maximum(c["lens"], 0).sum()) for c in cases])
+    cols = [FecCollector() for _ in devices]
+    rng = np.random.default_rng(201)
+    cuts = []
+    for c in cases:
+        a, b = sorted(rng.integers(1, len(c["lens"]), 2))
+        cuts.append([0, int(a), int(b), len(c["lens"])])
+    got = [[] for _ in range(ncon)]
+    errs = []
+
+    def shard(r, bi):
+        try:
+            dev = devices[r]
+            torch.cuda.set_device(dev)
+            lo, hi = ranges[r]
+            if hi <= lo:
+                return
+            chunks, offs_all, o = [], [], 0
+            for ci in range(lo, hi):
+                c = cases[ci]
+                a, b = cuts[ci][bi], cuts[ci][bi + 1]
+                offs = np.zeros(b - a, np.uint64)
+                for i in range(a, b):
+                    offs[i - a] = o
+                    if c["ev"][i] is not None:
+                        chunks.append(c["ev"][i])
+                        o += len(c["ev"][i])
+                offs_all.append(offs)
+            inbuf = torch.from_numpy(np.frombuffer(b"".join(chunks) + bytes(32), np.uint8).copy()).cuda(dev)
+            plans = [encs[ci].plan(cases[ci]["lens"][cuts[ci][bi]:cuts[ci][bi + 1]], offs_all[ci - lo], inbuf)
+                     for ci in range(lo, hi)]
+            S = FecEncoder.slot_stride_for(max(p.slot_stride_min for p in plans) - 128)
+            nsl = sum(p.n_slots for p in plans)
+            slots = torch.full((max(1, nsl) * S,), 0xEE, dtype=torch.uint8, device=f"cuda:{dev}")
+            cols[r].run_many(encs[lo:hi], slots, S)
+            torch.cuda.synchronize(dev)
+            h = slots.cpu().numpy()
+            for ci in range(lo, hi):
+                a = cuts[ci][bi]
+                for s, l, e in encs[ci].packets_now():
+                    got[ci].append((h[s * S + 120:s * S + 120 + l].tobytes(), int(e) + a))
+            del inbuf
+        except Exception as e:  # noqa: BLE001
+            errs.append(e)
+
+    for bi in range(3):
+        ths = [threading.Thread(target=shard, args=(r, bi)) for r in range(len(devices))]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join()
+        assert not errs, errs
+    for ci, c in enumerate(cases):
+        pk = [p for p, _ in got[ci]]
+        assert [e for _, e in got[ci]] == list(c["pk_event"]), ci
+        assert hashlib.sha256(b"".join(pk)).digest() == c["sha"], ci
+    for col in cols:
+        col.close()
+    for e in encs:
+        e.close()

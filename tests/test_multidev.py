@@ -95,3 +95,108 @@ def test_multidev_error_names_the_device(gpu):
         assert int(p.sum()) == 0
     finally:
         u.rs.set_devices([])
+
+
+def _ragged_batch(rng, G, kmax=20):
+    ks = rng.integers(1, kmax + 1, G)
+    ms = rng.integers(1, 11, G)
+    ls = rng.integers(1, 1300, G)
+    groups, total = u.make_groups(ks, ks + ms, ls)
+    return ks, ms, ls, groups, total
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("devs", [[], [0], [0, 0], [0, 0, 0]])
+def test_multidev_ragged_pinned(gpu, oracle, devs):
+    """rsmi_encode_ragged_pinned / rsmi_decode_ragged_pinned (a mode-0 mix in
+    host memory) over the device list, split by summed n*len: parity equal to
+    the oracle's for every group, then a non-codeword decode with random
+    erasures (some too many) equal to the oracle's rows and statuses."""
+    import torch
+    from udpspeeder_amd import synth
+    rng = np.random.default_rng(len(devs) + 70)
+    G = 2501
+    ks, ms, ls, groups, total = _ragged_batch(rng, G, kmax=40)
+    host = rng.integers(0, 256, total, dtype=np.uint8)
+    try:
+        u.rs.set_devices(devs)
+        h = torch.from_numpy(host.copy()).pin_memory()
+        u.rs.encode_ragged_pinned(h, groups, chunk_groups=300)
+        exp = host.copy()
+        for i in range(G):
+            d = groups[i]
+            seg = exp[d.offset:d.offset + d.n * d.shard_stride]
+            oracle.encode_batch(d.k, d.n, seg, 0, d.shard_stride, d.len, 1)
+            exp[d.offset:d.offset + d.n * d.shard_stride] = seg
+            got = h.numpy()[d.offset:d.offset + d.n * d.shard_stride].reshape(d.n, d.shard_stride)
+            assert np.array_equal(got[:, :d.len], seg.reshape(d.n, d.shard_stride)[:, :d.len]), i
+        # decode a non-codeword batch: every group's own (k, n, len), erasures up to m + 1
+        flags = np.zeros((G, 256), np.uint8)
+        for i in range(G):
+            n = int(ks[i] + ms[i])
+            flags[i, :n] = 1
+            flags[i, rng.choice(n, min(int(rng.integers(0, ms[i] + 2)), n), replace=False)] = 0
+        h2 = torch.from_numpy(host.copy()).pin_memory()
+        st = u.rs.decode_ragged_pinned(h2, groups, synth.present_bits(flags), chunk_groups=257)
+        for i in range(G):
+            d = groups[i]
+            seg = host[d.offset:d.offset + d.n * d.shard_stride].copy()
+            ost = oracle.decode_batch(d.k, d.n, seg, 0, d.shard_stride, d.len, 1, flags[i:i + 1, :d.n])
+            assert st[i] == ost[0], i
+            if st[i] == 0:
+                got = h2.numpy()[d.offset:d.offset + d.k * d.shard_stride].reshape(d.k, d.shard_stride)
+                assert np.array_equal(got[:, :d.len], seg.reshape(d.n, d.shard_stride)[:d.k, :d.len]), i
+    finally:
+        u.rs.set_devices([])
+
+
+def test_ragged_pinned_rejects_unordered_groups():
+    """The host ragged entries need ascending, non-overlapping group spans
+    (each chunk is one contiguous copy); checked before any GPU work."""
+    from udpspeeder_amd._lib import RsmiError
+    groups, total = u.make_groups([2, 3], [4, 5], [100, 100])
+    groups[0].offset, groups[1].offset = groups[1].offset, groups[0].offset
+    host = np.zeros(total + 64, np.uint8)
+    with pytest.raises(RsmiError, match="ascending"):
+        u.rs.encode_ragged_pinned(host, groups)
+
+
+@pytest.mark.gpu
+def test_multidev_set_devices_during_calls(gpu, oracle):
+    """rsmi_set_devices racing split calls from another thread: every call
+    either runs on the list it saw or on the current device -- never a silent
+    no-op (run_split decides under its lock) -- and its parity is
+    right either way."""
+    import threading
+    import torch
+    k, n, ln, S, G = 10, 14, 400, 400, 777
+    rng = np.random.default_rng(9)
+    data = rng.integers(0, 256, (G, k, S), dtype=np.uint8)
+    ref = np.zeros((G, n, S), np.uint8)
+    ref[:, :k] = data
+    oracle.encode_batch(k, n, ref.reshape(-1), n * S, S, ln, G)
+    stop = threading.Event()
+    errs = []
+
+    def flip():
+        i = 0
+        while not stop.is_set():
+            try:
+                u.rs.set_devices([0, 0] if i % 2 == 0 else [])
+            except Exception as e:  # noqa: BLE001
+                errs.append(e)
+            i += 1
+
+    th = threading.Thread(target=flip)
+    th.start()
+    try:
+        d = torch.from_numpy(data).pin_memory()
+        for _ in range(30):
+            par = torch.zeros((G, n - k, S), dtype=torch.uint8).pin_memory()
+            u.rs.encode_pinned(d, par, k, n, ln, chunk_groups=128)
+            assert np.array_equal(par.numpy()[:, :, :ln], ref[:, k:, :ln])
+    finally:
+        stop.set()
+        th.join()
+        u.rs.set_devices([])
+    assert not errs

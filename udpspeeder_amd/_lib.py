@@ -124,6 +124,8 @@ def _bind(lib: C.CDLL) -> C.CDLL:
         "rsmi_encode_pinned": ([i32, i32, vp, i64, vp, i64, i64, i32, i64, i64], i32),
         "rsmi_decode_pinned": ([i32, i32, vp, i64, i64, i32, i64, vp, vp, i64], i32),
         "rsmi_last_decode_pinned_path": ([], i32),
+        "rsmi_encode_ragged_pinned": ([vp, i64, vp, i64], i32),
+        "rsmi_decode_ragged_pinned": ([vp, i64, vp, vp, vp, i64], i32),
         "rsmi_set_devices": ([vp, i32], i32),
         "rsmi_get_devices": ([vp, i32], i32),
         "rsmi_split_ranges": ([i64, vp, i32, vp], i32),

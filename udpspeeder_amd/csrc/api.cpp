@@ -93,6 +93,7 @@ struct Device {
     int32_t *hstatus_dev = nullptr;
     size_t hstatus_cap = 0;
     Pipeline penc, pdec, pzc;  // pzc: rsmi_decode_pinned's zero-copy path
+    Pipeline prag;             // rsmi_encode_ragged_pinned / rsmi_decode_ragged_pinned
     // one group per call (oneshot.hip): pinned staging the kernel reads and
     // writes over PCIe, a completion flag, guarded by one_mu
     std::mutex one_mu;
@@ -1045,7 +1046,7 @@ int decode_pinned_on(Device &Dref, Pipeline &pdec, Pipeline &pzc, int k, int n, 
 // two pipelines on one device: the 1-GPU test of the partition).
 struct Worker {
     int dev = -1;
-    Pipeline penc, pdec, pzc;  // this worker's own pipelines
+    Pipeline penc, pdec, pzc, prag;  // this worker's own pipelines
     std::thread th;
     std::mutex mu;
     std::condition_variable cv;
@@ -1102,6 +1103,7 @@ void worker_loop(Worker *W) {
     free_pipeline(W->penc);
     free_pipeline(W->pdec);
     free_pipeline(W->pzc);
+    free_pipeline(W->prag);
 }
 
 void stop_workers(std::vector<std::unique_ptr<Worker>> &ws) {
@@ -1268,6 +1270,154 @@ int decode_pinned(int k, int n, uint8_t *hs, int64_t hgs, int64_t ss, int len, i
     return decode_pinned_on(*D, D->pdec, D->pzc, k, n, hs, hgs, ss, len, ngroups, present, status, chunk);
 }
 
+// ---- ragged host batches (mode-0 mixes in pinned host memory) -------------------
+// rsmi_encode_ragged_pinned / rsmi_decode_ragged_pinned: a range of groups
+// [g0, g0 + cnt) in chunks of at most `chunk` groups, each chunk's byte span
+// H2D -> the ragged kernel on rebased descriptors -> span D2H, on the
+// pipeline's three streams.  The groups are in ascending, non-overlapping
+// offset order (check_ragged_host), so a chunk is one contiguous span.
+int ragged_pinned_on(Pipeline &P, bool decode, const rsmi_group *groups, int64_t g0, int64_t cnt,
+                     uint8_t *hb, const uint32_t *pbits, int32_t *status, int64_t chunk, int kmax) {
+    std::lock_guard<std::mutex> lk(P.mu);
+    // the range's codes resident on this thread's device (get_code's role)
+    {
+        std::vector<int> seen;
+        for (int64_t g = g0; g < g0 + cnt; ++g) {
+            const int key = groups[g].k * 257 + groups[g].n;
+            if (std::find(seen.begin(), seen.end(), key) != seen.end()) continue;
+            seen.push_back(key);
+            const int rc = prepare_code(groups[g].k, groups[g].n);
+            if (rc) return rc;
+        }
+    }
+    auto span = [&](int64_t a, int64_t b) {  // bytes of groups [a, b)
+        const rsmi_group &l = groups[b - 1];
+        return (size_t)(l.offset + (uint64_t)l.n * l.shard_stride - groups[a].offset);
+    };
+    size_t need = 16;
+    for (int64_t c0 = g0; c0 < g0 + cnt; c0 += chunk) need = std::max(need, span(c0, std::min(g0 + cnt, c0 + chunk)));
+    const size_t meta = (size_t)chunk * (sizeof(rsmi_group) + 32 + 4) + 64;  // descriptors | bits | status
+    if (P.bytes < need || P.cap < chunk) {
+        for (int i = 0; i < Pipeline::kDepth; ++i) {
+            if (P.dev[i]) (void)hipFree(P.dev[i]);
+            if (P.dpres[i]) (void)hipFree(P.dpres[i]);
+            P.dev[i] = P.dpres[i] = nullptr;
+        }
+        if (P.hpin) (void)hipHostFree(P.hpin);
+        P.hpin = nullptr;
+        P.bytes = P.hpin_bytes = 0;
+        P.cap = 0;
+        for (int i = 0; i < Pipeline::kDepth; ++i) {
+            RSMI_HIP(hipMalloc(&P.dev[i], need), "hipMalloc(ragged pipeline)");
+            RSMI_HIP(hipMalloc(&P.dpres[i], meta), "hipMalloc(ragged pipeline meta)");
+        }
+        RSMI_HIP(hipHostMalloc(&P.hpin, meta * Pipeline::kDepth, hipHostMallocDefault), "hipHostMalloc(ragged)");
+        P.bytes = need;
+        P.hpin_bytes = meta * Pipeline::kDepth;
+        P.cap = chunk;
+    }
+    for (int i = 0; i < Pipeline::kDepth; ++i)
+        if (!P.st[i]) RSMI_HIP(hipStreamCreateWithFlags(&P.st[i], hipStreamNonBlocking), "hipStreamCreate(pipeline)");
+    const size_t o_bits = ((size_t)chunk * sizeof(rsmi_group) + 15) & ~(size_t)15;
+    const size_t o_stat = o_bits + (size_t)chunk * 32;
+    int64_t pend_g[Pipeline::kDepth], pend_n[Pipeline::kDepth];
+    for (int i = 0; i < Pipeline::kDepth; ++i) pend_n[i] = 0;
+    // a stage's status comes back through its pinned meta area: copied out
+    // once the stage's stream has drained, before the stage is reused
+    auto drain = [&](int b) -> int {
+        RSMI_HIP(hipStreamSynchronize(P.st[b]), "hipStreamSynchronize(ragged pipeline)");
+        if (decode && pend_n[b] > 0 && status)
+            std::memcpy(status + pend_g[b], P.hpin + (size_t)b * meta + o_stat, (size_t)pend_n[b] * 4);
+        pend_n[b] = 0;
+        return RSMI_OK;
+    };
+    int64_t c = 0;
+    for (int64_t c0 = g0; c0 < g0 + cnt; c0 += chunk, ++c) {
+        const int64_t c1 = std::min(g0 + cnt, c0 + chunk), nc = c1 - c0;
+        const int b = (int)(c % Pipeline::kDepth);
+        int rc = drain(b);
+        if (rc) return rc;
+        hipStream_t s = P.st[b];
+        uint8_t *hm = P.hpin + (size_t)b * meta;
+        rsmi_group *rd = reinterpret_cast<rsmi_group *>(hm);
+        const uint64_t base_off = groups[c0].offset;
+        int km = 1;
+        for (int64_t g = c0; g < c1; ++g) {
+            rd[g - c0] = groups[g];
+            rd[g - c0].offset -= base_off;
+            km = std::max<int>(km, groups[g].k);
+        }
+        const size_t bytes = span(c0, c1);
+        if (decode) std::memcpy(hm + o_bits, pbits + (size_t)c0 * 8, (size_t)nc * 32);
+        RSMI_HIP(hipMemcpyAsync(P.dpres[b], hm, decode ? o_stat : (size_t)nc * sizeof(rsmi_group),
+                                hipMemcpyHostToDevice, s), "H2D ragged meta");
+        RSMI_HIP(hipMemcpyAsync(P.dev[b], hb + base_off, bytes, hipMemcpyHostToDevice, s), "H2D ragged span");
+        const rsmi_group *dg = reinterpret_cast<const rsmi_group *>(P.dpres[b]);
+        if (decode) {
+            int32_t *dst = reinterpret_cast<int32_t *>(P.dpres[b] + o_stat);
+            rc = decode_ragged_dev(dg, nc, P.dev[b], reinterpret_cast<const uint32_t *>(P.dpres[b] + o_bits), dst,
+                                   std::min(km, kmax), s);
+            if (rc) return rc;
+            RSMI_HIP(hipMemcpyAsync(hm + o_stat, dst, (size_t)nc * 4, hipMemcpyDeviceToHost, s), "D2H status");
+            pend_g[b] = c0;
+            pend_n[b] = nc;
+        } else {
+            rc = encode_ragged_dev(dg, nc, P.dev[b], s);
+            if (rc) return rc;
+        }
+        RSMI_HIP(hipMemcpyAsync(hb + base_off, P.dev[b], bytes, hipMemcpyDeviceToHost, s), "D2H ragged span");
+    }
+    for (int i = 0; i < Pipeline::kDepth; ++i) {
+        const int rc = drain(i);
+        if (rc) return rc;
+    }
+    return RSMI_OK;
+}
+
+int check_ragged_host(const rsmi_group *groups, int64_t ngroups, const uint8_t *hb, int64_t chunk) {
+    if (ngroups < 0 || chunk < 1) return fail(RSMI_ERR_INVALID, "negative ngroups or chunk_groups < 1");
+    if (ngroups > 0 && (!groups || !hb)) return fail(RSMI_ERR_INVALID, "null groups/host_base");
+    uint64_t end = 0;
+    for (int64_t g = 0; g < ngroups; ++g) {
+        const rsmi_group &d = groups[g];
+        if (d.k < 1 || d.n < d.k || d.n > 256 || d.shard_stride % 16 || d.shard_stride < d.len ||
+            d.offset % 16 || d.reserved)
+            return fail(RSMI_ERR_INVALID, "invalid descriptor at group " + std::to_string(g));
+        if (d.offset < end)
+            return fail(RSMI_ERR_INVALID, "groups must be in ascending, non-overlapping offset order (group " +
+                                              std::to_string(g) + ")");
+        end = d.offset + (uint64_t)d.n * d.shard_stride;
+    }
+    if (((uintptr_t)hb) % 16) return fail(RSMI_ERR_INVALID, "host_base must be 16-aligned");
+    return RSMI_OK;
+}
+
+// Split over the device list by each group's bytes n * len (the PCIe and HBM
+// work both scale with them: SURVEY 8(e)'s balanced ranges for C3).
+int ragged_pinned(bool decode, const rsmi_group *groups, int64_t ngroups, uint8_t *hb, const uint32_t *pbits,
+                  int32_t *status, int64_t chunk) {
+    int rc = check_ragged_host(groups, ngroups, hb, chunk);
+    if (rc) return rc;
+    if (decode && ngroups > 0 && !pbits) return fail(RSMI_ERR_INVALID, "null present_bits");
+    if (ngroups == 0) return RSMI_OK;
+    int kmax = 1;
+    std::vector<int64_t> cost((size_t)ngroups);
+    for (int64_t g = 0; g < ngroups; ++g) {
+        cost[(size_t)g] = (int64_t)groups[g].n * groups[g].len;
+        kmax = std::max<int>(kmax, groups[g].k);
+    }
+    rc = run_split(
+        ngroups,
+        [&](Worker &W, int64_t g0, int64_t cnt) {
+            return ragged_pinned_on(W.prag, decode, groups, g0, cnt, hb, pbits, status, chunk, kmax);
+        },
+        cost.data());
+    if (rc != kNoWorkers) return rc;
+    Device *D = current(&rc);
+    if (!D) return rc;
+    return ragged_pinned_on(D->prag, decode, groups, 0, ngroups, hb, pbits, status, chunk, kmax);
+}
+
 const char *last_error() { return g_err.c_str(); }
 std::atomic<int> &opt_bitslice() { return g_opt_bitslice; }
 
@@ -1308,6 +1458,16 @@ int rsmi_set_option(int option, int value) {
 }
 
 int rsmi_quiesce(void) { return rsmi::stop_all_servers(); }
+
+int rsmi_encode_ragged_pinned(const rsmi_group *groups, int64_t ngroups, uint8_t *host_base,
+                              int64_t chunk_groups) {
+    return rsmi::ragged_pinned(false, groups, ngroups, host_base, nullptr, nullptr, chunk_groups);
+}
+
+int rsmi_decode_ragged_pinned(const rsmi_group *groups, int64_t ngroups, uint8_t *host_base,
+                              const uint32_t *present_bits, int32_t *status, int64_t chunk_groups) {
+    return rsmi::ragged_pinned(true, groups, ngroups, host_base, present_bits, status, chunk_groups);
+}
 
 int rsmi_init(void) {
     int rc;

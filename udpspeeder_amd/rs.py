@@ -527,6 +527,32 @@ def decode_pinned(shards, present, k: int, n: int, length: int, chunk_groups: in
     return st
 
 
+def _host_ptr(x):
+    return x.data_ptr() if hasattr(x, "data_ptr") else x.ctypes.data
+
+
+def encode_ragged_pinned(host_base, groups, chunk_groups: int = 8192) -> None:
+    """rsmi_encode_ragged_pinned: a ragged batch (``groups`` from make_groups,
+    ascending offsets) in host memory ``host_base`` (uint8 CPU tensor/array;
+    pin it for overlap): parity rows written in place, chunks pipelined
+    H2D -> encode -> D2H (split by n*len over the device list, if one is set)."""
+    check(lib().rsmi_encode_ragged_pinned(groups, len(groups), _host_ptr(host_base), chunk_groups),
+          "rsmi_encode_ragged_pinned")
+
+
+def decode_ragged_pinned(host_base, groups, present_bits, chunk_groups: int = 8192):
+    """rsmi_decode_ragged_pinned: missing data rows of every group rebuilt in
+    place in host memory; ``present_bits`` uint32/int32 [G, 8] host array
+    (synth.present_bits).  Returns the int32 [G] status array."""
+    bits = np.ascontiguousarray(np.asarray(present_bits).view(np.uint32))
+    if bits.shape != (len(groups), 8):
+        raise ValueError("present_bits must be [G, 8]")
+    st = np.zeros(len(groups), np.int32)
+    check(lib().rsmi_decode_ragged_pinned(groups, len(groups), _host_ptr(host_base), bits.ctypes.data,
+                                          st.ctypes.data, chunk_groups), "rsmi_decode_ragged_pinned")
+    return st
+
+
 def set_devices(devices) -> None:
     """rsmi_set_devices: split the host-memory batch entry points
     (encode_pinned / decode_pinned) over these devices, one contiguous group
