@@ -412,3 +412,38 @@ def test_gpu_decode_collectors_split_over_device_list(fx, gpu, devices):
         col.close()
     for d in decs:
         d.close()
+
+
+@pytest.mark.gpu
+def test_gpu_decode_collector_reused_set_is_detected(fx, gpu):
+    """A decoder run by collector call t and left out of calls t+1 and t+2:
+    call t+2 reuses the set that held its rows, so its outputs are refused
+    with an error (ADVICE r05: they pointed at overwritten or freed memory);
+    read before that, they are the reference's."""
+    import torch
+    from udpspeeder_amd._lib import RsmiError
+    from udpspeeder_amd.fec import FecDecodeCollector, FecDecoder
+    cases = [_case(fx, NAMES[i % len(NAMES)]) for i in range(3)]
+    packed = [_pack(c["chan"]) for c in cases]
+    devs = [torch.from_numpy(h).cuda() for h, _, _ in packed]
+    decs = [FecDecoder() for _ in range(3)]
+    col = FecDecodeCollector()
+
+    def plan(i):
+        host, lens, offs = packed[i]
+        return list(decs[i].plan(host, lens, offs, devs[i]).ret)
+
+    assert plan(0) == cases[0]["ret"]
+    col.run_many([decs[0]])            # call t: decoder 0's rows in set A
+    plan(1)
+    col.run_many([decs[1]])            # call t+1: set B
+    first = decs[1].outputs()          # (read in time: fine)
+    assert hashlib.sha256(b"".join(b for b, _ in first)).digest() == cases[1]["sha"]
+    plan(2)
+    col.run_many([decs[2]])            # call t+2: set A again
+    with pytest.raises(RsmiError, match="reused"):
+        decs[0].outputs()
+    assert hashlib.sha256(b"".join(b for b, _ in decs[2].outputs())).digest() == cases[2]["sha"]
+    col.close()
+    for d in decs:
+        d.close()

@@ -105,6 +105,12 @@ constexpr int kTile = 1280;    // bytes per lane-tile pass (64 x 16 + 64 x 4)
 #ifndef DEC_RAG_UNCOND_W
 #define DEC_RAG_UNCOND_W 4  // ragged kernels: unconditional ring refills for tile widths >= this
 #endif
+#ifndef DEC_RAG_ALLROWS
+#define DEC_RAG_ALLROWS 0  // ragged kernels: tile widths <= this multiply every row of a pass
+                           // (no per-row scalar compare and branch per survivor).  Round 6
+                           // (profiles/r06/c3_allrows_ab.txt): C3 decode 0.153 ms for W <= 2,
+                           // 0.477 ms for every width, against 0.138-0.142 ms guarded
+#endif
 #ifndef DEC_RAG_DEEP
 #define DEC_RAG_DEEP 1  // ragged kernel: 16 / W survivors in flight for 4- and 8-byte lane pieces
 #endif
@@ -331,6 +337,7 @@ struct Rebuild {
     // (8-16 slots) would issue that many dead loads per group, and the depth
     // hides the wait anyway.
     static constexpr bool kUncond = W >= DEC_RAG_UNCOND_W;
+    static constexpr bool kAllRows = W <= DEC_RAG_ALLROWS;
     __device__ __forceinline__ void load(int q, int j) {
         if (kUncond) {
             const bool ok = j < k;
@@ -386,7 +393,9 @@ struct Rebuild {
                             asm volatile("" : "+s"(nr));
 #pragma unroll
                             for (int r = 0; r < kPass; ++r) {
-                                if (r < nr) {
+                                // kAllRows: every row of the pass, no per-row branch (rows
+                                // past nr read stale table entries and are never stored)
+                                if (kAllRows || r < nr) {
                                     const uint4 t = ta[r];
                                     const uint32_t t2 = ta2[r];
 #pragma unroll

@@ -306,6 +306,11 @@ struct Batch {
     // a collector run: the rows came back into the collector's pinned buffer
     // (one copy for every decoder), and its event stands for this batch's
     const uint8_t *hblob_view = nullptr;
+    // ... stamped with the collector set's generation: the set is reused (its
+    // buffer overwritten or freed) two runs later, or freed with the collector
+    std::shared_ptr<std::atomic<uint64_t>> view_gen_src;
+    uint64_t view_gen = 0;
+    bool view_stale() const { return view_gen_src && view_gen_src->load() != view_gen; }
     std::shared_ptr<rsmi::SharedEv> ext;
     hipStream_t stream = nullptr;
     hipEvent_t done = nullptr;
@@ -984,6 +989,7 @@ int rsmi_fdec_run_dev(rsmi_fdec *D, void *stream) {
     }
     D->B->ext.reset();
     D->B->hblob_view = nullptr;
+    D->B->view_gen_src.reset();
     D->B->stream = s;
     if (e != hipSuccess) return fail(RSMI_ERR_HIP, std::string("fdec run: ") + hipGetErrorString(e));
     D->B->in_flight = true;
@@ -997,6 +1003,10 @@ int rsmi_fdec_outputs(rsmi_fdec *D, int64_t *n_out) {
     // the older batch first: it ran, and batch i+1 may have been planned since
     const int xi = (D->bat[D->bi ^ 1].ran && !D->bat[D->bi ^ 1].resolved) ? (D->bi ^ 1) : D->bi;
     Batch &X = D->bat[xi];
+    if (X.view_stale())
+        return fail(RSMI_ERR_INVALID, "rsmi_fdec_outputs: this decoder's rows were in a collector set that "
+                                      "has been reused or destroyed since (read outputs before the "
+                                      "collector's second next rsmi_fdec_run_many)");
     if (!X.resolved) {
         bool any_job = !X.jobs.empty();
         if (any_job && !X.ran) return fail(RSMI_ERR_INVALID, "rsmi_fdec_outputs before rsmi_fdec_run_dev");
@@ -1046,6 +1056,9 @@ int rsmi_fdec_output_list(const rsmi_fdec *D, const uint8_t **ptr, int32_t *len,
     if (!D || D->out_b < 0 || !D->bat[D->out_b].resolved)
         return fail(RSMI_ERR_INVALID, "call rsmi_fdec_outputs first");
     const Batch &X = D->bat[D->out_b];
+    if (X.view_stale())
+        return fail(RSMI_ERR_INVALID, "rsmi_fdec_output_list: the collector set holding these outputs has been "
+                                      "reused or destroyed since rsmi_fdec_outputs");
     for (size_t i = 0; i < X.outs.size(); ++i) {
         if (ptr) ptr[i] = X.outs[i].ptr;
         if (len) len[i] = X.outs[i].len;
@@ -1083,6 +1096,10 @@ struct rsmi_fdcol {
     // (per set: a decoder's outputs point into the set it ran in)
     uint8_t *dback = nullptr, *hback[2] = {nullptr, nullptr};
     size_t dback_cap = 0, hback_cap[2] = {0, 0};
+    // per set: bumped whenever the set's hback is about to be rewritten (and
+    // at destroy), so decoders still pointing into it can tell
+    std::shared_ptr<std::atomic<uint64_t>> gen[2] = {std::make_shared<std::atomic<uint64_t>>(0),
+                                                     std::make_shared<std::atomic<uint64_t>>(0)};
 };
 
 extern "C" {
@@ -1100,6 +1117,7 @@ void rsmi_fdcol_destroy(rsmi_fdcol *C) {
         C->done[i].reset();  // (destroyed once no decoder's batch holds it)
         if (C->hmeta[i]) (void)hipHostFree(C->hmeta[i]);
         if (C->hback[i]) (void)hipHostFree(C->hback[i]);
+        C->gen[i]->fetch_add(1);  // any decoder's view into this set is gone
     }
     for (uint8_t *p : {C->dstage, C->dmeta, C->dback}) if (p) (void)hipFree(p);
     if (C->dstatus) (void)hipFree(C->dstatus);
@@ -1225,6 +1243,7 @@ int rsmi_fdec_run_many(rsmi_fdcol *C, rsmi_fdec *const *dec, int32_t n, void *st
     const size_t go = 0, pof = (gb + 255) & ~size_t(255), ko = (pof + pb + 255) & ~size_t(255),
                  co = (ko + kb + 255) & ~size_t(255), all = co + cb + 16;
     C->cur ^= 1;
+    C->gen[C->cur]->fetch_add(1);  // the set's previous views end here
     rc = dev_grow(&C->dmeta, &C->meta_cap, all);
     if (!rc) rc = host_grow(&C->hmeta[C->cur], &C->hmeta_cap[C->cur], all);
     if (!rc) rc = host_grow(&C->hback[C->cur], &C->hback_cap[C->cur], (size_t)boff[(size_t)n] + 16);
@@ -1259,6 +1278,8 @@ int rsmi_fdec_run_many(rsmi_fdcol *C, rsmi_fdec *const *dec, int32_t n, void *st
     for (int i = 0; i < n; ++i) {  // one event for all (a record per decoder cost ~5 us each)
         rsmi_fdec *D = dec[i];
         D->B->hblob_view = C->hback[C->cur] + boff[(size_t)i];
+        D->B->view_gen_src = C->gen[C->cur];
+        D->B->view_gen = C->gen[C->cur]->load();
         D->B->ext = C->done[C->cur];
         D->B->stream = s;
         D->B->in_flight = true;
