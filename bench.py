@@ -324,6 +324,7 @@ def run_c3(args, world, rank, dev, scaling):
     flags = synth.ragged_erasures(synth.ERASE_SEED, g0, ks + ms_, ms_, ERASURES)
     bits = torch.from_numpy(synth.present_bits(flags).view(np.int32)).to(dev)
     status = torch.empty(G, dtype=torch.int32, device=dev)
+    smap = torch.empty((G, 20), dtype=torch.uint8, device=dev)  # rs_decode's data[] permutation
     stream = torch.cuda.current_stream()
     ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
 
@@ -333,7 +334,8 @@ def run_c3(args, world, rank, dev, scaling):
         plan.encode(base)
         if i is not None:
             ev[i][1].record(stream)
-        plan.decode(base, bits, status=status)
+        # the reference's placement, as the C2 step (the next encode restores the parity)
+        plan.decode(base, bits, status=status, placement="reference", slot_map=smap)
         if i is not None:
             ev[i][2].record(stream)
 
@@ -358,6 +360,8 @@ def run_c3(args, world, rank, dev, scaling):
     enc_ms = statistics.mean(a.elapsed_time(b) for a, b, _ in ev)
     dec_ms = statistics.mean(b.elapsed_time(c) for _, b, c in ev)
     bad = int((status != 0).sum().item())
+    plan.encode(base)  # the parity the last decode wrote rows over (untimed)
+    torch.cuda.synchronize()
     cpu = None
     if rank == 0 and not args.no_cpu_baseline:
         cpu = c3_cpu_baseline(u, base, groups, ks, ms_, ls, flags)
@@ -433,13 +437,16 @@ def c3_verify(u, synth, torch, base, groups, ks, ms_, ls, g0, plan, bits, status
         for j in np.nonzero(flags[g, :int(ks[g] + ms_[g])] == 0)[0]:
             host[off + j * ss:off + (j + 1) * ss] = 0xA5
     base.copy_(torch.from_numpy(host))
-    plan.decode(base, bits, status=status)
+    smap = torch.empty((G, 20), dtype=torch.uint8, device=base.device)
+    plan.decode(base, bits, status=status, placement="reference", slot_map=smap)
     torch.cuda.synchronize()
     host = base.cpu().numpy()
+    m = smap.cpu().numpy()
     ok &= int((status != 0).sum().item()) == 0
-    for g in range(G):
-        off, ss, k, ln = int(groups[g].offset), int(groups[g].shard_stride), int(ks[g]), int(ls[g])
-        got = host[off:off + k * ss].reshape(k, ss)[:, :ln]
+    for g in range(G):  # each data[i] read through the slot map (rs_decode's pointer permutation)
+        off, ss, k, ln, n = (int(groups[g].offset), int(groups[g].shard_stride), int(ks[g]), int(ls[g]),
+                             int(ks[g] + ms_[g]))
+        got = host[off:off + n * ss].reshape(n, ss)[m[g, :k].astype(np.int64), :ln]
         ok &= bool((got == data[g].reshape(k, ss)[:, :ln]).all())
         if not ok:
             break
@@ -668,7 +675,11 @@ def c3_configs(u, synth, torch, dev, G):
     flags = synth.ragged_erasures(synth.ERASE_SEED, 0, ks + ms_, ms_, ERASURES)
     bits = torch.from_numpy(synth.present_bits(flags).view(np.int32)).to(dev)
     st = torch.empty(G, dtype=torch.int32, device=dev)
-    t = _time_ms(torch, lambda: plan.decode(base, bits, status=st), spread=sp_d)
+    sm = torch.empty((G, 20), dtype=torch.uint8, device=dev)
+    # the reference's placement (as the headline step): rows over the parity
+    # survivors, so repeated calls decode changed inputs -- the same work
+    t = _time_ms(torch, lambda: plan.decode(base, bits, status=st, placement="reference", slot_map=sm),
+                 spread=sp_d)
     e = ((flags[:, :20] == 0) & (np.arange(20)[None, :] < ks[:, None])).sum(1)
     alg = int((((e > 0) * ks + e) * ls).sum())  # k*len read + e*len written, groups with e > 0
     out["c3_ragged_decode"] = {
