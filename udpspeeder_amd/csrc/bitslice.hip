@@ -16,6 +16,13 @@
 #ifndef BS_PERSIST
 #define BS_PERSIST 0  // 1: balanced persistent grid (measured 5 % slower than one wave per chunk)
 #endif
+#ifndef BS_RAG_PERSIST
+#define BS_RAG_PERSIST 0  // k_bs_ragged: persistent waves (blocks per CU) that load the next chunk's
+                          // wave record and column map during this chunk's network.  Round 6
+                          // (profiles/r06/c3_persist_ab.txt): 3 blocks/CU 0.175-0.178 ms, 6 blocks/CU
+                          // 0.175-0.176, against 0.166-0.167 one wave per chunk (the carried words
+                          // spill 20 VGPRs at 3 waves/SIMD)
+#endif
 #ifdef BS_INC
 #include BS_INC
 #else
@@ -46,6 +53,44 @@ __global__ __launch_bounds__(256, BS_OCC) void k_bs_ragged(const BsGroup *groups
                                                            const uint32_t *colmap,
                                                            const uint32_t *waves, uint32_t nwaves,
                                                            uint8_t *base, uint32_t bytes) {
+#if BS_RAG_PERSIST
+    // wave w's chunks w, w + wstep, ...: the next chunk's wave record and
+    // column-map words load while this chunk's network runs, so only the
+    // group-record load stays in front of each chunk
+    const uint32_t wstep = gridDim.x * 4u;
+    uint32_t w = blockIdx.x * 4u + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (w >= nwaves) return;
+    const uint32_t lane = threadIdx.x & 63u;
+    uint32_t code = __builtin_amdgcn_readfirstlane(waves[2 * w]);
+    uint32_t c0 = __builtin_amdgcn_readfirstlane(waves[2 * w + 1]) + lane;
+    uint32_t m0 = colmap[c0], m1 = colmap[c0 + 64];
+    for (;;) {
+        RagIO io;
+        io.rsrc = __builtin_amdgcn_make_buffer_rsrc(base, 0, (int)bytes, 0x00020000);
+        bs_rag_lane(groups, m0, io.o0, io.ss0);
+        bs_rag_lane(groups, m1, io.o1, io.ss1);
+        const uint32_t wn = w + wstep;
+        const bool more = wn < nwaves;
+        uint32_t coden = 0, m0n = 0xFFFFFFFFu, m1n = 0xFFFFFFFFu;
+        if (more) {
+            coden = __builtin_amdgcn_readfirstlane(waves[2 * wn]);
+            const uint32_t cn = __builtin_amdgcn_readfirstlane(waves[2 * wn + 1]) + lane;
+            m0n = colmap[cn];
+            m1n = colmap[cn + 64];
+        }
+        int idx = 0;
+#define BS_RAG_CASE(K, N)              \
+    if (code == (uint32_t)idx) bs_code_##K##_##N(io); \
+    ++idx;
+        BS_FOR_EACH_CODE(BS_RAG_CASE)
+#undef BS_RAG_CASE
+        if (!more) break;
+        w = wn;
+        code = coden;
+        m0 = m0n;
+        m1 = m1n;
+    }
+#else
     RagIO io;
     uint32_t code;
     if (!bs_rag_setup(groups, colmap, waves, nwaves, base, bytes, io, code)) return;
@@ -58,6 +103,7 @@ __global__ __launch_bounds__(256, BS_OCC) void k_bs_ragged(const BsGroup *groups
     ++idx;
     BS_FOR_EACH_CODE(BS_RAG_CASE)
 #undef BS_RAG_CASE
+#endif
 }
 
 }  // namespace
@@ -100,6 +146,7 @@ hipError_t launch_encode_bitslice_ragged(const rsmi_group *groups, const uint32_
     if (nwaves == 0) return hipSuccess;
     uint32_t blocks = (nwaves + 3) / 4;
     if (BS_RAG_XCD) blocks = (blocks + 7) & ~7u;  // whole rounds of 8 XCDs (the remap)
+    if (BS_RAG_PERSIST && blocks > 256u * BS_RAG_PERSIST) blocks = 256u * BS_RAG_PERSIST;
     k_bs_ragged<<<blocks, 256, 0, s>>>(reinterpret_cast<const BsGroup *>(groups), colmap, waves,
                                        nwaves, base, bytes);
     return hipGetLastError();
