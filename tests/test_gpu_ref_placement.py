@@ -277,3 +277,38 @@ def test_ref_ragged_c3_full_sha(gpu, golden):
         rows = out[d.offset:d.offset + d.n * d.shard_stride].reshape(d.n, d.shard_stride)
         h.update(rows[m[i, :d.k].astype(np.int64), :d.len].tobytes())
     assert h.hexdigest() == F["data_out_sha256"]
+
+
+def test_ref_placement_graph_capture_replay(gpu, oracle):
+    """The headline step (encode, then the reference-placement decode with its
+    slot map) captured in a hipGraph: each replay recomputes from the current
+    data, the rows read through the map equal the data, and the map equals the
+    host closed form (the present flags are fixed)."""
+    import torch
+    import udpspeeder_amd as u
+    from udpspeeder_amd import synth
+    k, n, ln, G = 20, 30, 1250, 777
+    t = torch.zeros((G, n, 1280), dtype=torch.uint8, device=gpu)
+    pres_h = synth.erasure_present(4, 0, G, n, 5)
+    pres = upload(pres_h, gpu)
+    st = torch.empty(G, dtype=torch.int32, device=gpu)
+    sm = torch.empty((G, k), dtype=torch.uint8, device=gpu)
+    u.fill_data(t, k, ln, 1)
+    u.reserve(k, n, G)
+    u.encode(t, k, n, ln)
+    u.decode(t, pres, k, n, ln, status=st, placement="reference", slot_map=sm)  # warm-up
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        u.encode(t, k, n, ln)
+        u.decode(t, pres, k, n, ln, status=st, placement="reference", slot_map=sm)
+    for seed in (2, 3):
+        u.fill_data(t, k, ln, seed)
+        sm.fill_(0xEE)
+        g.replay()
+        torch.cuda.synchronize()
+        assert int((st != 0).sum()) == 0
+        assert torch.equal(u.reference_rows(t, sm)[:, :, :ln], t[:, :k, :ln])
+        m = sm.cpu().numpy()
+        for gi in range(0, G, 37):
+            assert (m[gi] == u.ref_slot_map(k, n, pres_h[gi])).all()
