@@ -37,14 +37,14 @@
 #endif
 #ifndef BS_XCD
 #define BS_XCD 1  // blocks b, b+8, ... (dispatched to one XCD) take one contiguous range of
-                  // chunks (measured 1.5 % faster than the plain order, scripts/gpu_bench_ab.sh)
+                  // chunks (measured 1.5 % faster than the plain order, scripts/archive/gpu_bench_ab.sh)
 #endif
 #ifndef BS_RAG_XCD
 #define BS_RAG_XCD 0  // 1: the same remap for the ragged kernels, so the blocks one CU holds come
                       // from one narrow window of the code-sorted wave list (one code's network
                       // of the ~550 KB in k_bs_ragged).  Measured 10 % slower on C3: each XCD
                       // then owns one slice of the codes and the slice of the largest ones
-                      // finishes last (scripts/gpu_c3enc_ab.sh)
+                      // finishes last (scripts/gpu_ab.sh c3)
 #endif
 #define BS_ACC3(acc, a, b) ((acc) = __builtin_amdgcn_bitop3_b32((acc), (a), (b), 0x96))
 #define BS_ACC2(acc, a) ((acc) ^= (a))

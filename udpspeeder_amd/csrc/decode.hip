@@ -51,7 +51,7 @@ constexpr int kWaves = 4;      // waves per block (one group each)
 #endif
 #ifndef DEC_ST_AUX
 #define DEC_ST_AUX 16          // cache policy of the uniform kernel's rebuilt-row stores: sc1
-                               // (round 5, scripts/gpu_ab_c2.sh: C2 random 0.389-0.395 vs 0.397-0.403 ms
+                               // (round 5, scripts/gpu_ab.sh c2: C2 random 0.389-0.395 vs 0.397-0.403 ms
                                // with default stores; profiles/r05/c2_store_policy_ab)
 #endif
 #ifndef DEC_ST_AUX_BIG
