@@ -24,6 +24,12 @@
 #ifndef RSMI_DEC_CLASSES
 #define RSMI_DEC_CLASSES 1  // plan decodes: one register-cut kernel per tile-width class
 #endif
+#ifndef RAG_CLS_SLOTS_DIV
+#define RAG_CLS_SLOTS_DIV 1  // decode classes: resident wave slots per class / this = its waves.
+                             // Round 6 (profiles/r06/c3_clsdiv_ab.txt): 2 -> C3 decode 0.138-0.140 ms,
+                             // 4 -> 0.142-0.143, against 0.138-0.139 at 1: the workgroups' prologues
+                             // overlap the older ones' streams, fewer and longer-lived ones buy nothing
+#endif
 #ifndef RAG_LPT
 #define RAG_LPT 1  // bit-sliced ragged waves: costliest code first (0: code-list order)
 #endif
@@ -216,7 +222,12 @@ extern "C" int rsmi_ragged_plan_create(const rsmi_group *g, int64_t ngroups,
             auto &v = by[(size_t)c];
             const int W = c == 0 ? 1 : (c == 1 ? 2 : (c == 2 ? 4 : 5));
             const int occ = rsmi::decode_cls_occupancy(c);
-            const int64_t slots = (int64_t)ncu * 4 * occ;
+            // RAG_CLS_SLOTS_DIV: the classes share one launch (DEC_MIX), so a
+            // class sized to fill the device alone makes the launch several
+            // rounds of short-lived workgroups, each paying its prologue
+            // (tables, records, present words: 3-14 K cycles per wave,
+            // profiles/r06/c3_trace.txt) for 1.3-3.4 groups a wave
+            const int64_t slots = (int64_t)ncu * 4 * occ / RAG_CLS_SLOTS_DIV;
             // one wave per group at least: blocks of kClsWaves waves
             int64_t nb64 = (std::min<int64_t>((int64_t)v.size(), slots) + rsmi::kClsWaves - 1) /
                            rsmi::kClsWaves;
