@@ -77,6 +77,12 @@ constexpr int kPpl = 96 / kLpp;         // pieces per lane per round
                       // bit 1: the round's stores after the round (in vmcnt, a store made
                       // the next piece's key-stream load wait for it)
 #endif
+#ifndef COOK_LINE
+#define COOK_LINE 0  // k_cook: lane pieces on the 128-byte line grid of the packet (one-chain fold).
+                     // Round 6 (profiles/r06/cook_line_ab.txt): cook 1.309-1.316 ms vs 1.275-1.278
+                     // without, the fused run 2.87-2.91 vs 2.88-3.00 ms -- off (k_cook_frame's
+                     // COOKF_LINE, whose plain stream it fixed, stays on)
+#endif
 #ifndef COOK_THREADS
 #define COOK_THREADS (kLpp == 32 ? 512 : 256)
 #endif
@@ -297,18 +303,19 @@ __device__ __forceinline__ uint32_t zh2(const uint32_t *T, uint32_t c) {
 template <bool TWO>
 struct RoundCrc {
     uint32_t h[2] = {0, 0};
-    int last = -1;
+    int last = -1, last_slot = -1;
     __device__ __forceinline__ void add(const uint32_t *T, u32x4 v, int p, int q, int qr) {
         const int c = TWO ? (p & 1) : 0;
         const uint32_t hn = (TWO ? zh2(T, h[c]) : zh(T, h[c])) ^ crc16(T, v);
         h[c] = q < qr ? hn : h[c];
         last = q < qr ? q : last;
+        last_slot = q < qr ? p : last_slot;  // (a line-aligned grid shifts q against the slot)
     }
     // The round's raw CRC relative to the end of its data, in all kLpp lanes.
     __device__ __forceinline__ uint32_t finish(const uint32_t *T, int qr) const {
         uint32_t hh = h[0];
         if (TWO) {  // Z(0) = 0: an empty chain adds nothing
-            const bool odd = last >= 0 && ((last / kLpp) & 1);
+            const bool odd = last >= 0 && (last_slot & 1);
             hh = zh(T, odd ? h[0] : h[1]) ^ (odd ? h[1] : h[0]);
         }
         int k = qr - 1 - last;
@@ -368,11 +375,12 @@ __device__ __forceinline__ int packet_len(const CookArgs &a, int64_t pk) {
 
 // The N pieces of round r (N kLpp pieces a packet) owned by lane hl: zeros past ext.
 template <int N>
-__device__ __forceinline__ void load_round(u32x4 (&d)[N], const uint8_t *pkt, int r, int hl, int ext) {
+__device__ __forceinline__ void load_round(u32x4 (&d)[N], const uint8_t *pkt, int r, int hl, int ext,
+                                           int lead = 0) {
 #pragma unroll
     for (int p = 0; p < N; ++p) {
-        const int P = r * (16 * kLpp * N) + 16 * (kLpp * p + hl);
-        d[p] = P < ext ? ld_piece(pkt + P) : u32x4{0, 0, 0, 0};
+        const int P = r * (16 * kLpp * N) + 16 * (kLpp * p + hl - lead);
+        d[p] = (P >= 0 && P < ext) ? ld_piece(pkt + P) : u32x4{0, 0, 0, 0};
     }
 }
 
@@ -445,10 +453,17 @@ __global__ __launch_bounds__(kThreads, COOK_OCC) void k_cook(CookArgs a) {
                            ? (int)((uintptr_t)pkt & 15) : 0;
         const uint8_t *pga = pkt - ph;
         uint8_t *oga = opkt - ph;
+        // COOK_LINE: the lanes count pieces from the 128-byte line the grid
+        // starts in (`lead` pieces before it, untouched), so a load or store
+        // instruction covers whole lines (an FEC packet's grid starts 112 B
+        // into its slot's line: two instructions per line, as k_cook_frame's)
+        const int lead = (COOK_LINE && have && (((uintptr_t)pga ^ (uintptr_t)oga) & 127) == 0)
+                             ? (int)(((uintptr_t)pga & 127) >> 4) : 0;
         // round 0 is read up to the packet's cap (every packet owns cap bytes), so
         // these loads fly together with the length load instead of after it
         u32x4 cur[kPplC];
-        load_round(cur, pga, 0, hl, have && ((uintptr_t)pkt & 3) == 0 ? min((a.cap + ph) & ~15, kRoundC) : 0);
+        load_round(cur, pga, 0, hl, have && ((uintptr_t)pkt & 3) == 0 ? min((a.cap + ph) & ~15, kRoundC) : 0,
+                   lead);
         if (have) {
             L = packet_len(a, pk);
             if (obs) ivl = a.iv ? a.iv_len[pk] : 4 + (int)(splitmix(a.seed, (uint64_t)gi, 0) % 29u);
@@ -478,7 +493,7 @@ __global__ __launch_bounds__(kThreads, COOK_OCC) void k_cook(CookArgs a) {
         const uint32_t sstep = ivl ? mod_ivl(16u * kLpp, (uint32_t)ivl, magic) : 0u;
         const int Q = (Lg + 15) >> 4;           // pieces holding payload (crc input)
         const int P0 = Lg & ~15;                // first piece that holds tail bytes
-        const int nrm = wave_max((ext + kRoundC - 1) / kRoundC);
+        const int nrm = wave_max((ext + 16 * lead + kRoundC - 1) / kRoundC);
         uint32_t acc = 0;
         u32x4 dt = {0, 0, 0, 0};                // this lane's tail piece, if any
         int Pt = -1;
@@ -488,8 +503,9 @@ __global__ __launch_bounds__(kThreads, COOK_OCC) void k_cook(CookArgs a) {
         for (int r = 0; r < nrm; ++r) {
             // rounds past the first (long packets); a packed output's tail may
             // end past the source slot, whose bytes there are never used
-            if (r) load_round(cur, pga, r, hl, min(ext, (a.cap + ph) & ~15));
-            const int qr = min(max(Q - kPplC * kLpp * r, 0), kPplC * kLpp);
+            if (r) load_round(cur, pga, r, hl, min(ext, (a.cap + ph) & ~15), lead);
+            // (round r's slot p holds piece kLpp (r kPplC + p) + hl - lead)
+            const int qr = min(max(Q + lead - kPplC * kLpp * r, 0), kPplC * kLpp);
             // pieces at or past every packet's last crc piece in this round:
             // skip their CRC (a wave-uniform branch per piece slot)
             const int qr_max = COOK_SKIP ? wave_max(qr) : kPplC * kLpp;
@@ -498,22 +514,23 @@ __global__ __launch_bounds__(kThreads, COOK_OCC) void k_cook(CookArgs a) {
 #else
             RoundCrc<COOK_2CH != 0> rc;
 #endif
-            uint32_t ivr = ivl ? mod_ivl((uint32_t)(r * kRoundC + 16 * hl + 16 * ivl - ph), (uint32_t)ivl, magic)
+            uint32_t ivr = ivl ? mod_ivl((uint32_t)(r * kRoundC + 16 * (hl - lead) + 128 * ivl - ph),
+                                         (uint32_t)ivl, magic)
                                : 0u;
 #pragma unroll
             for (int p = 0; p < kPplC; ++p) {
-                const int P = r * kRoundC + 16 * (kLpp * p + hl);  // grid offset
+                const int P = r * kRoundC + 16 * (kLpp * p + hl - lead);  // grid offset
                 // wholly payload (the head piece's bytes before the packet are scratch)
-                const bool whole = P < ext && P + 16 <= Lg;
+                const bool whole = P >= 0 && P < ext && P + 16 <= Lg;
                 u32x4 m = {0, 0, 0, 0};
                 if ((COOK_DEFER & 1) && whole) {  // the key stream's load flies during the CRC
                     m = ks_piece(a, P - ph);
                     if (ivl) m ^= iv_window_at(iv2w, ivr);
                 }
 #if COOK_ONE_CHAIN
-                if (ck && kLpp * p < qr_max) {
+                if (ck && kLpp * p < qr_max && P >= 0) {
                     const int sl = r * kPplC + p;
-                    rc.add(T, crc_in_ph(cur[p], P, Lg, ph), sl, kLpp * sl + hl, Q);
+                    rc.add(T, crc_in_ph(cur[p], P, Lg, ph), sl, kLpp * sl + hl - lead, Q);
                 }
 #else
                 if (ck && kLpp * p < qr_max) rc.add(T, crc_in_ph(cur[p], P, Lg, ph), p, kLpp * p + hl, qr);
@@ -536,8 +553,8 @@ __global__ __launch_bounds__(kThreads, COOK_OCC) void k_cook(CookArgs a) {
             if (COOK_DEFER & 2) {
 #pragma unroll
                 for (int p = 0; p < kPplC; ++p) {
-                    const int P = r * kRoundC + 16 * (kLpp * p + hl);
-                    if (P < ext && P + 16 <= Lg) st_piece(oga + P, cur[p]);
+                    const int P = r * kRoundC + 16 * (kLpp * p + hl - lead);
+                    if (P >= 0 && P < ext && P + 16 <= Lg) st_piece(oga + P, cur[p]);
                 }
             }
 #if !COOK_ONE_CHAIN
@@ -755,6 +772,7 @@ static_assert(kFuseRecs <= kLpp, "k_cook_frame needs a lane per source record (C
 #define COOKF_LINE 1  // k_cook_frame: lane pieces on the 128-byte line grid of the slot
 #endif
 static_assert(!COOKF_LINE || COOKF_ONE_CHAIN, "COOKF_LINE shifts the pieces of the one-chain fold only");
+static_assert(!COOK_LINE || COOK_ONE_CHAIN, "COOK_LINE shifts the pieces of the one-chain fold only");
 constexpr int kPplF = COOKF_PPL;
 constexpr int kRoundF = 16 * kLpp * kPplF;
 
