@@ -155,7 +155,6 @@ def main():
     u.fill_data(buf, K, LEN, synth.DATA_SEED, g0=g0)
     present = torch.from_numpy(synth.erasure_present(synth.ERASE_SEED, g0, G, n, ERASURES)).to(dev)
     status = torch.empty(G, dtype=torch.int32, device=dev)
-    smap = torch.empty((G, K), dtype=torch.uint8, device=dev)  # rs_decode's data[] permutation
     stream = torch.cuda.current_stream()
     u.reserve(K, n, G, stream)
 
@@ -167,11 +166,12 @@ def main():
         u.encode(buf, K, n, LEN, stream=stream)
         if i is not None:
             ev[i][1].record(stream)
-        # the reference's placement (lib/fec.cpp:872-877): rebuilt rows over
-        # the parity survivors, data[] permutation into smap; the next step's
-        # encode rewrites the parity from the untouched data slots
-        u.decode(buf, present, K, n, LEN, status=status, stream=stream, placement="reference",
-                 slot_map=smap)
+        # rebuilt rows in their own slots.  The reference's placement
+        # (rows over the parity survivors, lib/fec.cpp:872-877, and rs_decode's
+        # pointer permutation as a slot map) decodes as fast but makes this
+        # step's next encode 2.6 % slower (it overwrites the lines the decode
+        # just wrote; profiles/r06/place_step_ab.txt); verify_slice checks both
+        u.decode(buf, present, K, n, LEN, status=status, stream=stream)
         if i is not None:
             ev[i][2].record(stream)
 
@@ -199,16 +199,6 @@ def main():
     enc_ms = statistics.mean(a.elapsed_time(b) for a, b, _ in ev)
     dec_ms = statistics.mean(b.elapsed_time(c) for _, b, c in ev)
     bad = int((status != 0).sum().item())
-    # the last timed decode's output, read through its slot map (the pointer
-    # permutation rs_decode2 leaves in data[]): the rows it rebuilt over the
-    # parity survivors equal the data they replace (e <= 5: the erased data
-    # slots were never written, so they still hold the data)
-    timed_ok = all(bool(torch.equal(u.reference_rows(buf[c:c + 65536], smap[c:c + 65536])[:, :, :LEN],
-                                    buf[c:c + 65536, :K, :LEN])) for c in range(0, G, 65536))
-    # ... and the parity those survivors held comes back with one more encode
-    # (untimed), for the lines below and the parity digest
-    u.encode(buf, K, n, LEN, stream=stream)
-    torch.cuda.synchronize()
     extras = None
     if rank == 0 and world == 1 and not args.no_extras:
         extras = extra_configs(u, synth, torch, dev, buf, G)
@@ -219,9 +209,7 @@ def main():
     # parity): this rank's bytes against the reference's digests
     check = None if args.no_verify else verify_slice(u, synth, torch, buf, present, g0, G)
     ok_flags = [-1.0] * world
-    ok_flags[rank] = -1.0 if check is None or check.get("ok") is None else float(check["ok"] and timed_ok)
-    if check is not None:
-        check["timed_decode_rows_match"] = timed_ok
+    ok_flags[rank] = -1.0 if check is None or check.get("ok") is None else float(check["ok"])
     parity_ok = [None if f < 0 else bool(f) for f in ok_flags]
     if world > 1:
         # max over ranks: the job is as slow as its slowest GPU; every rank's
@@ -324,7 +312,6 @@ def run_c3(args, world, rank, dev, scaling):
     flags = synth.ragged_erasures(synth.ERASE_SEED, g0, ks + ms_, ms_, ERASURES)
     bits = torch.from_numpy(synth.present_bits(flags).view(np.int32)).to(dev)
     status = torch.empty(G, dtype=torch.int32, device=dev)
-    smap = torch.empty((G, 20), dtype=torch.uint8, device=dev)  # rs_decode's data[] permutation
     stream = torch.cuda.current_stream()
     ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
 
@@ -334,8 +321,7 @@ def run_c3(args, world, rank, dev, scaling):
         plan.encode(base)
         if i is not None:
             ev[i][1].record(stream)
-        # the reference's placement, as the C2 step (the next encode restores the parity)
-        plan.decode(base, bits, status=status, placement="reference", slot_map=smap)
+        plan.decode(base, bits, status=status)  # own slots, as the C2 step
         if i is not None:
             ev[i][2].record(stream)
 
@@ -360,8 +346,6 @@ def run_c3(args, world, rank, dev, scaling):
     enc_ms = statistics.mean(a.elapsed_time(b) for a, b, _ in ev)
     dec_ms = statistics.mean(b.elapsed_time(c) for _, b, c in ev)
     bad = int((status != 0).sum().item())
-    plan.encode(base)  # the parity the last decode wrote rows over (untimed)
-    torch.cuda.synchronize()
     cpu = None
     if rank == 0 and not args.no_cpu_baseline:
         cpu = c3_cpu_baseline(u, base, groups, ks, ms_, ls, flags)
@@ -436,17 +420,31 @@ def c3_verify(u, synth, torch, base, groups, ks, ms_, ls, g0, plan, bits, status
         off, ss = int(groups[g].offset), int(groups[g].shard_stride)
         for j in np.nonzero(flags[g, :int(ks[g] + ms_[g])] == 0)[0]:
             host[off + j * ss:off + (j + 1) * ss] = 0xA5
-    base.copy_(torch.from_numpy(host))
+    poisoned = torch.from_numpy(host)
+    base.copy_(poisoned)
+    plan.decode(base, bits, status=status)  # the step's call: rows in their own slots
+    torch.cuda.synchronize()
+    out = base.cpu().numpy()
+    ok &= int((status != 0).sum().item()) == 0
+    for g in range(G):
+        off, ss, k, ln = int(groups[g].offset), int(groups[g].shard_stride), int(ks[g]), int(ls[g])
+        got = out[off:off + k * ss].reshape(k, ss)[:, :ln]
+        ok &= bool((got == data[g].reshape(k, ss)[:, :ln]).all())
+        if not ok:
+            return ok
+    # the reference's placement on the same input: each data[i] read through
+    # the slot map (rs_decode's pointer permutation)
+    base.copy_(poisoned)
     smap = torch.empty((G, 20), dtype=torch.uint8, device=base.device)
     plan.decode(base, bits, status=status, placement="reference", slot_map=smap)
     torch.cuda.synchronize()
-    host = base.cpu().numpy()
+    out = base.cpu().numpy()
     m = smap.cpu().numpy()
     ok &= int((status != 0).sum().item()) == 0
-    for g in range(G):  # each data[i] read through the slot map (rs_decode's pointer permutation)
+    for g in range(G):
         off, ss, k, ln, n = (int(groups[g].offset), int(groups[g].shard_stride), int(ks[g]), int(ls[g]),
                              int(ks[g] + ms_[g]))
-        got = host[off:off + n * ss].reshape(n, ss)[m[g, :k].astype(np.int64), :ln]
+        got = out[off:off + n * ss].reshape(n, ss)[m[g, :k].astype(np.int64), :ln]
         ok &= bool((got == data[g].reshape(k, ss)[:, :ln]).all())
         if not ok:
             break
@@ -490,13 +488,14 @@ def verify_slice(u, synth, torch, buf, present, g0, G):
     """This rank's bytes, checked after the timed region against digests the
     real reference produced (tests/golden/full_hashes.json, c4_rank_slices
     ranges, made by oracle/gen_golden.py --c4) for exactly this group range:
-    * parity: the timed loop's encode kernel's output (rerun once after the
-      loop: its last decode wrote rows over the parity survivors, as
-      rs_decode2 does);
+    * parity: the timed loop's encode output (the parity rows now in buf);
     * decode: the rank's slice refilled as the non-codeword input (data from
       DATA_SEED, parity from DATA_SEED ^ 0xFFFF), every erased slot poisoned,
       one decode through the same call as the step, the k data rows compared
-      (pins which survivors rs_decode uses, lib/rs.cpp:24-39).
+      (pins which survivors rs_decode uses, lib/rs.cpp:24-39); then the same
+      input again through the reference's placement (rows over the parity
+      survivors), its rows read through the slot map and the map compared
+      with the host closed form (rs_decode's pointer permutation).
     Digests are sha256 over per-group checksums (synth.group_hashes_dev), so
     8 B per group leave the device.  ``ok`` is None when no fixture covers the
     range (e.g. a --groups the fixtures were not made for)."""
@@ -511,21 +510,30 @@ def verify_slice(u, synth, torch, buf, present, g0, G):
         return {"ok": None, "range": [g0, g0 + G], "why": "no reference digest for this range"}
     n = K + M
     par = synth.hashes_digest(synth.group_hashes_dev(buf[:, K:, :LEN]))
-    u.fill_data(buf, K, LEN, F["seed"], g0=g0)
-    u.fill_data(buf[:, K:], M, LEN, F["parity_seed"], g0=g0)
-    buf.masked_fill_((present == 0).unsqueeze(-1), 0xA5)  # erased slots hold junk
+    def refill():
+        u.fill_data(buf, K, LEN, F["seed"], g0=g0)
+        u.fill_data(buf[:, K:], M, LEN, F["parity_seed"], g0=g0)
+        buf.masked_fill_((present == 0).unsqueeze(-1), 0xA5)  # erased slots hold junk
+
+    refill()
+    st = u.decode(buf, present, K, n, LEN)
+    fails = int((st != 0).sum().item())
+    dat_own = synth.hashes_digest(synth.group_hashes_dev(buf[:, :K, :LEN]))
+    refill()
     smap = torch.empty((G, K), dtype=torch.uint8, device=buf.device)
     st = u.decode(buf, present, K, n, LEN, placement="reference", slot_map=smap)
-    fails = int((st != 0).sum().item())
+    fails += int((st != 0).sum().item())
     # the data rows read through the slot map, in data[] order (the pointer
     # permutation rs_decode leaves the caller), and the map itself against the
     # host closed form on a sample of groups
     map_ok = all((smap[g].cpu().numpy() == u.ref_slot_map(K, n, present[g].cpu().numpy())).all()
                  for g in range(0, G, max(1, G // 64)))
     dat = synth.hashes_digest(synth.group_hashes_dev(u.reference_rows(buf, smap)[:, :, :LEN]))
-    ok = par == R["parity_gsum"] and dat == R["data_out_gsum"] and fails == 0 and map_ok
+    ok = (par == R["parity_gsum"] and dat_own == R["data_out_gsum"] and dat == R["data_out_gsum"]
+          and fails == 0 and map_ok)
     return {"ok": ok, "range": [g0, g0 + G], "parity_match": par == R["parity_gsum"],
-            "decode_match": dat == R["data_out_gsum"], "slot_map_match": map_ok,
+            "decode_match": dat_own == R["data_out_gsum"], "ref_placement_decode_match": dat == R["data_out_gsum"],
+            "slot_map_match": map_ok,
             "decode_failures": fails,
             "check_s": round(time.perf_counter() - t0, 2),
             "what": "reference digests of this rank's encode parity and non-codeword decode"}
@@ -630,9 +638,7 @@ def extra_configs(u, synth, torch, dev, buf, G):
     pres = torch.from_numpy(synth.erasure_present(synth.ERASE_SEED + 1, 0, G, n, ERASURES,
                                                   limit=K)).to(dev)
     st = torch.empty(G, dtype=torch.int32, device=dev)
-    sm = torch.empty((G, K), dtype=torch.uint8, device=dev)
-    ms = _time_ms(torch, lambda: u.decode(buf, pres, K, n, LEN, status=st, placement="reference",
-                                          slot_map=sm))
+    ms = _time_ms(torch, lambda: u.decode(buf, pres, K, n, LEN, status=st))
     alg = G * (K + ERASURES) * LEN
     out["c2_worst_5_data_erasures"] = {
         "decode_ms": round(ms, 4), "groups": G,
@@ -640,7 +646,6 @@ def extra_configs(u, synth, torch, dev, buf, G):
         "alg_GBps": round(alg / (ms * 1e-3) / 1e9, 1),
         "roofline_frac": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
         "failures": int((st != 0).sum().item())}
-    u.encode(buf, K, n, LEN)  # the parity those decodes wrote rows over, back for the lines below
     out.update(c3_configs(u, synth, torch, dev, G))
     out["c4_one_gpu"] = c4_one_gpu(u, synth, torch, dev)
     out["rtc_f10_5_encode"] = rtc_config(u, synth, torch, dev)
@@ -675,11 +680,7 @@ def c3_configs(u, synth, torch, dev, G):
     flags = synth.ragged_erasures(synth.ERASE_SEED, 0, ks + ms_, ms_, ERASURES)
     bits = torch.from_numpy(synth.present_bits(flags).view(np.int32)).to(dev)
     st = torch.empty(G, dtype=torch.int32, device=dev)
-    sm = torch.empty((G, 20), dtype=torch.uint8, device=dev)
-    # the reference's placement (as the headline step): rows over the parity
-    # survivors, so repeated calls decode changed inputs -- the same work
-    t = _time_ms(torch, lambda: plan.decode(base, bits, status=st, placement="reference", slot_map=sm),
-                 spread=sp_d)
+    t = _time_ms(torch, lambda: plan.decode(base, bits, status=st), spread=sp_d)
     e = ((flags[:, :20] == 0) & (np.arange(20)[None, :] < ks[:, None])).sum(1)
     alg = int((((e > 0) * ks + e) * ls).sum())  # k*len read + e*len written, groups with e > 0
     out["c3_ragged_decode"] = {
@@ -733,12 +734,11 @@ def c4_one_gpu(u, synth, torch, dev, steps=5):
     u.fill_data(b, K, LEN, synth.DATA_SEED)
     p = torch.from_numpy(synth.erasure_present(synth.ERASE_SEED, 0, Gc, n, ERASURES)).to(dev)
     st = torch.empty(Gc, dtype=torch.int32, device=dev)
-    sm = torch.empty((Gc, K), dtype=torch.uint8, device=dev)
     u.reserve(K, n, Gc)
 
     def step():
         u.encode(b, K, n, LEN)
-        u.decode(b, p, K, n, LEN, status=st, placement="reference", slot_map=sm)
+        u.decode(b, p, K, n, LEN, status=st)
     ms = _time_ms(torch, step, reps=steps, warm=1)
     r = {"groups": Gc, "ms_per_step": round(ms, 3),
          "GiBps": round(2.0 * Gc * K * LEN / (ms * 1e-3) / 2**30, 1),
