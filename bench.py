@@ -200,8 +200,10 @@ def main():
     dec_ms = statistics.mean(b.elapsed_time(c) for _, b, c in ev)
     bad = int((status != 0).sum().item())
     extras = None
+    copy_peak = None
     if rank == 0 and world == 1 and not args.no_extras:
         extras = extra_configs(u, synth, torch, dev, buf, G)
+        copy_peak = hbm_copy_peak(torch, dev)
     cpu = None
     if rank == 0 and not args.no_cpu_baseline:  # after the timed region, every N
         cpu = cpu_baseline(buf, present, G, args.cpu_threads)
@@ -265,6 +267,7 @@ def main():
                 k_: v for k_, v in check.items() if k_ != "ok"},
             "roofline": roof[dominant],
             f"roofline_{other}": roof[other],
+            "hbm_copy_peak": copy_peak,
             "cpu_baseline": cpu,
             "other_configs": extras,
         }
@@ -537,6 +540,28 @@ def verify_slice(u, synth, torch, buf, present, g0, G):
             "decode_failures": fails,
             "check_s": round(time.perf_counter() - t0, 2),
             "what": "reference digests of this rank's encode parity and non-codeword decode"}
+
+
+def hbm_copy_peak(torch, dev, nbytes=2 << 30, reps=8):
+    """SURVEY 8(d)'s second reference line: a measured device-to-device copy
+    of 2 GiB on this box (read + written bytes / time, median of `reps`),
+    against which the kernels' achieved rates are also stated."""
+    a = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    b = torch.empty_like(a)
+    a.fill_(7)
+    ts = []
+    for i in range(reps + 2):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        b.copy_(a)
+        e1.record()
+        torch.cuda.synchronize()
+        if i >= 2:
+            ts.append(e0.elapsed_time(e1))
+    ms = statistics.median(ts)
+    del a, b
+    return {"GBps": round(2 * nbytes / (ms * 1e-3) / 1e9, 1), "bytes_each_way": nbytes,
+            "how": "torch copy_ of a 2 GiB device tensor (read + write), median of 8 after 2 warm"}
 
 
 def roofline(which, kernel, alg_bytes, ms, G):
