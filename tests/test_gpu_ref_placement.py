@@ -199,20 +199,23 @@ def _ragged_ref_check(u, oracle, groups, host, flags, out, st, smap, stride):
         assert (got[:, pad:] == org[:, pad:]).all(), i
 
 
-@pytest.mark.parametrize("form", ["plan", "dev"])
-def test_ref_ragged_many_codes_vs_oracle(gpu, oracle, form):
+@pytest.mark.parametrize("form,kmax,stride", [("plan", 60, 48), ("dev", 60, 48), ("plan", 200, 200),
+                                               ("dev", 200, 160)])
+def test_ref_ragged_many_codes_vs_oracle(gpu, oracle, form, kmax, stride):
     """Ragged reference-placement decode over ~200 codes: e up to 10 (row
     blocks of 5: the earlier blocks parked and moved), k up to 60 (k > 32:
-    the workgroup kernel), lengths 1..3000 (several tiles), too-few groups;
+    the workgroup kernel) or 200 (k > 64, too-few groups among them: their
+    map entries past 64), lengths 1..3000 (several tiles), too-few groups;
     slot maps with a stride smaller than some k."""
     import torch
     import udpspeeder_amd as u
     from udpspeeder_amd import synth
-    rng = np.random.default_rng(606)
-    G = 500
-    ks = rng.integers(1, 61, G)
+    rng = np.random.default_rng(606 + kmax)
+    G = 500 if kmax <= 60 else 160
+    ks = rng.integers(1, kmax + 1, G)
     ms = rng.integers(1, 21, G)
-    ls = rng.integers(1, 3000, G)
+    ms = np.minimum(ms, 256 - ks)
+    ls = rng.integers(1, 3000 if kmax <= 60 else 700, G)
     ls[:4] = [1, 16, 1280, 1281]
     groups, total = u.make_groups(ks, ks + ms, ls)
     host = rng.integers(0, 256, total, dtype=np.uint8)
@@ -225,7 +228,6 @@ def test_ref_ragged_many_codes_vs_oracle(gpu, oracle, form):
         u.prepare_code(*c)
     base = upload(host, gpu)
     bits = torch.from_numpy(synth.present_bits(flags).view(np.int32)).to(gpu)
-    stride = 48
     smap = torch.full((G, stride), 0xEE, dtype=torch.uint8, device=gpu)
     if form == "plan":
         plan = u.rs.RaggedPlan(groups, wait_codes=False)
@@ -237,7 +239,7 @@ def test_ref_ragged_many_codes_vs_oracle(gpu, oracle, form):
         st = torch.empty(G, dtype=torch.int32, device=gpu)
         dg = u.rs.groups_to_device(groups, gpu)
         check(u.lib().rsmi_decode_ragged_dev_ref(dg.data_ptr(), G, base.data_ptr(), bits.data_ptr(),
-                                                 st.data_ptr(), 60, smap.data_ptr(), stride, None),
+                                                 st.data_ptr(), kmax, smap.data_ptr(), stride, None),
               "rsmi_decode_ragged_dev_ref")
     _ragged_ref_check(u, oracle, groups, host, flags, base.cpu().numpy(), st.cpu().numpy(),
                       smap.cpu().numpy(), stride)

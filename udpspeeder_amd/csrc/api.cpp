@@ -1145,7 +1145,7 @@ void split_ranges(int64_t n, const int64_t *cost, int parts, int64_t *bounds) {
 // run_split's answer when no device list is set: the caller runs the call on
 // its own current device.  Decided under call_mu, so a concurrent
 // rsmi_set_devices(.., 0) cannot turn a split call into a silent no-op.
-constexpr int kNoWorkers = 1;
+constexpr int kNoWorkers = 0x52534d31;  // never a status: fn returns RSMI_OK or a negative RSMI_ERR_*
 
 // Runs fn(worker, g0, count) for every listed device's range, in parallel, and
 // returns the first failure (its message moved to the calling thread), or

@@ -827,16 +827,21 @@ __device__ __forceinline__ int ref_slot_lds(const uint8_t *sel, int k, int e, in
     return sel[x];
 }
 
-// A group's slot map (lanes i < k <= 64): i for a present data row, its
-// reference slot for a rebuilt one, 0xFF for an erased row of a group that
-// was not decoded.
+// A group's slot map: i for a present data row, its reference slot for a
+// rebuilt one (decoded groups: k <= 64 on these kernels), 0xFF for an erased
+// row of a group that was not decoded (any k).
 template <class Flag>
 __device__ __forceinline__ void write_slot_map(const RefOut &ro, int64_t g, int k, int e, bool decoded,
                                                Flag flag, const WaveLds &L, int lane) {
-    if (!ro.map || lane >= k || lane >= ro.stride) return;
-    const bool p = flag(0, lane);
-    ro.map[g * ro.stride + lane] =
-        p ? (uint8_t)lane : decoded ? (uint8_t)ref_slot_lds(L.sel, k, e, lane) : (uint8_t)0xFF;
+    if (!ro.map) return;
+    const int lim = k < ro.stride ? k : ro.stride;
+    for (int b = 0; b < lim; b += 64) {
+        const int i = b + lane;
+        const bool p = flag(b, i);  // (wave-wide: flag reads lanes of the present words)
+        if (i < lim)
+            ro.map[g * ro.stride + i] =
+                p ? (uint8_t)i : decoded ? (uint8_t)ref_slot_lds(L.sel, k, e, i) : (uint8_t)0xFF;
+    }
 }
 
 // Move rows [0, nrows) of the group from their own (erased) slots to their
