@@ -203,7 +203,7 @@ def main():
     copy_peak = None
     if rank == 0 and world == 1 and not args.no_extras:
         extras = extra_configs(u, synth, torch, dev, buf, G)
-        copy_peak = hbm_copy_peak(torch, dev)
+        copy_peak = hbm_copy_peak(u, torch, dev)
     cpu = None
     if rank == 0 and not args.no_cpu_baseline:  # after the timed region, every N
         cpu = cpu_baseline(buf, present, G, args.cpu_threads)
@@ -247,6 +247,9 @@ def main():
         else:
             workload = (f"C4: RS(20,10) encode + decode (5 random erasures), 1250-B shards, "
                         f"{total_groups} groups split over {world} GPU(s), device-resident")
+        if copy_peak:
+            for r in roof.values():  # the same achieved rate against the measured copy
+                r["frac_of_copy_peak"] = round(r["achieved"] / copy_peak["GBps"], 4)
         line = {
             "metric": METRIC, "value": round(value, 2), "unit": "GiB/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup,
@@ -542,26 +545,44 @@ def verify_slice(u, synth, torch, buf, present, g0, G):
             "what": "reference digests of this rank's encode parity and non-codeword decode"}
 
 
-def hbm_copy_peak(torch, dev, nbytes=2 << 30, reps=8):
+def hbm_copy_peak(u, torch, dev, nbytes=2 << 30, reps=8):
     """SURVEY 8(d)'s second reference line: a measured device-to-device copy
-    of 2 GiB on this box (read + written bytes / time, median of `reps`),
-    against which the kernels' achieved rates are also stated."""
+    of 2 GiB on this box (read + written bytes / time, median of `reps` after
+    2 warm), the best of librsmi's copy kernel (`rsmi_copy_peak`, 4 or 8
+    16-byte words per thread, plain or nontemporal) and torch's `copy_`,
+    each variant's rate listed."""
+    from udpspeeder_amd._lib import check
     a = torch.empty(nbytes, dtype=torch.uint8, device=dev)
     b = torch.empty_like(a)
     a.fill_(7)
-    ts = []
-    for i in range(reps + 2):
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        b.copy_(a)
-        e1.record()
-        torch.cuda.synchronize()
-        if i >= 2:
-            ts.append(e0.elapsed_time(e1))
-    ms = statistics.median(ts)
+    L = u.lib()
+
+    def rate(fn):
+        ts = []
+        for i in range(reps + 2):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            fn()
+            e1.record()
+            torch.cuda.synchronize()
+            if i >= 2:
+                ts.append(e0.elapsed_time(e1))
+        return round(2 * nbytes / (statistics.median(ts) * 1e-3) / 1e9, 1)
+
+    names = ["rsmi_u4", "rsmi_u8", "rsmi_u4_nt", "rsmi_u8_nt"]
+    got = {}
+    for v, name in enumerate(names):
+        # (torch's current stream: the events above are recorded on it)
+        got[name] = rate(lambda: check(L.rsmi_copy_peak(b.data_ptr(), a.data_ptr(), nbytes, v,
+                                                        torch.cuda.current_stream().cuda_stream),
+                                       "rsmi_copy_peak"))
+    assert torch.equal(a[:1 << 20], b[:1 << 20]) and torch.equal(a[-(1 << 20):], b[-(1 << 20):])
+    got["torch_copy_"] = rate(lambda: b.copy_(a))
     del a, b
-    return {"GBps": round(2 * nbytes / (ms * 1e-3) / 1e9, 1), "bytes_each_way": nbytes,
-            "how": "torch copy_ of a 2 GiB device tensor (read + write), median of 8 after 2 warm"}
+    best = max(got, key=got.get)
+    return {"GBps": got[best], "best": best, "variants_GBps": got, "bytes_each_way": nbytes,
+            "how": "device-to-device copy of 2 GiB (read + write bytes / time), median of 8 after 2 warm, "
+                   "best variant"}
 
 
 def roofline(which, kernel, alg_bytes, ms, G):
@@ -676,6 +697,16 @@ def extra_configs(u, synth, torch, dev, buf, G):
     out["rtc_f10_5_encode"] = rtc_config(u, synth, torch, dev)
     out["f2_cook_decook"] = cook_config(torch, dev, buf, G)
     out["f1_f2_frame_encode_cook"] = frame_cook_config(torch, dev)
+    # the other setting of RSMI_OPT_PARITY_COOK (the parity cooked in the
+    # encoder's epilogue), same workload
+    from udpspeeder_amd._lib import RSMI_OPT_PARITY_COOK
+    cur = u.lib().rsmi_set_option(RSMI_OPT_PARITY_COOK, 0)
+    u.lib().rsmi_set_option(RSMI_OPT_PARITY_COOK, cur)
+    alt = frame_cook_config(torch, dev, parity_cook=not cur)
+    out["f1_f2_frame_encode_cook"]["parity_cook_option"] = bool(cur)
+    out["f1_f2_frame_encode_cook"]["other_setting"] = {
+        "parity_cook_option": not cur, "run_ms": alt["run_ms"], "parity_cook_runs": alt["parity_cook_runs"],
+        "lengths_ok": alt.get("lengths_ok")}
     out["f1_collector_200_connections"] = collector_config(torch, dev)
     out["dropin_latency_us"] = dropin_latency_both(u)
     return out
@@ -812,7 +843,7 @@ def cook_config(torch, dev, buf, G):
             "roundtrip_ok": ok}
 
 
-def frame_cook_config(torch, dev, groups=65536, reps=4):
+def frame_cook_config(torch, dev, groups=65536, reps=4, parity_cook=None):
     """f1 + f2 fused: one connection's 1200-B datagrams (mode 0, -f 20:10, mtu
     1250: 65,536 RS(20,10) groups) through rsmi_fenc_run_cooked_dev -- framing,
     bit-sliced encode and do_cook of every emitted packet in one run into a
@@ -821,6 +852,9 @@ def frame_cook_config(torch, dev, groups=65536, reps=4):
     import numpy as np
     from udpspeeder_amd.cook import CookContext
     from udpspeeder_amd.fec import FecEncoder
+    import udpspeeder_amd as u
+    from udpspeeder_amd._lib import RSMI_OPT_PARITY_COOK
+    prev = None if parity_cook is None else u.lib().rsmi_set_option(RSMI_OPT_PARITY_COOK, int(parity_cook))
     plen = 1200
     npk = groups * 20
     lens = np.full(npk, plen, np.int32)
@@ -829,7 +863,7 @@ def frame_cook_config(torch, dev, groups=65536, reps=4):
     enc = FecEncoder("20:10", 0, 1250, 200, seq0=1)
     ctx = CookContext(b"bench-key")
     slots = out = None
-    ts, nout, ok = [], 0, True
+    ts, nout, ok, epi = [], 0, True, 0
     for i in range(reps + 1):
         p = enc.plan(lens, offs, inbuf)
         S = FecEncoder.slot_stride_for(int(p.groups["fec_len"].max()))
@@ -845,14 +879,17 @@ def frame_cook_config(torch, dev, groups=65536, reps=4):
         torch.cuda.synchronize()
         nout = len(p.packets)
         ok = ok and bool((ol[:nout] > torch.from_numpy(p.packets["len"]).to(dev)).all())
+        epi = enc.last_parity_cooked()
         if i:
             ts.append(e0.elapsed_time(e1))
     t = statistics.median(ts)
     enc.close()
     ctx.close()
+    if prev is not None:
+        u.lib().rsmi_set_option(RSMI_OPT_PARITY_COOK, prev)
     del slots, out, inbuf
     return {"datagrams_in": npk, "datagram_len": plen, "groups": groups, "packets_out": nout,
-            "run_ms": round(t, 4), "datagrams_in_per_s": round(npk / (t * 1e-3), 1),
+            "run_ms": round(t, 4), "parity_cook_runs": epi, "datagrams_in_per_s": round(npk / (t * 1e-3), 1),
             "cooked_packets_per_s": round(nout / (t * 1e-3), 1),
             "what": "rsmi_fenc_run_cooked_dev: plan upload (groups, packet runs; source records "
                     "read in place) + k_expand_packets + k_cook_frame (data packets framed into "

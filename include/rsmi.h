@@ -101,6 +101,16 @@ const char *rsmi_last_error(void);
  * device-wide synchronisation can wait for it under steady traffic; each
  * relaunch costs the call that makes it one kernel launch. */
 #define RSMI_OPT_ONE_SERVER_LIFE 6
+/* RSMI_OPT_PARITY_COOK: 1 cooks the parity packets of a fused cooked FEC run
+ * (rsmi_fenc_run_cooked_dev into device memory) in the encoder's epilogue:
+ * the encoder stores their payload already obscured and keyed into the
+ * output, and the cook pass adds only the header, the CRC and the tail --
+ * the parity is never written plain to the slots, nor written twice.  Taken
+ * when every encoder run of the batch has a build-time split-k network;
+ * otherwise (and with 0, the default, or RSMI_PARITY_COOK=0 in the
+ * environment) the parity is written into the slots and cooked after the
+ * encoder.  The cooked bytes are the same either way. */
+#define RSMI_OPT_PARITY_COOK 7
 
 int rsmi_set_option(int option, int value);
 
@@ -406,6 +416,14 @@ int rsmi_fill_data(int k, int len, uint8_t *base, int64_t group_stride,
  * descriptor array) get the stream of group id g0 + i. */
 int rsmi_fill_ragged(const rsmi_group *dev_groups, int64_t ngroups, uint8_t *base,
                      int64_t g0, uint64_t seed, void *stream);
+
+/* ---- measurement ---------------------------------------------------------
+ * Device-to-device copy of nbytes (a multiple of 16; both pointers 16-byte
+ * aligned, not overlapping): bench.py's measured HBM copy peak, the line the
+ * codec kernels' achieved rates are read against besides the 8 TB/s spec.
+ * variant: 0 / 1 = 4 / 8 16-byte words per thread, 2 / 3 = the same with
+ * nontemporal loads and stores.  No reference counterpart. */
+int rsmi_copy_peak(uint8_t *dst, const uint8_t *src, int64_t nbytes, int variant, void *stream);
 
 #ifdef __cplusplus
 }

@@ -137,6 +137,12 @@ int rsmi_fenc_run_cooked_dev(rsmi_fenc *enc, uint8_t *slots_base, int64_t slot_s
                              const struct rsmi_cook_ctx *ctx, uint64_t seed, uint8_t *out,
                              int32_t *out_len, void *stream);
 
+/* Encoder runs (groups of one code, length and consecutive slots) of the
+ * last cooked run that cooked their parity packets in the encoder's epilogue
+ * (RSMI_OPT_PARITY_COOK, include/rsmi.h): their parity slots were not
+ * written, the output holds the cooked packets as always. */
+int64_t rsmi_fenc_last_parity_cooked(const rsmi_fenc *enc);
+
 /* The last plan's packet list as runs (diagnostics and tests): packets first
  * .. first + count - 1 sit in slots slot .. slot + count - 1 of framing job
  * `job`, len bytes each; the first ndata are data packets of clean shards

@@ -22,6 +22,9 @@ RSMI_OPT_BITSLICE = 1
 RSMI_OPT_FUSED_DECODE = 2
 RSMI_OPT_ONE_GROUP = 3
 RSMI_OPT_CLS_REC_CAP = 4
+RSMI_OPT_ONE_SERVER = 5
+RSMI_OPT_ONE_SERVER_LIFE = 6
+RSMI_OPT_PARITY_COOK = 7
 RSMI_DEC_OK = 0
 RSMI_DEC_TOO_FEW = -1
 RSMI_DEC_SINGULAR = 1
@@ -111,6 +114,7 @@ def _bind(lib: C.CDLL) -> C.CDLL:
         "rsmi_encode_host": ([i32, i32, vp, i64, i64, i32, i64], i32),
         "rsmi_decode_host": ([i32, i32, vp, i64, i64, i32, i64, vp, vp], i32),
         "rsmi_fill_data": ([i32, i32, vp, i64, i64, i64, i64, C.c_uint64, vp], i32),
+        "rsmi_copy_peak": ([vp, vp, i64, i32, vp], i32),
         "rsmi_fill_ragged": ([vp, i64, vp, i64, C.c_uint64, vp], i32),
         "rsmi_ragged_plan_create": ([vp, i64, vp], i32),
         "rsmi_encode_ragged_plan": ([vp, vp, vp], i32),
@@ -149,6 +153,7 @@ def _bind(lib: C.CDLL) -> C.CDLL:
         "rsmi_fenc_run_dev": ([vp, vp, i64, vp], i32),
         "rsmi_fenc_run_cooked_dev": ([vp, vp, i64, vp, C.c_uint64, vp, vp, vp], i32),
         "rsmi_fenc_run_cooked_packed_dev": ([vp, vp, i64, vp, C.c_uint64, vp, i64, vp, vp], i32),
+        "rsmi_fenc_last_parity_cooked": ([vp], i64),
         "rsmi_fcol_create": ([vp], i32),
         "rsmi_fcol_destroy": ([vp], None),
         "rsmi_debug_fcol_fail": ([i32], i32),

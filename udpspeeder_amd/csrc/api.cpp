@@ -33,6 +33,7 @@ std::atomic<int> g_opt_server{-1};              // RSMI_OPT_ONE_SERVER: idle us 
 std::atomic<int> g_opt_server_life{-1};         // RSMI_OPT_ONE_SERVER_LIFE: ms (-1: not read yet)
 std::atomic<int> g_opt_bitslice{1};
 std::atomic<int> g_opt_fused{1};
+std::atomic<int> g_opt_parity_cook{-1};        // RSMI_OPT_PARITY_COOK (-1: not read yet)
 
 int fail(int code, const std::string &msg) {
     g_err = msg;
@@ -278,6 +279,48 @@ int encode_dev(int k, int n, uint8_t *base, int64_t gs, int64_t ss, int len, int
                                            : RSMI_ENC_BITSLICE_RTC;
     if (e == hipErrorNotSupported) e = launch_encode_generic(a, W, C->dev_rows, D->ptab, s);
     if (e != hipSuccess) return hip_fail(e, "encode launch");
+    return RSMI_OK;
+}
+
+bool parity_cook_enabled() {
+    int v = g_opt_parity_cook.load();
+    if (v < 0) {  // RSMI_PARITY_COOK=1 turns it on for a process (A/B runs)
+        const char *e = std::getenv("RSMI_PARITY_COOK");
+        v = (e && *e && *e != '0') ? 1 : 0;
+        int expect = -1;
+        g_opt_parity_cook.compare_exchange_strong(expect, v);
+        v = g_opt_parity_cook.load();
+    }
+    return v > 0;
+}
+
+bool encode_cooked_ok(int k, int n, int64_t gs, int64_t ss, int len, int64_t ngroups) {
+    if (!g_opt_bitslice.load() || n <= k || len <= 0 || ngroups <= 0 || k > 256 || n > 256 || ss % 16 ||
+        gs % 16 || ss < len)
+        return false;
+    int W;
+    return bitslice_cooked_ok(make_args(k, n, nullptr, gs, ss, len, ngroups, &W));
+}
+
+// encode_dev with the parity cook in the epilogue (the caller checked
+// encode_cooked_ok; the kernels and records are described at EpiRec).
+int encode_dev_cooked(int k, int n, uint8_t *base, int64_t gs, int64_t ss, int len, int64_t ngroups,
+                      const CookEpi &ep, hipStream_t s) {
+    int rc = check_uniform(k, n, base, gs, ss, len, ngroups);
+    if (rc) return rc;
+    Device *D = current(&rc);
+    if (!D) return rc;
+    const Code *C;
+    {
+        std::lock_guard<std::mutex> lk(D->mu);
+        rc = ensure_code(*D, k, n, &C);
+        if (rc) return rc;
+    }
+    int W;
+    UniformArgs a = make_args(k, n, base, gs, ss, len, ngroups, &W);
+    const hipError_t e = launch_encode_bitslice_cooked(a, ep, s);
+    if (e != hipSuccess) return hip_fail(e, "cooking encode launch");
+    g_last_enc = RSMI_ENC_BITSLICE;
     return RSMI_OK;
 }
 
@@ -1444,6 +1487,11 @@ int rsmi_set_option(int option, int value) {
         }
         return prev;
     }
+    if (option == RSMI_OPT_PARITY_COOK) {
+        const int prev = rsmi::parity_cook_enabled() ? 1 : 0;
+        rsmi::g_opt_parity_cook.store(value ? 1 : 0);
+        return prev;
+    }
     if (option == RSMI_OPT_ONE_SERVER_LIFE) {
         const int prev = rsmi::server_life_ms();
         if (value < 1) {
@@ -1666,6 +1714,21 @@ int rsmi_fill_ragged(const rsmi_group *groups, int64_t ngroups, uint8_t *base, i
     hipError_t e = rsmi::launch_fill_ragged(groups, ngroups, base, g0, seed, (hipStream_t)stream);
     if (e != hipSuccess) {
         rsmi::set_error(std::string("fill_ragged launch: ") + hipGetErrorString(e));
+        return RSMI_ERR_HIP;
+    }
+    return RSMI_OK;
+}
+
+int rsmi_copy_peak(uint8_t *dst, const uint8_t *src, int64_t nbytes, int variant, void *stream) {
+    if (nbytes < 0 || nbytes % 16 || variant < 0 || variant > 3 || ((uintptr_t)dst | (uintptr_t)src) % 16 ||
+        (nbytes > 0 && (!dst || !src)) || nbytes / 16 / (256 * 4) >= 0x7FFFFFFF) {
+        rsmi::set_error("invalid copy_peak arguments");
+        return RSMI_ERR_INVALID;
+    }
+    if (nbytes == 0) return RSMI_OK;
+    hipError_t e = rsmi::launch_copy_peak(dst, src, nbytes, variant, (hipStream_t)stream);
+    if (e != hipSuccess) {
+        rsmi::set_error(std::string("copy_peak launch: ") + hipGetErrorString(e));
         return RSMI_ERR_HIP;
     }
     return RSMI_OK;

@@ -419,6 +419,13 @@ __device__ __forceinline__ u32x4 crc_in_ph(u32x4 v, int P, int n, int ph) {
 constexpr int kPplC = COOK_PPL;
 constexpr int kRoundC = 16 * kLpp * kPplC;
 
+// PREX (a fused cooked run's list B with the parity cook in the encoder's
+// epilogue, rsmi_internal.hpp EpiRec): an entry flagged kPrexFlag in len is
+// read from the output, where the encoder stored its whole payload pieces
+// already obscured and keyed and its other pieces plain (and k_expand_packets
+// its header): those pieces' plain bytes are recovered for the CRC and not
+// stored again; the header piece and the tail are cooked as usual.
+template <bool PREX>
 __global__ __launch_bounds__(kThreads, COOK_OCC) void k_cook(CookArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const bool ck = !(a.flags & RSMI_COOK_NO_CHECKSUM);
@@ -453,6 +460,8 @@ __global__ __launch_bounds__(kThreads, COOK_OCC) void k_cook(CookArgs a) {
                            ? (int)((uintptr_t)pkt & 15) : 0;
         const uint8_t *pga = pkt - ph;
         uint8_t *oga = opkt - ph;
+        const bool pre = PREX && have && (a.pk[pk].len & kPrexFlag);
+        const uint8_t *sga = pre ? oga : pga;  // where the packet's bytes are read
         // COOK_LINE: the lanes count pieces from the 128-byte line the grid
         // starts in (`lead` pieces before it, untouched), so a load or store
         // instruction covers whole lines (an FEC packet's grid starts 112 B
@@ -462,10 +471,10 @@ __global__ __launch_bounds__(kThreads, COOK_OCC) void k_cook(CookArgs a) {
         // round 0 is read up to the packet's cap (every packet owns cap bytes), so
         // these loads fly together with the length load instead of after it
         u32x4 cur[kPplC];
-        load_round(cur, pga, 0, hl, have && ((uintptr_t)pkt & 3) == 0 ? min((a.cap + ph) & ~15, kRoundC) : 0,
+        load_round(cur, sga, 0, hl, have && ((uintptr_t)pkt & 3) == 0 ? min((a.cap + ph) & ~15, kRoundC) : 0,
                    lead);
         if (have) {
-            L = packet_len(a, pk);
+            L = PREX ? (packet_len(a, pk) & ~kPrexFlag) : packet_len(a, pk);
             if (obs) ivl = a.iv ? a.iv_len[pk] : 4 + (int)(splitmix(a.seed, (uint64_t)gi, 0) % 29u);
         }
         const int out = L + (ck ? 4 : 0) + (obs ? ivl + 1 : 0);
@@ -503,7 +512,7 @@ __global__ __launch_bounds__(kThreads, COOK_OCC) void k_cook(CookArgs a) {
         for (int r = 0; r < nrm; ++r) {
             // rounds past the first (long packets); a packed output's tail may
             // end past the source slot, whose bytes there are never used
-            if (r) load_round(cur, pga, r, hl, min(ext, (a.cap + ph) & ~15), lead);
+            if (r) load_round(cur, sga, r, hl, min(ext, (a.cap + ph) & ~15), lead);
             // (round r's slot p holds piece kLpp (r kPplC + p) + hl - lead)
             const int qr = min(max(Q + lead - kPplC * kLpp * r, 0), kPplC * kLpp);
             // pieces at or past every packet's last crc piece in this round:
@@ -522,7 +531,14 @@ __global__ __launch_bounds__(kThreads, COOK_OCC) void k_cook(CookArgs a) {
                 const int P = r * kRoundC + 16 * (kLpp * p + hl - lead);  // grid offset
                 // wholly payload (the head piece's bytes before the packet are scratch)
                 const bool whole = P >= 0 && P < ext && P + 16 <= Lg;
+                // cooked by the encoder: a payload piece (past the header piece)
+                const bool done = PREX && pre && whole && P >= 16;
                 u32x4 m = {0, 0, 0, 0};
+                if (done) {
+                    m = ks_piece(a, P - ph);
+                    if (ivl) m ^= iv_window_at(iv2w, ivr);
+                    cur[p] ^= m;  // its plain bytes, for the CRC
+                }
                 if ((COOK_DEFER & 1) && whole) {  // the key stream's load flies during the CRC
                     m = ks_piece(a, P - ph);
                     if (ivl) m ^= iv_window_at(iv2w, ivr);
@@ -535,7 +551,8 @@ __global__ __launch_bounds__(kThreads, COOK_OCC) void k_cook(CookArgs a) {
 #else
                 if (ck && kLpp * p < qr_max) rc.add(T, crc_in_ph(cur[p], P, Lg, ph), p, kLpp * p + hl, qr);
 #endif
-                if (whole) {  // obscure + xor
+                if (done) {
+                } else if (whole) {  // obscure + xor
                     if (!(COOK_DEFER & 1)) {
                         m = ks_piece(a, P - ph);
                         if (ivl) m ^= iv_window_at(iv2w, ivr);
@@ -554,7 +571,7 @@ __global__ __launch_bounds__(kThreads, COOK_OCC) void k_cook(CookArgs a) {
 #pragma unroll
                 for (int p = 0; p < kPplC; ++p) {
                     const int P = r * kRoundC + 16 * (kLpp * p + hl - lead);
-                    if (P >= 0 && P < ext && P + 16 <= Lg) st_piece(oga + P, cur[p]);
+                    if (P >= 0 && P < ext && P + 16 <= Lg && !(PREX && pre && P >= 16)) st_piece(oga + P, cur[p]);
                 }
             }
 #if !COOK_ONE_CHAIN
@@ -1035,8 +1052,10 @@ hipError_t launch_cook(const CookArgs &a, bool decook, int max_blocks, hipStream
     const size_t lds = cook_lds_bytes(decook);
     if (decook)
         k_decook<<<(unsigned)blocks, kThreads, lds, s>>>(a);
+    else if (a.prex)
+        k_cook<true><<<(unsigned)blocks, kThreads, lds, s>>>(a);
     else
-        k_cook<<<(unsigned)blocks, kThreads, lds, s>>>(a);
+        k_cook<false><<<(unsigned)blocks, kThreads, lds, s>>>(a);
     return hipGetLastError();
 }
 

@@ -25,6 +25,7 @@ struct rsmi_cook_ctx {
     uint32_t *tabs = nullptr;
     uint8_t *ks = nullptr;  // NULL when there is no XOR stage; position p at ks[p], p >= -kCookKsLead
     uint8_t *ks_mem = nullptr;  // the allocation (ks - kCookKsLead)
+    uint8_t *zks = nullptr;     // no XOR stage: a zero stream of the same extent (the encoder epilogue's)
     // synchronous host path
     std::mutex mu;
     uint8_t *hbuf = nullptr;
@@ -186,6 +187,13 @@ extern "C" int rsmi_cook_ctx_create(const char *key, int flags, rsmi_cook_ctx **
         e = hipMalloc(&c->ks_mem, ks.size());
         if (e == hipSuccess) e = hipMemcpy(c->ks_mem, ks.data(), ks.size(), hipMemcpyHostToDevice);
         if (e == hipSuccess) c->ks = c->ks_mem + lead;
+    } else if (e == hipSuccess) {
+        // the cooking encoder XORs a key stream unconditionally (a branch there
+        // costs it its registers): zeros
+        const size_t bytes = rsmi::kCookKsBytes + rsmi::kCookKsLead;
+        e = hipMalloc(&c->ks_mem, bytes);
+        if (e == hipSuccess) e = hipMemset(c->ks_mem, 0, bytes);
+        if (e == hipSuccess) c->zks = c->ks_mem + rsmi::kCookKsLead;
     }
     if (e != hipSuccess) {
         rsmi_cook_ctx_destroy(c);
@@ -259,10 +267,14 @@ extern "C" int rsmi_decook_to(const rsmi_cook_ctx *c, const rsmi_packet_batch *b
 }
 
 namespace rsmi {
+int cook_ctx_flags(const rsmi_cook_ctx *c) { return c->flags; }
+const uint8_t *cook_ctx_ks(const rsmi_cook_ctx *c) { return c->ks ? c->ks : c->zks; }
+
 int cook_packets(const rsmi_cook_ctx *c, uint8_t *slots, int64_t S, const rsmi_fenc_packet *pk,
                  int64_t npk, int32_t *out_len, uint8_t *dst, const int64_t *dst_off, uint64_t seed,
-                 hipStream_t s) {
+                 hipStream_t s, bool prex) {
     CookArgs a{};
+    a.prex = prex ? 1 : 0;
     a.base = slots;
     a.dst = dst;
     a.dst_off = dst_off;

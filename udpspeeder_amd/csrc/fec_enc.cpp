@@ -177,6 +177,10 @@ struct rsmi_fenc {
     size_t plan_cap = 0;
     uint8_t *dshadow = nullptr;  // kBlobBufBytes, zeroed at the first run
     uint8_t *dcarry[2] = {nullptr, nullptr};
+    rsmi::EpiRec *depi = nullptr;  // parity cook in the encoder's epilogue: one record per slot
+    size_t epi_cap = 0;            // records
+    uint32_t epi_tag = 0;          // this encoder's runs' tags (records of older runs never match)
+    int64_t last_epi_runs = 0;     // encoder runs of the last run_dev that cooked their parity
     size_t carry_cap[2] = {0, 0};
     int carry_cur = 0;  // pending packets live in dcarry[carry_cur] (or the batch input)
     size_t carry_need = 0;  // bytes of dcarry[carry_cur] the last plan fills
@@ -402,6 +406,13 @@ void close_group(rsmi_fenc *E, int k, int m, int fec_len) {
         if (!extend) E->runs.push_back(Run{slot0, 0, k, n, fec_len});
         E->runs.back().count += 1;
     }
+    // the group's encoder run (pad[0..1]; the cooked run sets pad[2] when that
+    // run cooks its parity in the epilogue)
+    const uint32_t ri = m > 0 ? (uint32_t)(E->runs.size() - 1) : 0xFFFFFFFFu;
+    FrameGroup &J = E->P->jobs[E->P->jobs.size() - 1];
+    J.pad[0] = (uint16_t)ri;
+    J.pad[1] = (uint16_t)(ri >> 16);
+    J.pad[2] = 0;
 }
 
 // Mode 1: the open group's last input goes out as a data packet now; its slot
@@ -615,6 +626,7 @@ void rsmi_fenc_destroy(rsmi_fenc *E) {
     for (PlanSet &B : E->ps) (void)wait_set(B);
     if (E->dplan) (void)hipFree(E->dplan);
     if (E->dshadow) (void)hipFree(E->dshadow);
+    if (E->depi) (void)hipFree(E->depi);
     for (int i = 0; i < 2; ++i)
         if (E->dcarry[i]) (void)hipFree(E->dcarry[i]);
     for (PlanSet &B : E->ps)
@@ -686,6 +698,7 @@ int rsmi_fenc_plan(rsmi_fenc *E, int64_t n_events, const int32_t *len, const uin
         G.mode = 1;
         G.idx0 = (uint8_t)j;
         G.nclean = G.nfr = 1;
+        G.pad[0] = G.pad[1] = 0xFFFF;  // no encoder run
         E->P->srcs.push_back(FrameSrc{p.addr, p.len, 0});
         E->P->jobs.push_back(G);
         E->P->packets[(size_t)p.emitted].slot = slot;
@@ -754,6 +767,8 @@ int rsmi_fenc_run_cooked_dev(rsmi_fenc *E, uint8_t *slots, int64_t S, const rsmi
     const CookSpec ck{ctx, seed, out, out_len, -1};
     return run_dev(E, slots, S, stream, &ck);
 }
+
+int64_t rsmi_fenc_last_parity_cooked(const rsmi_fenc *E) { return E ? E->last_epi_runs : 0; }
 
 int rsmi_fenc_run_cooked_packed_dev(rsmi_fenc *E, uint8_t *slots, int64_t S, const rsmi_cook_ctx *ctx,
                                     uint64_t seed, uint8_t *out, int64_t out_cap, int32_t *out_len,
@@ -887,6 +902,60 @@ int run_dev(rsmi_fenc *E, uint8_t *slots, int64_t S, void *stream, const CookSpe
             return fail(RSMI_ERR_INVALID, "rsmi_fenc_run_cooked_packed_dev: out_cap " + std::to_string(ck->out_cap) +
                                               " < packed bytes " + std::to_string(o));
     }
+    // the parity packets cooked in the encoder's epilogue (RSMI_OPT_PARITY_COOK,
+    // rsmi_internal.hpp EpiRec): a fused run into device memory, every encoder
+    // run on a cooking split-k network
+    bool epi = fuse && !packed && E->P->n_par_pk > 0 && rsmi::parity_cook_enabled();
+    if (epi) {
+        hipPointerAttribute_t at;
+        epi = hipPointerGetAttributes(&at, ck->out) == hipSuccess && at.type == hipMemoryTypeDevice;
+        (void)hipGetLastError();
+    }
+    E->last_epi_runs = 0;
+    // per encoder run: does it have the cooking encoder (its groups' parity
+    // packets are then flagged for k_cook's PREX form through FrameGroup.pad[2])
+    std::vector<uint8_t> run_epi(epi ? E->runs.size() : 0, 0);
+    if (epi) {
+        bool any = false;
+        for (size_t i = 0; i < E->runs.size(); ++i) {
+            const Run &r = E->runs[i];
+            run_epi[i] = rsmi::encode_cooked_ok(r.k, r.n, (int64_t)r.n * S, S, r.len, r.count) ? 1 : 0;
+            any = any || run_epi[i];
+            E->last_epi_runs += run_epi[i];
+        }
+        epi = any;
+    }
+    if (epi) {
+        for (size_t g = 0; g < E->P->jobs.size(); ++g) {
+            FrameGroup &J = E->P->jobs[g];
+            const uint32_t ri = (uint32_t)J.pad[0] | (uint32_t)J.pad[1] << 16;
+            J.pad[2] = ri < run_epi.size() ? run_epi[ri] : 0;
+        }
+    }
+    if (epi) {
+        // records are zero when allocated and carry the tag of the run that
+        // wrote them, so a slot this run does not cook never matches
+        const bool wrap = E->epi_tag == 0xFFFFFFFFu;
+        if ((size_t)E->n_slots > E->epi_cap || wrap) {
+            int rcw = wait_set(prev);
+            if (rcw) return rcw;
+            if ((size_t)E->n_slots > E->epi_cap) {
+                if (E->depi) (void)hipFree(E->depi);
+                E->depi = nullptr;
+                E->epi_cap = 0;
+                const size_t cap = (size_t)E->n_slots + (size_t)E->n_slots / 4;
+                if (hipMalloc(&E->depi, cap * sizeof(rsmi::EpiRec)) != hipSuccess)
+                    return fail(RSMI_ERR_NOMEM, "fenc: hipMalloc(epilogue records)");
+                E->epi_cap = cap;
+            }
+            if (hipMemsetAsync(E->depi, 0, E->epi_cap * sizeof(rsmi::EpiRec), s) != hipSuccess)
+                return fail(RSMI_ERR_HIP, "fenc: clear epilogue records");
+            if (wrap) E->epi_tag = 0;
+        }
+        ++E->epi_tag;
+    }
+    const rsmi::EpiArgs epa{epi ? E->depi : nullptr, epi ? ck->out : nullptr, ck ? ck->seed : 0, E->epi_tag,
+                            ck && !(rsmi::cook_ctx_flags(ck->ctx) & RSMI_COOK_NO_OBSCURE) ? 1 : 0};
     const uint32_t *zrec = fuse ? mapped(E->P->recs) : nullptr;  // read in place by k_cook_frame
     const size_t db = packed ? npk * sizeof(int64_t) : 0, jb = fuse ? (size_t)na * 2 * sizeof(int32_t) : 0;
     const size_t go = 0, so = (gb + 255) & ~size_t(255), co = (so + sb + 255) & ~size_t(255),
@@ -918,7 +987,7 @@ int run_dev(rsmi_fenc *E, uint8_t *slots, int64_t S, void *stream, const CookSpe
                                         reinterpret_cast<rsmi_fenc_packet *>(E->dplan + xo) + na,
                                         packed ? reinterpret_cast<int64_t *>(E->dplan + dq) : nullptr,
                                         fuse ? reinterpret_cast<int32_t *>(E->dplan + jo) : nullptr, s,
-                                        reinterpret_cast<const FrameGroup *>(E->dplan + go), slots, S);
+                                        reinterpret_cast<const FrameGroup *>(E->dplan + go), slots, S, epa);
     if (e == hipSuccess && fuse && !zrec)
         e = hipMemcpyAsync(reinterpret_cast<uint32_t *>(E->dplan + jo) + na, E->P->recs.p, (size_t)na * 4,
                            hipMemcpyHostToDevice, s);
@@ -945,12 +1014,19 @@ int run_dev(rsmi_fenc *E, uint8_t *slots, int64_t S, void *stream, const CookSpe
                                    (int64_t)E->P->stale.size(), slots, S, E->dshadow, s);
     if (e != hipSuccess) return fail(RSMI_ERR_HIP, std::string("fenc frame: ") + hipGetErrorString(e));
     // parity of every group
-    for (const Run &r : E->runs) {
-        rc = rsmi_encode_dev(r.k, r.n, slots + r.slot0 * S + rsmi::kSlotShard, (int64_t)r.n * S, S,
-                             r.len, r.count, stream);
+    for (size_t ri = 0; ri < E->runs.size(); ++ri) {
+        const Run &r = E->runs[ri];
+        const int64_t so = r.slot0 * S + rsmi::kSlotShard;
+        if (epi && run_epi[ri]) {
+            const rsmi::CookEpi ce{ck->out + so, E->depi + r.slot0, rsmi::cook_ctx_ks(ck->ctx), E->epi_tag,
+                                   (uint32_t)r.n};
+            rc = rsmi::encode_dev_cooked(r.k, r.n, slots + so, (int64_t)r.n * S, S, r.len, r.count, ce, s);
+        } else {
+            rc = rsmi_encode_dev(r.k, r.n, slots + so, (int64_t)r.n * S, S, r.len, r.count, stream);
+        }
         if (rc) return rc;
     }
-    ht.mark("encode");
+    ht.mark(epi ? "encode+parity cook" : "encode");
     // the blob buffer as this batch leaves it (read by the next batch's stale runs)
     e = rsmi::launch_byte_runs(reinterpret_cast<const rsmi::ByteRun *>(E->dplan + uo),
                                (int64_t)E->P->shadow_upd.size(), slots, S, E->dshadow, s);
@@ -964,7 +1040,8 @@ int run_dev(rsmi_fenc *E, uint8_t *slots, int64_t S, void *stream, const CookSpe
     // stream beside the encoder measured no faster: the two kernels slow each
     // other down)
     if (nlist > na) {
-        rc = rsmi::cook_packets(ck->ctx, slots, S, lists + na, nlist - na, ck->out_len, ck->out, doff, ck->seed, s);
+        rc = rsmi::cook_packets(ck->ctx, slots, S, lists + na, nlist - na, ck->out_len, ck->out, doff, ck->seed, s,
+                                epi);
         if (rc) return rc;
         ht.mark("tail+cook");
     }

@@ -315,11 +315,56 @@ __global__ __launch_bounds__(kThreads) void k_byte_runs(const ByteRun *runs, int
 // with their jobs in job_a) and B (packets [ndata, count)), and the parity
 // packets' 8-byte headers (fec_manager.cpp:318-333), which k_frame may not be
 // run to write.  With dst_off, also each packet's offset in the packed output.
+// k_cook's IV draw (cook.hip splitmix): word w of packet i's stream.
+__device__ __forceinline__ uint64_t iv_draw(uint64_t seed, uint64_t idx, uint64_t w) {
+    uint64_t z = (seed ^ idx) + (w + 1) * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+// A parity packet cooked in the encoder's epilogue: its record (the IV k_cook
+// would draw for batch index gi, repeated to 48 bytes) and its header in the
+// output's header piece, where k_cook's PREX form reads the packet.
+__device__ void write_epi(const EpiArgs &ep, int64_t slot, int64_t gi, int32_t len, uint8_t *hdr_out,
+                          u32x2 hdr) {
+    EpiRec *r = ep.rec + slot;
+    uint32_t ivl = 0, magic = 0;
+    uint64_t z[4] = {0, 0, 0, 0};
+    if (ep.obs) {
+        ivl = 4u + (uint32_t)(iv_draw(ep.seed, (uint64_t)gi, 0) % 29u);
+        magic = 0xFFFFFFFFu / ivl;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) z[w] = 8 * w < (int)ivl ? iv_draw(ep.seed, (uint64_t)gi, 1 + (uint64_t)w) : 0;
+    }
+    uint32_t iv[12];
+    uint32_t t8 = 0;  // t % ivl
+#pragma unroll
+    for (int d = 0; d < 12; ++d) {
+        uint32_t v = 0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const uint32_t w = t8 >> 3;
+            const uint64_t zw = w == 0 ? z[0] : w == 1 ? z[1] : w == 2 ? z[2] : z[3];
+            v |= (uint32_t)((zw >> (8 * (t8 & 7))) & 0xffu) << (8 * b);
+            t8 = (ivl && t8 + 1 >= ivl) ? 0 : t8 + 1;
+        }
+        iv[d] = v;
+    }
+    typedef uint32_t v4 __attribute__((ext_vector_type(4)));
+    v4 *rv = reinterpret_cast<v4 *>(r);
+    rv[0] = v4{ep.tag, (uint32_t)len | ivl << 16, magic, 0u};
+    rv[1] = v4{iv[0], iv[1], iv[2], iv[3]};
+    rv[2] = v4{iv[4], iv[5], iv[6], iv[7]};
+    rv[3] = v4{iv[8], iv[9], iv[10], iv[11]};
+    *reinterpret_cast<u32x2 *>(hdr_out) = hdr;
+}
+
 __global__ __launch_bounds__(kThreads) void k_expand_packets(const PacketRun *runs, int64_t nruns,
                                                               rsmi_fenc_packet *pk_a, rsmi_fenc_packet *pk_b,
                                                               int64_t *dst_off, int32_t *job_a,
                                                               const FrameGroup *groups, uint8_t *slots,
-                                                              int64_t slot_stride) {
+                                                              int64_t slot_stride, EpiArgs ep) {
     const int lane = threadIdx.x & 63;
     const int64_t w0 = (int64_t)blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
     for (int64_t w = w0; w < nruns; w += (int64_t)gridDim.x * (kThreads / 64)) {
@@ -333,7 +378,7 @@ __global__ __launch_bounds__(kThreads) void k_expand_packets(const PacketRun *ru
                     pk_a[R.afirst + c] = p;
                     job_a[R.afirst + c] = R.job;
                 }
-                if (c >= (int)R.ndata) pk_b[R.bfirst + c - (int)R.ndata] = p;
+                if (c >= (int)R.ndata) pk_b[R.bfirst + c - (int)R.ndata] = p;  // (flagged below)
             }
             if (dst_off) dst_off[R.first + c] = R.out0 + (int64_t)c * RSMI_FEC_COOK_SPAN(R.len);
             if (job_a) {
@@ -342,8 +387,14 @@ __global__ __launch_bounds__(kThreads) void k_expand_packets(const PacketRun *ru
                 if (j >= G.nframe) {  // a parity packet: seq | mode | k | m | index
                     const uint32_t w1 = (uint32_t)G.mode | ((uint32_t)G.k << 8 | (uint32_t)G.m << 16) |
                                         ((G.idx0 + j) & 0xffu) << 24;
-                    *reinterpret_cast<u32x2 *>(slots + (R.slot + c) * slot_stride + kSlotHeader) =
-                        u32x2{bswap32(G.seq), w1};
+                    const u32x2 hdr{bswap32(G.seq), w1};
+                    if (ep.rec && G.pad[2] && c >= (int)R.ndata) {  // cooked by the encoder: header to the output
+                        write_epi(ep, R.slot + c, p.event, p.len,
+                                  ep.out + (R.slot + c) * slot_stride + kSlotHeader, hdr);
+                        pk_b[R.bfirst + c - (int)R.ndata].len = p.len | kPrexFlag;
+                    } else {
+                        *reinterpret_cast<u32x2 *>(slots + (R.slot + c) * slot_stride + kSlotHeader) = hdr;
+                    }
                 }
             }
         }
@@ -354,12 +405,12 @@ __global__ __launch_bounds__(kThreads) void k_expand_packets(const PacketRun *ru
 
 hipError_t launch_expand_packets(const PacketRun *runs, int64_t nruns, rsmi_fenc_packet *pk_a,
                                  rsmi_fenc_packet *pk_b, int64_t *dst_off, int32_t *job_a, hipStream_t s,
-                                 const FrameGroup *groups, uint8_t *slots, int64_t slot_stride) {
+                                 const FrameGroup *groups, uint8_t *slots, int64_t slot_stride, EpiArgs epi) {
     if (nruns <= 0) return hipSuccess;
     int64_t blocks = (nruns + kThreads / 64 - 1) / (kThreads / 64);
     if (blocks > 8192) blocks = 8192;
     k_expand_packets<<<(unsigned)blocks, kThreads, 0, s>>>(runs, nruns, pk_a, pk_b, dst_off, job_a, groups,
-                                                           slots, slot_stride);
+                                                           slots, slot_stride, epi);
     return hipGetLastError();
 }
 

@@ -382,6 +382,32 @@ __global__ __launch_bounds__(256) void k_fill_ragged(const rsmi_group *groups, i
     }
 }
 
+// ---- measured copy peak (bench.py's hbm_copy_peak) ---------------------------
+// Each thread moves U 16-byte words spaced one block-width apart (coalesced,
+// every load issued before the first store); NT: nontemporal loads and stores.
+// nbytes % 16 == 0; the tail block checks each word.
+typedef uint32_t cp_word __attribute__((ext_vector_type(4)));
+
+template <int U, bool NT>
+__global__ __launch_bounds__(256) void k_copy_peak(cp_word *__restrict__ dst, const cp_word *__restrict__ src,
+                                                   int64_t nwords) {
+    const int64_t w0 = (int64_t)blockIdx.x * (256 * U) + threadIdx.x;
+    cp_word v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int64_t w = w0 + u * 256;
+        if (w < nwords) v[u] = NT ? __builtin_nontemporal_load(src + w) : src[w];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int64_t w = w0 + u * 256;
+        if (w < nwords) {
+            if (NT) __builtin_nontemporal_store(v[u], dst + w);
+            else dst[w] = v[u];
+        }
+    }
+}
+
 int grid_for(int64_t waves) {
     int64_t blocks = (waves + 3) / 4;
     const int64_t cap = 256 * 8;  // ~8 resident 256-thread blocks per CU
@@ -434,6 +460,21 @@ hipError_t launch_decode_ref_move(const UniformArgs &a, const uint8_t *plans, co
     int64_t grid = a.ngroups < 256 * 16 ? a.ngroups : 256 * 16;
     if (grid < 1) grid = 1;
     k_decode_ref_move<<<(int)grid, 64, 0, s>>>(a, plans, present, slot_map);
+    return hipGetLastError();
+}
+
+hipError_t launch_copy_peak(uint8_t *dst, const uint8_t *src, int64_t nbytes, int variant, hipStream_t s) {
+    const int64_t nw = nbytes / 16;
+    const int U = (variant & 1) ? 8 : 4;
+    const int64_t grid = (nw + 256 * U - 1) / (256 * U);
+    auto d = reinterpret_cast<cp_word *>(dst);
+    auto r = reinterpret_cast<const cp_word *>(src);
+    switch (variant) {
+        case 0: k_copy_peak<4, false><<<(unsigned)grid, 256, 0, s>>>(d, r, nw); break;
+        case 1: k_copy_peak<8, false><<<(unsigned)grid, 256, 0, s>>>(d, r, nw); break;
+        case 2: k_copy_peak<4, true><<<(unsigned)grid, 256, 0, s>>>(d, r, nw); break;
+        default: k_copy_peak<8, true><<<(unsigned)grid, 256, 0, s>>>(d, r, nw); break;
+    }
     return hipGetLastError();
 }
 

@@ -63,6 +63,7 @@ hipError_t launch_encode_ragged(const rsmi_group *groups, int64_t ngroups, uint8
 // (rsmi_decode_dev_ref); present is the call's [ngroups][n] flags.
 hipError_t launch_decode_ref_move(const UniformArgs &a, const uint8_t *plans, const uint8_t *present,
                                   uint8_t *slot_map, hipStream_t s);
+hipError_t launch_copy_peak(uint8_t *dst, const uint8_t *src, int64_t nbytes, int variant, hipStream_t s);
 hipError_t launch_fill_data(int k, int len, uint8_t *base, int64_t group_stride,
                             int64_t shard_stride, int64_t g0, int64_t ngroups, uint64_t seed,
                             hipStream_t s);
@@ -293,6 +294,7 @@ struct CookArgs {
     uint64_t seed;
     const uint32_t *tabs;        // device CRC blob
     const uint8_t *ks;           // device key stream, NULL when there is no XOR stage
+    int32_t prex;                // cook only: entries with kPrexFlag were cooked by the encoder
 };
 size_t cook_lds_bytes(bool decook);
 // do_cook over an FEC packet list (rsmi_fenc_run_cooked_dev): packet p at
@@ -300,9 +302,13 @@ size_t cook_lds_bytes(bool decook);
 // cook list of k_expand_packets: pk[p].event = the packet's index i in the
 // batch); output at the same offset of dst (NULL: in place) or at dst +
 // dst_off[i], out_len[i], IVs drawn on the device from (seed, i) (cook_host.cpp).
+int cook_ctx_flags(const rsmi_cook_ctx *ctx);
+const uint8_t *cook_ctx_ks(const rsmi_cook_ctx *ctx);  // key stream at packet offset 0 (zeros: no XOR)
+// prex: list entries flagged kPrexFlag had their body cooked by the encoder's
+// epilogue into dst (EpiRec above).
 int cook_packets(const rsmi_cook_ctx *ctx, uint8_t *slots, int64_t S, const rsmi_fenc_packet *pk,
                  int64_t npk, int32_t *out_len, uint8_t *dst, const int64_t *dst_off, uint64_t seed,
-                 hipStream_t s);
+                 hipStream_t s, bool prex = false);
 hipError_t launch_cook(const CookArgs &a, bool decook, int max_blocks, hipStream_t s);
 
 
@@ -324,7 +330,8 @@ struct FrameGroup {
     // the fused framing cook (k_cook_frame) frames data shards cfirst..nfr-1
     // (packets emitted in this batch, at most kFuseRecs source records each)
     // and cooks cfirst..nclean-1 (no stale blob bytes: final once framed)
-    uint16_t cfirst, nclean, nfr, pad[3];
+    uint16_t cfirst, nclean, nfr;
+    uint16_t pad[3];    // the planner's: [0..1] its encoder run, [2] that run cooks parity in its epilogue
 };
 // A payload address in a plan: a device address, or (kCarryTag set) an offset
 // into carry buffer 0 or 1 (kCarryBuf1), resolved by the kernels.
@@ -410,10 +417,53 @@ struct PacketRun {
 };
 // job_a (optional, the fused run): list A's entries' jobs; then the parity
 // packets' headers are written too (groups: the plan's; slots, slot_stride).
+// ---- the parity packets cooked in the encoder's epilogue (RSMI_OPT_PARITY_COOK) ----
+// A fused cooked run normally has the encoder write the parity shards plain
+// into their slots and k_cook read them back.  With the epilogue, the encoder
+// (k_bs2c_<k>_<n>) stores every whole 16-byte payload piece of a parity packet
+// already obscured and keyed (the piece XOR its IV and key-stream windows)
+// into the output, and the rest of the packet's pieces (the partial last one
+// and any line padding) plain into the output; k_cook's PREX form then reads
+// the packet back from the output, recovers the plain bytes for the CRC, and
+// writes only the header piece and the tail (crc / IV / iv_len).  The parity
+// slots are never written.  k_expand_packets fills one record per parity slot
+// with what the encoder needs, and flags those packets' list-B entries
+// (kPrexFlag in len).
+struct EpiRec {
+    uint32_t tag;    // the run's tag: records of other runs (or never written) do not match
+    uint32_t meta;   // packet length (header included) | iv_len << 16 (0: no obscure stage)
+    uint32_t magic;  // 0xFFFFFFFF / iv_len (mod by multiply-high, as k_cook)
+    uint32_t pad;
+    uint32_t iv[12]; // the IV repeated: byte t = iv[t % iv_len], t < 48
+};
+static_assert(sizeof(EpiRec) == 64, "EpiRec is one 64-byte record per slot");
+constexpr int32_t kPrexFlag = 1 << 30;  // list-B entry len: the encoder cooked its body
+struct EpiArgs {     // k_expand_packets' side (rec == nullptr: no epilogue)
+    EpiRec *rec;     // indexed by slot
+    uint8_t *out;    // the cooked output (slot geometry): parity headers go there too
+    uint64_t seed;   // the run's IV seed (the draw k_cook would make)
+    uint32_t tag;
+    int32_t obs;     // the obscure stage is on
+};
+struct CookEpi {     // the encoder's side, per encoder run
+    uint8_t *out;    // the run's shard base in the output (the slots' base + (out - slots))
+    const EpiRec *rec;  // records of the run's first slot
+    const uint8_t *ks;  // key stream at packet offset 0 (zeros without an XOR stage; never NULL)
+    uint32_t tag, n;    // slots per group
+};
 hipError_t launch_expand_packets(const PacketRun *runs, int64_t nruns, rsmi_fenc_packet *pk_a,
                                  rsmi_fenc_packet *pk_b, int64_t *dst_off, int32_t *job_a, hipStream_t s,
                                  const FrameGroup *groups = nullptr, uint8_t *slots = nullptr,
-                                 int64_t slot_stride = 0);
+                                 int64_t slot_stride = 0, EpiArgs epi = EpiArgs{nullptr, nullptr, 0, 0, 0});
+// The cooking split-k encoder exists for (k, n) and this geometry (the
+// checks launch_encode_bitslice_cooked makes).
+bool bitslice_cooked_ok(const UniformArgs &a);
+hipError_t launch_encode_bitslice_cooked(const UniformArgs &a, const CookEpi &e, hipStream_t s);
+// encode_dev's checks and code setup, then the cooking encoder (api.cpp).
+bool encode_cooked_ok(int k, int n, int64_t gs, int64_t ss, int len, int64_t ngroups);
+int encode_dev_cooked(int k, int n, uint8_t *base, int64_t gs, int64_t ss, int len, int64_t ngroups,
+                      const CookEpi &e, hipStream_t s);
+bool parity_cook_enabled();
 // The fused framing cook (k_cook_frame): list A's packets are data packets of
 // clean shards (FrameGroup.nclean), framed from their source records into
 // their slots (for the encoder) and cooked into the output in the same pass.

@@ -173,6 +173,12 @@ class FecEncoder:
               "rsmi_fenc_run_cooked_dev")
         return out_len
 
+    def last_parity_cooked(self) -> int:
+        """Encoder runs of the last cooked run whose parity packets were cooked
+        in the encoder's epilogue (RSMI_OPT_PARITY_COOK) --
+        rsmi_fenc_last_parity_cooked."""
+        return int(lib().rsmi_fenc_last_parity_cooked(self._h))
+
     RUN_DTYPE = np.dtype([("slot", np.int64), ("out0", np.int64), ("first", np.int32),
                           ("afirst", np.int32), ("bfirst", np.int32), ("len", np.int32),
                           ("job", np.int32), ("count", np.uint16), ("ndata", np.uint16),
