@@ -16,6 +16,9 @@
 #ifndef BS_PERSIST
 #define BS_PERSIST 0  // 1: balanced persistent grid (measured 5 % slower than one wave per chunk)
 #endif
+#ifndef BS_RAG_SPLIT
+#define BS_RAG_SPLIT 1  // ragged plans run the buckets of split-k codes in the 2-wave form
+#endif
 #ifndef BS_COOK_EPI
 #define BS_COOK_EPI 1  // build the cooking split-k encoders (k_bs2c_*, RSMI_OPT_PARITY_COOK)
 #endif
@@ -204,7 +207,73 @@ __global__ __launch_bounds__(256, BS_OCC) void k_bs_ragged(const BsGroup *groups
 #endif
 }
 
+// Position of (k, n) in the generated code list (compile time).
+constexpr int bs_code_idx(int k, int n) {
+    int i = 0;
+#define BS_IDX_C(K, N)                  \
+    if (k == K && n == N) return i;     \
+    ++i;
+    BS_FOR_EACH_CODE(BS_IDX_C)
+#undef BS_IDX_C
+    return -1;
+}
+#define BS_SPLIT_IN_LIST(K, N) static_assert(bs_code_idx(K, N) >= 0, "split code without a one-wave network");
+BS_FOR_EACH_SPLIT(BS_SPLIT_IN_LIST)
+#undef BS_SPLIT_IN_LIST
+
+// Ragged launch with the split-k form for the buckets that have one (BS_RAG_SPLIT):
+// 2-wave blocks; block b < nsplit runs wave record b split-k (the two waves
+// share its 128 columns, half the data shards each, as k_bs2_*), the blocks
+// after it run two one-wave records each (no barrier there).  The plan lists
+// the split buckets' records first.
+__global__ __launch_bounds__(128, BS_OCC) void k_bs_ragged_split(const BsGroup *groups, const uint32_t *colmap,
+                                                                 const uint32_t *waves, uint32_t nsplit,
+                                                                 uint32_t nwaves, uint8_t *base, uint32_t bytes) {
+    __shared__ bs_u32x4 xch[2][2 * 5][64];
+    const uint32_t b = blockIdx.x;
+    const uint32_t h = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t w = b < nsplit ? b : nsplit + 2u * (b - nsplit) + h;
+    if (w >= nwaves) return;  // (a one-wave block's second wave only: no barrier follows)
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t code = __builtin_amdgcn_readfirstlane(waves[2 * w]);
+    const uint32_t c0 = __builtin_amdgcn_readfirstlane(waves[2 * w + 1]) + lane;
+    RagIO io;
+    io.rsrc = __builtin_amdgcn_make_buffer_rsrc(base, 0, (int)bytes, 0x00020000);
+    bs_rag_lane(groups, colmap[c0], io.o0, io.ss0);
+    bs_rag_lane(groups, colmap[c0 + 64], io.o1, io.ss1);
+    if (b < nsplit) {
+        BsXch x{xch[h], xch[h ^ 1u]};
+        switch (code) {
+#define BS_RAG_SPLIT_CASE(K, N)                  \
+    case (uint32_t)bs_code_idx(K, N):            \
+        bs_split_##K##_##N(io, h, x);            \
+        return;
+            BS_FOR_EACH_SPLIT(BS_RAG_SPLIT_CASE)
+#undef BS_RAG_SPLIT_CASE
+            default: return;
+        }
+    }
+    int idx = 0;
+#define BS_RAG_CASE(K, N)              \
+    if (code == (uint32_t)idx) {       \
+        bs_code_##K##_##N(io);         \
+        return;                        \
+    }                                  \
+    ++idx;
+    BS_FOR_EACH_CODE(BS_RAG_CASE)
+#undef BS_RAG_CASE
+}
+
 }  // namespace
+
+bool bitslice_has_split(int k, int n) {
+    switch (k * 257 + n) {
+#define BS_CASE(K, N) case K * 257 + N: return BS_RAG_SPLIT != 0;
+        BS_FOR_EACH_SPLIT(BS_CASE)
+#undef BS_CASE
+        default: return false;
+    }
+}
 
 int bitslice_code_index(int k, int n) {
     int idx = 0;
@@ -240,8 +309,14 @@ int bitslice_code_n(int i) {
 
 hipError_t launch_encode_bitslice_ragged(const rsmi_group *groups, const uint32_t *colmap,
                                          const uint32_t *waves, uint32_t nwaves, uint8_t *base,
-                                         uint32_t bytes, hipStream_t s) {
+                                         uint32_t bytes, hipStream_t s, uint32_t nsplit) {
     if (nwaves == 0) return hipSuccess;
+    if (BS_RAG_SPLIT && nsplit > 0) {
+        const uint32_t blocks = nsplit + (nwaves - nsplit + 1) / 2;
+        k_bs_ragged_split<<<blocks, 128, 0, s>>>(reinterpret_cast<const BsGroup *>(groups), colmap, waves,
+                                                 nsplit, nwaves, base, bytes);
+        return hipGetLastError();
+    }
     uint32_t blocks = (nwaves + 3) / 4;
     if (BS_RAG_XCD) blocks = (blocks + 7) & ~7u;  // whole rounds of 8 XCDs (the remap)
     if (BS_RAG_PERSIST && blocks > 256u * BS_RAG_PERSIST) blocks = 256u * BS_RAG_PERSIST;
