@@ -17,7 +17,11 @@
 #define BS_PERSIST 0  // 1: balanced persistent grid (measured 5 % slower than one wave per chunk)
 #endif
 #ifndef BS_RAG_SPLIT
-#define BS_RAG_SPLIT 1  // ragged plans run the buckets of split-k codes in the 2-wave form
+#define BS_RAG_SPLIT 0  // 1: ragged plans run the buckets of split-k codes in the 2-wave form
+                        // (k_bs_ragged_split).  Round 6 (profiles/r06/ragsplit/): C3 encode
+                        // 0.177 ms against 0.166 one wave per record -- both waves repeat the
+                        // record's column-map and group loads, and the exchange adds a barrier
+                        // per chunk, which the uniform C1 launch (one descriptor) does not pay
 #endif
 #ifndef BS_COOK_EPI
 #define BS_COOK_EPI 1  // build the cooking split-k encoders (k_bs2c_*, RSMI_OPT_PARITY_COOK)
@@ -221,6 +225,7 @@ constexpr int bs_code_idx(int k, int n) {
 BS_FOR_EACH_SPLIT(BS_SPLIT_IN_LIST)
 #undef BS_SPLIT_IN_LIST
 
+#if BS_RAG_SPLIT
 // Ragged launch with the split-k form for the buckets that have one (BS_RAG_SPLIT):
 // 2-wave blocks; block b < nsplit runs wave record b split-k (the two waves
 // share its 128 columns, half the data shards each, as k_bs2_*), the blocks
@@ -263,6 +268,7 @@ __global__ __launch_bounds__(128, BS_OCC) void k_bs_ragged_split(const BsGroup *
     BS_FOR_EACH_CODE(BS_RAG_CASE)
 #undef BS_RAG_CASE
 }
+#endif
 
 }  // namespace
 
@@ -311,12 +317,16 @@ hipError_t launch_encode_bitslice_ragged(const rsmi_group *groups, const uint32_
                                          const uint32_t *waves, uint32_t nwaves, uint8_t *base,
                                          uint32_t bytes, hipStream_t s, uint32_t nsplit) {
     if (nwaves == 0) return hipSuccess;
-    if (BS_RAG_SPLIT && nsplit > 0) {
+#if BS_RAG_SPLIT
+    if (nsplit > 0) {
         const uint32_t blocks = nsplit + (nwaves - nsplit + 1) / 2;
         k_bs_ragged_split<<<blocks, 128, 0, s>>>(reinterpret_cast<const BsGroup *>(groups), colmap, waves,
                                                  nsplit, nwaves, base, bytes);
         return hipGetLastError();
     }
+#else
+    (void)nsplit;
+#endif
     uint32_t blocks = (nwaves + 3) / 4;
     if (BS_RAG_XCD) blocks = (blocks + 7) & ~7u;  // whole rounds of 8 XCDs (the remap)
     if (BS_RAG_PERSIST && blocks > 256u * BS_RAG_PERSIST) blocks = 256u * BS_RAG_PERSIST;
