@@ -248,8 +248,10 @@ def main():
             workload = (f"C4: RS(20,10) encode + decode (5 random erasures), 1250-B shards, "
                         f"{total_groups} groups split over {world} GPU(s), device-resident")
         if copy_peak:
-            for r in roof.values():  # the same achieved rate against the measured copy
+            for which, r in roof.items():  # the same achieved rate against the measured copy / mix
                 r["frac_of_copy_peak"] = round(r["achieved"] / copy_peak["GBps"], 4)
+                mix = copy_peak["mixes_GBps"]["2:1 (encode)" if which == "encode" else "6:1 (decode)"]
+                r["frac_of_mix_peak"] = round(r["achieved"] / mix, 4)
         line = {
             "metric": METRIC, "value": round(value, 2), "unit": "GiB/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup,
@@ -578,11 +580,21 @@ def hbm_copy_peak(u, torch, dev, nbytes=2 << 30, reps=8):
                                        "rsmi_copy_peak"))
     assert torch.equal(a[:1 << 20], b[:1 << 20]) and torch.equal(a[-(1 << 20):], b[-(1 << 20):])
     got["torch_copy_"] = rate(lambda: b.copy_(a))
+    # read:write mixes of the codec kernels (rsmi_copy_peak variants 4-6):
+    # bytes read + written per second
+    a.random_(0, 256)
+    nr = nbytes // (16 * 256 * 24) * (16 * 256 * 24)
+    mixes = {}
+    for v, name, wfrac in [(4, "read_only", 0.0), (5, "2:1 (encode)", 0.5), (6, "6:1 (decode)", 1 / 6)]:
+        r = rate(lambda: check(L.rsmi_copy_peak(b.data_ptr(), a.data_ptr(), nr, v,
+                                                torch.cuda.current_stream().cuda_stream), "rsmi_copy_peak"))
+        mixes[name] = round(r / 2 * nr * (1 + wfrac) / nbytes, 1)  # rate() counted 2 * nbytes
     del a, b
     best = max(got, key=got.get)
     return {"GBps": got[best], "best": best, "variants_GBps": got, "bytes_each_way": nbytes,
+            "mixes_GBps": mixes,
             "how": "device-to-device copy of 2 GiB (read + write bytes / time), median of 8 after 2 warm, "
-                   "best variant"}
+                   "best variant; mixes: the same for kernels that read 2 GiB and write none, half, a sixth"}
 
 
 def roofline(which, kernel, alg_bytes, ms, G):

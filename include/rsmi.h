@@ -422,7 +422,11 @@ int rsmi_fill_ragged(const rsmi_group *dev_groups, int64_t ngroups, uint8_t *bas
  * aligned, not overlapping): bench.py's measured HBM copy peak, the line the
  * codec kernels' achieved rates are read against besides the 8 TB/s spec.
  * variant: 0 / 1 = 4 / 8 16-byte words per thread, 2 / 3 = the same with
- * nontemporal loads and stores.  No reference counterpart. */
+ * nontemporal loads and stores.  Variants 4-6 are read:write mixes that read
+ * nbytes (a multiple of 16 * 256 * 24) from src and write a share of it to
+ * dst: 4 = read only (nothing written), 5 = 2:1 (the encoders' mix: nbytes / 2
+ * written), 6 = 6:1 (the decode's mix: nbytes / 6 written).  No reference
+ * counterpart. */
 int rsmi_copy_peak(uint8_t *dst, const uint8_t *src, int64_t nbytes, int variant, void *stream);
 
 #ifdef __cplusplus

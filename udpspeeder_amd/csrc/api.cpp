@@ -1720,7 +1720,8 @@ int rsmi_fill_ragged(const rsmi_group *groups, int64_t ngroups, uint8_t *base, i
 }
 
 int rsmi_copy_peak(uint8_t *dst, const uint8_t *src, int64_t nbytes, int variant, void *stream) {
-    if (nbytes < 0 || nbytes % 16 || variant < 0 || variant > 3 || ((uintptr_t)dst | (uintptr_t)src) % 16 ||
+    if (nbytes < 0 || nbytes % 16 || variant < 0 || variant > 6 || ((uintptr_t)dst | (uintptr_t)src) % 16 ||
+        (variant >= 4 && nbytes % (16 * 256 * 24)) ||
         (nbytes > 0 && (!dst || !src)) || nbytes / 16 / (256 * 4) >= 0x7FFFFFFF) {
         rsmi::set_error("invalid copy_peak arguments");
         return RSMI_ERR_INVALID;

@@ -408,6 +408,35 @@ __global__ __launch_bounds__(256) void k_copy_peak(cp_word *__restrict__ dst, co
     }
 }
 
+// Read:write mixes (bench.py's hbm_mix_peaks): each thread reads R 16-byte
+// words, block-strided (coalesced), and writes W words, each the XOR of a
+// share of what it read (W = 0: nothing is written unless the XOR of all R
+// words is the sentinel, which synthetic input never holds).  Whole blocks
+// only (the host rounds the read size down).
+template <int R, int W>
+__global__ __launch_bounds__(256) void k_mix_peak(cp_word *__restrict__ dst, const cp_word *__restrict__ src) {
+    const int64_t r0 = (int64_t)blockIdx.x * (256 * R) + threadIdx.x;
+    cp_word v[R];
+#pragma unroll
+    for (int u = 0; u < R; ++u) v[u] = src[r0 + u * 256];
+    if (W == 0) {
+        cp_word x = v[0];
+#pragma unroll
+        for (int u = 1; u < R; ++u) x ^= v[u];
+        if (x.x == 0x9E3779B9u && x.y == 0x7F4A7C15u && x.z == 0xF39CC060u && x.w == 0x5CEDC834u)
+            dst[threadIdx.x] = x;
+        return;
+    }
+    const int64_t w0 = (int64_t)blockIdx.x * (256 * W) + threadIdx.x;
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+        cp_word x = v[w];
+#pragma unroll
+        for (int u = w + W; u < R; u += W) x ^= v[u];
+        dst[w0 + w * 256] = x;
+    }
+}
+
 int grid_for(int64_t waves) {
     int64_t blocks = (waves + 3) / 4;
     const int64_t cap = 256 * 8;  // ~8 resident 256-thread blocks per CU
@@ -465,6 +494,16 @@ hipError_t launch_decode_ref_move(const UniformArgs &a, const uint8_t *plans, co
 
 hipError_t launch_copy_peak(uint8_t *dst, const uint8_t *src, int64_t nbytes, int variant, hipStream_t s) {
     const int64_t nw = nbytes / 16;
+    if (variant >= 4) {  // read:write mixes, nbytes read
+        auto d = reinterpret_cast<cp_word *>(dst);
+        auto r = reinterpret_cast<const cp_word *>(src);
+        switch (variant) {
+            case 4: k_mix_peak<8, 0><<<(unsigned)(nw / (256 * 8)), 256, 0, s>>>(d, r); break;
+            case 5: k_mix_peak<8, 4><<<(unsigned)(nw / (256 * 8)), 256, 0, s>>>(d, r); break;
+            default: k_mix_peak<12, 2><<<(unsigned)(nw / (256 * 12)), 256, 0, s>>>(d, r); break;
+        }
+        return hipGetLastError();
+    }
     const int U = (variant & 1) ? 8 : 4;
     const int64_t grid = (nw + 256 * U - 1) / (256 * U);
     auto d = reinterpret_cast<cp_word *>(dst);
