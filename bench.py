@@ -712,8 +712,8 @@ def extra_configs(u, synth, torch, dev, buf, G):
     # the other setting of RSMI_OPT_PARITY_COOK (the parity cooked in the
     # encoder's epilogue), same workload
     from udpspeeder_amd._lib import RSMI_OPT_PARITY_COOK
-    cur = u.lib().rsmi_set_option(RSMI_OPT_PARITY_COOK, 0)
-    u.lib().rsmi_set_option(RSMI_OPT_PARITY_COOK, cur)
+    cur = u.lib().rsmi_option(RSMI_OPT_PARITY_COOK, 0)
+    u.lib().rsmi_option(RSMI_OPT_PARITY_COOK, cur)
     alt = frame_cook_config(torch, dev, parity_cook=not cur)
     out["f1_f2_frame_encode_cook"]["parity_cook_option"] = bool(cur)
     out["f1_f2_frame_encode_cook"]["other_setting"] = {
@@ -866,7 +866,7 @@ def frame_cook_config(torch, dev, groups=65536, reps=4, parity_cook=None):
     from udpspeeder_amd.fec import FecEncoder
     import udpspeeder_amd as u
     from udpspeeder_amd._lib import RSMI_OPT_PARITY_COOK
-    prev = None if parity_cook is None else u.lib().rsmi_set_option(RSMI_OPT_PARITY_COOK, int(parity_cook))
+    prev = None if parity_cook is None else u.lib().rsmi_option(RSMI_OPT_PARITY_COOK, int(parity_cook))
     plen = 1200
     npk = groups * 20
     lens = np.full(npk, plen, np.int32)
@@ -898,7 +898,7 @@ def frame_cook_config(torch, dev, groups=65536, reps=4, parity_cook=None):
     enc.close()
     ctx.close()
     if prev is not None:
-        u.lib().rsmi_set_option(RSMI_OPT_PARITY_COOK, prev)
+        u.lib().rsmi_option(RSMI_OPT_PARITY_COOK, prev)
     del slots, out, inbuf
     return {"datagrams_in": npk, "datagram_len": plen, "groups": groups, "packets_out": nout,
             "run_ms": round(t, 4), "parity_cook_runs": epi, "datagrams_in_per_s": round(npk / (t * 1e-3), 1),
@@ -1055,17 +1055,17 @@ def dropin_latency_both(u):
     and, beside it, the same kernel launched per call and the staged copy
     path (H2D, kernel, D2H, stream sync)."""
     L = u.lib()
-    prev = L.rsmi_set_option(3, 1)
-    prev_srv = L.rsmi_set_option(5, 20000)
+    prev = L.rsmi_option(3, 1)
+    prev_srv = L.rsmi_option(5, 20000)
     try:
         one = dropin_latency(u)
-        L.rsmi_set_option(5, 0)
+        L.rsmi_option(5, 0)
         launched = dropin_latency(u)
-        L.rsmi_set_option(3, 0)
+        L.rsmi_option(3, 0)
         staged = dropin_latency(u)
     finally:
-        L.rsmi_set_option(3, prev)
-        L.rsmi_set_option(5, prev_srv)
+        L.rsmi_option(3, prev)
+        L.rsmi_option(5, prev_srv)
     one["what"] += (": posted to the resident server (oneshot.hip k_one_server), which reads pinned staging "
                     "over PCIe; per-workgroup flags polled")
     one["launch_per_call"] = {"rs_encode2": launched["rs_encode2"], "rs_decode2": launched["rs_decode2"],

@@ -112,7 +112,7 @@ const char *rsmi_last_error(void);
  * encoder.  The cooked bytes are the same either way. */
 #define RSMI_OPT_PARITY_COOK 7
 
-int rsmi_set_option(int option, int value);
+int rsmi_option(int option, int value);
 
 /* Stop the resident one-group server on every device and wait for it to end
  * (the next drop-in call relaunches it).  Call before a device-wide
@@ -367,7 +367,7 @@ int rsmi_last_decode_pinned_path(void);
  * written) or decode (rebuilt data rows in their own slots; present_bits HOST
  * uint32[ngroups * 8] as rsmi_decode_ragged_plan's, status HOST int32[ngroups],
  * may be NULL) -> span D2H on three streams.  Host memory should be pinned.
- * With a device list (rsmi_set_devices) the groups split into contiguous
+ * With a device list (rsmi_use_devices) the groups split into contiguous
  * ranges of near-equal summed n * len, one per listed device.  Synchronous. */
 int rsmi_encode_ragged_pinned(const rsmi_group *groups, int64_t ngroups, uint8_t *host_base,
                               int64_t chunk_groups);
@@ -380,7 +380,7 @@ int rsmi_decode_ragged_pinned(const rsmi_group *groups, int64_t ngroups, uint8_t
  * thread (common.h:112, tunnel_server.cpp:159-196), one FEC manager pair each
  * (connection.h:244-245).  FEC groups are independent, so a host batch splits
  * into contiguous group ranges, one per listed device, with no exchange
- * between them.  After rsmi_set_devices(devs, n) (n >= 1; a device may be
+ * between them.  After rsmi_use_devices(devs, n) (n >= 1; a device may be
  * listed more than once), rsmi_encode_pinned and rsmi_decode_pinned run range
  * i = [G*i/n, G*(i+1)/n) on devs[i] (the ragged host entries: ranges of
  * near-equal summed n * len), each on its own host thread with its own
@@ -398,7 +398,7 @@ int rsmi_decode_ragged_pinned(const rsmi_group *groups, int64_t ngroups, uint8_t
  * of n items into `parts` contiguous ranges: near-equal counts (cost NULL), or
  * near-equal summed cost (the cut before part i is the first item whose prefix
  * sum reaches i/parts of the total), as udpspeeder_amd.shard.balanced_ranges. */
-int rsmi_set_devices(const int32_t *devices, int32_t n);
+int rsmi_use_devices(const int32_t *devices, int32_t n);
 int rsmi_get_devices(int32_t *out, int32_t cap);
 int rsmi_split_ranges(int64_t n, const int64_t *cost, int32_t parts, int64_t *bounds);
 

@@ -74,7 +74,7 @@ void rsmi_fenc_destroy(rsmi_fenc *enc);
 
 /* New parameters, taken up when the next group starts -- the reference's
  * fec_par.clone(g_fec_par) at counter == 0 (fec_manager.cpp:207-209). */
-int rsmi_fenc_set_config(rsmi_fenc *enc, const rsmi_fec_config *cfg);
+int rsmi_fenc_next_config(rsmi_fenc *enc, const rsmi_fec_config *cfg);
 
 /* One emitted packet: output() after input() call `event` returned it. */
 typedef struct rsmi_fenc_packet {

@@ -34,7 +34,7 @@ same = True
 for i in range(REPS + 1):
     ol, plan = {}, None
     for on in ([False, True] if i % 2 == 0 else [True, False]):
-        u.lib().rsmi_set_option(RSMI_OPT_PARITY_COOK, int(on))
+        u.lib().rsmi_option(RSMI_OPT_PARITY_COOK, int(on))
         p = encs[on].plan(lens, offs, inbuf)
         S = FecEncoder.slot_stride_for(int(p.groups["fec_len"].max()))
         if on not in bufs or bufs[on][0].numel() < p.n_slots * S:

@@ -43,12 +43,12 @@ def med(calls=400):
 
 
 res = {}
-L.rsmi_set_option(3, 1)
-L.rsmi_set_option(5, 20000)
+L.rsmi_option(3, 1)
+L.rsmi_option(5, 20000)
 res["server"] = med()
-L.rsmi_set_option(5, 0)
+L.rsmi_option(5, 0)
 res["launch_per_call"] = med()
-L.rsmi_set_option(3, 0)
+L.rsmi_option(3, 0)
 res["staged"] = med()
-L.rsmi_set_option(3, 1)
+L.rsmi_option(3, 1)
 print(json.dumps(res))

@@ -7,7 +7,7 @@ L = u.lib()
 k, n, ln = 20, 30, 1250
 pres = np.ones(n, np.uint8); pres[[1, 4, 9, 22, 27]] = 0
 for life in (8, 10000, 8, 10000):
-    L.rsmi_set_option(6, life)
+    L.rsmi_option(6, life)
     L.rsmi_quiesce()
     d, e = C.c_double(), C.c_double()
     L.rsmi_dropin_latency(1, k, n, ln, pres.ctypes.data, 300, C.byref(d))

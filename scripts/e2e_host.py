@@ -12,7 +12,7 @@ k, n, ln, G, S = 20, 30, 1250, 65536, 1280
 m = n - k
 dev = torch.device("cuda:0")
 # E2E_DEVICES="0,0": the host entry points split over that device list
-# (rsmi_set_devices; one worker thread, streams and pipelines per entry)
+# (rsmi_use_devices; one worker thread, streams and pipelines per entry)
 DEVS = [int(x) for x in os.environ.get("E2E_DEVICES", "").split(",") if x != ""]
 if DEVS:
     u.rs.set_devices(DEVS)

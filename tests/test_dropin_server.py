@@ -40,8 +40,8 @@ def test_server_calls_relaunch_and_stop(gpu, oracle):
     import torch
     import udpspeeder_amd as u
     L = u.lib()
-    prev1 = L.rsmi_set_option(OPT_ONE_GROUP, 1)
-    prev = L.rsmi_set_option(OPT_SERVER, 3000)  # 3 ms idle: relaunches happen below
+    prev1 = L.rsmi_option(OPT_ONE_GROUP, 1)
+    prev = L.rsmi_option(OPT_SERVER, 3000)  # 3 ms idle: relaunches happen below
     try:
         rng = np.random.default_rng(9)
         shapes = [(20, 30, 1250), (3, 6, 3), (10, 16, 900), (1, 2, 1), (20, 30, 17)]
@@ -56,13 +56,13 @@ def test_server_calls_relaunch_and_stop(gpu, oracle):
         assert time.perf_counter() - t0 < 1.0
         # switched off: a running server is stopped, calls launch per call
         _roundtrip(u, oracle, rng, 20, 30, 1250)
-        assert L.rsmi_set_option(OPT_SERVER, 0) == 3000
+        assert L.rsmi_option(OPT_SERVER, 0) == 3000
         _roundtrip(u, oracle, rng, 20, 30, 1250)
-        L.rsmi_set_option(OPT_SERVER, 3000)
+        L.rsmi_option(OPT_SERVER, 3000)
         _roundtrip(u, oracle, rng, 20, 30, 1250)
     finally:
-        L.rsmi_set_option(OPT_SERVER, prev)
-        L.rsmi_set_option(OPT_ONE_GROUP, prev1)
+        L.rsmi_option(OPT_SERVER, prev)
+        L.rsmi_option(OPT_ONE_GROUP, prev1)
 
 
 @pytest.mark.gpu
@@ -88,15 +88,15 @@ def test_server_latency_beats_launch_per_call(gpu):
             ts.append(time.perf_counter() - t0)
         return statistics.median(ts[20:]) * 1e6
 
-    prev1 = L.rsmi_set_option(OPT_ONE_GROUP, 1)
-    prev = L.rsmi_set_option(OPT_SERVER, 20000)
+    prev1 = L.rsmi_option(OPT_ONE_GROUP, 1)
+    prev = L.rsmi_option(OPT_SERVER, 20000)
     try:
         t_srv = med()
-        L.rsmi_set_option(OPT_SERVER, 0)
+        L.rsmi_option(OPT_SERVER, 0)
         t_launch = med()
     finally:
-        L.rsmi_set_option(OPT_SERVER, prev)
-        L.rsmi_set_option(OPT_ONE_GROUP, prev1)
+        L.rsmi_option(OPT_SERVER, prev)
+        L.rsmi_option(OPT_ONE_GROUP, prev1)
     print(f"rs_decode2 median: server {t_srv:.1f} us, launch per call {t_launch:.1f} us")
     assert t_srv < t_launch
 
@@ -134,9 +134,9 @@ def test_server_bounded_sync_under_steady_traffic(gpu):
     rows = np.random.default_rng(5).integers(0, 256, (n, ln), dtype=np.uint8)
     dec = L.compat["rs_decode2"]
     erased = {0, 3, 11, 24, 29}
-    prev1 = L.rsmi_set_option(OPT_ONE_GROUP, 1)
-    prev = L.rsmi_set_option(OPT_SERVER, 20000)
-    assert L.rsmi_set_option(OPT_SERVER_LIFE, 8) >= 1
+    prev1 = L.rsmi_option(OPT_ONE_GROUP, 1)
+    prev = L.rsmi_option(OPT_SERVER, 20000)
+    assert L.rsmi_option(OPT_SERVER_LIFE, 8) >= 1
     stop = threading.Event()
     errors, calls = [], [0]
 
@@ -167,8 +167,8 @@ def test_server_bounded_sync_under_steady_traffic(gpu):
             time.sleep(0.01)
         th.join()
     finally:
-        L.rsmi_set_option(OPT_SERVER, prev)
-        L.rsmi_set_option(OPT_ONE_GROUP, prev1)
+        L.rsmi_option(OPT_SERVER, prev)
+        L.rsmi_option(OPT_ONE_GROUP, prev1)
     assert not errors
     assert calls[0] > 100 and len(waits) > 10
     print(f"{calls[0]} calls; sync wait max {max(waits) * 1e3:.1f} ms, "
@@ -182,10 +182,10 @@ def test_server_bounded_sync_under_steady_traffic(gpu):
 def test_server_lifetime_option(gpu):
     import udpspeeder_amd as u
     L = u.lib()
-    prev = L.rsmi_set_option(OPT_SERVER_LIFE, 5)
+    prev = L.rsmi_option(OPT_SERVER_LIFE, 5)
     try:
-        assert L.rsmi_set_option(OPT_SERVER_LIFE, 8) == 5
-        assert L.rsmi_set_option(OPT_SERVER_LIFE, 0) < 0  # invalid: the lifetime stays
-        assert L.rsmi_set_option(OPT_SERVER_LIFE, 8) == 8
+        assert L.rsmi_option(OPT_SERVER_LIFE, 8) == 5
+        assert L.rsmi_option(OPT_SERVER_LIFE, 0) < 0  # invalid: the lifetime stays
+        assert L.rsmi_option(OPT_SERVER_LIFE, 8) == 8
     finally:
-        L.rsmi_set_option(OPT_SERVER_LIFE, prev)
+        L.rsmi_option(OPT_SERVER_LIFE, prev)

@@ -33,7 +33,7 @@ def test_copy_peak_rejects(gpu):
     assert L.rsmi_copy_peak(a.data_ptr(), a.data_ptr() + 2048, 0, 0, None) == 0
 
 
-@pytest.mark.parametrize("variant,R,W", [(5, 8, 4), (6, 12, 2), (4, 8, 0)])
+@pytest.mark.parametrize("variant,R,W", [(5, 4, 2), (6, 6, 1), (4, 4, 0)])
 def test_mix_peak_writes_its_share(gpu, variant, R, W):
     """The read:write mixes write, per thread, the XOR of its words u = w mod W
     (variant 4 writes nothing)."""
@@ -49,8 +49,8 @@ def test_mix_peak_writes_its_share(gpu, variant, R, W):
     if W == 0:
         assert int(dst.count_nonzero()) == 0
         return
-    words = src.view(torch.int32).view(-1, R, 256, 4)
-    exp = torch.zeros((words.shape[0], W, 256, 4), dtype=torch.int32, device=gpu)
+    words = src.view(torch.int32).view(-1, R, 64, 4)  # per wave: R instructions of 64 lanes
+    exp = torch.zeros((words.shape[0], W, 64, 4), dtype=torch.int32, device=gpu)
     for uu in range(R):
         exp[:, uu % W] ^= words[:, uu]
     got = dst.view(torch.int32)[:exp.numel()].view(exp.shape)

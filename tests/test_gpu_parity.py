@@ -636,11 +636,11 @@ def test_ragged_plan_decode_record_cap(gpu, oracle, cap):
         flags[i, :n] = 1
         flags[i, rng.choice(n, min(5, int(ms[i])), replace=False)] = 0
     L = u.lib()
-    prev = L.rsmi_set_option(RSMI_OPT_CLS_REC_CAP, cap)
+    prev = L.rsmi_option(RSMI_OPT_CLS_REC_CAP, cap)
     try:
         plan = u.rs.RaggedPlan(groups, wait_codes=False)
     finally:
-        L.rsmi_set_option(RSMI_OPT_CLS_REC_CAP, prev)
+        L.rsmi_option(RSMI_OPT_CLS_REC_CAP, prev)
     base = upload(host, gpu)
     bits = torch.from_numpy(synth.present_bits(flags).view(np.int32)).to(gpu)
     st = plan.decode(base, bits).cpu().numpy()
@@ -795,7 +795,7 @@ def test_dropin_one_group_vs_oracle(gpu, oracle, one_group, k, n, ln):
     with e = 13 and 20 has more than 10 rows."""
     import udpspeeder_amd as u
     L = u.lib()
-    prev = L.rsmi_set_option(3, int(one_group))
+    prev = L.rsmi_option(3, int(one_group))
     try:
         rng = np.random.default_rng(k * 31 + n + ln)
         es = [1, 5, 9] + ([13, 20] if min(k, n - k) > 10 else [])
@@ -826,7 +826,7 @@ def test_dropin_one_group_vs_oracle(gpu, oracle, one_group, k, n, ln):
             for j in range(k):
                 assert bytes(ptrs[j]) == buf[j].tobytes(), ("decode", trial, j)
     finally:
-        L.rsmi_set_option(3, prev)
+        L.rsmi_option(3, prev)
 
 
 def test_compat_lower_api(gpu, oracle):

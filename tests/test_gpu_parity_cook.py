@@ -27,7 +27,7 @@ def _run(torch, rs, mode, lens, ev, cuts, key, flags, on, stride_extra=0):
     from udpspeeder_amd._lib import RSMI_OPT_PARITY_COOK
     from udpspeeder_amd.cook import CookContext
     from udpspeeder_amd.fec import FecEncoder
-    prev = u.lib().rsmi_set_option(RSMI_OPT_PARITY_COOK, 1 if on else 0)
+    prev = u.lib().rsmi_option(RSMI_OPT_PARITY_COOK, 1 if on else 0)
     try:
         enc = FecEncoder(rs, mode, 1250, 200, seq0=0xFFFFFF00)
         ctx = CookContext(key, flags)
@@ -56,7 +56,7 @@ def _run(torch, rs, mode, lens, ev, cuts, key, flags, on, stride_extra=0):
         ctx.close()
         return pk, used
     finally:
-        u.lib().rsmi_set_option(RSMI_OPT_PARITY_COOK, prev)
+        u.lib().rsmi_option(RSMI_OPT_PARITY_COOK, prev)
 
 
 @pytest.mark.parametrize("rs,mode,lmax,flags,key", [

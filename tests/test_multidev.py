@@ -1,5 +1,5 @@
 """Several GPUs behind the host-memory entry points (SURVEY.md §8e,
-include/rsmi.h rsmi_set_devices): the range split on the CPU, and on the GPU
+include/rsmi.h rsmi_use_devices): the range split on the CPU, and on the GPU
 the split pipelines bit-exact against the single-device path and the oracle.
 On the 1-GPU box the device list [0, 0] (and [0, 0, 0]) runs two (three)
 workers with their own streams and buffers on one device: the same partition,
@@ -31,8 +31,8 @@ def test_split_ranges_and_set_devices_reject_bad_args():
         u.rs.split_ranges(10, 0)
     with pytest.raises(RsmiError):
         u.rs.split_ranges(3, 2, [1, -1, 2])
-    assert u.lib().rsmi_set_devices(None, -1) != 0
-    assert u.lib().rsmi_set_devices(None, 2) != 0
+    assert u.lib().rsmi_use_devices(None, -1) != 0
+    assert u.lib().rsmi_use_devices(None, 2) != 0
     assert u.rs.get_devices() == []
 
 
@@ -163,7 +163,7 @@ def test_ragged_pinned_rejects_unordered_groups():
 
 @pytest.mark.gpu
 def test_multidev_set_devices_during_calls(gpu, oracle):
-    """rsmi_set_devices racing split calls from another thread: every call
+    """rsmi_use_devices racing split calls from another thread: every call
     either runs on the list it saw or on the current device -- never a silent
     no-op (run_split decides under its lock) -- and its parity is
     right either way."""

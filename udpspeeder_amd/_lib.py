@@ -88,7 +88,7 @@ def _bind(lib: C.CDLL) -> C.CDLL:
     vp, i64, i32 = C.c_void_p, C.c_int64, C.c_int
     sig = {
         "rsmi_version": ([], i32),
-        "rsmi_set_option": ([i32, i32], i32),
+        "rsmi_option": ([i32, i32], i32),
         "rsmi_dropin_latency": ([i32, i32, i32, i32, vp, i32, vp], i32),
         "rsmi_init": ([], i32),
         "rsmi_quiesce": ([], i32),
@@ -130,7 +130,7 @@ def _bind(lib: C.CDLL) -> C.CDLL:
         "rsmi_last_decode_pinned_path": ([], i32),
         "rsmi_encode_ragged_pinned": ([vp, i64, vp, i64], i32),
         "rsmi_decode_ragged_pinned": ([vp, i64, vp, vp, vp, i64], i32),
-        "rsmi_set_devices": ([vp, i32], i32),
+        "rsmi_use_devices": ([vp, i32], i32),
         "rsmi_get_devices": ([vp, i32], i32),
         "rsmi_split_ranges": ([i64, vp, i32, vp], i32),
         "rsmi_cook_ctx_create": ([C.c_char_p, i32, vp], i32),
@@ -144,7 +144,7 @@ def _bind(lib: C.CDLL) -> C.CDLL:
         "rsmi_decook_host": ([vp, vp, i64, i64, C.c_int32, vp, vp], i32),
         "rsmi_fec_config_init": ([vp, C.c_char_p, i32, i32, i32], i32),
         "rsmi_fenc_create": ([vp, C.c_uint32, vp], i32),
-        "rsmi_fenc_set_config": ([vp, vp], i32),
+        "rsmi_fenc_next_config": ([vp, vp], i32),
         "rsmi_fenc_destroy": ([vp], None),
         "rsmi_fenc_plan": ([vp, i64, vp, vp, vp, vp, vp, vp, vp], i32),
         "rsmi_fenc_packets": ([vp, vp], i32),

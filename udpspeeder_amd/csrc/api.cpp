@@ -831,7 +831,7 @@ int check_encode_pinned(int k, int n, const uint8_t *hd, int64_t dgs, uint8_t *h
 }
 
 // The pipeline on the calling thread's current device (D), with pipeline P:
-// the device's own, or a multi-device worker's (rsmi_set_devices).
+// the device's own, or a multi-device worker's (rsmi_use_devices).
 int encode_pinned_on(Device &D, Pipeline &P, int k, int n, const uint8_t *hd, int64_t dgs, uint8_t *hp,
                      int64_t pgs, int64_t ss, int len, int64_t ngroups, int64_t chunk) {
     int rc;
@@ -1187,7 +1187,7 @@ void split_ranges(int64_t n, const int64_t *cost, int parts, int64_t *bounds) {
 
 // run_split's answer when no device list is set: the caller runs the call on
 // its own current device.  Decided under call_mu, so a concurrent
-// rsmi_set_devices(.., 0) cannot turn a split call into a silent no-op.
+// rsmi_use_devices(.., 0) cannot turn a split call into a silent no-op.
 constexpr int kNoWorkers = 0x52534d31;  // never a status: fn returns RSMI_OK or a negative RSMI_ERR_*
 
 // Runs fn(worker, g0, count) for every listed device's range, in parallel, and
@@ -1232,14 +1232,14 @@ int run_split(int64_t ngroups, const std::function<int(Worker &, int64_t, int64_
 }
 
 int set_devices(const int32_t *devs, int32_t n) {
-    if (n < 0 || n > 64 || (n > 0 && !devs)) return fail(RSMI_ERR_INVALID, "rsmi_set_devices: bad arguments");
+    if (n < 0 || n > 64 || (n > 0 && !devs)) return fail(RSMI_ERR_INVALID, "rsmi_use_devices: bad arguments");
     if (n > 0) {
         int count = 0;
         hipError_t e = hipGetDeviceCount(&count);
         if (e != hipSuccess) return hip_fail(e, "hipGetDeviceCount (no usable GPU?)");
         for (int i = 0; i < n; ++i)
             if (devs[i] < 0 || devs[i] >= count)
-                return fail(RSMI_ERR_INVALID, "rsmi_set_devices: device " + std::to_string(devs[i]) +
+                return fail(RSMI_ERR_INVALID, "rsmi_use_devices: device " + std::to_string(devs[i]) +
                                                   " out of range (" + std::to_string(count) + " devices)");
     }
     MultiDev &M = multi();
@@ -1473,7 +1473,7 @@ extern "C" {
 
 int rsmi_version(void) { return 0x000100; }
 
-int rsmi_set_option(int option, int value) {
+int rsmi_option(int option, int value) {
     if (option == RSMI_OPT_BITSLICE) return rsmi::g_opt_bitslice.exchange(value ? 1 : 0);
     if (option == RSMI_OPT_FUSED_DECODE) return rsmi::g_opt_fused.exchange(value ? 1 : 0);
     if (option == RSMI_OPT_ONE_GROUP) return rsmi::g_opt_oneshot.exchange(value ? 1 : 0);
@@ -1560,7 +1560,7 @@ int rsmi_last_encoder(void) { return rsmi::g_last_enc; }
 int rsmi_last_decode_pinned_path(void) { return rsmi::g_last_pinned; }
 
 
-int rsmi_set_devices(const int32_t *devices, int32_t n) { return rsmi::set_devices(devices, n); }
+int rsmi_use_devices(const int32_t *devices, int32_t n) { return rsmi::set_devices(devices, n); }
 
 int rsmi_get_devices(int32_t *out, int32_t cap) { return rsmi::get_devices(out, cap); }
 

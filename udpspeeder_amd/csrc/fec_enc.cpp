@@ -611,7 +611,7 @@ int rsmi_fenc_create(const rsmi_fec_config *cfg, uint32_t seq0, rsmi_fenc **out)
     return RSMI_OK;
 }
 
-int rsmi_fenc_set_config(rsmi_fenc *E, const rsmi_fec_config *cfg) {
+int rsmi_fenc_next_config(rsmi_fenc *E, const rsmi_fec_config *cfg) {
     if (!E || !cfg) return fail(RSMI_ERR_INVALID, "null encoder/config");
     if ((cfg->mode != 0 && cfg->mode != 1) || cfg->rs_cnt < 1 || cfg->rs_cnt > RSMI_FEC_MAX_PACKETS ||
         cfg->mtu < 1 || cfg->queue_len < 1)

@@ -382,25 +382,27 @@ __global__ __launch_bounds__(256) void k_fill_ragged(const rsmi_group *groups, i
     }
 }
 
-// ---- measured copy peak (bench.py's hbm_copy_peak) ---------------------------
-// Each thread moves U 16-byte words spaced one block-width apart (coalesced,
-// every load issued before the first store); NT: nontemporal loads and stores.
-// nbytes % 16 == 0; the tail block checks each word.
+// ---- measured copy peak and read:write mixes (bench.py's hbm_copy_peak) -------
+// A wave moves U (or R) 16-byte words per lane from one contiguous range of
+// its own, 1 KiB per instruction (a block-strided layout, words 4 KiB apart
+// per thread, measured 27 % slower at 8 words per thread: each wave's loads
+// then fall 4 KiB apart); every load is issued before the first store; NT:
+// nontemporal loads and stores.  nbytes % 16 == 0; the tail checks each word.
 typedef uint32_t cp_word __attribute__((ext_vector_type(4)));
 
 template <int U, bool NT>
 __global__ __launch_bounds__(256) void k_copy_peak(cp_word *__restrict__ dst, const cp_word *__restrict__ src,
                                                    int64_t nwords) {
-    const int64_t w0 = (int64_t)blockIdx.x * (256 * U) + threadIdx.x;
+    const int64_t w0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * (64 * U) + (threadIdx.x & 63);
     cp_word v[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-        const int64_t w = w0 + u * 256;
+        const int64_t w = w0 + u * 64;
         if (w < nwords) v[u] = NT ? __builtin_nontemporal_load(src + w) : src[w];
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-        const int64_t w = w0 + u * 256;
+        const int64_t w = w0 + u * 64;
         if (w < nwords) {
             if (NT) __builtin_nontemporal_store(v[u], dst + w);
             else dst[w] = v[u];
@@ -408,32 +410,34 @@ __global__ __launch_bounds__(256) void k_copy_peak(cp_word *__restrict__ dst, co
     }
 }
 
-// Read:write mixes (bench.py's hbm_mix_peaks): each thread reads R 16-byte
-// words, block-strided (coalesced), and writes W words, each the XOR of a
-// share of what it read (W = 0: nothing is written unless the XOR of all R
-// words is the sentinel, which synthetic input never holds).  Whole blocks
-// only (the host rounds the read size down).
+// Read:write mixes: each lane reads R words (its wave's contiguous range, as
+// above) and writes W, each the XOR of a share of what it read (W = 0: nothing
+// is written unless the XOR of all R words is the sentinel, which synthetic
+// input never holds).  Nontemporal, like the codec kernels' streams.  Whole
+// blocks only (the host rounds the read size down).
 template <int R, int W>
 __global__ __launch_bounds__(256) void k_mix_peak(cp_word *__restrict__ dst, const cp_word *__restrict__ src) {
-    const int64_t r0 = (int64_t)blockIdx.x * (256 * R) + threadIdx.x;
+    const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int64_t r0 = wave * (64 * R) + lane;
     cp_word v[R];
 #pragma unroll
-    for (int u = 0; u < R; ++u) v[u] = src[r0 + u * 256];
+    for (int u = 0; u < R; ++u) v[u] = __builtin_nontemporal_load(src + r0 + u * 64);
     if (W == 0) {
         cp_word x = v[0];
 #pragma unroll
         for (int u = 1; u < R; ++u) x ^= v[u];
         if (x.x == 0x9E3779B9u && x.y == 0x7F4A7C15u && x.z == 0xF39CC060u && x.w == 0x5CEDC834u)
-            dst[threadIdx.x] = x;
+            dst[lane] = x;
         return;
     }
-    const int64_t w0 = (int64_t)blockIdx.x * (256 * W) + threadIdx.x;
+    const int64_t w0 = wave * (64 * W) + lane;
 #pragma unroll
     for (int w = 0; w < W; ++w) {
         cp_word x = v[w];
 #pragma unroll
         for (int u = w + W; u < R; u += W) x ^= v[u];
-        dst[w0 + w * 256] = x;
+        __builtin_nontemporal_store(x, dst + w0 + w * 64);
     }
 }
 
@@ -498,9 +502,9 @@ hipError_t launch_copy_peak(uint8_t *dst, const uint8_t *src, int64_t nbytes, in
         auto d = reinterpret_cast<cp_word *>(dst);
         auto r = reinterpret_cast<const cp_word *>(src);
         switch (variant) {
-            case 4: k_mix_peak<8, 0><<<(unsigned)(nw / (256 * 8)), 256, 0, s>>>(d, r); break;
-            case 5: k_mix_peak<8, 4><<<(unsigned)(nw / (256 * 8)), 256, 0, s>>>(d, r); break;
-            default: k_mix_peak<12, 2><<<(unsigned)(nw / (256 * 12)), 256, 0, s>>>(d, r); break;
+            case 4: k_mix_peak<4, 0><<<(unsigned)(nw / (256 * 4)), 256, 0, s>>>(d, r); break;
+            case 5: k_mix_peak<4, 2><<<(unsigned)(nw / (256 * 4)), 256, 0, s>>>(d, r); break;
+            default: k_mix_peak<6, 1><<<(unsigned)(nw / (256 * 6)), 256, 0, s>>>(d, r); break;
         }
         return hipGetLastError();
     }

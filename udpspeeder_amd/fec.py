@@ -79,7 +79,7 @@ class FecEncoder:
     def set_config(self, rs_str: str, mode: int = 0, mtu: int = 1250, queue_len: int = 200):
         """g_fec_par update: taken up at the next group start (fec_manager.cpp:207-209)."""
         cfg = fec_config(rs_str, mode, mtu, queue_len)
-        check(lib().rsmi_fenc_set_config(self._h, C.byref(cfg)), "rsmi_fenc_set_config")
+        check(lib().rsmi_fenc_next_config(self._h, C.byref(cfg)), "rsmi_fenc_next_config")
 
     def plan(self, lens, offsets=None, in_buf=None) -> FencPlan:
         """Plan input() for every event: lens[i] >= 0 is a packet of that many

@@ -166,14 +166,14 @@ def set_bitslice(enabled: bool) -> bool:
     """Use (default) or bypass the specialised bit-sliced encoders; returns
     the previous setting.  For A/B tests of the generic kernel."""
     from ._lib import RSMI_OPT_BITSLICE
-    return bool(lib().rsmi_set_option(RSMI_OPT_BITSLICE, int(bool(enabled))))
+    return bool(lib().rsmi_option(RSMI_OPT_BITSLICE, int(bool(enabled))))
 
 
 def set_fused_decode(enabled: bool) -> bool:
     """Use (default) or bypass the fused decode kernel; returns the previous
     setting.  For A/B tests of the two-kernel (plan + apply) decode path."""
     from ._lib import RSMI_OPT_FUSED_DECODE
-    return bool(lib().rsmi_set_option(RSMI_OPT_FUSED_DECODE, int(bool(enabled))))
+    return bool(lib().rsmi_option(RSMI_OPT_FUSED_DECODE, int(bool(enabled))))
 
 
 def version() -> int:
@@ -554,11 +554,11 @@ def decode_ragged_pinned(host_base, groups, present_bits, chunk_groups: int = 81
 
 
 def set_devices(devices) -> None:
-    """rsmi_set_devices: split the host-memory batch entry points
+    """rsmi_use_devices: split the host-memory batch entry points
     (encode_pinned / decode_pinned) over these devices, one contiguous group
     range each (a device may repeat); [] restores the current device."""
     d = np.ascontiguousarray(np.asarray(list(devices), np.int32))
-    check(lib().rsmi_set_devices(d.ctypes.data if d.size else None, int(d.size)), "rsmi_set_devices")
+    check(lib().rsmi_use_devices(d.ctypes.data if d.size else None, int(d.size)), "rsmi_use_devices")
 
 
 def get_devices():
