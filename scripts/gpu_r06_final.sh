@@ -22,4 +22,9 @@ bash scripts/gpu_traffic.sh > $O/traffic.txt 2>&1 || { tail $O/traffic.txt; exit
 cp gpurun_out/traffic/traffic_encode.json gpurun_out/traffic/traffic_decode.json $O/
 cp gpurun_out/traffic/p1/run_counter_collection.csv $O/traffic_fetch_counters.csv
 cp gpurun_out/traffic/p2/run_counter_collection.csv $O/traffic_write_counters.csv
+# the counters behind DESIGN's C3 and cook paragraphs (one set per pass)
+bash scripts/pmc_passes.sh pmc6_c3 k_bs_ragged k_decode_ragged_mix -- scripts/bench_c3.py > $O/pmc6_c3.txt 2>&1 || { tail $O/pmc6_c3.txt; exit 1; }
+PMC_SETS="FETCH_SIZE;WRITE_SIZE;SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_INSTS_LDS SQ_INSTS_VALU SQ_WAVES;SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU" \
+    bash scripts/pmc_passes.sh pmc6_cook k_cook k_decook -- scripts/bench_cook.py > $O/pmc6_cook.txt 2>&1 || { tail $O/pmc6_cook.txt; exit 1; }
+cat $O/pmc6_c3.txt $O/pmc6_cook.txt
 head -30 $O/kernel_by_grid.txt

@@ -56,7 +56,6 @@ struct rsmi_ragged_plan {
     uint32_t bytes = 0;       // extent of the batch from base (bitslice path)
     uint32_t nwaves = 0;
     uint32_t nwaves_builtin = 0;  // waves [0, nwaves_builtin) belong to build-time codes
-    uint32_t nwaves_split = 0;    // waves [0, nwaves_split): codes with a split-k network
     struct RtcBucket {
         int k, n;
         uint32_t first, count;  // slice of the wave list
@@ -184,13 +183,7 @@ extern "C" int rsmi_ragged_plan_create(const rsmi_group *g, int64_t ngroups,
                 const int na = rsmi::bitslice_code_n(a), nb2 = rsmi::bitslice_code_n(b);
                 return na != nb2 ? na > nb2 : ka > kb;
             });
-        // the buckets of split-k codes first (2-wave blocks, k_bs_ragged_split)
-        std::stable_partition(order.begin(), order.begin() + std::min(nb, nbuiltin), [](int b) {
-            return rsmi::bitslice_has_split(rsmi::bitslice_code_k(b), rsmi::bitslice_code_n(b));
-        });
         for (int b : order) {
-            if (b < nbuiltin && rsmi::bitslice_has_split(rsmi::bitslice_code_k(b), rsmi::bitslice_code_n(b)))
-                P->nwaves_split = (uint32_t)(waves.size() / 2) + (uint32_t)((cols[(size_t)b] + 127) / 128);
             if (b == nbuiltin) P->nwaves_builtin = (uint32_t)(waves.size() / 2);
             const uint32_t first = (uint32_t)(waves.size() / 2);
             for (uint64_t w = 0; w < (cols[(size_t)b] + 127) / 128; ++w) {
@@ -345,7 +338,7 @@ extern "C" int rsmi_encode_ragged_plan(const rsmi_ragged_plan *P, uint8_t *base,
     hipError_t e;
     if (P->bitslice) {
         e = rsmi::launch_encode_bitslice_ragged(P->d_groups, P->d_colmap, P->d_waves,
-                                                P->nwaves_builtin, base, P->bytes, s, P->nwaves_split);
+                                                P->nwaves_builtin, base, P->bytes, s);
         for (size_t i = 0; e == hipSuccess && i < P->rtc.size(); ++i) {
             const auto &b = P->rtc[i];
             e = rsmi::launch_encode_bitslice_ragged_rtc(b.k, b.n, P->d_groups, P->d_colmap,

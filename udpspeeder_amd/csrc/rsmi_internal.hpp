@@ -158,12 +158,9 @@ int bitslice_code_k(int idx);  // (k, n) of generated code idx
 int bitslice_code_n(int idx);
 // Ragged bucketed launch over a host-built plan (ragged.cpp): colmap entries
 // (group << 12) | piece, waves = {code index, first column} pairs.
-// The first nsplit wave records belong to buckets whose code has a split-k
-// network (bitslice_has_split): those run as 2-wave blocks.
 hipError_t launch_encode_bitslice_ragged(const rsmi_group *groups, const uint32_t *colmap,
                                          const uint32_t *waves, uint32_t nwaves, uint8_t *base,
-                                         uint32_t bytes, hipStream_t s, uint32_t nsplit = 0);
-bool bitslice_has_split(int k, int n);
+                                         uint32_t bytes, hipStream_t s);
 
 // Codes without a build-time network (bitslice_rtc.cpp): emitted and compiled
 // with hipRTC in the background when first made resident.
