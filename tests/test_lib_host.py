@@ -205,3 +205,19 @@ def test_fec_decode_invalid_index_permutes_like_reference(index):
     assert rc == rc_ref == 1
     assert oidx == list(idx)
     assert [next(i for i, b in enumerate(pkt) if b is p) for p in ours] == ref_slots
+
+
+def test_parity_cook_option_roundtrip():
+    """RSMI_OPT_PARITY_COOK (no GPU needed): off by default (RSMI_PARITY_COOK
+    unset), rsmi_option returns the previous value, any nonzero turns it on."""
+    import os
+    import udpspeeder_amd as u
+    from udpspeeder_amd._lib import RSMI_OPT_PARITY_COOK
+    L = u.lib()
+    first = L.rsmi_option(RSMI_OPT_PARITY_COOK, 1)
+    if not os.environ.get("RSMI_PARITY_COOK"):
+        assert first == 0
+    assert L.rsmi_option(RSMI_OPT_PARITY_COOK, 7) == 1
+    assert L.rsmi_option(RSMI_OPT_PARITY_COOK, 0) == 1
+    assert L.rsmi_option(RSMI_OPT_PARITY_COOK, first) == 0
+    assert L.rsmi_option(12345, 1) == -2  # unknown option: RSMI_ERR_INVALID
