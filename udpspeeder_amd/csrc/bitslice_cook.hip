@@ -33,8 +33,7 @@ namespace {
 // piece wholly inside its packet's payload is stored into the output XOR its
 // IV window and key stream at its packet offset x = 8 + 16 col (do_obscure +
 // encrypt_0, packet.cpp:77-91, 32-39; the CRC and tail are k_cook's), the
-// other pieces plain into the output; a slot without this run's record keeps
-// the plain store into the slot.
+// other pieces plain into the output.  The parity slots are not written.
 typedef uint32_t bs_u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
 struct CookIO {
     DevIO io;
